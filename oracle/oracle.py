@@ -1,0 +1,138 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of ``oracle/liboracle.so``, the CPU restatement of the reference's
+hot path (see ``oracle/oracle.h`` for the reference file:line each function
+follows).  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg import this module; the product package ``mosaic_amd``
+never does.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError("oracle/liboracle.so is not built (run `make -C oracle`)")
+        L = ctypes.CDLL(path)
+        L.orc_h3_geo_to_h3.restype = ctypes.c_uint64
+        L.orc_h3_geo_to_h3.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int]
+        L.orc_h3_point_to_index.restype = ctypes.c_uint64
+        L.orc_h3_point_to_index.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int]
+        L.orc_h3_points_to_cells.restype = None
+        L.orc_h3_points_to_cells.argtypes = [_dp, _dp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _u64p, ctypes.c_int]
+        L.orc_h3_geo_to_hex2d.restype = None
+        L.orc_h3_geo_to_hex2d.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_int), _dp, _dp]
+        L.orc_bng_point_to_index.restype = ctypes.c_int64
+        L.orc_bng_point_to_index.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_int)]
+        L.orc_bng_points_to_cells.restype = None
+        L.orc_bng_points_to_cells.argtypes = [_dp, _dp, ctypes.c_int64, ctypes.c_int, _i64p, ctypes.c_int]
+        L.orc_wkb_contains.restype = ctypes.c_int
+        L.orc_wkb_contains.argtypes = [_u8p, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
+                                       ctypes.POINTER(ctypes.c_int)]
+        L.orc_pip_join.restype = ctypes.c_int64
+        L.orc_pip_join.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _dp, ctypes.c_int64,
+                                   ctypes.c_int64, _i64p, _i32p, _u8p, _i64p, _u8p, _i64p, _i32p,
+                                   ctypes.c_int64, ctypes.c_int]
+        _LIB = L
+    return _LIB
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(t)
+
+
+def h3_point_to_index(lon, lat, res, jdk=8):
+    return int(lib().orc_h3_point_to_index(float(lon), float(lat), int(res), int(jdk)))
+
+
+def h3_points_to_cells(lon, lat, res, jdk=8, threads=None):
+    lon = np.ascontiguousarray(lon, dtype=np.float64)
+    lat = np.ascontiguousarray(lat, dtype=np.float64)
+    out = np.empty(lon.shape[0], dtype=np.uint64)
+    lib().orc_h3_points_to_cells(_ptr(lon, _dp), _ptr(lat, _dp), lon.shape[0], int(res), int(jdk),
+                                 _ptr(out, _u64p), int(threads or os.cpu_count() or 1))
+    return out.view(np.int64)
+
+
+def h3_geo_to_hex2d(lat_rad, lon_rad, res):
+    f = ctypes.c_int()
+    x = ctypes.c_double()
+    y = ctypes.c_double()
+    lib().orc_h3_geo_to_hex2d(lat_rad, lon_rad, res, ctypes.byref(f), ctypes.byref(x), ctypes.byref(y))
+    return f.value, x.value, y.value
+
+
+def bng_point_to_index(e, n, res):
+    err = ctypes.c_int()
+    v = lib().orc_bng_point_to_index(float(e), float(n), int(res), ctypes.byref(err))
+    if err.value:
+        raise ValueError("NaN coordinates are not supported.")
+    return int(v)
+
+
+def bng_points_to_cells(e, n, res, threads=None):
+    e = np.ascontiguousarray(e, dtype=np.float64)
+    n = np.ascontiguousarray(n, dtype=np.float64)
+    out = np.empty(e.shape[0], dtype=np.int64)
+    lib().orc_bng_points_to_cells(_ptr(e, _dp), _ptr(n, _dp), e.shape[0], int(res), _ptr(out, _i64p),
+                                  int(threads or os.cpu_count() or 1))
+    return out
+
+
+LOC_EXTERIOR, LOC_BOUNDARY, LOC_INTERIOR = 0, 1, 2
+
+
+def wkb_locate(wkb: bytes, x, y):
+    buf = np.frombuffer(wkb, dtype=np.uint8)
+    err = ctypes.c_int()
+    loc = lib().orc_wkb_contains(_ptr(buf, _u8p), len(wkb), float(x), float(y), ctypes.byref(err))
+    if err.value:
+        raise ValueError("unsupported or malformed WKB (%d)" % err.value)
+    return loc
+
+
+def st_contains(wkb: bytes, x, y):
+    return wkb_locate(wkb, x, y) == LOC_INTERIOR
+
+
+def pip_join(index_system, res, x, y, chip_cell, chip_poly, chip_core, wkb_offsets, wkb_blob,
+             jdk=8, threads=None):
+    """Sorted (point index, polygon id) pairs of the reference's join + filter."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    cc = np.ascontiguousarray(chip_cell, dtype=np.int64)
+    cp = np.ascontiguousarray(chip_poly, dtype=np.int32)
+    co = np.ascontiguousarray(chip_core, dtype=np.uint8)
+    off = np.ascontiguousarray(wkb_offsets, dtype=np.int64)
+    blob = np.ascontiguousarray(np.frombuffer(bytes(wkb_blob), dtype=np.uint8) if not isinstance(wkb_blob, np.ndarray)
+                                else wkb_blob, dtype=np.uint8)
+    if blob.size == 0:
+        blob = np.zeros(1, dtype=np.uint8)
+    nt = int(threads or os.cpu_count() or 1)
+    L = lib()
+    args = [int(index_system), int(res), int(jdk), _ptr(x, _dp), _ptr(y, _dp), x.shape[0], cc.shape[0],
+            _ptr(cc, _i64p), _ptr(cp, _i32p), _ptr(co, _u8p), _ptr(off, _i64p), _ptr(blob, _u8p)]
+    cnt = L.orc_pip_join(*args, None, None, 0, nt)
+    if cnt < 0:
+        raise ValueError("oracle join failed (NaN BNG coordinates or unsupported chip WKB)")
+    pts = np.empty(max(cnt, 1), dtype=np.int64)
+    polys = np.empty(max(cnt, 1), dtype=np.int32)
+    cnt2 = L.orc_pip_join(*args, _ptr(pts, _i64p), _ptr(polys, _i32p), cnt, nt)
+    assert cnt2 == cnt
+    return pts[:cnt], polys[:cnt]
