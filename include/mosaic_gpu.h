@@ -1,0 +1,162 @@
+/*
+ * mosaic_gpu.h -- C ABI of the MI355X grid-indexed point-in-polygon join.
+ *
+ * The drop-in boundary for the reference's hot path (tiems90/mosaic 0.4.3):
+ *   points -> cell id        grid_pointascellid / grid_longlatascellid
+ *   polygons -> chips        grid_tessellateexplode rows (is_core, index_id, wkb)
+ *   join + filter            cell == index_id AND (is_core OR st_contains(wkb, pt))
+ * behind the reference's IndexSystem plugin interface
+ *   src/main/scala/com/databricks/labs/mosaic/core/index/IndexSystem.scala:15-318
+ * Each entry point below names the reference interface it replaces.  A JVM host
+ * binds them through a thin JNI shim; this repository's Python
+ * host (mosaic_amd/) binds them with ctypes.
+ *
+ * Conventions
+ *  - Plain C types only.  Status codes: 0 = ok, negative = error class; the
+ *    message of the calling thread's last error is mgpu_last_error().
+ *  - "device" pointers are HBM allocations on the context's GPU (hipMalloc /
+ *    torch tensors); "host" pointers are ordinary memory.  `stream` is a
+ *    hipStream_t (NULL = the legacy default stream).
+ *  - Functions are thread-safe for distinct contexts; one context must not be used
+ *    concurrently from several threads (one context per executor thread/GPU).
+ *  - index_system: MGPU_H3 (H3IndexSystem) or MGPU_BNG (BNGIndexSystem);
+ *    resolutions are validated like IndexSystem.getResolution
+ *    (H3IndexSystem.scala:45-60: 0..15; BNGIndexSystem.scala:349-360: +-1..+-6).
+ */
+#ifndef MOSAIC_GPU_H
+#define MOSAIC_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGPU_OK 0
+#define MGPU_E_INVALID_ARG -1       /* IllegalArgumentException (bad argument, NaN H3 coordinate) */
+#define MGPU_E_RESOLUTION -2        /* IllegalStateException (resolution not supported) */
+#define MGPU_E_NAN -3               /* IllegalStateException (BNG: "NaN coordinates are not supported.") */
+#define MGPU_E_WKB -4               /* JTS ParseException / unsupported chip geometry */
+#define MGPU_E_CAPACITY -5          /* output arrays too small; the required count is returned */
+#define MGPU_E_DEVICE -6            /* HIP runtime error */
+#define MGPU_E_INTERNAL -7          /* kernel protocol failure (look-back timeout) */
+
+#define MGPU_H3 0
+#define MGPU_BNG 1
+
+typedef struct mgpu_ctx mgpu_ctx;
+typedef struct mgpu_chips mgpu_chips;
+
+/* Per-call statistics (optional out-parameter). */
+typedef struct mgpu_stats {
+    int64_t n_points;       /* points processed */
+    int64_t n_pairs;        /* (point, polygon) pairs produced */
+    int64_t n_near_ties;    /* H3 points whose hex2d coordinate is within 2^-40 (relative)
+                               of a cell edge: the only points where an ulp-level libm
+                               difference could change the cell */
+    int64_t n_candidates;   /* (point, border chip) PIP evaluations */
+    float kernel_ms;        /* device time of the main kernel (HIP events) */
+} mgpu_stats;
+
+const char* mgpu_last_error(void);
+const char* mgpu_version(void);
+
+/* One context per GPU/executor: owns the stream-ordered workspace. */
+int32_t mgpu_ctx_create(int32_t device_id, mgpu_ctx** out);
+int32_t mgpu_ctx_destroy(mgpu_ctx* ctx);
+
+/* IndexSystem.getResolution for an integer resolution (H3IndexSystem.scala:45-60,
+ * BNGIndexSystem.scala:349-360).  Returns the resolution or MGPU_E_RESOLUTION. */
+int32_t mgpu_check_resolution(int32_t index_system, int32_t res);
+
+/* IndexSystem.pointToIndex(x, y, res) over a batch (IndexSystem.scala:237;
+ * H3IndexSystem.scala:168-170 = H3Core.geoToH3(lat, lon, res);
+ * BNGIndexSystem.scala:284-298).  x = lon / eastings, y = lat / northings.
+ * Device pointers, asynchronous on `stream`; `stats` (optional) is filled after
+ * a stream synchronisation. */
+int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t index_system, int32_t res,
+                             const double* x, const double* y, int64_t n,
+                             int64_t* out_cell, void* stream, mgpu_stats* stats);
+
+/* Host-pointer convenience form (copies over PCIe). */
+int32_t mgpu_points_to_cells_host(mgpu_ctx* ctx, int32_t index_system, int32_t res,
+                                  const double* x, const double* y, int64_t n, int64_t* out_cell);
+
+/* BNGIndexSystem.format / parse (BNGIndexSystem.scala:119-134, 440-442; parse at
+ * the `parse` method) -- the StringType cell id (default for BNG).  `out` receives
+ * concatenated ASCII ids, out_offsets[n + 1] their boundaries; out_bytes is the
+ * capacity of `out` (ids are at most 16 chars). Host pointers. */
+int32_t mgpu_bng_format(const int64_t* cells, int64_t n, char* out, int64_t out_bytes, int64_t* out_offsets);
+int32_t mgpu_bng_parse(const char* ids, const int64_t* offsets, int64_t n, int64_t* out_cells);
+
+/* Upload a chip table (the rows of grid_tessellateexplode, MosaicExplode.scala:70-83,
+ * ChipType.scala:17-29): cell id, owning polygon id, is_core, and the chip WKB
+ * (big- or little-endian, Polygon / MultiPolygon / GeometryCollection of those;
+ * a NULL geometry is wkb_offsets[i] == wkb_offsets[i+1]).  Host pointers.  The WKB
+ * is parsed once here (the reference re-parses it per candidate row). */
+int32_t mgpu_chips_upload(mgpu_ctx* ctx, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
+                          const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb,
+                          mgpu_chips** out);
+int32_t mgpu_chips_destroy(mgpu_chips* chips);
+/* The chip table is one device allocation: expose it for replication (RCCL
+ * broadcast of `bytes` at `device_ptr`), and rebuild a handle on another GPU from
+ * a received copy (the received buffer is copied into a new allocation). */
+int32_t mgpu_chips_device_blob(const mgpu_chips* chips, void** device_ptr, int64_t* bytes);
+int32_t mgpu_chips_from_device_blob(mgpu_ctx* ctx, const void* device_ptr, int64_t bytes, mgpu_chips** out);
+int32_t mgpu_chips_info(const mgpu_chips* chips, int64_t* n_chips, int64_t* n_cells, int64_t* n_vertices);
+
+/* st_contains(chip.wkb, point) for explicit (chip row, point) pairs
+ * (ST_Contains.scala:21-44 -> MosaicGeometryJTS.contains, MosaicGeometryJTS.scala:197).
+ * out[i] = 1 / 0, or -1 when the chip's geometry is NULL.  Device pointers. */
+int32_t mgpu_st_contains(mgpu_ctx* ctx, const mgpu_chips* chips, const int64_t* chip_row,
+                         const double* x, const double* y, int64_t n, int8_t* out, void* stream);
+
+/* The fused hot path: cell id per point, equi-join against the chip table's
+ * cell ids, `is_core OR st_contains` filter; emits (point_id, polygon_id) pairs
+ * ordered by input position then polygon id (sorted by point_id when point ids
+ * ascend, e.g. contiguous id shards).  point_id may be NULL: ids are
+ * point_id_base + index.  Device pointers.  Synchronises `stream` to return the
+ * pair count in *out_n_pairs; if it exceeds `capacity` only the first `capacity`
+ * pairs are written and MGPU_E_CAPACITY is returned. */
+int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t index_system, int32_t res,
+                      const double* x, const double* y, const int64_t* point_id, int64_t point_id_base,
+                      int64_t n, int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id,
+                      int32_t* out_polygon_id, void* stream, mgpu_stats* stats);
+
+/* Asynchronous form: the pair count is left in device memory (*d_n_pairs, one
+ * int64) and nothing synchronises -- graph-capturable once mgpu_ctx_reserve has
+ * sized the workspace. */
+int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t index_system, int32_t res,
+                            const double* x, const double* y, const int64_t* point_id, int64_t point_id_base,
+                            int64_t n, int64_t capacity, int64_t* d_n_pairs, int64_t* out_point_id,
+                            int32_t* out_polygon_id, void* stream);
+int32_t mgpu_ctx_reserve(mgpu_ctx* ctx, int64_t max_points);
+
+/* Host-pointer convenience form of mgpu_pip_join (copies points in, pairs out). */
+int32_t mgpu_pip_join_host(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t index_system, int32_t res,
+                           const double* x, const double* y, const int64_t* point_id, int64_t n,
+                           int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id,
+                           int32_t* out_polygon_id);
+
+/* grid_tessellateexplode for a polygon set (Mosaic.getChips / mosaicFill,
+ * core/Mosaic.scala:22-99; IndexSystem.getCoreChips/getBorderChips,
+ * IndexSystem.scala:178-213).  Polygons are given as flat rings:
+ *   polygon p has parts [poly_part_off[p], poly_part_off[p+1]),
+ *   part q has rings [part_ring_off[q], part_ring_off[q+1]) (first = shell),
+ *   ring r has vertices xy[2*ring_off[r] .. 2*ring_off[r+1]) (closed rings).
+ * Output rows are returned through an opaque result read with
+ * mgpu_tess_result_*; chip WKB is big-endian (JTS WKBWriter).  Host only. */
+typedef struct mgpu_tess mgpu_tess;
+int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, const int32_t* polygon_id,
+                        const int64_t* poly_part_off, const int64_t* part_ring_off, const int64_t* ring_off,
+                        const double* xy, int32_t keep_core_geometries, mgpu_tess** out);
+int32_t mgpu_tess_result_sizes(const mgpu_tess* t, int64_t* n_chips, int64_t* wkb_bytes);
+int32_t mgpu_tess_result_copy(const mgpu_tess* t, int64_t* cell, int32_t* polygon_id, uint8_t* is_core,
+                              int64_t* wkb_offsets, uint8_t* wkb);
+int32_t mgpu_tess_destroy(mgpu_tess* t);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MOSAIC_GPU_H */

@@ -1,0 +1,132 @@
+"""ctypes binding of ``mosaic_amd/libmosaic_gpu.so`` (the C ABI in include/mosaic_gpu.h).
+
+There is no fallback: if the library is missing, or a compute entry point is
+called without a GPU, the call raises.  Device memory is passed as raw pointers
+(``torch.Tensor.data_ptr()``); torch is only the allocator / stream provider.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmosaic_gpu.so")
+
+MGPU_OK = 0
+MGPU_E_INVALID_ARG = -1
+MGPU_E_RESOLUTION = -2
+MGPU_E_NAN = -3
+MGPU_E_WKB = -4
+MGPU_E_CAPACITY = -5
+MGPU_E_DEVICE = -6
+MGPU_E_INTERNAL = -7
+
+MGPU_H3 = 0
+MGPU_BNG = 1
+
+# every symbol include/mosaic_gpu.h declares
+EXPORTS = (
+    "mgpu_last_error", "mgpu_version", "mgpu_ctx_create", "mgpu_ctx_destroy", "mgpu_check_resolution",
+    "mgpu_points_to_cells", "mgpu_points_to_cells_host", "mgpu_bng_format", "mgpu_bng_parse",
+    "mgpu_chips_upload", "mgpu_chips_destroy", "mgpu_chips_device_blob", "mgpu_chips_from_device_blob",
+    "mgpu_chips_info", "mgpu_st_contains", "mgpu_pip_join", "mgpu_pip_join_async", "mgpu_ctx_reserve",
+    "mgpu_pip_join_host", "mgpu_tessellate", "mgpu_tess_result_sizes", "mgpu_tess_result_copy",
+    "mgpu_tess_destroy",
+)
+
+
+class MosaicGpuError(RuntimeError):
+    """A non-zero status from the C ABI; ``code`` is the MGPU_E_* class."""
+
+    def __init__(self, code, msg):
+        super().__init__("%s (status %d)" % (msg, code))
+        self.code = code
+
+
+class IllegalArgumentException(MosaicGpuError, ValueError):
+    pass
+
+
+class IllegalStateException(MosaicGpuError):
+    pass
+
+
+class CapacityError(MosaicGpuError):
+    def __init__(self, code, msg, required):
+        super().__init__(code, msg)
+        self.required = required
+
+
+class MgpuStats(ctypes.Structure):
+    _fields_ = [("n_points", ctypes.c_int64), ("n_pairs", ctypes.c_int64), ("n_near_ties", ctypes.c_int64),
+                ("n_candidates", ctypes.c_int64), ("kernel_ms", ctypes.c_float)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("mosaic_amd/libmosaic_gpu.so is not built: run `python -c 'import __graft_entry__ as g; "
+                           "g.build()'` (the HIP path has no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "mgpu_last_error": (ctypes.c_char_p, []),
+        "mgpu_version": (ctypes.c_char_p, []),
+        "mgpu_ctx_create": (I32, [I32, ctypes.POINTER(P)]),
+        "mgpu_ctx_destroy": (I32, [P]),
+        "mgpu_check_resolution": (I32, [I32, I32]),
+        "mgpu_points_to_cells": (I32, [P, I32, I32, P, P, I64, P, P, ctypes.POINTER(MgpuStats)]),
+        "mgpu_points_to_cells_host": (I32, [P, I32, I32, P, P, I64, P]),
+        "mgpu_bng_format": (I32, [P, I64, P, I64, P]),
+        "mgpu_bng_parse": (I32, [P, P, I64, P]),
+        "mgpu_chips_upload": (I32, [P, I64, P, P, P, P, P, ctypes.POINTER(P)]),
+        "mgpu_chips_destroy": (I32, [P]),
+        "mgpu_chips_device_blob": (I32, [P, ctypes.POINTER(P), ctypes.POINTER(I64)]),
+        "mgpu_chips_from_device_blob": (I32, [P, P, I64, ctypes.POINTER(P)]),
+        "mgpu_chips_info": (I32, [P, ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(I64)]),
+        "mgpu_st_contains": (I32, [P, P, P, P, P, I64, P, P]),
+        "mgpu_pip_join": (I32, [P, P, I32, I32, P, P, P, I64, I64, I64, ctypes.POINTER(I64), P, P, P,
+                                ctypes.POINTER(MgpuStats)]),
+        "mgpu_pip_join_async": (I32, [P, P, I32, I32, P, P, P, I64, I64, I64, P, P, P, P]),
+        "mgpu_ctx_reserve": (I32, [P, I64]),
+        "mgpu_pip_join_host": (I32, [P, P, I32, I32, P, P, P, I64, I64, ctypes.POINTER(I64), P, P]),
+        "mgpu_tessellate": (I32, [I32, I32, I64, P, P, P, P, P, I32, ctypes.POINTER(P)]),
+        "mgpu_tess_result_sizes": (I32, [P, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
+        "mgpu_tess_result_copy": (I32, [P, P, P, P, P, P]),
+        "mgpu_tess_destroy": (I32, [P]),
+    }
+    for name, (rt, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = rt
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def last_error():
+    m = lib().mgpu_last_error()
+    return m.decode() if m else ""
+
+
+def check(status, what="", required=None):
+    """Map a status code to the reference's exception classes (IndexSystem.scala:54-58,
+    BNGIndexSystem.scala:285, H3Core.geoToH3's IllegalArgumentException)."""
+    if status == MGPU_OK:
+        return
+    msg = last_error() or what
+    if status == MGPU_E_CAPACITY:
+        raise CapacityError(status, msg, required)
+    if status in (MGPU_E_RESOLUTION, MGPU_E_NAN, MGPU_E_INTERNAL):
+        raise IllegalStateException(status, msg)
+    if status in (MGPU_E_INVALID_ARG, MGPU_E_WKB):
+        raise IllegalArgumentException(status, msg)
+    raise MosaicGpuError(status, msg)

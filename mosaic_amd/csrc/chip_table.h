@@ -1,0 +1,67 @@
+// Device-resident chip table: the ChipType rows `(is_core, index_id, wkb)` of
+// `grid_tessellateexplode` (reference core/types/ChipType.scala:17-29,
+// core/types/model/MosaicChip.scala:20-83), plus the owning polygon id, flattened
+// to structure-of-arrays in ONE device allocation (so it can be replicated to
+// other GPUs with a single RCCL broadcast).
+//
+// Layout (all arrays 16-byte aligned inside the blob):
+//   cell hash  : open addressing, linear probing, `hash_cap` slots of
+//                {u64 cell, u32 first_chip, u32 n_chips}; n_chips == 0 = empty
+//   chips      : sorted by (cell, polygon id, input row)  -> matches come out in
+//                polygon-id order for every point
+//                chip_poly[i32], chip_flags[u8], chip_part[u32 n_chips+1],
+//                chip_env[double4 minx,miny,maxx,maxy], chip_row[i64 input row]
+//   geometry   : part_ring[u32 n_parts+1], ring_vtx[u32 n_rings+1],
+//                ring_env[double4], vtx[double2 x,y]
+//   row map    : row_to_chip[u32 n_chips] (input row -> sorted position)
+#pragma once
+#include <stdint.h>
+
+namespace mgpu {
+
+enum ChipFlags : uint8_t {
+  kChipCore = 1,       // is_core: every point of the cell matches
+  kChipRect = 2,       // Polygon.isRectangle(): RectangleContains shortcut
+  kChipMulti = 4,      // MultiPolygon / GeometryCollection: Mod-2 PointLocator
+  kChipEmpty = 8,      // no coordinates: contains nothing
+  kChipNoGeom = 16,    // WKB was NULL (core chip with keep_core_geometries=false)
+};
+
+struct alignas(16) HashSlot {
+  uint64_t cell;
+  uint32_t first;
+  uint32_t count;
+};
+
+struct ChipTableView {
+  const HashSlot* slots;
+  uint32_t hash_mask;
+  uint32_t max_probe;
+  uint32_t n_chips;
+  uint32_t n_cells;
+  const int32_t* chip_poly;
+  const uint8_t* chip_flags;
+  const uint32_t* chip_part;   // [n_chips + 1]
+  const double* chip_env;      // 4 per chip
+  const int64_t* chip_row;     // input row of each sorted chip
+  const uint32_t* part_ring;   // [n_parts + 1]
+  const uint32_t* ring_vtx;    // [n_rings + 1]
+  const double* ring_env;      // 4 per ring
+  const double* vtx;           // 2 per vertex
+  const uint32_t* row_to_chip; // [n_chips]
+};
+
+#ifdef __HIPCC__
+#define MGPU_HDI __host__ __device__ __forceinline__
+#else
+#define MGPU_HDI inline
+#endif
+
+MGPU_HDI uint32_t cell_hash(uint64_t cell) {
+  uint64_t z = cell * 0x9E3779B97F4A7C15ULL;
+  z ^= z >> 29;
+  z *= 0xBF58476D1CE4E5B9ULL;
+  return (uint32_t)(z >> 32);
+}
+
+}  // namespace mgpu

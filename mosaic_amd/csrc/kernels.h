@@ -1,0 +1,35 @@
+// Launch interface between the C-ABI layer (capi.cpp) and the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mosaic_gpu.h"
+#include "chip_table.h"
+
+namespace mgpu {
+
+struct JoinArgs {
+  const double* x;
+  const double* y;
+  const int64_t* point_id;
+  int64_t id_base;
+  int64_t n;
+  int64_t n_tiles;
+  int res;
+  ChipTableView chips;
+  int64_t capacity;
+  int64_t* out_point;
+  int32_t* out_poly;
+  uint64_t* tile_status;            // [n_tiles], zeroed before launch
+  uint32_t* tile_ticket;            // zeroed before launch
+  unsigned long long* counters;     // [0] pairs [1] near-ties [2] invalid [3] candidates [4] look-back timeouts
+};
+
+hipError_t launch_cells(int is, int res, const double* x, const double* y, int64_t n, int64_t* out,
+                        unsigned long long* counters, hipStream_t s);
+int64_t join_tiles(int64_t n);
+hipError_t launch_join(int is, const JoinArgs& a, hipStream_t s);
+hipError_t launch_st_contains(const ChipTableView& t, const int64_t* row, const double* x, const double* y, int64_t n,
+                              int8_t* out, hipStream_t s);
+
+}  // namespace mgpu

@@ -1,0 +1,173 @@
+// `st_contains(chip.wkb, point)` on the device-resident chip table.
+//
+// Replaces (per candidate row): ST_Contains.scala:34-42 ->
+// MosaicGeometryIOCodeGenJTS.fromWKB (codegen/format/MosaicGeometryIOCodeGenJTS.scala:23-29)
+// -> MosaicGeometryJTS.contains (core/geometry/MosaicGeometryJTS.scala:197) ->
+// JTS 1.20 Geometry.contains(Point).  The WKB is parsed ONCE at upload instead of
+// per candidate; the decision procedure is JTS's:
+//   empty -> false; chip envelope must contain p (inclusive);
+//   Polygon.isRectangle -> strictly inside the rectangle;
+//   else PointLocator: Polygon = shell, then holes (a ring whose envelope misses p
+//   is EXTERIOR); Multi/Collection = Mod-2 rule over the polygons.
+//   Ring test = RayCrossingCounter.locatePointInRing (p1 = ring[i], p2 = ring[i-1])
+//   with CGAlgorithmsDD.orientationIndex (1e-15 filter, DoubleDouble fallback).
+// Built with -ffp-contract=off: every product is rounded separately as on the JVM.
+#pragma once
+#include "chip_table.h"
+
+namespace mgpu {
+namespace pip {
+
+enum { kExterior = 0, kBoundary = 1, kInterior = 2 };
+
+struct DD {
+  double hi, lo;
+};
+
+MGPU_HDI DD dd_add(DD a, double yhi, double ylo) {
+  double S = a.hi + yhi;
+  double T = a.lo + ylo;
+  double e = S - a.hi;
+  double f = T - a.lo;
+  double s = S - e;
+  double t = T - f;
+  s = (yhi - e) + (a.hi - s);
+  t = (ylo - f) + (a.lo - t);
+  e = s + T;
+  double H = S + e;
+  double h = e + (S - H);
+  e = t + h;
+  DD z;
+  z.hi = H + e;
+  z.lo = e + (H - z.hi);
+  return z;
+}
+
+MGPU_HDI DD dd_mul(DD a, double yhi, double ylo) {
+  const double SPLIT = 134217729.0;
+  double C = SPLIT * a.hi;
+  double hx = C - a.hi;
+  double c = SPLIT * yhi;
+  hx = C - hx;
+  double tx = a.hi - hx;
+  double hy = c - yhi;
+  C = a.hi * yhi;
+  hy = c - hy;
+  double ty = yhi - hy;
+  c = ((((hx * hy - C) + hx * ty) + tx * hy) + tx * ty) + (a.hi * ylo + a.lo * yhi);
+  DD z;
+  z.hi = C + c;
+  hx = C - z.hi;
+  z.lo = c + hx;
+  return z;
+}
+
+MGPU_HDI int sgn(double x) { return x > 0 ? 1 : (x < 0 ? -1 : 0); }
+
+// CGAlgorithmsDD.orientationIndex(p1, p2, q)
+MGPU_HDI int orientation(double p1x, double p1y, double p2x, double p2y, double qx, double qy) {
+  double detleft = (p1x - qx) * (p2y - qy);
+  double detright = (p1y - qy) * (p2x - qx);
+  double det = detleft - detright;
+  double detsum;
+  if (detleft > 0.0) {
+    if (detright <= 0.0) return sgn(det);
+    detsum = detleft + detright;
+  } else if (detleft < 0.0) {
+    if (detright >= 0.0) return sgn(det);
+    detsum = -detleft - detright;
+  } else {
+    return sgn(det);
+  }
+  double errbound = 1e-15 * detsum;
+  if ((det >= errbound) || (-det >= errbound)) return sgn(det);
+  DD dx1 = dd_add(DD{p2x, 0.0}, -p1x, 0.0);
+  DD dy1 = dd_add(DD{p2y, 0.0}, -p1y, 0.0);
+  DD dx2 = dd_add(DD{qx, 0.0}, -p2x, 0.0);
+  DD dy2 = dd_add(DD{qy, 0.0}, -p2y, 0.0);
+  DD a = dd_mul(dx1, dy2.hi, dy2.lo);
+  DD b = dd_mul(dy1, dx2.hi, dx2.lo);
+  DD d = dd_add(a, -b.hi, -b.lo);
+  if (d.hi > 0) return 1;
+  if (d.hi < 0) return -1;
+  if (d.lo > 0) return 1;
+  if (d.lo < 0) return -1;
+  return 0;
+}
+
+// RayCrossingCounter.locatePointInRing over vertices [vb, ve)
+MGPU_HDI int ring_locate(const double* __restrict__ vtx, uint32_t vb, uint32_t ve, double px, double py) {
+  if (ve <= vb) return kExterior;
+  double prevx = vtx[2 * vb], prevy = vtx[2 * vb + 1];
+  int crossings = 0;
+  for (uint32_t i = vb + 1; i < ve; i++) {
+    double p1x = vtx[2 * i], p1y = vtx[2 * i + 1];
+    double p2x = prevx, p2y = prevy;
+    prevx = p1x;
+    prevy = p1y;
+    if (p1x < px && p2x < px) continue;
+    if (px == p2x && py == p2y) return kBoundary;
+    if (p1y == py && p2y == py) {
+      double mn = p1x, mx = p2x;
+      if (mn > mx) { mn = p2x; mx = p1x; }
+      if (px >= mn && px <= mx) return kBoundary;
+      continue;
+    }
+    if (((p1y > py) && (p2y <= py)) || ((p2y > py) && (p1y <= py))) {
+      int o = orientation(p1x, p1y, p2x, p2y, px, py);
+      if (o == 0) return kBoundary;
+      if (p2y < p1y) o = -o;
+      if (o == 1) crossings++;
+    }
+  }
+  return (crossings & 1) ? kInterior : kExterior;
+}
+
+MGPU_HDI bool env_has(const double* env, double px, double py) {
+  return px >= env[0] && px <= env[2] && py >= env[1] && py <= env[3];
+}
+
+// PointLocator.locateInPolygon for part `p`
+MGPU_HDI int polygon_locate(const ChipTableView& t, uint32_t p, double px, double py) {
+  uint32_t rb = t.part_ring[p], re = t.part_ring[p + 1];
+  if (re == rb) return kExterior;
+  for (uint32_t r = rb; r < re; r++) {
+    uint32_t vb = t.ring_vtx[r], ve = t.ring_vtx[r + 1];
+    if (r == rb && ve == vb) return kExterior;  // empty shell = empty polygon
+    int loc = env_has(t.ring_env + 4 * r, px, py) ? ring_locate(t.vtx, vb, ve, px, py) : kExterior;
+    if (r == rb) {
+      if (loc != kInterior) return loc;  // EXTERIOR or BOUNDARY
+    } else {
+      if (loc == kInterior) return kExterior;
+      if (loc == kBoundary) return kBoundary;
+    }
+  }
+  return kInterior;
+}
+
+// Geometry.contains(point) == (location == INTERIOR), for sorted chip `c`
+MGPU_HDI int chip_locate(const ChipTableView& t, uint32_t c, double px, double py) {
+  const uint8_t fl = t.chip_flags[c];
+  if (fl & (kChipEmpty | kChipNoGeom)) return kExterior;
+  const double* env = t.chip_env + 4 * c;
+  if (!env_has(env, px, py)) return kExterior;
+  if (fl & kChipRect) {
+    if (px == env[0] || px == env[2] || py == env[1] || py == env[3]) return kBoundary;
+    return kInterior;
+  }
+  uint32_t pb = t.chip_part[c], pe = t.chip_part[c + 1];
+  if (!(fl & kChipMulti)) return polygon_locate(t, pb, px, py);
+  bool is_in = false;
+  int n_bnd = 0;
+  for (uint32_t p = pb; p < pe; p++) {
+    int loc = polygon_locate(t, p, px, py);
+    if (loc == kInterior) is_in = true;
+    if (loc == kBoundary) n_bnd++;
+  }
+  if (n_bnd & 1) return kBoundary;
+  if (n_bnd > 0 || is_in) return kInterior;
+  return kExterior;
+}
+
+}  // namespace pip
+}  // namespace mgpu

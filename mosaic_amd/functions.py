@@ -1,0 +1,113 @@
+"""The hot-path function surface, as the reference registers it.
+
+  grid_longlatascellid(lon, lat, res)   MosaicContext.scala:429-432 -> PointIndexLonLat.scala:44-51
+  grid_pointascellid(point, res)        MosaicContext.scala:453-457 -> PointIndexGeom.scala:33-47
+  grid_tessellateexplode(geom, res)     MosaicContext.scala:400-408 -> MosaicExplode.scala:70-79
+  st_contains(chip.wkb, point)          MosaicContext.scala:166     -> ST_Contains.scala:21-44
+  pip_join(points, chips, res)          the user-level join of the Quickstart notebooks
+                                        (QuickstartNotebook.ipynb:1835): cell == index_id
+                                        AND (is_core OR st_contains(wkb, point))
+
+Column arguments are float64 device tensors (structure of arrays); results stay in HBM.
+"""
+import numpy as np
+
+from . import _native as N
+from .chips import ChipTable, DeviceChips, tessellate
+from .index_system import H3IndexSystem, _check_points
+
+_H3 = H3IndexSystem()
+
+
+def grid_longlatascellid(lon, lat, resolution, index_system=None, ctx=None, stream=None, stats=False):
+    """Cell id of every (lon, lat) -- (eastings, northings) for BNG."""
+    return (index_system or _H3).points_to_index(lon, lat, resolution, ctx=ctx, stream=stream, stats=stats)
+
+
+def grid_pointascellid(points_xy, resolution, index_system=None, **kw):
+    """grid_pointascellid on POINT geometries given as an (n, 2) float64 tensor or an (x, y) pair.
+    For a point, getCentroid is the point itself (MosaicGeometryJTS.scala:60-64)."""
+    if isinstance(points_xy, (tuple, list)):
+        x, y = points_xy
+    else:
+        x, y = points_xy[:, 0].contiguous(), points_xy[:, 1].contiguous()
+    return grid_longlatascellid(x, y, resolution, index_system=index_system, **kw)
+
+
+def grid_tessellateexplode(polygons, resolution, keep_core_geometries=True, index_system=None):
+    """Chip rows (is_core, index_id, wkb) of every polygon -> ChipTable (host columns)."""
+    return tessellate(polygons, index_system or _H3, resolution, keep_core_geometries)
+
+
+def st_contains(chips, chip_rows, x, y, stream=None):
+    """st_contains(chip.wkb, point) for explicit pairs: int8 tensor of 1 / 0, -1 where the
+    chip geometry is NULL (SQL null)."""
+    import torch
+    if isinstance(chips, ChipTable):
+        chips = chips.upload()
+    _check_points(x, y)
+    rows = chip_rows.to(device=x.device, dtype=torch.int64).contiguous()
+    if rows.numel() != x.numel():
+        raise N.IllegalArgumentException(N.MGPU_E_INVALID_ARG, "chip_rows and points differ in length")
+    out = torch.empty(x.numel(), dtype=torch.int8, device=x.device)
+    s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+    N.check(N.lib().mgpu_st_contains(chips.ctx.handle, chips.handle, rows.data_ptr(), x.data_ptr(), y.data_ptr(),
+                                     x.numel(), out.data_ptr(), s))
+    return out
+
+
+class JoinResult:
+    def __init__(self, point_id, polygon_id, stats):
+        self.point_id = point_id
+        self.polygon_id = polygon_id
+        self.stats = stats
+
+    def __len__(self):
+        return self.point_id.numel()
+
+    def numpy(self):
+        return self.point_id.cpu().numpy(), self.polygon_id.cpu().numpy()
+
+
+def pip_join(x, y, chips, resolution, index_system=None, point_id=None, point_id_base=0, capacity=None,
+             out=None, stream=None):
+    """The grid-indexed point-in-polygon join (fused, one kernel).
+
+    Returns a JoinResult with int64 point ids and int32 polygon ids ordered by input
+    position then polygon id.  ``capacity`` bounds the output (default: n + 1/8 n
+    headroom, grown and re-run once if exceeded)."""
+    import torch
+    isys = index_system or _H3
+    res = isys.get_resolution(resolution)
+    if isinstance(chips, ChipTable):
+        chips = chips.upload()
+    _check_points(x, y)
+    n = x.numel()
+    pid_ptr = None
+    if point_id is not None:
+        if point_id.dtype != torch.int64 or point_id.numel() != n or point_id.device != x.device:
+            raise N.IllegalArgumentException(N.MGPU_E_INVALID_ARG, "point_id must be int64 on the points' device")
+        pid_ptr = point_id.contiguous().data_ptr()
+    s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+    cap = int(capacity if capacity is not None else max(16, n + n // 8))
+    for attempt in range(2):
+        if out is not None and attempt == 0:
+            op, oq = out
+            cap = min(op.numel(), oq.numel())
+        else:
+            op = torch.empty(cap, dtype=torch.int64, device=x.device)
+            oq = torch.empty(cap, dtype=torch.int32, device=x.device)
+        import ctypes
+        cnt = ctypes.c_int64()
+        st = N.MgpuStats()
+        status = N.lib().mgpu_pip_join(chips.ctx.handle, chips.handle, isys.code, res, x.data_ptr(), y.data_ptr(),
+                                       pid_ptr, int(point_id_base), n, cap, ctypes.byref(cnt), op.data_ptr(),
+                                       oq.data_ptr(), s, st)
+        if status == N.MGPU_E_CAPACITY and capacity is None and attempt == 0:
+            cap = int(cnt.value)
+            out = None
+            continue
+        N.check(status, required=cnt.value)
+        m = int(cnt.value)
+        return JoinResult(op[:m], oq[:m], st.as_dict())
+    raise AssertionError("unreachable")

@@ -461,22 +461,25 @@ def emit(path, home, bc_of, rot):
     L = []
     L.append("/* Generated by tools/gen_h3_tables.py -- H3 v3.7 icosahedron and base-cell tables")
     L.append("   (data restated for com.uber:h3:3.7.0, see the generator's docstring). */")
+    L.append("#ifndef H3T_QUAL")
+    L.append("#define H3T_QUAL static const")
+    L.append("#endif")
     L.append("#define H3T_NUM_FACES 20")
     L.append("#define H3T_NUM_BASE_CELLS 122")
-    L.append("static const double H3T_FACE_CENTER_GEO[20][2] = {")
+    L.append("H3T_QUAL double H3T_FACE_CENTER_GEO[20][2] = {")
     for lat, lon in FACE_CENTER_GEO:
         L.append("    {%s, %s}," % (repr(lat), repr(lon)))
     L.append("};")
-    L.append("static const double H3T_FACE_CENTER_POINT[20][3] = {")
+    L.append("H3T_QUAL double H3T_FACE_CENTER_POINT[20][3] = {")
     for p in FACE_CENTER_POINT:
         L.append("    {%s, %s, %s}," % tuple(repr(x) for x in p))
     L.append("};")
-    L.append("static const double H3T_FACE_AXES_AZ_CII[20][3] = {")
+    L.append("H3T_QUAL double H3T_FACE_AXES_AZ_CII[20][3] = {")
     for p in FACE_AXES_AZ_CII:
         L.append("    {%s, %s, %s}," % tuple(repr(x) for x in p))
     L.append("};")
     L.append("/* faceIjkBaseCells[face][i][j][k] = base cell | (ccwRot60 << 8) */")
-    L.append("static const unsigned short H3T_FACE_IJK_BASE_CELLS[20][3][3][3] = {")
+    L.append("H3T_QUAL unsigned short H3T_FACE_IJK_BASE_CELLS[20][3][3][3] = {")
     for f in range(20):
         rows = []
         for i in range(3):
@@ -488,7 +491,7 @@ def emit(path, home, bc_of, rot):
         L.append("    {" + ", ".join(rows) + "},")
     L.append("};")
     L.append("/* baseCellData: home face, home i, j, k, isPentagon, cwOffsetPent[2] */")
-    L.append("static const signed char H3T_BASE_CELL_DATA[122][7] = {")
+    L.append("H3T_QUAL signed char H3T_BASE_CELL_DATA[122][7] = {")
     for b in range(122):
         f, (i, j, k) = home[b]
         cw = PENT_CW_OFFSET.get(b, (0, 0))
