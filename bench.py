@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X grid-indexed point-in-polygon join (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], "C2"): 100M synthetic points per GPU, uniform in
+the NYC taxi-zone bounding box, joined against the 263 NYC taxi zones
+(python/test/data/NYC_Taxi_Zones.geojson, committed as tests/golden/nyc_taxi_zones.npz)
+tessellated at H3 resolution 9.  One step = one fused pass (cell id -> chip probe ->
+is_core OR st_contains -> ordered pair output) over the GPU's resident points.
+
+Multi-GPU (torchrun, one process per GPU): points are sharded by contiguous id range
+(weak scaling: the per-GPU point count is fixed), the chip table is built on rank 0
+and replicated with one RCCL broadcast, per-rank pair counts are all-gathered (RCCL)
+for the global output offsets.  Time = max over ranks of the barrier-bracketed K steps.
+
+Also reported: the fused kernel's achieved bandwidth against the HBM roofline
+(algorithmic bytes: 16 B per point read + 12 B per output pair written; kernel time
+from HIP events on the launch stream) and a CPU baseline (the oracle's multithreaded
+restatement of the reference path on a bounded sample, rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+NYC_BBOX = (-74.25559136315209, 40.496115395170364, -73.7000090639354, 40.91553277700258)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "PIP-join points/sec (H3 res 9) at 1/2/4/8 GPUs + achieved HBM GB/s"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--points", type=int, default=100_000_000, help="points per GPU")
+    ap.add_argument("--res", type=int, default=9)
+    ap.add_argument("--seed", type=int, default=0x20250314)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    return ap.parse_args()
+
+
+def gen_points(n, begin, seed, dev):
+    """Uniform points in the NYC bbox; the shard starting at global index `begin` is
+    generated from its own seeded stream so any world size sees the same workload shape."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed * 1000003 + begin)
+    x = torch.rand(n, dtype=torch.float64, device=dev, generator=g)
+    y = torch.rand(n, dtype=torch.float64, device=dev, generator=g)
+    x.mul_(NYC_BBOX[2] - NYC_BBOX[0]).add_(NYC_BBOX[0])
+    y.mul_(NYC_BBOX[3] - NYC_BBOX[1]).add_(NYC_BBOX[1])
+    return x, y
+
+
+def cpu_baseline(chips, res, seed, target_s):
+    """Oracle (CPU restatement of the reference path) on a bounded sample: points/s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, 64))
+    rng = np.random.default_rng(seed)
+
+    def run(n):
+        x = rng.uniform(NYC_BBOX[0], NYC_BBOX[2], n)
+        y = rng.uniform(NYC_BBOX[1], NYC_BBOX[3], n)
+        t = time.perf_counter()
+        O.pip_join(0, res, x, y, chips.cell, chips.polygon_id, chips.is_core, chips.wkb_offsets, chips.wkb,
+                   threads=threads)
+        return time.perf_counter() - t
+
+    n0 = 200_000
+    dt = run(n0)
+    n = int(min(60_000_000, max(n0, n0 * target_s / max(dt, 1e-6))))
+    dt = run(n)
+    return {"value": n / dt, "unit": "points/s", "cores": threads, "kind": "port",
+            "sample": "%d uniform NYC-bbox points x 263 zones, H3 res %d, oracle pip_join (C restatement of "
+                      "H3 geoToH3 + hash join + JTS PointLocator, per-candidate WKB re-parse), %d threads, %.1f s"
+                      % (n, res, threads, dt)}
+
+
+def main():
+    a = parse()
+    import mosaic_amd as M
+    from mosaic_amd import dist as D
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world > 1:
+        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (a.gpus, world))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    ctx = M.default_context(dev)
+    isys = M.H3IndexSystem()
+
+    zones = M.Polygons.from_npz(os.path.join(ROOT, "tests", "golden", "nyc_taxi_zones.npz"))
+    table = None
+    if rank == 0:
+        table = M.tessellate(zones, isys, a.res)
+        chips = table.upload(ctx)
+    else:
+        chips = None
+    if world > 1:
+        chips = D.broadcast_chips(chips, ctx)
+    info = chips.info()
+
+    n = a.points
+    begin = rank * n
+    x, y = gen_points(n, begin, a.seed, dev)
+    cap = n // 2 + 1024  # ~36% of uniform bbox points fall in a zone
+    out_p = torch.empty(cap, dtype=torch.int64, device=dev)
+    out_q = torch.empty(cap, dtype=torch.int32, device=dev)
+    ctx.reserve(n)
+
+    def step():
+        return M.pip_join(x, y, chips, a.res, point_id_base=begin, out=(out_p, out_q), capacity=cap)
+
+    for _ in range(a.warmup):
+        r = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    kms = []
+    pairs = 0
+    ties = 0
+    for _ in range(a.steps):
+        r = step()
+        kms.append(r.stats["kernel_ms"])
+        pairs = len(r)
+        ties = r.stats["n_near_ties"]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        off, total_pairs, _ = D.global_offsets(pairs, dev)
+    else:
+        total_pairs = pairs
+
+    ms_step = elapsed / a.steps * 1e3
+    kernel_ms = float(np.mean(kms))
+    alg_bytes = 16.0 * n + 12.0 * pairs
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    out = {
+        "metric": METRIC,
+        "value": world * n / (elapsed / a.steps),
+        "unit": "points/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (uniform points in the NYC zone bbox; real NYC taxi-zone polygons from the reference)",
+        "config": {"workload": "C2: %d points/GPU uniform in NYC bbox x 263 NYC taxi zones, H3 res %d"
+                               % (n, a.res),
+                   "points_per_gpu": n, "polygons": len(zones), "chips": info["chips"], "chip_cells": info["cells"],
+                   "index_system": "H3", "resolution": a.res,
+                   "parallelism": "points sharded x%d, chip table replicated (RCCL broadcast)" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "pip_join_kernel<H3>", "kernel_ms": kernel_ms,
+                     "alg_bytes_per_launch": alg_bytes},
+        "pairs_per_gpu": pairs,
+        "pairs_total": total_pairs,
+        "near_ties": ties,
+        "candidates_per_point": float(r.stats["n_candidates"]) / n,
+    }
+    if os.environ.get("MGPU_ABLATE"):
+        out["ablate"] = os.environ["MGPU_ABLATE"]
+    prof = os.path.join(ROOT, "profiles", "pmc_join_traffic.json")
+    if os.path.exists(prof):
+        try:
+            p = json.load(open(prof))
+            if p.get("points") == n and p.get("res") == a.res:
+                out["roofline"]["traffic"] = p["hbm_bytes_per_launch"]
+        except (ValueError, KeyError):
+            pass
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        if table is None:
+            table = M.tessellate(zones, isys, a.res)
+        out["cpu_baseline"] = cpu_baseline(table, a.res, a.seed, a.cpu_seconds)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

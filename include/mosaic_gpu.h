@@ -66,7 +66,7 @@ int32_t mgpu_ctx_create(int32_t device_id, mgpu_ctx** out);
 int32_t mgpu_ctx_destroy(mgpu_ctx* ctx);
 
 /* IndexSystem.getResolution for an integer resolution (H3IndexSystem.scala:45-60,
- * BNGIndexSystem.scala:349-360).  Returns the resolution or MGPU_E_RESOLUTION. */
+ * BNGIndexSystem.scala:349-360).  Returns MGPU_OK or MGPU_E_RESOLUTION. */
 int32_t mgpu_check_resolution(int32_t index_system, int32_t res);
 
 /* IndexSystem.pointToIndex(x, y, res) over a batch (IndexSystem.scala:237;
@@ -93,10 +93,11 @@ int32_t mgpu_bng_parse(const char* ids, const int64_t* offsets, int64_t n, int64
  * ChipType.scala:17-29): cell id, owning polygon id, is_core, and the chip WKB
  * (big- or little-endian, Polygon / MultiPolygon / GeometryCollection of those;
  * a NULL geometry is wkb_offsets[i] == wkb_offsets[i+1]).  Host pointers.  The WKB
- * is parsed once here (the reference re-parses it per candidate row). */
-int32_t mgpu_chips_upload(mgpu_ctx* ctx, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
-                          const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb,
-                          mgpu_chips** out);
+ * is parsed once here (the reference re-parses it per candidate row).  For H3 the
+ * cell hash is keyed by lattice position (see mosaic_amd/csrc/chip_table.h). */
+int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, const int64_t* cell,
+                          const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
+                          const uint8_t* wkb, mgpu_chips** out);
 int32_t mgpu_chips_destroy(mgpu_chips* chips);
 /* The chip table is one device allocation: expose it for replication (RCCL
  * broadcast of `bytes` at `device_ptr`), and rebuild a handle on another GPU from

@@ -88,7 +88,7 @@ def lib():
         "mgpu_points_to_cells_host": (I32, [P, I32, I32, P, P, I64, P]),
         "mgpu_bng_format": (I32, [P, I64, P, I64, P]),
         "mgpu_bng_parse": (I32, [P, P, I64, P]),
-        "mgpu_chips_upload": (I32, [P, I64, P, P, P, P, P, ctypes.POINTER(P)]),
+        "mgpu_chips_upload": (I32, [P, I32, I64, P, P, P, P, P, ctypes.POINTER(P)]),
         "mgpu_chips_destroy": (I32, [P]),
         "mgpu_chips_device_blob": (I32, [P, ctypes.POINTER(P), ctypes.POINTER(I64)]),
         "mgpu_chips_from_device_blob": (I32, [P, P, I64, ctypes.POINTER(P)]),

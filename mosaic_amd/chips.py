@@ -16,13 +16,14 @@ from . import _native as N
 class ChipTable:
     """Host columns of chip rows (one row per (polygon, cell) chip)."""
 
-    def __init__(self, cell, polygon_id, is_core, wkb_offsets, wkb):
+    def __init__(self, cell, polygon_id, is_core, wkb_offsets, wkb, index_system=N.MGPU_H3):
         self.cell = np.ascontiguousarray(cell, dtype=np.int64)
         self.polygon_id = np.ascontiguousarray(polygon_id, dtype=np.int32)
         self.is_core = np.ascontiguousarray(is_core, dtype=np.uint8)
         self.wkb_offsets = np.ascontiguousarray(wkb_offsets, dtype=np.int64)
         self.wkb = np.ascontiguousarray(np.frombuffer(wkb, dtype=np.uint8) if isinstance(wkb, (bytes, bytearray))
                                         else wkb, dtype=np.uint8)
+        self.index_system = int(index_system)
         n = self.cell.shape[0]
         assert self.polygon_id.shape[0] == n and self.is_core.shape[0] == n and self.wkb_offsets.shape[0] == n + 1
 
@@ -36,14 +37,14 @@ class ChipTable:
                 int(self.polygon_id[i]))
 
     @classmethod
-    def from_rows(cls, rows):
+    def from_rows(cls, rows, index_system=N.MGPU_H3):
         """rows: iterable of (is_core, index_id, wkb|None, polygon_id)."""
         rows = list(rows)
         blobs = [r[2] or b"" for r in rows]
         off = np.zeros(len(rows) + 1, dtype=np.int64)
         off[1:] = np.cumsum([len(b) for b in blobs])
         return cls([r[1] for r in rows], [r[3] for r in rows], [1 if r[0] else 0 for r in rows], off,
-                   np.frombuffer(b"".join(blobs) or b"", dtype=np.uint8))
+                   np.frombuffer(b"".join(blobs) or b"", dtype=np.uint8), index_system)
 
     def upload(self, ctx=None):
         from .context import default_context
@@ -63,7 +64,7 @@ class DeviceChips:
         if handle is None:
             h = ctypes.c_void_p()
             wkb = table.wkb if table.wkb.size else np.zeros(1, np.uint8)
-            N.check(N.lib().mgpu_chips_upload(ctx.handle, len(table), table.cell.ctypes.data,
+            N.check(N.lib().mgpu_chips_upload(ctx.handle, table.index_system, len(table), table.cell.ctypes.data,
                                               table.polygon_id.ctypes.data, table.is_core.ctypes.data,
                                               table.wkb_offsets.ctypes.data, wkb.ctypes.data, ctypes.byref(h)))
             handle = h
@@ -172,4 +173,4 @@ def tessellate(polygons, index_system, resolution, keep_core_geometries=True):
                                         wkb.ctypes.data))
     finally:
         L.mgpu_tess_destroy(h)
-    return ChipTable(cell, pid, core, off, wkb[:b.value])
+    return ChipTable(cell, pid, core, off, wkb[:b.value], index_system.code)

@@ -11,12 +11,14 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <limits>
 #include <string>
 #include <vector>
 
 #include "../../include/mosaic_gpu.h"
 #include "chip_table.h"
+#include "h3_core.h"
 #include "kernels.h"
 #include "wkb.h"
 
@@ -52,6 +54,10 @@ struct BlobHeader {
   uint32_t version, hash_mask, max_probe, n_chips, n_cells, pad;
   int64_t n_vertices;
   uint64_t off[kBlobArrays];
+  int32_t probe_mode, res;
+  uint32_t face_mask, pad2;
+  double bbox[4];
+  double k_res;
 };
 constexpr size_t kBlobHeaderBytes = 256;
 static_assert(sizeof(BlobHeader) <= kBlobHeaderBytes, "header too large");
@@ -73,8 +79,140 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.ring_env = (const double*)(base + h.off[8]);
   v.vtx = (const double*)(base + h.off[9]);
   v.row_to_chip = (const uint32_t*)(base + h.off[10]);
+  v.probe_mode = h.probe_mode;
+  v.res = h.res;
+  v.face_mask = h.face_mask;
+  for (int k = 0; k < 4; k++) v.bbox[k] = h.bbox[k];
+  v.k_res = h.k_res;
   return v;
 }
+
+constexpr double kPi = 3.14159265358979323846;
+
+double angle_between(const double* a, const double* b) {
+  double d = a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+  d = d > 1 ? 1 : (d < -1 ? -1 : d);
+  return acos(d);
+}
+
+// H3 lattice probing (chip_table.h).  For every distinct chip cell: its centre (home
+// face lattice -> sphere), every face a point of the cell can be nearest to (angle
+// within 3 rho of the nearest, rho = circumradius bound), and on each such face the
+// lattice positions within hex distance 3 of the centre's projection whose
+// face_ijk_to_h3 IS the cell.  Points outside the chip cells' bounding box match
+// nothing; inside it, only faces that can be nearest somewhere in the box are
+// tested (65 x 65 sampling with a 2-Lipschitz margin).  Returns false (caller keeps
+// cell-id probing) for mixed resolutions, res < 5, or pentagon base cells.
+bool build_lattice(const std::vector<mgpu::HashSlot>& cells, std::vector<std::pair<uint64_t, uint32_t>>& keys,
+                   int* res_out, uint32_t* face_mask, double bbox[4]) {
+  namespace H = mgpu::h3;
+  if (cells.empty()) return false;
+  int res = (int)((cells[0].cell >> 52) & 15);
+  if (res < 5) return false;
+  const double rho = 0.3 / pow(H::kSqrt7, res);
+  double k_res = H::k_of_res(res);
+  double lat_lo = 1e9, lat_hi = -1e9, lon_lo = 1e9, lon_hi = -1e9;
+  for (size_t ci = 0; ci < cells.size(); ci++) {
+    uint64_t h = cells[ci].cell;
+    if (((h >> 59) & 15) != 1 || (int)((h >> 52) & 15) != res || (h >> 63)) return false;
+    int face, r;
+    H::IJK ijk;
+    if (!H::h3_home_face_ijk(h, &face, &ijk, &r)) return false;
+    double hx, hy, lat, lon;
+    H::ijk_to_hex2d(ijk, &hx, &hy);
+    H::hex2d_to_geo(hx, hy, face, res, &lat, &lon);
+    double v[3] = {cos(lat) * cos(lon), cos(lat) * sin(lon), sin(lat)};
+    double amin = 1e9, ang[20];
+    for (int f = 0; f < 20; f++) {
+      ang[f] = angle_between(v, H3T_FACE_CENTER_POINT[f]);
+      amin = std::min(amin, ang[f]);
+    }
+    bool found_home = false;
+    for (int f = 0; f < 20; f++) {
+      if (ang[f] > amin + 3 * rho) continue;
+      const double(*F)[3] = H3T_FACE_FRAME[f][res & 1];
+      double dc = v[0] * F[2][0] + v[1] * F[2][1] + v[2] * F[2][2];
+      if (dc <= 0.5) continue;
+      double x = k_res * (v[0] * F[0][0] + v[1] * F[0][1] + v[2] * F[0][2]) / dc;
+      double y = k_res * (v[0] * F[1][0] + v[1] * F[1][1] + v[2] * F[1][2]) / dc;
+      double mg;
+      H::IJK c0 = H::hex2d_to_ijk(x, y, &mg);
+      int i0 = c0.i - c0.k, j0 = c0.j - c0.k;
+      for (int di = -3; di <= 3; di++)
+        for (int dj = -3; dj <= 3; dj++) {
+          if (std::abs(di) + std::abs(dj) + std::abs(di - dj) > 6) continue;  // hex distance <= 3
+          H::IJK n{i0 + di, j0 + dj, 0};
+          H::ijk_normalize(n);
+          if (H::face_ijk_to_h3(f, n, res) == h) {
+            keys.push_back({H::lattice_key(f, n), (uint32_t)ci});
+            if (f == face) found_home = true;
+          }
+        }
+    }
+    (void)found_home;
+    double latd = lat * 180 / kPi, lond = lon * 180 / kPi;
+    lat_lo = std::min(lat_lo, latd);
+    lat_hi = std::max(lat_hi, latd);
+    lon_lo = std::min(lon_lo, lond);
+    lon_hi = std::max(lon_hi, lond);
+  }
+  // bounding box of every chip cell (centre +- 2 rho), or the whole sphere
+  double m = 2 * rho * 180 / kPi;
+  double latmax = std::max(std::fabs(lat_lo), std::fabs(lat_hi)) + m;
+  if (latmax < 80.0 && lon_hi - lon_lo < 180.0) {
+    double ml = m / cos(latmax * kPi / 180);
+    bbox[0] = lon_lo - ml;
+    bbox[1] = lat_lo - m;
+    bbox[2] = lon_hi + ml;
+    bbox[3] = lat_hi + m;
+    // faces that can be nearest somewhere in the box
+    const int G = 65;
+    double s_ang = 0;
+    uint32_t mask = 0;
+    std::vector<double> pts;
+    for (int a = 0; a < G; a++)
+      for (int b = 0; b < G; b++) {
+        double lond = bbox[0] + (bbox[2] - bbox[0]) * a / (G - 1), latd = bbox[1] + (bbox[3] - bbox[1]) * b / (G - 1);
+        double la = latd * kPi / 180, lo = lond * kPi / 180;
+        pts.push_back(cos(la) * cos(lo));
+        pts.push_back(cos(la) * sin(lo));
+        pts.push_back(sin(la));
+      }
+    // sample spacing (angle) bound: the box diagonal cell
+    {
+      double la0 = bbox[1] * kPi / 180, lo0 = bbox[0] * kPi / 180;
+      double la1 = (bbox[1] + (bbox[3] - bbox[1]) / (G - 1)) * kPi / 180,
+             lo1 = (bbox[0] + (bbox[2] - bbox[0]) / (G - 1)) * kPi / 180;
+      double p0[3] = {cos(la0) * cos(lo0), cos(la0) * sin(lo0), sin(la0)};
+      double p1[3] = {cos(la1) * cos(lo1), cos(la1) * sin(lo1), sin(la1)};
+      s_ang = angle_between(p0, p1);
+      // the equator-side rows are wider: scale by the cosine ratio
+      s_ang /= std::max(0.05, cos(latmax * kPi / 180) / std::max(cos(bbox[1] * kPi / 180), cos(bbox[3] * kPi / 180)));
+    }
+    for (size_t q = 0; q < pts.size(); q += 3) {
+      double ang[20], amin = 1e9;
+      for (int f = 0; f < 20; f++) {
+        ang[f] = angle_between(&pts[q], H3T_FACE_CENTER_POINT[f]);
+        amin = std::min(amin, ang[f]);
+      }
+      for (int f = 0; f < 20; f++)
+        if (ang[f] <= amin + 2 * s_ang + 1e-12) mask |= 1u << f;
+    }
+    *face_mask = mask;
+  } else {
+    bbox[0] = -1e300;
+    bbox[1] = -1e300;
+    bbox[2] = 1e300;
+    bbox[3] = 1e300;
+    *face_mask = (1u << 20) - 1;
+  }
+  *res_out = res;
+  return true;
+}
+
+}  // namespace
+
+namespace {
 
 }  // namespace
 
@@ -113,11 +251,11 @@ int32_t ensure_ws(mgpu_ctx* ctx, int64_t n_tiles) {
 int32_t check_res(int32_t is, int32_t res) {
   if (is == MGPU_H3) {
     if (res < 0 || res > 15) return fail(MGPU_E_RESOLUTION, "H3 resolution has to be between 0 and 15; found %d", res);
-    return res;
+    return MGPU_OK;
   }
   if (is == MGPU_BNG) {
     if (res == 0 || res < -6 || res > 6) return fail(MGPU_E_RESOLUTION, "BNG resolution not supported; found %d", res);
-    return res;
+    return MGPU_OK;
   }
   return fail(MGPU_E_INVALID_ARG, "unknown index system %d (0 = H3, 1 = BNG)", is);
 }
@@ -174,8 +312,7 @@ int32_t mgpu_ctx_reserve(mgpu_ctx* ctx, int64_t max_points) {
 int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t is, int32_t res, const double* x, const double* y, int64_t n,
                              int64_t* out_cell, void* stream, mgpu_stats* stats) {
   if (!ctx) return fail(MGPU_E_INVALID_ARG, "ctx is NULL");
-  int32_t r = check_res(is, res);
-  if (r < 0) return r;
+  if (int32_t r = check_res(is, res)) return r;
   if (n < 0 || (n > 0 && (!x || !y || !out_cell))) return fail(MGPU_E_INVALID_ARG, "bad point arrays");
   if (int32_t st = set_device(ctx->device)) return st;
   hipStream_t s = (hipStream_t)stream;
@@ -185,12 +322,10 @@ int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t is, int32_t res, const doubl
   HIP_TRY(mgpu::launch_cells(is, res, x, y, n, out_cell, counters, s));
   HIP_TRY(hipEventRecord(ctx->ev1, s));
   unsigned long long h[8] = {0};
-  bool need_sync = stats != nullptr;
-  if (need_sync || true) {
-    // invalid-coordinate detection must reach the caller (IllegalArgument/IllegalState)
-    HIP_TRY(hipMemcpyAsync(h, counters, sizeof h, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-  }
+  // invalid coordinates must reach the caller as IllegalArgument / IllegalState,
+  // so the status is read back (the cell column itself stays on the device)
+  HIP_TRY(hipMemcpyAsync(h, counters, sizeof h, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
   if (stats) {
     stats->n_points = n;
     stats->n_pairs = 0;
@@ -210,7 +345,7 @@ int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t is, int32_t res, const doubl
 int32_t mgpu_points_to_cells_host(mgpu_ctx* ctx, int32_t is, int32_t res, const double* x, const double* y, int64_t n,
                                   int64_t* out_cell) {
   if (!ctx) return fail(MGPU_E_INVALID_ARG, "ctx is NULL");
-  if (n == 0) return check_res(is, res) < 0 ? MGPU_E_RESOLUTION : MGPU_OK;
+  if (n == 0) return check_res(is, res);
   if (int32_t st = set_device(ctx->device)) return st;
   double *dx = nullptr, *dy = nullptr;
   int64_t* dc = nullptr;
@@ -229,9 +364,12 @@ int32_t mgpu_points_to_cells_host(mgpu_ctx* ctx, int32_t is, int32_t res, const 
 
 // ------------------------------------------------------------------ chips
 
-int32_t mgpu_chips_upload(mgpu_ctx* ctx, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
-                          const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb, mgpu_chips** out) {
+int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, const int64_t* cell,
+                          const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
+                          const uint8_t* wkb, mgpu_chips** out) {
   if (!ctx || !out) return fail(MGPU_E_INVALID_ARG, "ctx/out is NULL");
+  if (index_system != MGPU_H3 && index_system != MGPU_BNG)
+    return fail(MGPU_E_INVALID_ARG, "unknown index system %d (0 = H3, 1 = BNG)", index_system);
   if (n_chips < 0 || n_chips > (int64_t)std::numeric_limits<int32_t>::max())
     return fail(MGPU_E_INVALID_ARG, "n_chips out of range");
   if (n_chips > 0 && (!cell || !polygon_id || !is_core || !wkb_offsets))
@@ -292,11 +430,32 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int64_t n_chips, const int64_t* cell, c
     distinct.push_back(mgpu::HashSlot{c, (uint32_t)s, (uint32_t)(e - s)});
     s = e;
   }
+  // H3: probe by lattice key when possible (chip_table.h)
+  int32_t probe_mode = mgpu::kProbeCellId, lres = -1;
+  uint32_t face_mask = (1u << 20) - 1;
+  double bbox[4] = {-1e300, -1e300, 1e300, 1e300};
+  std::vector<mgpu::HashSlot> entries;
+  std::vector<std::pair<uint64_t, uint32_t>> keys;
+  if (index_system == MGPU_H3 && build_lattice(distinct, keys, &lres, &face_mask, bbox)) {
+    probe_mode = mgpu::kProbeLattice;
+    std::sort(keys.begin(), keys.end());
+    for (size_t k = 0; k < keys.size(); k++) {
+      if (k && keys[k].first == keys[k - 1].first) {
+        if (keys[k].second != keys[k - 1].second) return fail(MGPU_E_INTERNAL, "lattice key collision");
+        continue;
+      }
+      const mgpu::HashSlot& d = distinct[keys[k].second];
+      entries.push_back(mgpu::HashSlot{keys[k].first, d.first, d.count});
+    }
+  } else {
+    entries = distinct;
+    if (index_system == MGPU_H3 && !distinct.empty()) lres = (int32_t)((distinct[0].cell >> 52) & 15);
+  }
   uint32_t cap = 16;
-  while (cap < 2 * distinct.size()) cap <<= 1;
+  while (cap < 2 * entries.size()) cap <<= 1;
   std::vector<mgpu::HashSlot> slots(cap, mgpu::HashSlot{0, 0, 0});
   uint32_t max_probe = 0;
-  for (const auto& d : distinct) {
+  for (const auto& d : entries) {
     uint32_t h = mgpu::cell_hash(d.cell) & (cap - 1), k = 0;
     while (slots[h].count) {
       h = (h + 1) & (cap - 1);
@@ -328,12 +487,17 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int64_t n_chips, const int64_t* cell, c
   size_t total = kBlobHeaderBytes;
   BlobHeader hdr{};
   hdr.magic = kBlobMagic;
-  hdr.version = 1;
+  hdr.version = 2;
   hdr.hash_mask = cap - 1;
   hdr.max_probe = max_probe;
   hdr.n_chips = (uint32_t)n_chips;
   hdr.n_cells = (uint32_t)distinct.size();
   hdr.n_vertices = (int64_t)geo.vtx.size() / 2;
+  hdr.probe_mode = probe_mode;
+  hdr.res = lres;
+  hdr.face_mask = face_mask;
+  for (int k = 0; k < 4; k++) hdr.bbox[k] = bbox[k];
+  hdr.k_res = lres >= 0 ? mgpu::h3::k_of_res(lres) : 0.0;
   for (size_t k = 0; k < parts.size(); k++) {
     parts[k].off = total;
     hdr.off[k] = total;
@@ -392,7 +556,7 @@ int32_t mgpu_chips_from_device_blob(mgpu_ctx* ctx, const void* device_ptr, int64
   if (bytes < (int64_t)kBlobHeaderBytes) return fail(MGPU_E_INVALID_ARG, "blob too small");
   BlobHeader hdr;
   HIP_TRY(hipMemcpy(&hdr, device_ptr, sizeof hdr, hipMemcpyDeviceToHost));
-  if (hdr.magic != kBlobMagic || hdr.version != 1) return fail(MGPU_E_INVALID_ARG, "not a chip-table blob");
+  if (hdr.magic != kBlobMagic || hdr.version != 2) return fail(MGPU_E_INVALID_ARG, "not a chip-table blob");
   for (int k = 0; k < kBlobArrays; k++)
     if (hdr.off[k] >= (uint64_t)bytes) return fail(MGPU_E_INVALID_ARG, "corrupt chip-table blob");
   mgpu_chips* ch = new mgpu_chips();
@@ -421,8 +585,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
                          const double* y, const int64_t* point_id, int64_t id_base, int64_t n, int64_t capacity,
                          int64_t* out_point, int32_t* out_poly, hipStream_t s, bool timed) {
   if (!ctx || !chips) return fail(MGPU_E_INVALID_ARG, "ctx/chips is NULL");
-  int32_t r = check_res(is, res);
-  if (r < 0) return r;
+  if (int32_t r = check_res(is, res)) return r;
   if (n < 0 || (n > 0 && (!x || !y))) return fail(MGPU_E_INVALID_ARG, "bad point arrays");
   if (capacity < 0 || (capacity > 0 && (!out_point || !out_poly))) return fail(MGPU_E_INVALID_ARG, "bad output arrays");
   if (int32_t st = set_device(ctx->device)) return st;
@@ -437,11 +600,16 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   a.n = n;
   a.n_tiles = tiles;
   a.res = res;
+  a.res_match = (is == MGPU_BNG || chips->view.res < 0 || chips->view.res == res) ? 1 : 0;
   a.chips = chips->view;
   a.capacity = capacity;
   a.out_point = out_point;
   a.out_poly = out_poly;
   a.counters = (unsigned long long*)base;
+  {
+    const char* ab = getenv("MGPU_ABLATE");  // profiling switch, never set in production runs
+    a.ablate = ab ? atoi(ab) : 0;
+  }
   a.tile_ticket = (uint32_t*)(base + kWsCounters);
   a.tile_status = (uint64_t*)(base + kWsCounters + kWsTicket);
   HIP_TRY(hipMemsetAsync(base, 0, kWsCounters + kWsTicket + align_up((size_t)std::max<int64_t>(tiles, 1) * 8, 256), s));

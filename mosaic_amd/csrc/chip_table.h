@@ -14,6 +14,11 @@
 //   geometry   : part_ring[u32 n_parts+1], ring_vtx[u32 n_rings+1],
 //                ring_env[double4], vtx[double2 x,y]
 //   row map    : row_to_chip[u32 n_chips] (input row -> sorted position)
+// For H3 tables the hash is keyed by the (face, i, j) lattice position that the
+// kernel's projection yields, not by the 64-bit cell id: the kernel then never
+// assembles H3 digits.  Every lattice position of every chip cell on every face a
+// point of that cell can project to is present (built and verified at upload with
+// face_ijk_to_h3, mosaic_amd/csrc/capi.cpp build_lattice).
 #pragma once
 #include <stdint.h>
 
@@ -49,7 +54,15 @@ struct ChipTableView {
   const double* ring_env;      // 4 per ring
   const double* vtx;           // 2 per vertex
   const uint32_t* row_to_chip; // [n_chips]
+  // H3 probing (index system H3 only)
+  int32_t probe_mode;          // 0: hash keyed by cell id; 1: keyed by (face, i, j) lattice key
+  int32_t res;                 // resolution of the chip cells (H3), -1 if mixed / unknown
+  uint32_t face_mask;          // icosahedron faces a point inside `bbox` can be nearest to
+  double bbox[4];              // lon_min, lat_min, lon_max, lat_max (deg): points outside match no chip
+  double k_res;                // sqrt7^res / RES0_U_GNOMONIC
 };
+
+enum ProbeMode { kProbeCellId = 0, kProbeLattice = 1 };
 
 #ifdef __HIPCC__
 #define MGPU_HDI __host__ __device__ __forceinline__

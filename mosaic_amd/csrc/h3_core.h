@@ -292,22 +292,199 @@ MGPU_HD uint64_t face_ijk_to_h3(int face, IJK ijk, int res) {
 // java.lang.Math.toRadians as on the reference's JDK 8 toolchain
 MGPU_HD double to_radians(double deg) { return deg / 180.0 * 3.14159265358979323846; }
 
-// H3IndexSystem.pointToIndex(lon, lat, res).  Returns 0 for non-finite input
-// (H3-Java then throws IllegalArgumentException).  *near_tie is set when the
-// result sits within the fast path's error band of a cell edge.
-MGPU_HD uint64_t point_to_cell(double lon_deg, double lat_deg, int res, bool* near_tie) {
-  double lat = to_radians(lat_deg), lon = to_radians(lon_deg);
-  *near_tie = false;
-  if (!isfinite(lat) || !isfinite(lon)) return 0;
-  int face;
-  double vx, vy, gap;
-  geo_to_hex2d(lat, lon, res, &face, &vx, &vy, &gap);
-  double margin;
-  IJK ijk = hex2d_to_ijk(vx, vy, &margin);
+// Relative error band of the H3 route's hex2d coordinates: acos(1 - sqd/2) loses
+// precision near a face centre (dr = eps / sin r), so H3's own result -- and any
+// ulp-level libm difference -- carries a relative error ~eps / sin^2(r).  Decisions
+// closer than 2^-40 * (1 + 1/sin^2 r) * |coordinate| to a threshold are near-ties.
+MGPU_HD double tie_band(double vx, double vy, double sin2r) {
   double scale = fabs(vx) > fabs(vy) ? fabs(vx) : fabs(vy);
   if (scale < 1.0) scale = 1.0;
-  *near_tie = (margin < kTieRel * scale) || (gap < 1e-12);
+  double amp = 1.0 + (sin2r > 1e-300 ? 1.0 / sin2r : 1e300);
+  return kTieRel * amp * scale;
+}
+
+// H3IndexSystem.pointToIndex(lon, lat, res) by the H3 route (the near-tie slow path
+// and the reference for the fast path).  Returns 0 for non-finite input (H3-Java
+// then throws IllegalArgumentException).
+#ifdef __HIPCC__
+// the route's libm polynomials must not be hoisted into the caller's point loop
+// (that pins ~70 extra VGPRs for a path taken by ~1e-7 of the points)
+#define MGPU_COLD static __host__ __device__ __attribute__((noinline))
+#else
+#define MGPU_COLD static inline
+#endif
+MGPU_COLD bool route_face_ijk(double lat, double lon, int res, int* face, IJK* ijk, bool* near_tie) {
+  if (!isfinite(lat) || !isfinite(lon)) return false;
+  double vx, vy, gap;
+  geo_to_hex2d(lat, lon, res, face, &vx, &vy, &gap);
+  double margin;
+  *ijk = hex2d_to_ijk(vx, vy, &margin);
+  double cx = H3T_FACE_CENTER_POINT[*face][0], cy = H3T_FACE_CENTER_POINT[*face][1],
+         cz = H3T_FACE_CENTER_POINT[*face][2];
+  double slat, clat, slon, clon;
+  sincos(lat, &slat, &clat);
+  sincos(lon, &slon, &clon);
+  double cosr = cx * clon * clat + cy * slon * clat + cz * slat;
+  *near_tie = (margin < tie_band(vx, vy, 1.0 - cosr * cosr)) || (gap < 1e-12);
+  return true;
+}
+
+MGPU_HD uint64_t point_to_cell(double lon_deg, double lat_deg, int res, bool* near_tie) {
+  double lat = to_radians(lat_deg), lon = to_radians(lon_deg);
+  int face;
+  IJK ijk;
+  *near_tie = false;
+  if (!route_face_ijk(lat, lon, res, &face, &ijk, near_tie)) return 0;
   return face_ijk_to_h3(face, ijk, res);
+}
+
+// ------------------------------------------------------------------ fast path
+//
+// The closed form of H3's projection: with v the unit vector of the point and
+// (a, b, c) the face's gnomonic frame (H3T_FACE_FRAME, generated), H3's
+//   r = acos(1 - |c - v|^2 / 2), theta = az0 - azimuth(c -> v), R = tan(r) * sqrt7^res / U
+//   x = R cos(theta), y = R sin(theta)
+// equals  x = K (v.a) / (v.c),  y = K (v.b) / (v.c)  with K = sqrt7^res / U.
+// sin / cos of lat and lon come from a k/64-rad table plus a degree-9 Taylor series
+// of the remainder (exact by Sterbenz).  The result differs from H3's by rounding
+// only; every decision within tie_band() of a threshold goes to the H3 route.
+
+MGPU_HD void sincos_tab(double a, double* s, double* c) {
+  double kf = rint(a * 64.0);
+  int k = (int)kf;
+  double d = a - kf * 0.015625;
+  double d2 = d * d;
+  double sd = d + d * d2 * (-1.0 / 6.0 + d2 * (1.0 / 120.0 + d2 * (-1.0 / 5040.0 + d2 * (1.0 / 362880.0))));
+  double cd = 1.0 + d2 * (-0.5 + d2 * (1.0 / 24.0 + d2 * (-1.0 / 720.0 + d2 * (1.0 / 40320.0 - d2 / 3628800.0))));
+  double sk = H3T_SINCOS64[k + H3T_SC64_BIAS][0], ck = H3T_SINCOS64[k + H3T_SC64_BIAS][1];
+  *s = sk * cd + ck * sd;
+  *c = ck * cd - sk * sd;
+}
+
+struct FastHex {
+  int face;
+  IJK ijk;
+  bool tie;  // a decision may differ from the H3 route: recompute with route_face_ijk
+};
+
+// k_res = sqrt7^res / RES0_U_GNOMONIC; `faces` = the faces to consider (bit mask)
+MGPU_HD FastHex fast_hex2d(double lat, double lon, int res, double k_res, uint32_t faces) {
+  FastHex o;
+  double slat, clat, slon, clon;
+  sincos_tab(lat, &slat, &clat);
+  sincos_tab(lon, &slon, &clon);
+  double vx = clon * clat, vy = slon * clat, vz = slat;
+  double best = 5.0, second = 5.0;
+  int f0 = 0;
+  for (uint32_t m = faces; m; m &= m - 1) {
+    int f = __builtin_ctz(m);
+#ifdef __HIP_DEVICE_COMPILE__
+    // keep the face table in memory: hoisting all 20 rows out of the caller's point
+    // loop would pin 120 registers
+    asm volatile("" : "+s"(f));
+#endif
+    double dx = H3T_FACE_CENTER_POINT[f][0] - vx;
+    double dy = H3T_FACE_CENTER_POINT[f][1] - vy;
+    double dz = H3T_FACE_CENTER_POINT[f][2] - vz;
+    double s = dx * dx + dy * dy + dz * dz;
+    if (s < best) {
+      second = best;
+      best = s;
+      f0 = f;
+    } else if (s < second) {
+      second = s;
+    }
+  }
+  o.face = f0;
+  const double(*F)[3] = H3T_FACE_FRAME[f0][res & 1];
+  double dc = vx * F[2][0] + vy * F[2][1] + vz * F[2][2];
+  double da = vx * F[0][0] + vy * F[0][1] + vz * F[0][2];
+  double db = vx * F[1][0] + vy * F[1][1] + vz * F[1][2];
+  double q = k_res / dc;
+  double x = da * q, y = db * q;
+  double margin;
+  o.ijk = hex2d_to_ijk(x, y, &margin);
+  o.tie = (second - best < 1e-12) || !(dc > 0.5) || (margin < tie_band(x, y, 1.0 - dc * dc));
+  return o;
+}
+
+// lattice key of (face, ijk): face in bits 56..60, (i - k) and (j - k) biased by 2^27
+MGPU_HD uint64_t lattice_key(int face, IJK c) {
+  uint64_t a = (uint64_t)(uint32_t)(c.i - c.k + (1 << 27)) & 0xFFFFFFFULL;
+  uint64_t b = (uint64_t)(uint32_t)(c.j - c.k + (1 << 27)) & 0xFFFFFFFULL;
+  return ((uint64_t)face << 56) | (a << 28) | b;
+}
+
+// K(res) = sqrt7^res / RES0_U_GNOMONIC
+MGPU_HD double k_of_res(int res) {
+  double r = 1.0 / kRes0UGnomonic;
+  for (int i = 0; i < res; i++) r *= kSqrt7;
+  return r;
+}
+
+// ------------------------------------------------------------------ inverse (host)
+
+MGPU_HD void ijk_to_hex2d(IJK h, double* x, double* y) {
+  int i = h.i - h.k, j = h.j - h.k;
+  *x = i - 0.5 * j;
+  *y = j * kSin60;
+}
+
+// _hex2dToGeo (substrate 0): hex2d on `face` at `res` -> (lat, lon) radians
+MGPU_HD void hex2d_to_geo(double vx, double vy, int face, int res, double* lat, double* lon) {
+  double r = sqrt(vx * vx + vy * vy);
+  double lat0 = H3T_FACE_CENTER_GEO[face][0], lon0 = H3T_FACE_CENTER_GEO[face][1];
+  if (r < kEpsilon) {
+    *lat = lat0;
+    *lon = lon0;
+    return;
+  }
+  double theta = atan2(vy, vx);
+  for (int i = 0; i < res; i++) r /= kSqrt7;
+  r *= kRes0UGnomonic;
+  r = atan(r);
+  if (res % 2) theta = pos_angle(theta + kAp7Rot);
+  double az = pos_angle(H3T_FACE_AXES_AZ_CII[face][0] - theta);
+  double sinlat = sin(lat0) * cos(r) + cos(lat0) * sin(r) * cos(az);
+  if (sinlat > 1.0) sinlat = 1.0;
+  if (sinlat < -1.0) sinlat = -1.0;
+  *lat = asin(sinlat);
+  double sinlon = sin(az) * sin(r) / cos(*lat);
+  double coslon = (cos(r) - sin(lat0) * sin(*lat)) / cos(lat0) / cos(*lat);
+  if (sinlon > 1.0) sinlon = 1.0;
+  if (sinlon < -1.0) sinlon = -1.0;
+  if (coslon > 1.0) coslon = 1.0;
+  if (coslon < -1.0) coslon = -1.0;
+  double l = lon0 + atan2(sinlon, coslon);
+  while (l > 3.14159265358979323846) l -= 2 * 3.14159265358979323846;
+  while (l < -3.14159265358979323846) l += 2 * 3.14159265358979323846;
+  *lon = l;
+}
+
+// _h3ToFaceIjkWithInitializedFijk without the overage adjustment: the cell's
+// centre in its base cell's home-face lattice.  Returns false for pentagon base
+// cells (their digit space is rotated; callers fall back to cell-id probing).
+MGPU_HD bool h3_home_face_ijk(uint64_t h, int* face, IJK* ijk, int* res_out) {
+  int res = (int)((h >> 52) & 15);
+  int bc = (int)((h >> 45) & 127);
+  if (bc >= H3T_NUM_BASE_CELLS || H3T_BASE_CELL_DATA[bc][4]) return false;
+  *face = H3T_BASE_CELL_DATA[bc][0];
+  IJK c{H3T_BASE_CELL_DATA[bc][1], H3T_BASE_CELL_DATA[bc][2], H3T_BASE_CELL_DATA[bc][3]};
+  for (int r = 1; r <= res; r++) {
+    if (r & 1) down_ap7(c);
+    else down_ap7r(c);
+    int d = digit_at(h, r);
+    if (d == 7) return false;
+    if (d) {
+      c.i += (d >> 2) & 1;
+      c.j += (d >> 1) & 1;
+      c.k += d & 1;
+      ijk_normalize(c);
+    }
+  }
+  *ijk = c;
+  *res_out = res;
+  return true;
 }
 
 }  // namespace h3

@@ -16,6 +16,7 @@ struct JoinArgs {
   int64_t n;
   int64_t n_tiles;
   int res;
+  int res_match;                    // H3: the chips' resolution equals `res` (else nothing can match)
   ChipTableView chips;
   int64_t capacity;
   int64_t* out_point;
@@ -23,6 +24,7 @@ struct JoinArgs {
   uint64_t* tile_status;            // [n_tiles], zeroed before launch
   uint32_t* tile_ticket;            // zeroed before launch
   unsigned long long* counters;     // [0] pairs [1] near-ties [2] invalid [3] candidates [4] look-back timeouts
+  int ablate;                       // profiling only (MGPU_ABLATE): 1 = no PIP (border = miss), 2 = no probe
 };
 
 hipError_t launch_cells(int is, int res, const double* x, const double* y, int64_t n, int64_t* out,

@@ -95,6 +95,28 @@ MGPU_HDI int orientation(double p1x, double p1y, double p2x, double p2y, double 
   return 0;
 }
 
+// RayCrossingCounter.countSegment(p1, p2) for one segment, as bits: 1 = the point is
+// on the segment (BOUNDARY), 2 = the segment crosses the ray (one crossing).  The
+// ring's location is then BOUNDARY if any segment sets bit 1, else INTERIOR iff the
+// crossings are odd -- independent of the order the segments are visited in, which
+// lets a tile test all candidate edges in parallel (kernels.hip, phase 4).
+MGPU_HDI int count_segment(double p1x, double p1y, double p2x, double p2y, double px, double py) {
+  if (p1x < px && p2x < px) return 0;
+  if (px == p2x && py == p2y) return 1;
+  if (p1y == py && p2y == py) {
+    double mn = p1x, mx = p2x;
+    if (mn > mx) { mn = p2x; mx = p1x; }
+    return (px >= mn && px <= mx) ? 1 : 0;
+  }
+  if (((p1y > py) && (p2y <= py)) || ((p2y > py) && (p1y <= py))) {
+    int o = orientation(p1x, p1y, p2x, p2y, px, py);
+    if (o == 0) return 1;
+    if (p2y < p1y) o = -o;
+    return o == 1 ? 2 : 0;
+  }
+  return 0;
+}
+
 // RayCrossingCounter.locatePointInRing over vertices [vb, ve)
 MGPU_HDI int ring_locate(const double* __restrict__ vtx, uint32_t vb, uint32_t ve, double px, double py) {
   if (ve <= vb) return kExterior;
@@ -143,6 +165,45 @@ MGPU_HDI int polygon_locate(const ChipTableView& t, uint32_t p, double px, doubl
     }
   }
   return kInterior;
+}
+
+enum RingBits { kRingOnSegment = 1, kRingParity = 2, kRingSkipped = 4 };
+
+// Location of a ring from its accumulated bits (kRingSkipped: envelope miss / no edges)
+MGPU_HDI int ring_loc_from_bits(uint32_t b) {
+  if (b & kRingSkipped) return kExterior;
+  if (b & kRingOnSegment) return kBoundary;
+  return (b & kRingParity) ? kInterior : kExterior;
+}
+
+// PointLocator over chip `c` given the location bits of each of its rings (in chip
+// ring order, ring_bits[k] for ring part_ring[chip_part[c]] + k)
+MGPU_HDI int chip_locate_from_rings(const ChipTableView& t, uint32_t c, const uint32_t* ring_bits) {
+  const uint32_t pb = t.chip_part[c], pe = t.chip_part[c + 1];
+  const uint32_t r0 = t.part_ring[pb];
+  bool is_in = false;
+  int n_bnd = 0, single = -1;
+  for (uint32_t p = pb; p < pe; p++) {
+    uint32_t rb = t.part_ring[p], re = t.part_ring[p + 1];
+    int loc = kInterior;
+    if (re == rb) loc = kExterior;
+    for (uint32_t r = rb; r < re; r++) {
+      int l = ring_loc_from_bits(ring_bits[r - r0]);
+      if (r == rb) {
+        if (l != kInterior) { loc = l; break; }
+      } else {
+        if (l == kInterior) { loc = kExterior; break; }
+        if (l == kBoundary) { loc = kBoundary; break; }
+      }
+    }
+    if (single < 0) single = loc;
+    if (loc == kInterior) is_in = true;
+    if (loc == kBoundary) n_bnd++;
+  }
+  if (!(t.chip_flags[c] & kChipMulti)) return single < 0 ? kExterior : single;
+  if (n_bnd & 1) return kBoundary;
+  if (n_bnd > 0 || is_in) return kInterior;
+  return kExterior;
 }
 
 // Geometry.contains(point) == (location == INTERIOR), for sorted chip `c`

@@ -95,6 +95,26 @@ struct Polygon {
   std::vector<std::vector<std::vector<Pt>>> parts;  // part -> rings (first = shell)
 };
 
+double orient(Pt a, Pt b, Pt c) { return (b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x); }
+
+bool segments_touch(Pt a, Pt b, Pt c, Pt d) {
+  double o1 = orient(a, b, c), o2 = orient(a, b, d), o3 = orient(c, d, a), o4 = orient(c, d, b);
+  if (((o1 > 0 && o2 < 0) || (o1 < 0 && o2 > 0)) && ((o3 > 0 && o4 < 0) || (o3 < 0 && o4 > 0))) return true;
+  auto on = [](Pt p, Pt q, Pt r) {  // r on segment pq given collinear
+    return std::min(p.x, q.x) <= r.x && r.x <= std::max(p.x, q.x) && std::min(p.y, q.y) <= r.y &&
+           r.y <= std::max(p.y, q.y);
+  };
+  return (o1 == 0 && on(a, b, c)) || (o2 == 0 && on(a, b, d)) || (o3 == 0 && on(c, d, a)) || (o4 == 0 && on(c, d, b));
+}
+
+// convex ccw closed polygon: p inside or on the boundary
+bool in_convex(const std::vector<Pt>& cell, Pt p) {
+  for (size_t i = 0; i + 1 < cell.size(); i++)
+    if (orient(cell[i], cell[i + 1], p) < 0) return false;
+  return true;
+}
+
+
 // ---------------------------------------------------------------- grids
 
 struct Grid {
@@ -253,6 +273,39 @@ struct PairHash {
   size_t operator()(const std::pair<long, long>& p) const { return std::hash<long>()(p.first * 1000003L ^ p.second); }
 };
 
+// Exact test that the cell lies in the interior of one part of the polygon: no ring
+// vertex in/on the cell, no ring edge touching a cell edge, the cell centre inside
+// the shell and outside every hole.  Such a cell's chip IS the cell geometry
+// (isCore = coerced.equals(indexGeom), IndexSystem.scala:185).
+bool cell_in_polygon(const std::vector<Pt>& cellb, Pt cc, const Polygon& poly) {
+  double cminx = INFINITY, cminy = INFINITY, cmaxx = -INFINITY, cmaxy = -INFINITY;
+  for (auto& p : cellb) {
+    cminx = std::min(cminx, p.x);
+    cmaxx = std::max(cmaxx, p.x);
+    cminy = std::min(cminy, p.y);
+    cmaxy = std::max(cmaxy, p.y);
+  }
+  for (auto& part : poly.parts)
+    for (auto& ring : part)
+      for (size_t i = 0; i + 1 < ring.size(); i++) {
+        Pt a = ring[i], b = ring[i + 1];
+        if (std::max(a.x, b.x) < cminx || std::min(a.x, b.x) > cmaxx || std::max(a.y, b.y) < cminy ||
+            std::min(a.y, b.y) > cmaxy)
+          continue;
+        if (in_convex(cellb, a)) return false;
+        for (size_t k = 0; k + 1 < cellb.size(); k++)
+          if (segments_touch(a, b, cellb[k], cellb[k + 1])) return false;
+      }
+  for (auto& part : poly.parts) {
+    if (!point_in_ring(part[0], cc)) continue;
+    bool in_hole = false;
+    for (size_t r = 1; r < part.size(); r++)
+      if (point_in_ring(part[r], cc)) in_hole = true;
+    if (!in_hole) return true;
+  }
+  return false;
+}
+
 void tessellate_polygon(const Grid& g, const Polygon& poly, int32_t pid, bool keep_core, std::vector<Chip>& out) {
   // lattice-space copy of every ring
   std::vector<std::vector<Pt>> lat_rings;
@@ -341,6 +394,23 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, int32_t pid, bool ke
     }
     cc.x /= (cellb.size() - 1);
     cc.y /= (cellb.size() - 1);
+    if (cell_in_polygon(cellb, cc, poly)) {
+      int64_t id = g.cell_id(c.first, c.second);
+      if (!id) continue;
+      Chip ch{id, pid, 1, {}};
+      if (keep_core) {
+        std::vector<mgpu::wkb::Polygon> cp(1);
+        std::vector<double> flat;
+        for (auto& p : cellb) {
+          flat.push_back(p.x);
+          flat.push_back(p.y);
+        }
+        cp[0].push_back(flat);
+        mgpu::wkb::write_polygons(ch.wkb, cp);
+      }
+      out.push_back(std::move(ch));
+      continue;
+    }
     std::vector<mgpu::wkb::Polygon> parts;
     double area = 0;
     for (auto& part : poly.parts) {
@@ -378,22 +448,9 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, int32_t pid, bool ke
     if (parts.empty() || area <= 0) continue;  // empty chip: dropped
     int64_t id = g.cell_id(c.first, c.second);
     if (!id) continue;
-    bool core = area >= cell_area * (1.0 - 1e-9) && parts.size() == 1 && parts[0].size() == 1;
-    Chip ch{id, pid, (uint8_t)(core ? 1 : 0), {}};
-    if (core) {
-      if (keep_core) {
-        std::vector<mgpu::wkb::Polygon> cp(1);
-        std::vector<double> flat;
-        for (auto& p : cellb) {
-          flat.push_back(p.x);
-          flat.push_back(p.y);
-        }
-        cp[0].push_back(flat);
-        mgpu::wkb::write_polygons(ch.wkb, cp);
-      }
-    } else {
-      mgpu::wkb::write_polygons(ch.wkb, parts);
-    }
+    (void)cell_area;
+    Chip ch{id, pid, 0, {}};
+    mgpu::wkb::write_polygons(ch.wkb, parts);
     out.push_back(std::move(ch));
   }
 }
@@ -427,7 +484,7 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
                         const int64_t* poly_part_off, const int64_t* part_ring_off, const int64_t* ring_off,
                         const double* xy, int32_t keep_core_geometries, mgpu_tess** out) {
   if (!out || n_polys < 0) return MGPU_E_INVALID_ARG;
-  if (mgpu_check_resolution(index_system, res) < 0) return MGPU_E_RESOLUTION;
+  if (mgpu_check_resolution(index_system, res) != MGPU_OK) return MGPU_E_RESOLUTION;
   mgpu_tess* t = new mgpu_tess();
   for (int64_t p = 0; p < n_polys; p++) {
     Polygon poly;

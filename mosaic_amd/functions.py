@@ -80,6 +80,8 @@ def pip_join(x, y, chips, resolution, index_system=None, point_id=None, point_id
     isys = index_system or _H3
     res = isys.get_resolution(resolution)
     if isinstance(chips, ChipTable):
+        if chips.index_system != isys.code:
+            raise N.IllegalArgumentException(N.MGPU_E_INVALID_ARG, "chip table built for another index system")
         chips = chips.upload()
     _check_points(x, y)
     n = x.numel()

@@ -1,0 +1,283 @@
+"""Parity of the HIP path (through the C ABI) with the oracle, on the same seeded inputs.
+
+Bit-exact is the bar: identical cell ids, identical (point_id, polygon_id) pair
+sequences, identical st_contains results.  Sizes are what the oracle finishes in
+seconds; the full-size case checks size-independent properties plus a sampled
+slice against the oracle.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import mosaic_amd as M
+import oracle as O
+from geom_util import NYC_BBOX, nyc_points, wkt_to_wkb
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def T(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)
+
+
+def gpu_cells(x, y, res, dev, isys=None):
+    out, st = (isys or M.H3IndexSystem()).points_to_index(T(x, dev), T(y, dev), res, stats=True)
+    return out.cpu().numpy(), st
+
+
+# ---------------------------------------------------------------- cell ids
+
+def test_h3_kats_on_gpu(gpu):
+    kats = json.load(open(os.path.join(GOLDEN, "h3_kats.json")))["kats"]
+    for res in (9, 10):
+        ks = [k for k in kats if k["res"] == res]
+        got, _ = gpu_cells([k["lon"] for k in ks], [k["lat"] for k in ks], res, gpu)
+        assert got.tolist() == [k["cell"] for k in ks]
+
+
+@pytest.mark.parametrize("res", [0, 1, 5, 8, 9, 10, 11, 13, 15])
+def test_h3_cells_global_equal_oracle(gpu, res):
+    """Points uniform on the sphere: every icosahedron face, pentagons, overage."""
+    rng = np.random.default_rng(100 + res)
+    n = 400_000
+    lon = rng.uniform(-180, 180, n)
+    lat = np.degrees(np.arcsin(rng.uniform(-1, 1, n)))
+    got, st = gpu_cells(lon, lat, res, gpu)
+    ref = O.h3_points_to_cells(lon, lat, res)
+    bad = np.nonzero(got != ref)[0]
+    assert bad.size == 0, ("%d mismatches, near-ties %d; first: %s" %
+                           (bad.size, st["n_near_ties"], [(lon[i], lat[i], got[i], ref[i]) for i in bad[:3]]))
+
+
+def test_h3_cells_nyc_equal_oracle(gpu):
+    x, y = nyc_points(2_000_000, 1)
+    got, st = gpu_cells(x, y, 9, gpu)
+    assert np.array_equal(got, O.h3_points_to_cells(x, y, 9))
+
+
+def test_h3_invalid_coordinates_raise(gpu):
+    with pytest.raises(M.IllegalArgumentException):
+        gpu_cells([1.0, float("nan")], [1.0, 2.0], 9, gpu)
+    with pytest.raises(M.IllegalStateException):
+        gpu_cells([1.0], [1.0], 16, gpu)
+
+
+@pytest.mark.parametrize("res", [1, 2, 3, 4, 5, 6, -1, -2, -3, -4, -5, -6])
+def test_bng_cells_equal_oracle(gpu, res):
+    rng = np.random.default_rng(200 + abs(res))
+    n = 300_000
+    e = rng.uniform(-50_000, 750_000, n)
+    nn = rng.uniform(-50_000, 1_350_000, n)
+    e[:5] = [3e9, -3e9, 538825.0, 0.0, -0.5]   # d2i saturation, exact KAT point, zero, -0 truncation
+    nn[:5] = [1e3, 5e12, 179111.0, 0.0, 99999.99]
+    got, _ = gpu_cells(e, nn, res, gpu, M.BNGIndexSystem())
+    ref = O.bng_points_to_cells(e, nn, res)
+    assert np.array_equal(got, ref)
+
+
+def test_bng_nan_raises(gpu):
+    with pytest.raises(M.IllegalStateException):
+        gpu_cells([float("nan")], [100.0], 5, gpu, M.BNGIndexSystem())
+
+
+def test_empty_inputs(gpu, nyc_chips_r9):
+    e = torch.empty(0, dtype=torch.float64, device=gpu)
+    assert M.grid_longlatascellid(e, e, 9).numel() == 0
+    r = M.pip_join(e, e, nyc_chips_r9, 9)
+    assert len(r) == 0
+
+
+# ---------------------------------------------------------------- st_contains
+
+def test_st_contains_two_holes_on_gpu(gpu):
+    d = json.load(open(os.path.join(GOLDEN, "st_contains_kats.json")))
+    for le in (False, True):
+        w = wkt_to_wkb(d["polygon_wkt"], little_endian=le)
+        ct = M.ChipTable.from_rows([(False, 1, w, 7)])
+        pts = [(c["x"], c["y"]) for c in d["cases"]] + [(10, 50), (20, 25), (5, 5)]
+        out = M.st_contains(ct, torch.zeros(len(pts), dtype=torch.int64), T([p[0] for p in pts], gpu),
+                            T([p[1] for p in pts], gpu))
+        assert out.cpu().tolist() == [1, 0, 0, 0, 0]
+
+
+def test_st_contains_random_pairs_equal_oracle(gpu, nyc_chips_r9):
+    c = nyc_chips_r9
+    rng = np.random.default_rng(9)
+    n = 200_000
+    rows = rng.integers(0, len(c), n)
+    # points near each chosen chip: jitter around one of its vertices, plus exact vertices
+    x = np.empty(n)
+    y = np.empty(n)
+    import struct
+    for k, r in enumerate(rows):
+        b = c.wkb_offsets[r]
+        e = c.wkb_offsets[r + 1]
+        blob = bytes(c.wkb[b:e])
+        # first coordinate pair of the first ring: header(5) + nrings(4) + npts(4) for a Polygon,
+        # + 9 more bytes for a MultiPolygon's first part
+        off = 13 if blob[4] == 3 else 22
+        vx, vy = struct.unpack(">dd", blob[off:off + 16])
+        if k % 4 == 0:
+            x[k], y[k] = vx, vy
+        else:
+            x[k] = vx + rng.normal(0, 0.002)
+            y[k] = vy + rng.normal(0, 0.002)
+    out = M.st_contains(c, torch.from_numpy(rows), T(x, gpu), T(y, gpu)).cpu().numpy()
+    ref = np.array([O.st_contains(bytes(c.wkb[c.wkb_offsets[r]:c.wkb_offsets[r + 1]]), x[k], y[k])
+                    for k, r in enumerate(rows)], dtype=np.int8)
+    assert np.array_equal(out, ref)
+    assert ref.sum() > 0 and (ref == 0).sum() > 0
+
+
+# ---------------------------------------------------------------- the join
+
+def oracle_join(c, x, y, res=9, isys=0):
+    return O.pip_join(isys, res, x, y, c.cell, c.polygon_id, c.is_core, c.wkb_offsets, c.wkb)
+
+
+def test_pip_join_nyc_equals_oracle(gpu, nyc_chips_r9):
+    x, y = nyc_points(3_000_000, 2)
+    r = M.pip_join(T(x, gpu), T(y, gpu), nyc_chips_r9, 9)
+    gp, gq = r.numpy()
+    op, oq = oracle_join(nyc_chips_r9, x, y)
+    assert len(gp) == len(op) and np.array_equal(gp, op) and np.array_equal(gq, oq)
+    assert r.stats["n_pairs"] == len(op) and r.stats["n_candidates"] > 0
+    assert np.all(np.diff(gp) >= 0)
+
+
+def test_pip_join_explicit_point_ids_and_base(gpu, nyc_chips_r9):
+    x, y = nyc_points(300_000, 3)
+    ids = np.arange(300_000, dtype=np.int64) * 7 + 11
+    r = M.pip_join(T(x, gpu), T(y, gpu), nyc_chips_r9, 9, point_id=torch.from_numpy(ids).to(gpu))
+    op, oq = oracle_join(nyc_chips_r9, x, y)
+    gp, gq = r.numpy()
+    assert np.array_equal(gp, ids[op]) and np.array_equal(gq, oq)
+    r2 = M.pip_join(T(x, gpu), T(y, gpu), nyc_chips_r9, 9, point_id_base=10 ** 12)
+    assert np.array_equal(r2.numpy()[0], op + 10 ** 12)
+
+
+def test_pip_join_capacity(gpu, nyc_chips_r9):
+    x, y = nyc_points(100_000, 4)
+    op, oq = oracle_join(nyc_chips_r9, x, y)
+    with pytest.raises(M.CapacityError) as ei:
+        M.pip_join(T(x, gpu), T(y, gpu), nyc_chips_r9, 9, capacity=10)
+    assert ei.value.required == len(op)
+
+
+def test_pip_join_default_capacity_grows(gpu):
+    """Overlapping polygons: every point matches 5 zones (> the 2 kept in registers, and
+    more pairs than the default capacity), forcing both slow paths."""
+    sq = [(0.0, 0.0), (1.0, 0.0), (1.0, 1.0), (0.0, 1.0), (0.0, 0.0)]
+    polys = [(pid, [[[(x * (1 + 0.01 * pid), y * (1 + 0.01 * pid)) for x, y in sq]]]) for pid in (5, 3, 9, 1, 7)]
+    P = M.Polygons.from_lists(polys)
+    c = M.tessellate(P, M.H3IndexSystem(), 5)
+    rng = np.random.default_rng(8)
+    x = rng.uniform(0.05, 0.95, 50_000)
+    y = rng.uniform(0.05, 0.95, 50_000)
+    r = M.pip_join(T(x, gpu), T(y, gpu), c, 5)
+    op, oq = oracle_join(c, x, y, res=5)
+    gp, gq = r.numpy()
+    assert len(op) > 4 * len(x)
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+
+
+def adversarial_points(c):
+    """Points exactly on chip vertices and edge midpoints (most chip vertices are H3
+    cell vertices, i.e. within a few ulps of three cells' common corner)."""
+    import struct
+    xs, ys = [], []
+    for r in range(0, len(c), 3):
+        blob = bytes(c.wkb[c.wkb_offsets[r]:c.wkb_offsets[r + 1]])
+        if not blob or blob[4] != 3:
+            continue
+        (npts,) = struct.unpack(">I", blob[9:13])
+        pts = [struct.unpack(">dd", blob[13 + 16 * i:29 + 16 * i]) for i in range(npts)]
+        for i in range(npts - 1):
+            xs += [pts[i][0], 0.5 * (pts[i][0] + pts[i + 1][0])]
+            ys += [pts[i][1], 0.5 * (pts[i][1] + pts[i + 1][1])]
+    return np.array(xs), np.array(ys)
+
+
+def test_pip_join_adversarial_points(gpu, nyc_chips_r9):
+    """On points that sit on cell corners the cell id can flip with a 1-ulp libm
+    difference.  Every disagreement with the oracle must be a point the kernel itself
+    reported as a near-tie (counted and diagnosed, DESIGN.md "Numerics"); all other
+    points must agree exactly, cells and pairs."""
+    c = nyc_chips_r9
+    x, y = adversarial_points(c)
+    cells, st = gpu_cells(x, y, 9, gpu)
+    ref = O.h3_points_to_cells(x, y, 9)
+    bad = np.nonzero(cells != ref)[0]
+    assert bad.size <= st["n_near_ties"], (bad.size, st["n_near_ties"])
+    r = M.pip_join(T(x, gpu), T(y, gpu), c, 9)
+    op, oq = oracle_join(c, x, y)
+    gp, gq = r.numpy()
+    keep_g = ~np.isin(gp, bad)
+    keep_o = ~np.isin(op, bad)
+    assert np.array_equal(gp[keep_g], op[keep_o]) and np.array_equal(gq[keep_g], oq[keep_o])
+    print("adversarial: %d points, %d near-ties flagged, %d cell disagreements" % (len(x), st["n_near_ties"], bad.size))
+
+
+def test_pip_join_bng_equals_oracle(gpu):
+    from test_host import _bng_synthetic
+    P = _bng_synthetic(seed=21, n=40)
+    for res in (3, 4, -4):
+        c = M.tessellate(P, M.BNGIndexSystem(), res)
+        rng = np.random.default_rng(res + 50)
+        x = np.round(rng.uniform(505000, 560000, 1_000_000), 2)  # 0.01 m granularity like UPRNs
+        y = np.round(rng.uniform(155000, 200000, 1_000_000), 2)
+        r = M.pip_join(T(x, gpu), T(y, gpu), c, res, index_system=M.BNGIndexSystem())
+        op, oq = oracle_join(c, x, y, res=res, isys=1)
+        gp, gq = r.numpy()
+        assert np.array_equal(gp, op) and np.array_equal(gq, oq), res
+
+
+def test_pip_join_kats_on_gpu(gpu, nyc_chips_r9):
+    kats = json.load(open(os.path.join(GOLDEN, "pip_kats.json")))["kats"]
+    r = M.pip_join(T([k["lon"] for k in kats], gpu), T([k["lat"] for k in kats], gpu), nyc_chips_r9, 9)
+    gp, gq = r.numpy()
+    assert list(gp) == list(range(len(kats)))
+    for k, q in zip(kats, gq):
+        assert int(q) in k["objectids"]
+
+
+def test_chip_blob_roundtrip(gpu, nyc_chips_r9):
+    """The replicated chip table (what RCCL broadcast carries) joins identically."""
+    d = nyc_chips_r9.upload()
+    ptr, nbytes = d.device_blob()
+    buf = torch.empty(nbytes, dtype=torch.uint8, device=gpu)
+    from mosaic_amd.dist import _copy_device
+    _copy_device(ptr, buf.data_ptr(), nbytes)
+    d2 = M.DeviceChips.from_device_blob(d.ctx, buf.data_ptr(), nbytes)
+    del buf
+    x, y = nyc_points(200_000, 5)
+    a = M.pip_join(T(x, gpu), T(y, gpu), d, 9).numpy()
+    b = M.pip_join(T(x, gpu), T(y, gpu), d2, 9).numpy()
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert d2.info()["chips"] == len(nyc_chips_r9)
+
+
+def test_pip_join_full_size_properties(gpu, nyc_chips_r9):
+    """BASELINE C2 size (1e8 points): pairs ascend by point, every polygon id is a
+    real zone, and a 1e6-point strided slice equals the oracle on those points."""
+    n = 100_000_000
+    g = torch.Generator(device=gpu)
+    g.manual_seed(77)
+    x = torch.rand(n, dtype=torch.float64, device=gpu, generator=g) * (NYC_BBOX[2] - NYC_BBOX[0]) + NYC_BBOX[0]
+    y = torch.rand(n, dtype=torch.float64, device=gpu, generator=g) * (NYC_BBOX[3] - NYC_BBOX[1]) + NYC_BBOX[1]
+    r = M.pip_join(x, y, nyc_chips_r9, 9)
+    p = r.point_id
+    assert bool((p[1:] >= p[:-1]).all())
+    frac = len(r) / n
+    assert 0.30 < frac < 0.42, frac
+    idx = torch.arange(0, n, 100, device=gpu)
+    xs, ys = x[idx].cpu().numpy(), y[idx].cpu().numpy()
+    op, oq = oracle_join(nyc_chips_r9, xs, ys)
+    mask = (p % 100) == 0
+    gp = (p[mask] // 100).cpu().numpy()
+    gq = r.polygon_id[mask].cpu().numpy()
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)

@@ -1,0 +1,146 @@
+"""Host-side product logic (no GPU): the C-ABI library loads and exports what the
+header declares, BNG StringType ids, resolution validation, and the chip-table
+builder (grid_tessellateexplode) checked against the reference's invariants and
+against brute-force JTS-semantics containment on the original polygons."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import mosaic_amd as M
+import oracle as O
+from geom_util import brute_force_pairs, polygons_area, wkb_area, nyc_points
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def test_library_exports_every_header_symbol():
+    from mosaic_amd import _native as N
+    hdr = open(os.path.join(ROOT, "include", "mosaic_gpu.h")).read()
+    declared = set(re.findall(r"\b(mgpu_[a-z0-9_]+)\s*\(", hdr))
+    assert declared == set(N.EXPORTS)
+    L = N.lib()
+    for s in declared:
+        assert hasattr(L, s), s
+    assert b"gfx950" in L.mgpu_version()
+
+
+def test_resolution_validation():
+    h3, bng = M.H3IndexSystem(), M.BNGIndexSystem()
+    assert h3.get_resolution(9) == 9 and h3.get_resolution("10") == 10
+    with pytest.raises(M.IllegalStateException):
+        h3.get_resolution(16)
+    with pytest.raises(M.IllegalArgumentException):
+        h3.get_resolution(1.5)
+    assert bng.get_resolution("500m") == -4 and bng.get_resolution(4) == 4
+    with pytest.raises(M.IllegalStateException):
+        bng.get_resolution(0)
+    with pytest.raises(M.IllegalStateException):
+        bng.get_resolution(True)
+    from mosaic_amd import _native as N
+    assert N.lib().mgpu_check_resolution(0, 15) == 0 and N.lib().mgpu_check_resolution(1, -6) == 0
+    assert N.lib().mgpu_check_resolution(1, 7) == N.MGPU_E_RESOLUTION
+    assert M.get_index_system("bng").name == "BNG"
+    with pytest.raises(M.IllegalArgumentException):
+        M.get_index_system("CUSTOM(0,1,0,1,2,1,1)")
+
+
+def test_bng_format_parse_kats():
+    d = json.load(open(os.path.join(GOLDEN, "bng_kats.json")))
+    bng = M.BNGIndexSystem()
+    for k in d["point_to_index"]:
+        cell = O.bng_point_to_index(k["e"], k["n"], k["res"])
+        if k["cell"] is not None:
+            assert cell == k["cell"]
+        assert bng.format(cell) == k["str"], k
+    for p in d["parse"]:
+        assert bng.parse(p["str"]) == p["cell"]
+    # TestBNGIndexSystem.scala:84 parse("NW") == encode(1, 5, 0, 0, 0, 1, -2)
+    assert bng.parse("NW") == 100000 + 1 * 1000 + 5 * 10
+    # transform_join_bng.ipynb cell 51: the joined point lies in chip TQ3586NW
+    j = d["join"]
+    assert bng.format(O.bng_point_to_index(j["e"], j["n"], -4)) == j["index_id"]
+    with pytest.raises(M.IllegalArgumentException):
+        bng.format(-5)
+
+
+def test_bng_format_round_trip_random():
+    rng = np.random.default_rng(3)
+    bng = M.BNGIndexSystem()
+    e = rng.uniform(0, 700000, 2000)
+    n = rng.uniform(0, 1300000, 2000)
+    for res in (1, 2, 3, 4, 5, 6, -2, -3, -4, -5, -6):
+        cells = O.bng_points_to_cells(e, n, res)
+        strs = bng.format_many(cells)
+        assert np.array_equal(bng.parse_many(strs), cells), res
+
+
+def test_tessellation_covers_each_zone_exactly(nyc_zones, nyc_chips_r9):
+    """MosaicExplodeBehaviors.scala:415-457 (issue 382): the chips of a polygon
+    add up to the polygon's area; chips never overlap (one chip per cell)."""
+    c = nyc_chips_r9
+    assert len(c) > 10000 and c.is_core.sum() > 3000
+    for pid in (1, 2, 43, 132, 138, 161, 230, 263):
+        k = int(np.nonzero(nyc_zones.poly_id == pid)[0][0])
+        rows = np.nonzero(c.polygon_id == pid)[0]
+        assert len(np.unique(c.cell[rows])) == len(rows)
+        area = sum(wkb_area(bytes(c.wkb[c.wkb_offsets[i]:c.wkb_offsets[i + 1]])) for i in rows)
+        assert area == pytest.approx(polygons_area(nyc_zones, k), rel=1e-8), pid
+
+
+def test_tessellation_join_equals_brute_force(nyc_zones, nyc_chips_r9):
+    """is_core OR st_contains over the chips == contains over the original zones."""
+    x, y = nyc_points(20000, 11)
+    c = nyc_chips_r9
+    pts, polys = O.pip_join(0, 9, x, y, c.cell, c.polygon_id, c.is_core, c.wkb_offsets, c.wkb)
+    assert set(zip(pts.tolist(), polys.tolist())) == brute_force_pairs(nyc_zones, x, y, O)
+    # chip cells are exactly the cells the points are indexed to
+    cells = set(c.cell.tolist())
+    got = O.h3_points_to_cells(x[pts], y[pts], 9)
+    assert set(got.tolist()) <= cells
+
+
+def test_tessellation_no_core_geometry(nyc_zones):
+    c = M.tessellate(nyc_zones.select(range(10)), M.H3IndexSystem(), 9, keep_core_geometries=False)
+    core = c.is_core.astype(bool)
+    lens = np.diff(c.wkb_offsets)
+    assert (lens[core] == 0).all() and (lens[~core] > 0).all()
+
+
+def _bng_synthetic(seed=5, n=12):
+    """UK-style polygons in eastings/northings: jittered star polygons with holes."""
+    rng = np.random.default_rng(seed)
+    polys = []
+    for p in range(n):
+        cx, cy = rng.uniform(510000, 555000), rng.uniform(160000, 195000)
+        k = int(rng.integers(8, 40))
+        ang = np.sort(rng.uniform(0, 2 * np.pi, k))
+        rad = rng.uniform(800, 3000, k)
+        shell = [(cx + r * np.cos(a), cy + r * np.sin(a)) for a, r in zip(ang, rad)]
+        shell.append(shell[0])
+        hole = [(cx + 200 * np.cos(a), cy + 200 * np.sin(a)) for a in np.linspace(2 * np.pi, 0, 9)]
+        polys.append((p + 1, [[shell, hole]]))
+    return M.Polygons.from_lists(polys)
+
+
+@pytest.mark.parametrize("res", [3, 4, -3, -4])
+def test_bng_tessellation_join_equals_brute_force(res):
+    P = _bng_synthetic()
+    c = M.tessellate(P, M.BNGIndexSystem(), res)
+    assert len(c) > 0
+    rng = np.random.default_rng(7)
+    x = rng.uniform(505000, 560000, 20000)
+    y = rng.uniform(155000, 200000, 20000)
+    pts, polys = O.pip_join(1, res, x, y, c.cell, c.polygon_id, c.is_core, c.wkb_offsets, c.wkb)
+    assert set(zip(pts.tolist(), polys.tolist())) == brute_force_pairs(P, x, y, O)
+
+
+def test_tessellation_rejects_unsupported():
+    P = _bng_synthetic(n=2)
+    with pytest.raises(M.MosaicGpuError):
+        M.tessellate(P, M.BNGIndexSystem(), -1)
+    with pytest.raises(M.IllegalStateException):
+        M.tessellate(P, M.H3IndexSystem(), 16)

@@ -490,6 +490,33 @@ def emit(path, home, bc_of, rot):
             rows.append("{" + ", ".join(js) + "}")
         L.append("    {" + ", ".join(rows) + "},")
     L.append("};")
+    # Direct gnomonic frame per face and resolution class: hex2d x = K (v.a) / (v.c),
+    # y = K (v.b) / (v.c), the closed form of H3's acos / azimuth / tan route.
+    # a = cos(az0) n + sin(az0) e, b = sin(az0) n - cos(az0) e at the face centre, with
+    # az0 = faceAxesAzRadsCII[f][0] (Class II) or that minus M_AP7_ROT_RADS (Class III).
+    ap7 = 0.333473172251832115336090755351601070065900389
+    L.append("/* gnomonic frame [face][class II/III][a, b, c][xyz] (mgpu fast path) */")
+    L.append("H3T_QUAL double H3T_FACE_FRAME[20][2][3][3] = {")
+    for f in range(20):
+        lat, lon = FACE_CENTER_GEO[f]
+        n = (-math.sin(lat) * math.cos(lon), -math.sin(lat) * math.sin(lon), math.cos(lat))
+        e = (-math.sin(lon), math.cos(lon), 0.0)
+        c = tuple(FACE_CENTER_POINT[f])
+        cls = []
+        for k in (0, 1):
+            az0 = FACE_AXES_AZ_CII[f][0] - (ap7 if k else 0.0)
+            a = tuple(math.cos(az0) * n[q] + math.sin(az0) * e[q] for q in range(3))
+            b = tuple(math.sin(az0) * n[q] - math.cos(az0) * e[q] for q in range(3))
+            cls.append("{{%s}, {%s}, {%s}}" % (", ".join(repr(v) for v in a), ", ".join(repr(v) for v in b),
+                                                   ", ".join(repr(v) for v in c)))
+        L.append("    {" + ", ".join(cls) + "},")
+    L.append("};")
+    L.append("/* sin / cos of k / 64 rad, k = -202 .. 202 (index k + 202) */")
+    L.append("#define H3T_SC64_BIAS 202")
+    L.append("H3T_QUAL double H3T_SINCOS64[405][2] = {")
+    for k in range(-202, 203):
+        L.append("    {%s, %s}," % (repr(math.sin(k / 64.0)), repr(math.cos(k / 64.0))))
+    L.append("};")
     L.append("/* baseCellData: home face, home i, j, k, isPentagon, cwOffsetPent[2] */")
     L.append("H3T_QUAL signed char H3T_BASE_CELL_DATA[122][7] = {")
     for b in range(122):
