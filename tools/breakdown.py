@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Where the fused join's time goes (profiling aid, GPU box only).
+
+Times, on the bench workload (uniform NYC-bbox points x 263 zones, H3 res 9):
+  cells      mgpu_points_to_cells alone (H3 geoToH3 of every point, 24 B/pt)
+  join       the fused kernel
+  join/noPIP border chips counted as misses (MGPU_ABLATE=1)
+  join/noprobe  no chip-table probe, i.e. projection + output protocol only (MGPU_ABLATE=2)
+Prints one JSON object.  Kernel times come from HIP events around the launch.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=int, default=100_000_000)
+    ap.add_argument("--res", type=int, default=9)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    import mosaic_amd as M
+    import bench as B
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    ctx = M.default_context(dev)
+    zones = M.Polygons.from_npz(os.path.join(ROOT, "tests", "golden", "nyc_taxi_zones.npz"))
+    chips = M.tessellate(zones, M.H3IndexSystem(), a.res).upload(ctx)
+    x, y = B.gen_points(a.points, 0, 0x20250314, dev)
+    cap = a.points // 2 + 1024
+    op = torch.empty(cap, dtype=torch.int64, device=dev)
+    oq = torch.empty(cap, dtype=torch.int32, device=dev)
+    ctx.reserve(a.points)
+    out = {"points": a.points, "res": a.res}
+
+    def t_cells():
+        ms = []
+        for _ in range(a.reps + 1):
+            _, st = M.grid_longlatascellid(x, y, a.res, stats=True)
+            ms.append(st["kernel_ms"])
+        return float(np.median(ms[1:]))
+
+    def t_join(ablate):
+        if ablate:
+            os.environ["MGPU_ABLATE"] = str(ablate)
+        else:
+            os.environ.pop("MGPU_ABLATE", None)
+        ms = []
+        for _ in range(a.reps + 1):
+            r = M.pip_join(x, y, chips, a.res, out=(op, oq), capacity=cap)
+            ms.append(r.stats["kernel_ms"])
+        os.environ.pop("MGPU_ABLATE", None)
+        return float(np.median(ms[1:])), len(r)
+
+    out["cells_ms"] = t_cells()
+    out["join_ms"], out["pairs"] = t_join(0)
+    out["join_nopip_ms"], out["pairs_nopip"] = t_join(1)
+    out["join_noprobe_ms"], _ = t_join(2)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
