@@ -48,7 +48,8 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // offsets, so a byte copy of the blob on another GPU (RCCL broadcast) is a
 // complete chip table there.
 constexpr uint64_t kBlobMagic = 0x4d4f534149434850ULL;  // "MOSAICHP"
-constexpr int kBlobArrays = 11;
+constexpr int kBlobArrays = 16;
+constexpr uint32_t kBlobVersion = 3;
 struct BlobHeader {
   uint64_t magic;
   uint32_t version, hash_mask, max_probe, n_chips, n_cells, pad;
@@ -79,6 +80,11 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.ring_env = (const double*)(base + h.off[8]);
   v.vtx = (const double*)(base + h.off[9]);
   v.row_to_chip = (const uint32_t*)(base + h.off[10]);
+  v.chip_strip = (const uint32_t*)(base + h.off[11]);
+  v.chip_sy = (const double*)(base + h.off[12]);
+  v.strip_edge = (const uint32_t*)(base + h.off[13]);
+  v.edges = (const double*)(base + h.off[14]);
+  v.edge_ring = (const uint8_t*)(base + h.off[15]);
   v.probe_mode = h.probe_mode;
   v.res = h.res;
   v.face_mask = h.face_mask;
@@ -210,9 +216,75 @@ bool build_lattice(const std::vector<mgpu::HashSlot>& cells, std::vector<std::pa
   return true;
 }
 
-}  // namespace
+// Strip index of the border chips (chip_table.h "strips"): for chip c with E edges,
+// S = clamp(E / 2, 1, kMaxStrips) equal strips over its envelope's y-range; edge e
+// (p1 = ring[i], p2 = ring[i-1], as RayCrossingCounter visits it) is listed in the
+// strips strip_of(min y) .. strip_of(max y) -- the same function the kernel applies
+// to the point, so a point whose y lies in the edge's closed y-range always finds
+// the edge in its strip.
+struct Strips {
+  std::vector<uint32_t> chip_strip;
+  std::vector<double> chip_sy;
+  std::vector<uint32_t> strip_edge{0};
+  std::vector<double> edges;
+  std::vector<uint8_t> edge_ring;
+};
 
-namespace {
+void build_strips(int64_t n_chips, std::vector<uint8_t>& cflags, const std::vector<uint32_t>& cpart,
+                  const std::vector<double>& cenv, const mgpu::wkb::Flat& geo, Strips& st) {
+  st.chip_strip.assign(n_chips + 1, 0);
+  st.chip_sy.assign(2 * (size_t)n_chips, 0.0);
+  std::vector<std::vector<uint32_t>> bucket;
+  for (int64_t c = 0; c < n_chips; c++) {
+    st.chip_strip[c] = (uint32_t)(st.strip_edge.size() - 1);
+    uint8_t fl = cflags[c];
+    if (fl & (mgpu::kChipCore | mgpu::kChipEmpty | mgpu::kChipNoGeom | mgpu::kChipRect)) {
+      if (!(fl & (mgpu::kChipEmpty | mgpu::kChipNoGeom | mgpu::kChipRect))) cflags[c] |= mgpu::kChipNoStrips;
+      continue;
+    }
+    const uint32_t r0 = geo.part_ring[cpart[c]], r1 = geo.part_ring[cpart[c + 1]];
+    if (r1 - r0 > (uint32_t)mgpu::kStripRings) {
+      cflags[c] |= mgpu::kChipNoStrips;
+      continue;
+    }
+    int64_t E = 0;
+    for (uint32_t r = r0; r < r1; r++) {
+      uint32_t nv = geo.ring_vtx[r + 1] - geo.ring_vtx[r];
+      if (nv >= 2) E += nv - 1;
+    }
+    int S = (int)std::min<int64_t>(mgpu::kMaxStrips, std::max<int64_t>(1, E / 2));
+    const double y0 = cenv[4 * c + 1], H = cenv[4 * c + 3] - y0;
+    if (!(H > 0)) S = 1;
+    const double inv_h = (H > 0) ? (double)S / H : 0.0;
+    st.chip_sy[2 * c] = y0;
+    st.chip_sy[2 * c + 1] = inv_h;
+    bucket.assign(S, {});
+    std::vector<double> rec;
+    std::vector<uint8_t> rring;
+    uint32_t k = 0;
+    for (uint32_t r = r0; r < r1; r++) {
+      const uint32_t vb = geo.ring_vtx[r], ve = geo.ring_vtx[r + 1];
+      for (uint32_t i = vb + 1; i < ve; i++) {
+        const double p1x = geo.vtx[2 * i], p1y = geo.vtx[2 * i + 1];
+        const double p2x = geo.vtx[2 * i - 2], p2y = geo.vtx[2 * i - 1];
+        rec.insert(rec.end(), {p1x, p1y, p2x, p2y});
+        rring.push_back((uint8_t)(r - r0));
+        const int sa = mgpu::strip_of(std::min(p1y, p2y), y0, inv_h, S);
+        const int sb = mgpu::strip_of(std::max(p1y, p2y), y0, inv_h, S);
+        for (int q = sa; q <= sb; q++) bucket[q].push_back(k);
+        k++;
+      }
+    }
+    for (int q = 0; q < S; q++) {
+      for (uint32_t e : bucket[q]) {
+        st.edges.insert(st.edges.end(), rec.begin() + 4 * e, rec.begin() + 4 * e + 4);
+        st.edge_ring.push_back(rring[e]);
+      }
+      st.strip_edge.push_back((uint32_t)st.edge_ring.size());
+    }
+  }
+  st.chip_strip[n_chips] = (uint32_t)(st.strip_edge.size() - 1);
+}
 
 }  // namespace
 
@@ -427,9 +499,15 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
     int64_t e = s;
     uint64_t c = (uint64_t)cell[order[s]];
     while (e < n_chips && (uint64_t)cell[order[e]] == c) e++;
-    distinct.push_back(mgpu::HashSlot{c, (uint32_t)s, (uint32_t)(e - s)});
+    if (e - s > 0xFFFF) return fail(MGPU_E_INVALID_ARG, "more than 65535 chips share cell %lld", (long long)c);
+    uint16_t core = 0;
+    for (int64_t j = 0; j < e - s && j < 16; j++)
+      if (cflags[s + j] & mgpu::kChipCore) core |= (uint16_t)(1u << j);
+    distinct.push_back(mgpu::HashSlot{c, (uint32_t)s, (uint16_t)(e - s), core});
     s = e;
   }
+  Strips strips;
+  build_strips(n_chips, cflags, cpart, cenv, geo, strips);
   // H3: probe by lattice key when possible (chip_table.h)
   int32_t probe_mode = mgpu::kProbeCellId, lres = -1;
   uint32_t face_mask = (1u << 20) - 1;
@@ -445,7 +523,7 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
         continue;
       }
       const mgpu::HashSlot& d = distinct[keys[k].second];
-      entries.push_back(mgpu::HashSlot{keys[k].first, d.first, d.count});
+      entries.push_back(mgpu::HashSlot{keys[k].first, d.first, d.count, d.core_mask});
     }
   } else {
     entries = distinct;
@@ -453,7 +531,7 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
   }
   uint32_t cap = 16;
   while (cap < 2 * entries.size()) cap <<= 1;
-  std::vector<mgpu::HashSlot> slots(cap, mgpu::HashSlot{0, 0, 0});
+  std::vector<mgpu::HashSlot> slots(cap, mgpu::HashSlot{0, 0, 0, 0});
   uint32_t max_probe = 0;
   for (const auto& d : entries) {
     uint32_t h = mgpu::cell_hash(d.cell) & (cap - 1), k = 0;
@@ -483,11 +561,16 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
       {geo.ring_env.data(), geo.ring_env.size() * 8, 0},
       {geo.vtx.data(), geo.vtx.size() * 8, 0},
       {row2chip.data(), row2chip.size() * 4, 0},
+      {strips.chip_strip.data(), strips.chip_strip.size() * 4, 0},
+      {strips.chip_sy.data(), strips.chip_sy.size() * 8, 0},
+      {strips.strip_edge.data(), strips.strip_edge.size() * 4, 0},
+      {strips.edges.data(), strips.edges.size() * 8, 0},
+      {strips.edge_ring.data(), strips.edge_ring.size(), 0},
   };
   size_t total = kBlobHeaderBytes;
   BlobHeader hdr{};
   hdr.magic = kBlobMagic;
-  hdr.version = 2;
+  hdr.version = kBlobVersion;
   hdr.hash_mask = cap - 1;
   hdr.max_probe = max_probe;
   hdr.n_chips = (uint32_t)n_chips;
@@ -556,7 +639,7 @@ int32_t mgpu_chips_from_device_blob(mgpu_ctx* ctx, const void* device_ptr, int64
   if (bytes < (int64_t)kBlobHeaderBytes) return fail(MGPU_E_INVALID_ARG, "blob too small");
   BlobHeader hdr;
   HIP_TRY(hipMemcpy(&hdr, device_ptr, sizeof hdr, hipMemcpyDeviceToHost));
-  if (hdr.magic != kBlobMagic || hdr.version != 2) return fail(MGPU_E_INVALID_ARG, "not a chip-table blob");
+  if (hdr.magic != kBlobMagic || hdr.version != kBlobVersion) return fail(MGPU_E_INVALID_ARG, "not a chip-table blob");
   for (int k = 0; k < kBlobArrays; k++)
     if (hdr.off[k] >= (uint64_t)bytes) return fail(MGPU_E_INVALID_ARG, "corrupt chip-table blob");
   mgpu_chips* ch = new mgpu_chips();

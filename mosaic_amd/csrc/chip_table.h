@@ -14,6 +14,16 @@
 //   geometry   : part_ring[u32 n_parts+1], ring_vtx[u32 n_rings+1],
 //                ring_env[double4], vtx[double2 x,y]
 //   row map    : row_to_chip[u32 n_chips] (input row -> sorted position)
+//   strips     : per border chip, its envelope's y-range cut into S equal strips;
+//                chip_strip[u32 n_chips+1] (first strip of each chip), chip_sy
+//                [double2 y0, S/height], strip_edge[u32 n_strips+1] -> edge records
+//                edges[double4 p1x,p1y,p2x,p2y] + edge_ring[u8 ring within chip].
+//                A strip lists every chip edge whose closed y-range meets it (the
+//                strip of a y value is computed by strip_of() on host and device
+//                alike, which is monotone in y).  Exactness: RayCrossingCounter's
+//                countSegment contributes nothing for a segment whose closed y-range
+//                misses p.y, so the strip's edges give the same crossing parity and
+//                on-boundary bit as the whole ring (pip_core.h chip_contains_strips).
 // For H3 tables the hash is keyed by the (face, i, j) lattice position that the
 // kernel's projection yields, not by the 64-bit cell id: the kernel then never
 // assembles H3 digits.  Every lattice position of every chip cell on every face a
@@ -21,6 +31,12 @@
 // face_ijk_to_h3, mosaic_amd/csrc/capi.cpp build_lattice).
 #pragma once
 #include <stdint.h>
+
+#ifdef __HIPCC__
+#define MGPU_HDI_FWD __host__ __device__ __forceinline__
+#else
+#define MGPU_HDI_FWD inline
+#endif
 
 namespace mgpu {
 
@@ -30,12 +46,27 @@ enum ChipFlags : uint8_t {
   kChipMulti = 4,      // MultiPolygon / GeometryCollection: Mod-2 PointLocator
   kChipEmpty = 8,      // no coordinates: contains nothing
   kChipNoGeom = 16,    // WKB was NULL (core chip with keep_core_geometries=false)
+  kChipNoStrips = 32,  // more than 32 rings: evaluated by the sequential PointLocator
 };
 
+constexpr int kMaxStrips = 64;
+constexpr int kStripRings = 32;
+
+// strip of y within a chip of `S` strips (y >= y0 whenever it is used on a point,
+// since the chip envelope test comes first); monotone non-decreasing in y
+MGPU_HDI_FWD int strip_of(double y, double y0, double inv_h, int S) {
+  double v = (y - y0) * inv_h;
+  int s = v < (double)S ? (int)v : S - 1;
+  return s < 0 ? 0 : s;
+}
+
+// cell (or lattice key) -> its chips [first, first + count).  core_mask bit j: chip
+// first + j is a core chip (j < 16; chips past 16 are looked up in chip_flags).
 struct alignas(16) HashSlot {
   uint64_t cell;
   uint32_t first;
-  uint32_t count;
+  uint16_t count;
+  uint16_t core_mask;
 };
 
 struct ChipTableView {
@@ -54,6 +85,11 @@ struct ChipTableView {
   const double* ring_env;      // 4 per ring
   const double* vtx;           // 2 per vertex
   const uint32_t* row_to_chip; // [n_chips]
+  const uint32_t* chip_strip;  // [n_chips + 1]
+  const double* chip_sy;       // 2 per chip: y0, S / height
+  const uint32_t* strip_edge;  // [n_strips + 1]
+  const double* edges;         // 4 per edge record: p1x, p1y, p2x, p2y (p1 = ring[i], p2 = ring[i-1])
+  const uint8_t* edge_ring;    // ring index of the edge within its chip
   // H3 probing (index system H3 only)
   int32_t probe_mode;          // 0: hash keyed by cell id; 1: keyed by (face, i, j) lattice key
   int32_t res;                 // resolution of the chip cells (H3), -1 if mixed / unknown

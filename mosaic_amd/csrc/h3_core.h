@@ -52,6 +52,22 @@ struct IJK {
   int i, j, k;
 };
 
+// libm entry points of the H3 route.  On the device each is its own out-of-line
+// function: the route runs for ~1 point in 1e6, and inlining ocml's polynomials
+// into it made the route -- and with it every kernel that calls it -- allocate 120
+// VGPRs.
+#ifdef __HIP_DEVICE_COMPILE__
+#define MGPU_LIBM static __device__ __attribute__((noinline))
+#else
+#define MGPU_LIBM static inline
+#endif
+MGPU_LIBM void lm_sincos(double a, double* s, double* c) { sincos(a, s, c); }
+MGPU_LIBM double lm_acos(double a) { return acos(a); }
+MGPU_LIBM double lm_atan2(double y, double x) { return atan2(y, x); }
+MGPU_LIBM double lm_tan(double a) { return tan(a); }
+MGPU_LIBM double lm_sin(double a) { return sin(a); }
+MGPU_LIBM double lm_cos(double a) { return cos(a); }
+
 MGPU_HD double pos_angle(double rads) {
   double tmp = (rads < 0.0) ? rads + kTwoPi : rads;
   if (rads >= kTwoPi) tmp -= kTwoPi;
@@ -135,8 +151,8 @@ MGPU_HD IJK hex2d_to_ijk(double vx, double vy, double* margin) {
 // smallest squared chord distance (face-choice margin).
 MGPU_HD void geo_to_hex2d(double lat, double lon, int res, int* face, double* vx, double* vy, double* face_gap) {
   double slat, clat, slon, clon;
-  sincos(lat, &slat, &clat);
-  sincos(lon, &slon, &clon);
+  lm_sincos(lat, &slat, &clat);
+  lm_sincos(lon, &slon, &clon);
   double x = clon * clat, y = slon * clat, z = slat;
   int f0 = 0;
   double best = 5.0, second = 5.0;
@@ -155,7 +171,7 @@ MGPU_HD void geo_to_hex2d(double lat, double lon, int res, int* face, double* vx
   }
   *face = f0;
   *face_gap = second - best;
-  double r = acos(1 - best / 2);
+  double r = lm_acos(1 - best / 2);
   if (r < kEpsilon) {
     *vx = *vy = 0.0;
     return;
@@ -163,15 +179,15 @@ MGPU_HD void geo_to_hex2d(double lat, double lon, int res, int* face, double* vx
   // _geoAzimuthRads(faceCenterGeo[face], g)
   double flat = H3T_FACE_CENTER_GEO[f0][0], flon = H3T_FACE_CENTER_GEO[f0][1];
   double sdl, cdl;
-  sincos(lon - flon, &sdl, &cdl);
-  double az = atan2(clat * sdl, cos(flat) * slat - sin(flat) * clat * cdl);
+  lm_sincos(lon - flon, &sdl, &cdl);
+  double az = lm_atan2(clat * sdl, lm_cos(flat) * slat - lm_sin(flat) * clat * cdl);
   double theta = pos_angle(H3T_FACE_AXES_AZ_CII[f0][0] - pos_angle(az));
   if (res % 2) theta = pos_angle(theta - kAp7Rot);
-  r = tan(r);
+  r = lm_tan(r);
   r /= kRes0UGnomonic;
   for (int i = 0; i < res; i++) r *= kSqrt7;
   double st, ct;
-  sincos(theta, &st, &ct);
+  lm_sincos(theta, &st, &ct);
   *vx = r * ct;
   *vy = r * st;
 }
@@ -322,8 +338,8 @@ MGPU_COLD bool route_face_ijk(double lat, double lon, int res, int* face, IJK* i
   double cx = H3T_FACE_CENTER_POINT[*face][0], cy = H3T_FACE_CENTER_POINT[*face][1],
          cz = H3T_FACE_CENTER_POINT[*face][2];
   double slat, clat, slon, clon;
-  sincos(lat, &slat, &clat);
-  sincos(lon, &slon, &clon);
+  lm_sincos(lat, &slat, &clat);
+  lm_sincos(lon, &slon, &clon);
   double cosr = cx * clon * clat + cy * slon * clat + cz * slat;
   *near_tie = (margin < tie_band(vx, vy, 1.0 - cosr * cosr)) || (gap < 1e-12);
   return true;
@@ -349,16 +365,101 @@ MGPU_HD uint64_t point_to_cell(double lon_deg, double lat_deg, int res, bool* ne
 // of the remainder (exact by Sterbenz).  The result differs from H3's by rounding
 // only; every decision within tie_band() of a threshold goes to the H3 route.
 
+// Fast-path arithmetic: explicit FMAs and a refined reciprocal instead of IEEE
+// division.  Only the fast path uses these; its result is trusted only outside the
+// tie band, which is ~1e3 x wider than the few-ulp differences they introduce.
+MGPU_HD double fma_(double a, double b, double c) { return fma(a, b, c); }
+MGPU_HD double recip(double d) {
+#ifdef __HIP_DEVICE_COMPILE__
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+#else
+  return 1.0 / d;
+#endif
+}
+constexpr double kDegToRad = 0.017453292519943295769236907684886;
+constexpr double kInvSin60 = 1.1547005383792515290182975610039149112953;
+MGPU_HD double to_radians_fast(double deg) { return deg * kDegToRad; }
+
 MGPU_HD void sincos_tab(double a, double* s, double* c) {
   double kf = rint(a * 64.0);
   int k = (int)kf;
-  double d = a - kf * 0.015625;
+  double d = fma_(kf, -0.015625, a);  // exact (Sterbenz)
   double d2 = d * d;
-  double sd = d + d * d2 * (-1.0 / 6.0 + d2 * (1.0 / 120.0 + d2 * (-1.0 / 5040.0 + d2 * (1.0 / 362880.0))));
-  double cd = 1.0 + d2 * (-0.5 + d2 * (1.0 / 24.0 + d2 * (-1.0 / 720.0 + d2 * (1.0 / 40320.0 - d2 / 3628800.0))));
+  double sp = fma_(d2, fma_(d2, fma_(d2, 1.0 / 362880.0, -1.0 / 5040.0), 1.0 / 120.0), -1.0 / 6.0);
+  double sd = fma_(d * d2, sp, d);
+  double cp = fma_(d2, fma_(d2, fma_(d2, fma_(d2, -1.0 / 3628800.0, 1.0 / 40320.0), -1.0 / 720.0), 1.0 / 24.0), -0.5);
+  double cd = fma_(d2, cp, 1.0);
   double sk = H3T_SINCOS64[k + H3T_SC64_BIAS][0], ck = H3T_SINCOS64[k + H3T_SC64_BIAS][1];
-  *s = sk * cd + ck * sd;
-  *c = ck * cd - sk * sd;
+  *s = fma_(sk, cd, ck * sd);
+  *c = fma_(ck, cd, -(sk * sd));
+}
+
+// _hex2dToCoordIJK with the fast path's multiply-by-reciprocal and the decision
+// margin (same folds and thresholds as hex2d_to_ijk)
+MGPU_HD IJK hex2d_to_ijk_fast(double vx, double vy, double* margin) {
+  IJK h;
+  h.k = 0;
+  double a1 = fabs(vx), a2 = fabs(vy);
+  double x2 = a2 * kInvSin60;
+  double x1 = fma_(x2, 0.5, a1);
+  int m1 = (int)x1, m2 = (int)x2;
+  double r1 = x1 - m1, r2 = x2 - m2;
+  double mg = dmin(dmin(r1, 1.0 - r1), dmin(r2, 1.0 - r2));
+  double t, u;
+  if (r1 < 0.5) {
+    if (r1 < 1.0 / 3.0) {
+      t = (1.0 + r1) * 0.5;
+      u = t;
+      h.i = m1;
+      h.j = (r2 < t) ? m2 : m2 + 1;
+      mg = dmin(mg, fabs(r1 - 1.0 / 3.0));
+    } else {
+      t = 1.0 - r1;
+      u = 2.0 * r1;
+      h.j = (r2 < t) ? m2 : m2 + 1;
+      h.i = ((t <= r2) && (r2 < u)) ? m1 + 1 : m1;
+      mg = dmin(mg, fabs(r1 - 1.0 / 3.0));
+    }
+    mg = dmin(mg, fabs(r1 - 0.5));
+  } else {
+    if (r1 < 2.0 / 3.0) {
+      t = 1.0 - r1;
+      u = 2.0 * r1 - 1.0;
+      h.j = (r2 < t) ? m2 : m2 + 1;
+      h.i = ((u < r2) && (r2 < t)) ? m1 : m1 + 1;
+      mg = dmin(mg, fabs(r1 - 0.5));
+    } else {
+      t = r1 * 0.5;
+      u = t;
+      h.i = m1 + 1;
+      h.j = (r2 < t) ? m2 : m2 + 1;
+    }
+    mg = dmin(mg, fabs(r1 - 2.0 / 3.0));
+  }
+  mg = dmin(mg, dmin(fabs(r2 - t), fabs(r2 - u)));
+  if (vx < 0.0) {
+    if ((h.j % 2) == 0) {
+      int axisi = h.j / 2;
+      int diff = h.i - axisi;
+      h.i = h.i - 2 * diff;
+    } else {
+      int axisi = (h.j + 1) / 2;
+      int diff = h.i - axisi;
+      h.i = h.i - (2 * diff + 1);
+    }
+  }
+  if (vy < 0.0) {
+    h.i = h.i - (2 * h.j + 1) / 2;
+    h.j = -1 * h.j;
+  }
+  ijk_normalize(h);
+  mg = dmin(mg, dmin(a1, a2));
+  *margin = mg;
+  return h;
 }
 
 struct FastHex {
@@ -367,9 +468,14 @@ struct FastHex {
   bool tie;  // a decision may differ from the H3 route: recompute with route_face_ijk
 };
 
-// k_res = sqrt7^res / RES0_U_GNOMONIC; `faces` = the faces to consider (bit mask)
+// k_res = sqrt7^res / RES0_U_GNOMONIC; `faces` = the faces to consider (bit mask);
+// lat, lon in radians (to_radians_fast is fine: a 1-ulp input change is far inside
+// the tie band)
 MGPU_HD FastHex fast_hex2d(double lat, double lon, int res, double k_res, uint32_t faces) {
   FastHex o;
+  // the sine table spans |angle| <= 202/64 rad: anything else takes the H3 route
+  const bool in_table = fabs(lat) <= 3.14 && fabs(lon) <= 3.14;
+  if (!in_table) lat = lon = 0.0;
   double slat, clat, slon, clon;
   sincos_tab(lat, &slat, &clat);
   sincos_tab(lon, &slon, &clon);
@@ -386,7 +492,7 @@ MGPU_HD FastHex fast_hex2d(double lat, double lon, int res, double k_res, uint32
     double dx = H3T_FACE_CENTER_POINT[f][0] - vx;
     double dy = H3T_FACE_CENTER_POINT[f][1] - vy;
     double dz = H3T_FACE_CENTER_POINT[f][2] - vz;
-    double s = dx * dx + dy * dy + dz * dz;
+    double s = fma_(dx, dx, fma_(dy, dy, dz * dz));
     if (s < best) {
       second = best;
       best = s;
@@ -397,14 +503,20 @@ MGPU_HD FastHex fast_hex2d(double lat, double lon, int res, double k_res, uint32
   }
   o.face = f0;
   const double(*F)[3] = H3T_FACE_FRAME[f0][res & 1];
-  double dc = vx * F[2][0] + vy * F[2][1] + vz * F[2][2];
-  double da = vx * F[0][0] + vy * F[0][1] + vz * F[0][2];
-  double db = vx * F[1][0] + vy * F[1][1] + vz * F[1][2];
-  double q = k_res / dc;
+  double dc = fma_(vx, F[2][0], fma_(vy, F[2][1], vz * F[2][2]));
+  double da = fma_(vx, F[0][0], fma_(vy, F[0][1], vz * F[0][2]));
+  double db = fma_(vx, F[1][0], fma_(vy, F[1][1], vz * F[1][2]));
+  double q = k_res * recip(dc);
   double x = da * q, y = db * q;
   double margin;
-  o.ijk = hex2d_to_ijk(x, y, &margin);
-  o.tie = (second - best < 1e-12) || !(dc > 0.5) || (margin < tie_band(x, y, 1.0 - dc * dc));
+  o.ijk = hex2d_to_ijk_fast(x, y, &margin);
+  // margin < tie_band(x, y, sin2r) without the division: with sin2r = 1 - dc^2 > 0,
+  //   margin < kTieRel * (1 + 1/sin2r) * scale  <=>  margin * sin2r < kTieRel * (sin2r + 1) * scale
+  double scale = fabs(x) > fabs(y) ? fabs(x) : fabs(y);
+  if (scale < 1.0) scale = 1.0;
+  double sin2r = fma_(-dc, dc, 1.0);
+  o.tie = !in_table || (second - best < 1e-12) || !(dc > 0.5) || !(sin2r > 1e-300) ||
+          (margin * sin2r < kTieRel * (sin2r + 1.0) * scale);
   return o;
 }
 

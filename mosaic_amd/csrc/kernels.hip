@@ -28,7 +28,6 @@ namespace mgpu {
 constexpr int kBlock = 256;
 constexpr int kItems = 4;
 constexpr int kTile = kBlock * kItems;
-constexpr int kKeep = 2;  // matches per point kept in registers between the passes
 
 constexpr uint64_t kFlagAgg = 1ULL << 62;
 constexpr uint64_t kFlagPrefix = 2ULL << 62;
@@ -42,61 +41,17 @@ constexpr uint32_t kAllFaces = (1u << 20) - 1;
 // H3IndexSystem.pointToIndex: fast closed-form projection, H3 route on near-ties
 __device__ __forceinline__ uint64_t h3_cell(double lon_deg, double lat_deg, int res, double k_res, bool* ok,
                                            bool* tie) {
-  const double lat = h3::to_radians(lat_deg), lon = h3::to_radians(lon_deg);
   *tie = false;
-  if (!isfinite(lat) || !isfinite(lon)) {
+  if (!isfinite(lat_deg) || !isfinite(lon_deg)) {
     *ok = false;
     return 0;
   }
   *ok = true;
-  h3::FastHex f = h3::fast_hex2d(lat, lon, res, k_res, kAllFaces);
+  h3::FastHex f = h3::fast_hex2d(h3::to_radians_fast(lat_deg), h3::to_radians_fast(lon_deg), res, k_res, kAllFaces);
   if (f.tie) {
-    h3::route_face_ijk(lat, lon, res, &f.face, &f.ijk, tie);
+    h3::route_face_ijk(h3::to_radians(lat_deg), h3::to_radians(lon_deg), res, &f.face, &f.ijk, tie);
   }
   return h3::face_ijk_to_h3(f.face, f.ijk, res);
-}
-
-// probe the hash with `key`; returns the chip range [first, first + count)
-__device__ __forceinline__ uint2 probe(const ChipTableView& t, uint64_t key) {
-  uint32_t h = cell_hash(key) & t.hash_mask;
-  for (uint32_t k = 0; k <= t.max_probe; k++) {
-    HashSlot s = t.slots[h];
-    if (s.count == 0) break;
-    if (s.cell == key) return make_uint2(s.first, s.count);
-    h = (h + 1) & t.hash_mask;
-  }
-  return make_uint2(0, 0);
-}
-
-// The chips of the point's cell.  *ok = false for invalid coordinates (NaN), *tie
-// when the H3 route itself sits in its near-tie band (reported).
-template <int IS>
-__device__ __forceinline__ uint2 chips_of(const ChipTableView& t, double px, double py, int res, bool res_match,
-                                          bool* ok, bool* tie) {
-  *tie = false;
-  if (IS == MGPU_BNG) {
-    int64_t c;
-    *ok = bng::point_to_cell(px, py, res, &c);
-    if (!*ok || !res_match) return make_uint2(0, 0);
-    return probe(t, (uint64_t)c);
-  }
-  const double lat = h3::to_radians(py), lon = h3::to_radians(px);
-  if (!isfinite(lat) || !isfinite(lon)) {
-    *ok = false;
-    return make_uint2(0, 0);
-  }
-  *ok = true;
-  if (!res_match) return make_uint2(0, 0);
-  if (t.probe_mode == kProbeLattice) {
-    // outside the chip cells' bounding box no cell can match
-    if (!(px >= t.bbox[0] && px <= t.bbox[2] && py >= t.bbox[1] && py <= t.bbox[3])) return make_uint2(0, 0);
-    h3::FastHex f = h3::fast_hex2d(lat, lon, res, t.k_res, t.face_mask);
-    if (f.tie) h3::route_face_ijk(lat, lon, res, &f.face, &f.ijk, tie);
-    return probe(t, h3::lattice_key(f.face, f.ijk));
-  }
-  h3::FastHex f = h3::fast_hex2d(lat, lon, res, t.k_res > 0 ? t.k_res : h3::k_of_res(res), kAllFaces);
-  if (f.tie) h3::route_face_ijk(lat, lon, res, &f.face, &f.ijk, tie);
-  return probe(t, h3::face_ijk_to_h3(f.face, f.ijk, res));
 }
 
 __device__ __forceinline__ void count_wave(unsigned long long* ctr, bool pred) {
@@ -142,210 +97,165 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
   return v;
 }
 
-// One workgroup = one tile of kTile consecutive points, in six phases:
+// One workgroup = one tile of kTile consecutive points, in three phases:
 //  1  lane l evaluates points l, l+256, l+512, l+768 (coalesced 8-byte loads): cell
-//     -> chip range; every border chip of the point is appended to the tile's
-//     candidate list (LDS);
-//  2  per candidate: chip envelope / rectangle shortcuts, else one "ring entry" per
-//     ring of the chip (edge count, or skipped when the ring envelope misses);
-//  3  exclusive scan of the ring entries' edge counts;
-//  4  edge-parallel ray crossing: every lane tests one (candidate, edge) pair per
-//     step -- no divergence on ring length, consecutive lanes read consecutive
-//     vertices -- and ORs / XORs its result bits into the ring entry (LDS atomics);
-//  5  per candidate: PointLocator over its rings' bits -> contains?;
-//  6  lane l owns points 4l .. 4l+3 (input order): count matches (chip order ==
-//     polygon-id order), block scan + decoupled look-back over tiles, write pairs.
-// Tiles whose candidates or ring entries overflow the LDS lists evaluate the
-// overflowing points with the sequential PointLocator (pip::chip_locate).
-constexpr int kCandCap = 1536;
-constexpr int kRingCap = 1536;
-constexpr uint16_t kNoCand = 0xFFFF;
-constexpr uint32_t kNoChip = 0xFFFFFFFFu;
-enum CandRes : uint8_t { kResExterior = 0, kResInterior = 1, kResPending = 2, kResSequential = 3 };
+//     -> one hash probe -> the cell's chip range and core-chip mask.  Core chips are
+//     matches at once; every border chip becomes a candidate (chip, point, slot j)
+//     in the tile's LDS list (a full list: the lane evaluates it on the spot);
+//  2  lane per candidate: st_contains by the chip's strip index (pip_core.h
+//     chip_contains_strips: envelope, rectangle shortcut, ray crossing over the
+//     edges of the point's y-strip only); a hit sets bit j of the point's mask;
+//  3  lane l owns points 4l .. 4l+3 (input order): matches = mask bits (chip order
+//     == polygon-id order), block scan + decoupled look-back over tiles for the
+//     output offset, pairs staged in LDS and written as contiguous runs.
+// Chips past the 32nd of one cell (never seen in practice) are evaluated in phase 3.
+constexpr int kCandCap = 1024;
+constexpr int kOutCap = 2048;
+constexpr int kMaskBits = 32;
 
-__device__ __forceinline__ int64_t tile_point(const JoinArgs& a, int64_t base, int li) { return base + li; }
+// chips of a cell: first, count, core mask (bits < 16)
+struct Range {
+  uint32_t first;
+  uint32_t count;
+  uint32_t core;
+};
+
+__device__ __forceinline__ Range probe_range(const ChipTableView& t, uint64_t key) {
+  uint32_t h = cell_hash(key) & t.hash_mask;
+  for (uint32_t k = 0; k <= t.max_probe; k++) {
+    const HashSlot s = t.slots[h];
+    if (s.count == 0) break;
+    if (s.cell == key) return Range{s.first, s.count, s.core_mask};
+    h = (h + 1) & t.hash_mask;
+  }
+  return Range{0, 0, 0};
+}
+
+template <int IS>
+__device__ __forceinline__ Range chip_range(const ChipTableView& t, double px, double py, int res, bool res_match,
+                                            bool* ok, bool* tie) {
+  *tie = false;
+  if (IS == MGPU_BNG) {
+    int64_t c;
+    *ok = bng::point_to_cell(px, py, res, &c);
+    if (!*ok || !res_match) return Range{0, 0, 0};
+    return probe_range(t, (uint64_t)c);
+  }
+  *ok = isfinite(px) && isfinite(py);
+  if (!*ok || !res_match) return Range{0, 0, 0};
+  const double lat = h3::to_radians_fast(py), lon = h3::to_radians_fast(px);
+  if (t.probe_mode == kProbeLattice) {
+    // outside the chip cells' bounding box no cell can match
+    if (!(px >= t.bbox[0] && px <= t.bbox[2] && py >= t.bbox[1] && py <= t.bbox[3])) return Range{0, 0, 0};
+    h3::FastHex f = h3::fast_hex2d(lat, lon, res, t.k_res, t.face_mask);
+    if (f.tie) h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, tie);
+    return probe_range(t, h3::lattice_key(f.face, f.ijk));
+  }
+  h3::FastHex f = h3::fast_hex2d(lat, lon, res, t.k_res > 0 ? t.k_res : h3::k_of_res(res), kAllFaces);
+  if (f.tie) h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, tie);
+  return probe_range(t, h3::face_ijk_to_h3(f.face, f.ijk, res));
+}
+
+__device__ __forceinline__ bool chip_is_core(const ChipTableView& t, const Range& r, uint32_t j) {
+  return j < 16 ? ((r.core >> j) & 1) : (t.chip_flags[r.first + j] & kChipCore) != 0;
+}
 
 template <int IS>
 __global__ __launch_bounds__(kBlock) void pip_join_kernel(JoinArgs a) {
-  __shared__ uint32_t s_tile, s_ncand, s_nring, s_nedge;
+  __shared__ uint32_t s_tile, s_ncand;
   __shared__ uint32_t s_wave_tot[kBlock / 64];
   __shared__ unsigned long long s_prefix;
-  __shared__ uint2 s_range[kTile];               // chip range of each point
-  __shared__ uint16_t s_pfirst[kTile];           // first candidate of each point (kNoCand: sequential)
-  __shared__ uint32_t s_cand_chip[kCandCap];
-  __shared__ uint16_t s_cand_pt[kCandCap];
-  __shared__ uint16_t s_cand_ring[kCandCap];     // first ring entry of the candidate
-  __shared__ uint8_t s_cand_res[kCandCap];
-  __shared__ uint32_t s_ring_id[kRingCap];       // global ring index
-  __shared__ uint32_t s_ring_pref[kRingCap + 1]; // edge counts, then their exclusive scan
-  __shared__ uint32_t s_ring_bits[kRingCap];
-  __shared__ uint16_t s_ring_cand[kRingCap];
+  __shared__ uint32_t s_first[kTile];   // first chip of the point's cell
+  __shared__ uint32_t s_mask[kTile];    // bit j: chip first + j matches (j < 32)
+  __shared__ uint16_t s_cnt[kTile];     // chips of the point's cell (0: none)
+  // phases 1-2: candidate list; phase 3: output staging (same bytes)
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[kOutCap * 6];
+  uint32_t* s_cand_chip = (uint32_t*)s_buf;                       // [kCandCap]
+  uint16_t* s_cand_pj = (uint16_t*)(s_buf + kCandCap * 4);        // [kCandCap] li | j << 10
+  int32_t* s_out_poly = (int32_t*)s_buf;                          // [kOutCap]
+  uint16_t* s_out_li = (uint16_t*)(s_buf + kOutCap * 4);          // [kOutCap]
 
   if (threadIdx.x == 0) {
     s_tile = atomicAdd(a.tile_ticket, 1u);
     s_ncand = 0;
-    s_nring = 0;
   }
   __syncthreads();
   const uint32_t tile = s_tile;
   const ChipTableView& t = a.chips;
   const int64_t base = (int64_t)tile * kTile;
   const bool res_match = a.res_match;
+  const bool do_pip = a.ablate != 1;
 
-  // ---- phase 1: cells and candidates
+  // ---- phase 1: cells, core matches, candidates
   bool any_tie = false, any_bad = false;
 #pragma unroll 1
   for (int k = 0; k < kItems; k++) {
     const int li = k * kBlock + threadIdx.x;
     const int64_t p = base + li;
-    uint2 r = make_uint2(0, 0);
-    uint16_t first = 0;
+    Range r{0, 0, 0};
+    uint32_t mask = 0;
     if (p < a.n) {
       bool ok, tie;
-      r = chips_of<IS>(t, a.x[p], a.y[p], a.res, res_match, &ok, &tie);
-      if (a.ablate == 2) r = make_uint2(0, 0);
+      const double px = a.x[p], py = a.y[p];
+      r = chip_range<IS>(t, px, py, a.res, res_match, &ok, &tie);
+      if (a.ablate == 2) r.count = 0;
       any_bad |= !ok;
       any_tie |= tie;
-      uint32_t nb = 0;
-      for (uint32_t c = r.x; c < r.x + r.y; c++) nb += (t.chip_flags[c] & kChipCore) ? 0 : 1;
-      if (nb) {
-        uint32_t c0 = atomicAdd(&s_ncand, nb);
-        if (c0 + nb <= (uint32_t)kCandCap) {
-          first = (uint16_t)c0;
-          uint32_t j = c0;
-          for (uint32_t c = r.x; c < r.x + r.y; c++) {
-            if (t.chip_flags[c] & kChipCore) continue;
-            s_cand_chip[j] = c;
-            s_cand_pt[j] = (uint16_t)li;
-            j++;
+      const uint32_t nj = r.count < (uint32_t)kMaskBits ? r.count : (uint32_t)kMaskBits;
+      const uint32_t lowm = nj >= 32 ? 0xFFFFFFFFu : ((1u << nj) - 1);
+      uint32_t border = ~r.core & lowm;
+      for (uint32_t j = 16; j < nj; j++)
+        if (t.chip_flags[r.first + j] & kChipCore) border &= ~(1u << j);
+      mask = lowm & ~border;
+      if (border && do_pip) {
+        const uint32_t nb = __popc(border);
+        const uint32_t c0 = atomicAdd(&s_ncand, nb);
+        uint32_t j0 = c0;
+        for (uint32_t b = border; b; b &= b - 1) {
+          const uint32_t j = __builtin_ctz(b);
+          if (j0 < (uint32_t)kCandCap) {
+            s_cand_chip[j0] = r.first + j;
+            s_cand_pj[j0] = (uint16_t)(li | (j << 10));
+          } else if (pip::chip_contains_strips(t, r.first + j, px, py)) {
+            mask |= 1u << j;  // list full: evaluate here
           }
-        } else {
-          first = kNoCand;
-          // the part of the reservation inside the list must still be defined
-          for (uint32_t j = c0; j < c0 + nb && j < (uint32_t)kCandCap; j++) s_cand_chip[j] = kNoChip;
+          j0++;
         }
       }
     }
-    s_range[li] = r;
-    s_pfirst[li] = first;
+    s_first[li] = r.first;
+    s_cnt[li] = (uint16_t)(r.count > 0xFFFF ? 0xFFFF : r.count);
+    s_mask[li] = mask;
   }
   count_wave(&a.counters[1], any_tie);
   count_wave(&a.counters[2], any_bad);
   __syncthreads();
   const uint32_t ncand = s_ncand < (uint32_t)kCandCap ? s_ncand : (uint32_t)kCandCap;
-  if (threadIdx.x == 0 && ncand) atomicAdd(&a.counters[3], (unsigned long long)ncand);
+  if (threadIdx.x == 0 && s_ncand) atomicAdd(&a.counters[3], (unsigned long long)s_ncand);
 
-  // ---- phase 2: per candidate, shortcuts or ring entries
+  // ---- phase 2: lane per candidate
   for (uint32_t c = threadIdx.x; c < ncand; c += kBlock) {
     const uint32_t ch = s_cand_chip[c];
-    if (ch == kNoChip) continue;  // slot of an overflowed reservation (never read back)
-    const int64_t p = base + s_cand_pt[c];
-    const double px = a.x[p], py = a.y[p];
-    const uint8_t fl = t.chip_flags[ch];
-    uint8_t res = kResExterior;
-    if (a.ablate == 1 || (fl & (kChipEmpty | kChipNoGeom))) {
-      res = kResExterior;
-    } else if (!pip::env_has(t.chip_env + 4 * ch, px, py)) {
-      res = kResExterior;
-    } else if (fl & kChipRect) {
-      const double* e = t.chip_env + 4 * ch;
-      res = (px == e[0] || px == e[2] || py == e[1] || py == e[3]) ? kResExterior : kResInterior;
-    } else {
-      const uint32_t rb = t.part_ring[t.chip_part[ch]], re = t.part_ring[t.chip_part[ch + 1]];
-      const uint32_t nr = re - rb;
-      const uint32_t r0 = atomicAdd(&s_nring, nr);
-      if (r0 + nr <= (uint32_t)kRingCap) {
-        res = kResPending;
-        s_cand_ring[c] = (uint16_t)r0;
-        for (uint32_t q = 0; q < nr; q++) {
-          const uint32_t ring = rb + q;
-          const uint32_t vb = t.ring_vtx[ring], ve = t.ring_vtx[ring + 1];
-          const bool use = ve - vb >= 2 && pip::env_has(t.ring_env + 4 * ring, px, py);
-          s_ring_id[r0 + q] = ring;
-          s_ring_pref[r0 + q] = use ? ve - vb - 1 : 0;
-          s_ring_bits[r0 + q] = use ? 0u : (uint32_t)pip::kRingSkipped;
-          s_ring_cand[r0 + q] = (uint16_t)c;
-        }
-      } else {
-        res = kResSequential;
-        for (uint32_t q = r0; q < r0 + nr && q < (uint32_t)kRingCap; q++) {
-          s_ring_id[q] = rb;
-          s_ring_pref[q] = 0;
-          s_ring_bits[q] = (uint32_t)pip::kRingSkipped;
-          s_ring_cand[q] = (uint16_t)c;
-        }
-      }
-    }
-    s_cand_res[c] = res;
+    const uint32_t pj = s_cand_pj[c];
+    const int li = pj & 1023;
+    const int64_t p = base + li;
+    if (pip::chip_contains_strips(t, ch, a.x[p], a.y[p])) atomicOr(&s_mask[li], 1u << (pj >> 10));
   }
   __syncthreads();
 
-  // ---- phase 3: exclusive scan of the ring entries' edge counts (one wave)
-  const uint32_t nring = s_nring < (uint32_t)kRingCap ? s_nring : (uint32_t)kRingCap;
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < nring; b0 += 64) {
-      const uint32_t i = b0 + lane;
-      const uint32_t v = i < nring ? s_ring_pref[i] : 0;
-      const uint32_t inc = wave_incl_scan(v);
-      if (i < nring) s_ring_pref[i] = carry + inc - v;
-      carry += __shfl(inc, 63, 64);
-    }
-    if (lane == 0) {
-      s_ring_pref[nring] = carry;
-      s_nedge = carry;
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 4: edge-parallel ray crossing
-  const uint32_t nedge = s_nedge;
-  for (uint32_t f = threadIdx.x; f < nedge; f += kBlock) {
-    uint32_t lo = 0, hi = nring;  // last entry with pref <= f
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (s_ring_pref[mid] <= f) lo = mid; else hi = mid;
-    }
-    const uint32_t ring = s_ring_id[lo];
-    const uint32_t i = t.ring_vtx[ring] + 1 + (f - s_ring_pref[lo]);
-    const int64_t p = base + s_cand_pt[s_ring_cand[lo]];
-    const double px = a.x[p], py = a.y[p];
-    const double* v = t.vtx + 2 * (size_t)i;
-    const int bits = pip::count_segment(v[0], v[1], v[-2], v[-1], px, py);
-    if (bits & pip::kRingOnSegment) atomicOr(&s_ring_bits[lo], (uint32_t)pip::kRingOnSegment);
-    if (bits & 2) atomicXor(&s_ring_bits[lo], (uint32_t)pip::kRingParity);
-  }
-  __syncthreads();
-
-  // ---- phase 5: PointLocator per pending candidate
-  for (uint32_t c = threadIdx.x; c < ncand; c += kBlock) {
-    if (s_cand_res[c] != kResPending) continue;
-    const int loc = pip::chip_locate_from_rings(t, s_cand_chip[c], &s_ring_bits[s_cand_ring[c]]);
-    s_cand_res[c] = loc == pip::kInterior ? kResInterior : kResExterior;
-  }
-  __syncthreads();
-
-  // ---- phase 6: lane l owns points 4l .. 4l+3 (input order)
+  // ---- phase 3: lane l owns points 4l .. 4l+3 (input order)
   const int l0 = threadIdx.x * kItems;
   uint32_t mine = 0;
-#pragma unroll 1
+#pragma unroll
   for (int k = 0; k < kItems; k++) {
     const int li = l0 + k;
-    const uint2 r = s_range[li];
-    if (!r.y) continue;
-    uint32_t cj = s_pfirst[li];
-    const int64_t p = base + li;
-    for (uint32_t q = r.x; q < r.x + r.y; q++) {
-      bool m;
-      if (t.chip_flags[q] & kChipCore) {
-        m = true;
-      } else {
-        const uint8_t res = cj != kNoCand ? s_cand_res[cj++] : kResSequential;
-        m = res == kResInterior ||
-            (res == kResSequential && a.ablate != 1 && pip::chip_locate(t, q, a.x[p], a.y[p]) == pip::kInterior);
-      }
-      mine += m ? 1 : 0;
+    mine += __popc(s_mask[li]);
+    const uint32_t cnt = s_cnt[li];
+    if (cnt > (uint32_t)kMaskBits) {  // chips past the 32nd of the cell
+      const int64_t p = base + li;
+      const Range r{s_first[li], cnt, 0};
+      for (uint32_t j = kMaskBits; j < cnt; j++)
+        mine += (chip_is_core(t, r, j) || (do_pip && pip::chip_contains_strips(t, r.first + j, a.x[p], a.y[p]))) ? 1 : 0;
     }
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -402,33 +312,51 @@ __global__ __launch_bounds__(kBlock) void pip_join_kernel(JoinArgs a) {
     }
   }
   __syncthreads();
+  const int64_t prefix = (int64_t)s_prefix;
+  const bool staged = agg <= (uint32_t)kOutCap;
 
-  int64_t pos = (int64_t)s_prefix + excl;
+  // this lane's pairs: staged in LDS (then written as contiguous runs) or direct
+  uint32_t pos = excl;
 #pragma unroll 1
   for (int k = 0; k < kItems; k++) {
     const int li = l0 + k;
-    const uint2 r = s_range[li];
-    if (!r.y) continue;
-    uint32_t cj = s_pfirst[li];
+    const uint32_t cnt = s_cnt[li];
+    if (!cnt) continue;
+    const uint32_t first = s_first[li];
     const int64_t p = base + li;
-    const int64_t pid = a.point_id ? a.point_id[p] : a.id_base + p;
-    for (uint32_t q = r.x; q < r.x + r.y; q++) {
-      bool m;
-      if (t.chip_flags[q] & kChipCore) {
-        m = true;
+    uint32_t m = s_mask[li];
+    const uint32_t nj = cnt < (uint32_t)kMaskBits ? cnt : (uint32_t)kMaskBits;
+    for (uint32_t j = 0; j < cnt; j++) {
+      bool hit;
+      if (j < nj) {
+        hit = (m >> j) & 1;
       } else {
-        const uint8_t res = cj != kNoCand ? s_cand_res[cj++] : kResSequential;
-        m = res == kResInterior ||
-            (res == kResSequential && a.ablate != 1 && pip::chip_locate(t, q, a.x[p], a.y[p]) == pip::kInterior);
+        const Range r{first, cnt, 0};
+        hit = chip_is_core(t, r, j) || (do_pip && pip::chip_contains_strips(t, first + j, a.x[p], a.y[p]));
       }
-      if (m) {
-        if (pos < a.capacity) {
-          a.out_point[pos] = pid;
-          a.out_poly[pos] = t.chip_poly[q];
+      if (!hit) continue;
+      const int32_t poly = t.chip_poly[first + j];
+      if (staged) {
+        s_out_poly[pos] = poly;
+        s_out_li[pos] = (uint16_t)li;
+      } else {
+        const int64_t q = prefix + pos;
+        if (q < a.capacity) {
+          a.out_point[q] = a.point_id ? a.point_id[p] : a.id_base + p;
+          a.out_poly[q] = poly;
         }
-        pos++;
       }
+      pos++;
     }
+  }
+  if (!staged) return;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < agg; i += kBlock) {
+    const int64_t q = prefix + i;
+    if (q >= a.capacity) break;
+    const int64_t p = base + s_out_li[i];
+    a.out_point[q] = a.point_id ? a.point_id[p] : a.id_base + p;
+    a.out_poly[q] = s_out_poly[i];
   }
 }
 

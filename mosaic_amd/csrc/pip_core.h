@@ -230,5 +230,69 @@ MGPU_HDI int chip_locate(const ChipTableView& t, uint32_t c, double px, double p
   return kExterior;
 }
 
+// Geometry.contains(point) for sorted chip `c` by the strip index (chip_table.h): the
+// same decision as chip_locate() -- envelope, rectangle shortcut, PointLocator over
+// the rings -- with each ring's RayCrossingCounter run over the edges of the
+// point's strip only.  Chips flagged kChipNoStrips go to chip_locate().
+MGPU_HDI bool chip_contains_strips(const ChipTableView& t, uint32_t c, double px, double py) {
+  const uint8_t fl = t.chip_flags[c];
+  if (fl & (kChipEmpty | kChipNoGeom)) return false;
+  const double* env = t.chip_env + 4 * c;
+  if (!env_has(env, px, py)) return false;
+  if (fl & kChipRect) return !(px == env[0] || px == env[2] || py == env[1] || py == env[3]);
+  if (fl & kChipNoStrips) return chip_locate(t, c, px, py) == kInterior;
+  const uint32_t sb = t.chip_strip[c];
+  const int S = (int)(t.chip_strip[c + 1] - sb);
+  const int s = strip_of(py, t.chip_sy[2 * c], t.chip_sy[2 * c + 1], S);
+  const uint32_t eb = t.strip_edge[sb + s], ee = t.strip_edge[sb + s + 1];
+  uint32_t bnd = 0, par = 0;
+  for (uint32_t e = eb; e < ee; e++) {
+    const double* E = t.edges + 4 * (size_t)e;
+    const int bits = count_segment(E[0], E[1], E[2], E[3], px, py);
+    if (bits) {
+      const uint32_t rb = 1u << t.edge_ring[e];
+      if (bits & kRingOnSegment) bnd |= rb;
+      if (bits & 2) par ^= rb;
+    }
+  }
+  const uint32_t pb = t.chip_part[c], pe = t.chip_part[c + 1];
+  const uint32_t r0 = t.part_ring[pb];
+  if (pe - pb == 1 && t.part_ring[pb + 1] - r0 == 1 && !(fl & kChipMulti)) {
+    // one polygon, one ring (its envelope is the chip's): RayCrossingCounter's verdict
+    return !(bnd & 1) && (par & 1);
+  }
+  bool is_in = false;
+  int n_bnd = 0, single = -1;
+  for (uint32_t p = pb; p < pe; p++) {
+    const uint32_t rb = t.part_ring[p], re = t.part_ring[p + 1];
+    int loc = kInterior;
+    if (re == rb) loc = kExterior;
+    for (uint32_t r = rb; r < re; r++) {
+      const uint32_t vb = t.ring_vtx[r], ve = t.ring_vtx[r + 1];
+      int l;
+      if (r == rb && ve == vb) {
+        l = kExterior;  // empty shell = empty polygon
+      } else if (!env_has(t.ring_env + 4 * r, px, py)) {
+        l = kExterior;
+      } else {
+        const uint32_t m = 1u << (r - r0);
+        l = (bnd & m) ? kBoundary : ((par & m) ? kInterior : kExterior);
+      }
+      if (r == rb) {
+        if (l != kInterior) { loc = l; break; }
+      } else {
+        if (l == kInterior) { loc = kExterior; break; }
+        if (l == kBoundary) { loc = kBoundary; break; }
+      }
+    }
+    if (single < 0) single = loc;
+    if (loc == kInterior) is_in = true;
+    if (loc == kBoundary) n_bnd++;
+  }
+  if (!(fl & kChipMulti)) return single == kInterior;
+  if (n_bnd & 1) return false;
+  return n_bnd > 0 || is_in;
+}
+
 }  // namespace pip
 }  // namespace mgpu
