@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmosaic_gpu.so")
+# MOSAIC_AMD_LIB: profiling builds of the same sources (tools/variants.sh); default in-tree
+LIB_PATH = os.environ.get("MOSAIC_AMD_LIB") or os.path.join(_HERE, "libmosaic_gpu.so")
 
 MGPU_OK = 0
 MGPU_E_INVALID_ARG = -1

@@ -48,7 +48,7 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // offsets, so a byte copy of the blob on another GPU (RCCL broadcast) is a
 // complete chip table there.
 constexpr uint64_t kBlobMagic = 0x4d4f534149434850ULL;  // "MOSAICHP"
-constexpr int kBlobArrays = 16;
+constexpr int kBlobArrays = 17;
 constexpr uint32_t kBlobVersion = 3;
 struct BlobHeader {
   uint64_t magic;
@@ -85,6 +85,7 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.strip_edge = (const uint32_t*)(base + h.off[13]);
   v.edges = (const double*)(base + h.off[14]);
   v.edge_ring = (const uint8_t*)(base + h.off[15]);
+  v.chip_hdr = (const mgpu::ChipHdr*)(base + h.off[16]);
   v.probe_mode = h.probe_mode;
   v.res = h.res;
   v.face_mask = h.face_mask;
@@ -306,15 +307,34 @@ struct mgpu_chips {
 
 namespace {
 
-// Workspace layout: [counters 8 x u64][ticket u32 + pad to 64 B][tile status n_tiles x u64]
+// Workspace layout (each region 256-byte aligned):
+//   [counters 8 x u64] [tile_count u32 x T] [tile_where u64 x T] [tile_off u64 x T]
+//   [records u64 x (T * tile points + pool)]
+// T = tiles of the largest point batch reserved; pool = overflow records (tiles with
+// more pairs than points), at most the output capacity.
 constexpr size_t kWsCounters = 64;
-constexpr size_t kWsTicket = 64;
 
-int32_t ensure_ws(mgpu_ctx* ctx, int64_t n_tiles) {
-  size_t need = kWsCounters + kWsTicket + align_up((size_t)std::max<int64_t>(n_tiles, 1) * 8, 256);
+struct WsLayout {
+  size_t count, where, off, recs, total;
+};
+
+WsLayout ws_layout(int64_t n_tiles, int64_t pool) {
+  WsLayout L;
+  size_t T = (size_t)std::max<int64_t>(n_tiles, 1);
+  L.count = kWsCounters;
+  L.where = align_up(L.count + T * 4, 256);
+  L.off = align_up(L.where + T * 8, 256);
+  L.recs = align_up(L.off + T * 8, 256);
+  L.total = align_up(L.recs + (T * (size_t)mgpu::join_tile_points() + (size_t)std::max<int64_t>(pool, 0)) * 8, 256);
+  return L;
+}
+
+int32_t ensure_ws(mgpu_ctx* ctx, int64_t n_tiles, int64_t pool = 0) {
+  size_t need = ws_layout(n_tiles, pool).total;
   if (need <= ctx->ws_bytes) return MGPU_OK;
   if (ctx->ws) HIP_TRY(hipFree(ctx->ws));
   ctx->ws = nullptr;
+  ctx->ws_bytes = 0;
   HIP_TRY(hipMalloc(&ctx->ws, need));
   ctx->ws_bytes = need;
   return MGPU_OK;
@@ -356,7 +376,7 @@ int32_t mgpu_ctx_create(int32_t device_id, mgpu_ctx** out) {
   c->device = device_id;
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
-  int32_t st = ensure_ws(c, 1 << 16);
+  int32_t st = ensure_ws(c, 1);
   if (st) {
     delete c;
     return st;
@@ -378,7 +398,7 @@ int32_t mgpu_ctx_destroy(mgpu_ctx* ctx) {
 int32_t mgpu_ctx_reserve(mgpu_ctx* ctx, int64_t max_points) {
   if (!ctx) return fail(MGPU_E_INVALID_ARG, "ctx is NULL");
   if (int32_t st = set_device(ctx->device)) return st;
-  return ensure_ws(ctx, mgpu::join_tiles(max_points));
+  return ensure_ws(ctx, mgpu::join_tiles(max_points), max_points);
 }
 
 int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t is, int32_t res, const double* x, const double* y, int64_t n,
@@ -508,6 +528,21 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
   }
   Strips strips;
   build_strips(n_chips, cflags, cpart, cenv, geo, strips);
+  std::vector<mgpu::ChipHdr> chdr(n_chips);
+  for (int64_t c = 0; c < n_chips; c++) {
+    mgpu::ChipHdr& h = chdr[c];
+    memset(&h, 0, sizeof h);
+    for (int k = 0; k < 4; k++) h.env[k] = cenv[4 * c + k];
+    h.y0 = strips.chip_sy[2 * c];
+    h.inv_h = strips.chip_sy[2 * c + 1];
+    h.strip_base = strips.chip_strip[c];
+    h.n_strips = (uint16_t)(strips.chip_strip[c + 1] - strips.chip_strip[c]);
+    h.flags = cflags[c];
+    const uint32_t pb = cpart[c], pe = cpart[c + 1];
+    h.single_ring = (pe - pb == 1 && geo.part_ring[pb + 1] - geo.part_ring[pb] == 1 &&
+                     !(cflags[c] & mgpu::kChipMulti)) ? 1 : 0;
+    h.poly = cpoly[c];
+  }
   // H3: probe by lattice key when possible (chip_table.h)
   int32_t probe_mode = mgpu::kProbeCellId, lres = -1;
   uint32_t face_mask = (1u << 20) - 1;
@@ -566,6 +601,7 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
       {strips.strip_edge.data(), strips.strip_edge.size() * 4, 0},
       {strips.edges.data(), strips.edges.size() * 8, 0},
       {strips.edge_ring.data(), strips.edge_ring.size(), 0},
+      {chdr.data(), chdr.size() * sizeof(mgpu::ChipHdr), 0},
   };
   size_t total = kBlobHeaderBytes;
   BlobHeader hdr{};
@@ -673,31 +709,43 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   if (capacity < 0 || (capacity > 0 && (!out_point || !out_poly))) return fail(MGPU_E_INVALID_ARG, "bad output arrays");
   if (int32_t st = set_device(ctx->device)) return st;
   int64_t tiles = mgpu::join_tiles(n);
-  if (int32_t st = ensure_ws(ctx, tiles)) return st;
+  // pool: the records of tiles with more pairs than points (bounded by the capacity;
+  // a total beyond it is reported as MGPU_E_CAPACITY either way)
+  const int64_t pool = capacity;
+  if (int32_t st = ensure_ws(ctx, tiles, pool)) return st;
   auto* base = (uint8_t*)ctx->ws;
+  const WsLayout L = ws_layout(tiles, pool);
   mgpu::JoinArgs a;
   a.x = x;
   a.y = y;
-  a.point_id = point_id;
-  a.id_base = id_base;
   a.n = n;
   a.n_tiles = tiles;
   a.res = res;
   a.res_match = (is == MGPU_BNG || chips->view.res < 0 || chips->view.res == res) ? 1 : 0;
   a.chips = chips->view;
-  a.capacity = capacity;
-  a.out_point = out_point;
-  a.out_poly = out_poly;
   a.counters = (unsigned long long*)base;
+  a.pool_used = a.counters + 5;
+  a.pool_cap = pool;
+  a.tile_count = (uint32_t*)(base + L.count);
+  a.tile_where = (uint64_t*)(base + L.where);
+  a.recs = (uint64_t*)(base + L.recs);
   {
     const char* ab = getenv("MGPU_ABLATE");  // profiling switch, never set in production runs
     a.ablate = ab ? atoi(ab) : 0;
   }
-  a.tile_ticket = (uint32_t*)(base + kWsCounters);
-  a.tile_status = (uint64_t*)(base + kWsCounters + kWsTicket);
-  HIP_TRY(hipMemsetAsync(base, 0, kWsCounters + kWsTicket + align_up((size_t)std::max<int64_t>(tiles, 1) * 8, 256), s));
+  mgpu::EmitArgs e;
+  e.tile_count = a.tile_count;
+  e.tile_off = (uint64_t*)(base + L.off);
+  e.tile_where = a.tile_where;
+  e.recs = a.recs;
+  e.point_id = point_id;
+  e.id_base = id_base;
+  e.capacity = capacity;
+  e.out_point = out_point;
+  e.out_poly = out_poly;
+  HIP_TRY(hipMemsetAsync(base, 0, kWsCounters, s));
   if (timed) HIP_TRY(hipEventRecord(ctx->ev0, s));
-  HIP_TRY(mgpu::launch_join(is, a, s));
+  HIP_TRY(mgpu::launch_join(is, a, e, s));
   if (timed) HIP_TRY(hipEventRecord(ctx->ev1, s));
   return MGPU_OK;
 }
@@ -735,7 +783,6 @@ int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_
     hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
     stats->kernel_ms = ms;
   }
-  if (h[4]) return fail(MGPU_E_INTERNAL, "look-back scan timed out in %llu tiles", h[4]);
   if (h[2]) {
     if (is == MGPU_BNG) return fail(MGPU_E_NAN, "NaN coordinates are not supported. (%llu points)", h[2]);
     return fail(MGPU_E_INVALID_ARG, "Latitude or longitude were invalid. (%llu points)", h[2]);

@@ -69,6 +69,20 @@ struct alignas(16) HashSlot {
   uint16_t core_mask;
 };
 
+// Everything the join's PIP step needs about one chip, in one 64-byte line (the
+// per-array form above stays for st_contains and the sequential PointLocator).
+struct alignas(64) ChipHdr {
+  double env[4];        // minx, miny, maxx, maxy
+  double y0, inv_h;     // strip_of() parameters
+  uint32_t strip_base;  // first strip (index into strip_edge)
+  uint16_t n_strips;
+  uint8_t flags;        // ChipFlags
+  uint8_t single_ring;  // one polygon with one ring, not a collection
+  int32_t poly;         // polygon id
+  uint32_t pad;
+};
+static_assert(sizeof(ChipHdr) == 64, "ChipHdr is one line");
+
 struct ChipTableView {
   const HashSlot* slots;
   uint32_t hash_mask;
@@ -90,6 +104,7 @@ struct ChipTableView {
   const uint32_t* strip_edge;  // [n_strips + 1]
   const double* edges;         // 4 per edge record: p1x, p1y, p2x, p2y (p1 = ring[i], p2 = ring[i-1])
   const uint8_t* edge_ring;    // ring index of the edge within its chip
+  const ChipHdr* chip_hdr;     // [n_chips]
   // H3 probing (index system H3 only)
   int32_t probe_mode;          // 0: hash keyed by cell id; 1: keyed by (face, i, j) lattice key
   int32_t res;                 // resolution of the chip cells (H3), -1 if mixed / unknown

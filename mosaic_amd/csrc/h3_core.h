@@ -61,6 +61,12 @@ struct IJK {
 #else
 #define MGPU_LIBM static inline
 #endif
+// other pieces of the route, out of line on the device for the same reason
+#ifdef __HIP_DEVICE_COMPILE__
+#define MGPU_COLD_FN static __host__ __device__ __attribute__((noinline))
+#else
+#define MGPU_COLD_FN static inline
+#endif
 MGPU_LIBM void lm_sincos(double a, double* s, double* c) { sincos(a, s, c); }
 MGPU_LIBM double lm_acos(double a) { return acos(a); }
 MGPU_LIBM double lm_atan2(double y, double x) { return atan2(y, x); }
@@ -89,7 +95,7 @@ MGPU_HD double dmin(double a, double b) { return a < b ? a : b; }
 // _hex2dToCoordIJK; *margin receives the smallest distance between a quantity and
 // the threshold it was compared against (fractional parts, integer truncation,
 // the quadrant folds).
-MGPU_HD IJK hex2d_to_ijk(double vx, double vy, double* margin) {
+MGPU_COLD_FN IJK hex2d_to_ijk(double vx, double vy, double* margin) {
   IJK h;
   h.k = 0;
   double a1 = fabs(vx), a2 = fabs(vy);
@@ -149,7 +155,7 @@ MGPU_HD IJK hex2d_to_ijk(double vx, double vy, double* margin) {
 
 // _geoToHex2d (via _geoToClosestFace).  *face_gap = second-smallest minus
 // smallest squared chord distance (face-choice margin).
-MGPU_HD void geo_to_hex2d(double lat, double lon, int res, int* face, double* vx, double* vy, double* face_gap) {
+MGPU_COLD_FN void geo_to_hex2d(double lat, double lon, int res, int* face, double* vx, double* vy, double* face_gap) {
   double slat, clat, slon, clon;
   lm_sincos(lat, &slat, &clat);
   lm_sincos(lon, &slon, &clon);

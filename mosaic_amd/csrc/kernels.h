@@ -11,26 +11,38 @@ namespace mgpu {
 struct JoinArgs {
   const double* x;
   const double* y;
-  const int64_t* point_id;
-  int64_t id_base;
   int64_t n;
   int64_t n_tiles;
   int res;
   int res_match;                    // H3: the chips' resolution equals `res` (else nothing can match)
   ChipTableView chips;
+  uint32_t* tile_count;             // [n_tiles] pairs of each tile
+  uint64_t* tile_where;             // [n_tiles] first record of the tile in `recs` (~0: dropped)
+  uint64_t* recs;                   // [n_tiles * tile points] slots, then [pool_cap] overflow pool
+  int64_t pool_cap;
+  unsigned long long* pool_used;    // zeroed before launch
+  unsigned long long* counters;     // [0] pairs [1] near-ties [2] invalid [3] candidates
+  int ablate;                       // profiling only (MGPU_ABLATE): 1 = no PIP (border = miss), 2 = no probe
+};
+
+// pair_emit_kernel: tile records -> ordered (point_id, polygon_id) output
+struct EmitArgs {
+  const uint32_t* tile_count;
+  uint64_t* tile_off;               // written by the tile scan
+  const uint64_t* tile_where;
+  const uint64_t* recs;
+  const int64_t* point_id;
+  int64_t id_base;
   int64_t capacity;
   int64_t* out_point;
   int32_t* out_poly;
-  uint64_t* tile_status;            // [n_tiles], zeroed before launch
-  uint32_t* tile_ticket;            // zeroed before launch
-  unsigned long long* counters;     // [0] pairs [1] near-ties [2] invalid [3] candidates [4] look-back timeouts
-  int ablate;                       // profiling only (MGPU_ABLATE): 1 = no PIP (border = miss), 2 = no probe
 };
 
 hipError_t launch_cells(int is, int res, const double* x, const double* y, int64_t n, int64_t* out,
                         unsigned long long* counters, hipStream_t s);
 int64_t join_tiles(int64_t n);
-hipError_t launch_join(int is, const JoinArgs& a, hipStream_t s);
+int64_t join_tile_points();
+hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s);
 hipError_t launch_st_contains(const ChipTableView& t, const int64_t* row, const double* x, const double* y, int64_t n,
                               int8_t* out, hipStream_t s);
 

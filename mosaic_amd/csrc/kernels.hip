@@ -2,18 +2,20 @@
 //
 //   cells_kernel<IS>     IndexSystem.pointToIndex over a batch (H3 / BNG)
 //   pip_join_kernel<IS>  fused: cell id -> chip-table probe -> is_core OR
-//                        st_contains -> ordered (point_id, polygon_id) output
+//                        st_contains -> per-tile pair records
+//   tile_scan_kernel     tile pair counts -> output offsets
+//   pair_emit_kernel     records -> ordered (point_id, polygon_id) output
 //   st_contains_kernel   st_contains(chip.wkb, point) for explicit pairs
 //
 // Design (DESIGN.md has the roofline analysis): the hot path is one pass over the
-// points.  Each 256-thread workgroup owns a tile of 1024 consecutive points (4 per
-// lane, loaded as 32 contiguous bytes per lane per coordinate).  The chip table's
-// cell hash (16 B slots) and the border-chip vertex runs are small and read-only;
-// they stay in L2 / Infinity Cache while the point stream flows from HBM.  Output
-// positions come from a single-pass decoupled look-back scan over tiles (tile
-// ids taken from an atomic ticket, so every predecessor tile is already running),
-// which keeps the output ordered by input position without a second pass or a
-// sort.  Nothing here is a dense contraction, so MFMA is not used.
+// points plus two light launches.  pip_join_kernel gives each 256-thread workgroup a
+// tile of 1024 consecutive points (4 per lane); the chip table's cell hash and the
+// border chips' strip-indexed edges are small and read-only, so they stay in L2 /
+// Infinity Cache while the point stream flows from HBM.  A tile writes its pairs as
+// compact records into its own slot -- no workgroup ever waits for another --
+// tile_scan_kernel turns the tiles' pair counts into output offsets, and
+// pair_emit_kernel writes the pairs ordered by input position (then polygon id).
+// Nothing here is a dense contraction, so MFMA is not used.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -29,10 +31,7 @@ constexpr int kBlock = 256;
 constexpr int kItems = 4;
 constexpr int kTile = kBlock * kItems;
 
-constexpr uint64_t kFlagAgg = 1ULL << 62;
-constexpr uint64_t kFlagPrefix = 2ULL << 62;
-constexpr uint64_t kValueMask = (1ULL << 62) - 1;
-constexpr uint32_t kSpinLimit = 1u << 22;
+constexpr uint64_t kNoDst = ~0ULL;
 
 // ---------------------------------------------------------------- point -> cell
 
@@ -106,8 +105,9 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 //     chip_contains_strips: envelope, rectangle shortcut, ray crossing over the
 //     edges of the point's y-strip only); a hit sets bit j of the point's mask;
 //  3  lane l owns points 4l .. 4l+3 (input order): matches = mask bits (chip order
-//     == polygon-id order), block scan + decoupled look-back over tiles for the
-//     output offset, pairs staged in LDS and written as contiguous runs.
+//     == polygon-id order), block scan for positions within the tile, records
+//     {point-in-tile, polygon id} staged in LDS and written to the tile's slot as
+//     one contiguous run.
 // Chips past the 32nd of one cell (never seen in practice) are evaluated in phase 3.
 constexpr int kCandCap = 1024;
 constexpr int kOutCap = 2048;
@@ -160,11 +160,13 @@ __device__ __forceinline__ bool chip_is_core(const ChipTableView& t, const Range
   return j < 16 ? ((r.core >> j) & 1) : (t.chip_flags[r.first + j] & kChipCore) != 0;
 }
 
+#ifndef MGPU_JOIN_WAVES
+#define MGPU_JOIN_WAVES 1
+#endif
 template <int IS>
-__global__ __launch_bounds__(kBlock) void pip_join_kernel(JoinArgs a) {
-  __shared__ uint32_t s_tile, s_ncand;
+__global__ __launch_bounds__(kBlock, MGPU_JOIN_WAVES) void pip_join_kernel(JoinArgs a) {
+  __shared__ uint32_t s_ncand;
   __shared__ uint32_t s_wave_tot[kBlock / 64];
-  __shared__ unsigned long long s_prefix;
   __shared__ uint32_t s_first[kTile];   // first chip of the point's cell
   __shared__ uint32_t s_mask[kTile];    // bit j: chip first + j matches (j < 32)
   __shared__ uint16_t s_cnt[kTile];     // chips of the point's cell (0: none)
@@ -175,12 +177,9 @@ __global__ __launch_bounds__(kBlock) void pip_join_kernel(JoinArgs a) {
   int32_t* s_out_poly = (int32_t*)s_buf;                          // [kOutCap]
   uint16_t* s_out_li = (uint16_t*)(s_buf + kOutCap * 4);          // [kOutCap]
 
-  if (threadIdx.x == 0) {
-    s_tile = atomicAdd(a.tile_ticket, 1u);
-    s_ncand = 0;
-  }
+  if (threadIdx.x == 0) s_ncand = 0;
   __syncthreads();
-  const uint32_t tile = s_tile;
+  const uint32_t tile = blockIdx.x;
   const ChipTableView& t = a.chips;
   const int64_t base = (int64_t)tile * kTile;
   const bool res_match = a.res_match;
@@ -188,15 +187,54 @@ __global__ __launch_bounds__(kBlock) void pip_join_kernel(JoinArgs a) {
 
   // ---- phase 1: cells, core matches, candidates
   bool any_tie = false, any_bad = false;
+#ifndef MGPU_PREFETCH
+#define MGPU_PREFETCH 2
+#endif
+#if MGPU_PREFETCH == 1
+  // all of the lane's coordinates are loaded up front: one HBM latency per tile
+  double px_[kItems], py_[kItems];
+#pragma unroll
+  for (int k = 0; k < kItems; k++) {
+    const int64_t p = base + k * kBlock + threadIdx.x;
+    px_[k] = p < a.n ? a.x[p] : 0.0;
+    py_[k] = p < a.n ? a.y[p] : 0.0;
+  }
+#elif MGPU_PREFETCH == 2
+  // one item ahead: item k + 1's coordinates load while item k computes
+  double nx = 0.0, ny = 0.0;
+  if (base + threadIdx.x < a.n) {
+    nx = a.x[base + threadIdx.x];
+    ny = a.y[base + threadIdx.x];
+  }
+#endif
 #pragma unroll 1
   for (int k = 0; k < kItems; k++) {
     const int li = k * kBlock + threadIdx.x;
     const int64_t p = base + li;
     Range r{0, 0, 0};
     uint32_t mask = 0;
+#if MGPU_PREFETCH == 2
+    const double cx = nx, cy = ny;
+    if (k + 1 < kItems && p + kBlock < a.n) {
+      nx = a.x[p + kBlock];
+      ny = a.y[p + kBlock];
+    }
+#endif
     if (p < a.n) {
       bool ok, tie;
+#if MGPU_PREFETCH == 1
+      // register-resident pick (a runtime index into px_ would go to scratch)
+      double px = px_[0], py = py_[0];
+#pragma unroll
+      for (int q = 1; q < kItems; q++) {
+        px = k == q ? px_[q] : px;
+        py = k == q ? py_[q] : py;
+      }
+#elif MGPU_PREFETCH == 2
+      const double px = cx, py = cy;
+#else
       const double px = a.x[p], py = a.y[p];
+#endif
       r = chip_range<IS>(t, px, py, a.res, res_match, &ok, &tie);
       if (a.ablate == 2) r.count = 0;
       any_bad |= !ok;
@@ -271,51 +309,26 @@ __global__ __launch_bounds__(kBlock) void pip_join_kernel(JoinArgs a) {
   }
   const uint32_t excl = wave_off + incl - mine;
 
-  // decoupled look-back (wave 0): status word = {2-bit flag, 62-bit count}
-  if (wave == 0) {
-    unsigned long long prefix = 0;
-    if (tile == 0) {
-      if (lane == 0) __hip_atomic_store(&a.tile_status[0], kFlagPrefix | (uint64_t)agg, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (lane == 0) __hip_atomic_store(&a.tile_status[tile], kFlagAgg | (uint64_t)agg, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-      int64_t top = (int64_t)tile - 1;
-      uint32_t spins = 0;
-      while (true) {
-        const int64_t idx = top - lane;
-        uint64_t st = idx >= 0 ? __hip_atomic_load(&a.tile_status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : kFlagPrefix;
-        const uint32_t flag = (uint32_t)(st >> 62);
-        if (__any(flag == 0)) {
-          if (++spins > kSpinLimit) {
-            if (lane == 0) atomicAdd(&a.counters[4], 1ull);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        const unsigned long long pb = __ballot(flag == 2);
-        const int first = pb ? (__ffsll((long long)pb) - 1) : 64;
-        unsigned long long v = (lane <= first) ? (st & kValueMask) : 0ull;
-        prefix += wave_sum_u64(v);
-        if (pb) break;
-        top -= 64;
-      }
-      if (lane == 0)
-        __hip_atomic_store(&a.tile_status[tile], kFlagPrefix | (uint64_t)(prefix + agg), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+  // the tile's records go to its own slot (kTile records), or -- when it has more
+  // pairs than points -- to space reserved in the overflow pool
+  __shared__ uint64_t s_dst;
+  if (threadIdx.x == 0) {
+    uint64_t dst = (uint64_t)tile * kTile;
+    if (agg > (uint32_t)kTile) {
+      const unsigned long long off = atomicAdd(a.pool_used, (unsigned long long)agg);
+      dst = off + agg <= (unsigned long long)a.pool_cap ? (uint64_t)a.n_tiles * kTile + off : kNoDst;
     }
-    if (lane == 0) {
-      s_prefix = prefix;
-      if (tile == a.n_tiles - 1) a.counters[0] = prefix + agg;
-    }
+    a.tile_count[tile] = agg;
+    a.tile_where[tile] = dst;
+    s_dst = dst;
   }
-  __syncthreads();
-  const int64_t prefix = (int64_t)s_prefix;
   const bool staged = agg <= (uint32_t)kOutCap;
+  __syncthreads();
+  const uint64_t dst = s_dst;
+  uint64_t* const rec = dst == kNoDst ? nullptr : a.recs + dst;
 
-  // this lane's pairs: staged in LDS (then written as contiguous runs) or direct
+  // this lane's pairs {li << 32 | polygon id}: staged in LDS (then written as
+  // contiguous runs) or direct
   uint32_t pos = excl;
 #pragma unroll 1
   for (int k = 0; k < kItems; k++) {
@@ -339,24 +352,66 @@ __global__ __launch_bounds__(kBlock) void pip_join_kernel(JoinArgs a) {
       if (staged) {
         s_out_poly[pos] = poly;
         s_out_li[pos] = (uint16_t)li;
-      } else {
-        const int64_t q = prefix + pos;
-        if (q < a.capacity) {
-          a.out_point[q] = a.point_id ? a.point_id[p] : a.id_base + p;
-          a.out_poly[q] = poly;
-        }
+      } else if (rec) {
+        rec[pos] = ((uint64_t)li << 32) | (uint32_t)poly;
       }
       pos++;
     }
   }
-  if (!staged) return;
+  if (!staged || !rec) return;
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < agg; i += kBlock) {
-    const int64_t q = prefix + i;
+  for (uint32_t i = threadIdx.x; i < agg; i += kBlock) rec[i] = ((uint64_t)s_out_li[i] << 32) | (uint32_t)s_out_poly[i];
+}
+
+// Exclusive scan of the tiles' pair counts (one workgroup; ~1e5 tiles per 1e8
+// points): tile_off[t] = pairs of tiles < t; counters[0] = total.
+constexpr int kScanBlock = 1024;
+__global__ __launch_bounds__(kScanBlock) void tile_scan_kernel(const uint32_t* __restrict__ cnt, int64_t n,
+                                                               uint64_t* __restrict__ off,
+                                                               unsigned long long* __restrict__ counters) {
+  __shared__ unsigned long long s_w[kScanBlock / 64];
+  const int64_t per = (n + kScanBlock - 1) / kScanBlock;
+  const int64_t b = per * threadIdx.x, e = b + per < n ? b + per : n;
+  unsigned long long sum = 0;
+  for (int64_t i = b; i < e; i++) sum += cnt[i];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned long long incl = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    unsigned long long v = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += v;
+  }
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  unsigned long long run = incl - sum, tot = 0;
+  for (int w = 0; w < kScanBlock / 64; w++) {
+    if (w < wave) run += s_w[w];
+    tot += s_w[w];
+  }
+  for (int64_t i = b; i < e; i++) {
+    off[i] = run;
+    run += cnt[i];
+  }
+  if (threadIdx.x == 0) counters[0] = tot;
+}
+
+// Ordered output: tile t's records -> out[tile_off[t] ...] with point ids.
+__global__ __launch_bounds__(kBlock) void pair_emit_kernel(EmitArgs a) {
+  const int64_t t = blockIdx.x;
+  const uint32_t n = a.tile_count[t];
+  if (!n) return;
+  const uint64_t where = a.tile_where[t];
+  if (where == kNoDst) return;  // pool exhausted: the total exceeds the capacity
+  const int64_t off = (int64_t)a.tile_off[t];
+  const uint64_t* src = a.recs + where;
+  const int64_t base = t * kTile;
+  for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+    const int64_t q = off + i;
     if (q >= a.capacity) break;
-    const int64_t p = base + s_out_li[i];
+    const uint64_t r = src[i];
+    const int64_t p = base + (int64_t)(r >> 32);
     a.out_point[q] = a.point_id ? a.point_id[p] : a.id_base + p;
-    a.out_poly[q] = s_out_poly[i];
+    a.out_poly[q] = (int32_t)(uint32_t)r;
   }
 }
 
@@ -394,13 +449,17 @@ hipError_t launch_cells(int is, int res, const double* x, const double* y, int64
 }
 
 int64_t join_tiles(int64_t n) { return (n + kTile - 1) / kTile; }
+int64_t join_tile_points() { return kTile; }
 
-hipError_t launch_join(int is, const JoinArgs& a, hipStream_t s) {
+hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s) {
   if (a.n_tiles <= 0) return hipSuccess;
   if (is == MGPU_H3)
     hipLaunchKernelGGL(pip_join_kernel<MGPU_H3>, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, a);
   else
     hipLaunchKernelGGL(pip_join_kernel<MGPU_BNG>, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.tile_count, a.n_tiles, e.tile_off,
+                     a.counters);
+  hipLaunchKernelGGL(pair_emit_kernel, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, e);
   return hipGetLastError();
 }
 

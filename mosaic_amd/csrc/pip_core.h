@@ -99,7 +99,7 @@ MGPU_HDI int orientation(double p1x, double p1y, double p2x, double p2y, double 
 // on the segment (BOUNDARY), 2 = the segment crosses the ray (one crossing).  The
 // ring's location is then BOUNDARY if any segment sets bit 1, else INTERIOR iff the
 // crossings are odd -- independent of the order the segments are visited in, which
-// lets a tile test all candidate edges in parallel (kernels.hip, phase 4).
+// lets the join test only the edges of the point's y-strip (chip_contains_strips).
 MGPU_HDI int count_segment(double p1x, double p1y, double p2x, double p2y, double px, double py) {
   if (p1x < px && p2x < px) return 0;
   if (px == p2x && py == p2y) return 1;
@@ -167,44 +167,7 @@ MGPU_HDI int polygon_locate(const ChipTableView& t, uint32_t p, double px, doubl
   return kInterior;
 }
 
-enum RingBits { kRingOnSegment = 1, kRingParity = 2, kRingSkipped = 4 };
-
-// Location of a ring from its accumulated bits (kRingSkipped: envelope miss / no edges)
-MGPU_HDI int ring_loc_from_bits(uint32_t b) {
-  if (b & kRingSkipped) return kExterior;
-  if (b & kRingOnSegment) return kBoundary;
-  return (b & kRingParity) ? kInterior : kExterior;
-}
-
-// PointLocator over chip `c` given the location bits of each of its rings (in chip
-// ring order, ring_bits[k] for ring part_ring[chip_part[c]] + k)
-MGPU_HDI int chip_locate_from_rings(const ChipTableView& t, uint32_t c, const uint32_t* ring_bits) {
-  const uint32_t pb = t.chip_part[c], pe = t.chip_part[c + 1];
-  const uint32_t r0 = t.part_ring[pb];
-  bool is_in = false;
-  int n_bnd = 0, single = -1;
-  for (uint32_t p = pb; p < pe; p++) {
-    uint32_t rb = t.part_ring[p], re = t.part_ring[p + 1];
-    int loc = kInterior;
-    if (re == rb) loc = kExterior;
-    for (uint32_t r = rb; r < re; r++) {
-      int l = ring_loc_from_bits(ring_bits[r - r0]);
-      if (r == rb) {
-        if (l != kInterior) { loc = l; break; }
-      } else {
-        if (l == kInterior) { loc = kExterior; break; }
-        if (l == kBoundary) { loc = kBoundary; break; }
-      }
-    }
-    if (single < 0) single = loc;
-    if (loc == kInterior) is_in = true;
-    if (loc == kBoundary) n_bnd++;
-  }
-  if (!(t.chip_flags[c] & kChipMulti)) return single < 0 ? kExterior : single;
-  if (n_bnd & 1) return kBoundary;
-  if (n_bnd > 0 || is_in) return kInterior;
-  return kExterior;
-}
+enum RingBits { kRingOnSegment = 1 };
 
 // Geometry.contains(point) == (location == INTERIOR), for sorted chip `c`
 MGPU_HDI int chip_locate(const ChipTableView& t, uint32_t c, double px, double py) {
@@ -235,15 +198,15 @@ MGPU_HDI int chip_locate(const ChipTableView& t, uint32_t c, double px, double p
 // the rings -- with each ring's RayCrossingCounter run over the edges of the
 // point's strip only.  Chips flagged kChipNoStrips go to chip_locate().
 MGPU_HDI bool chip_contains_strips(const ChipTableView& t, uint32_t c, double px, double py) {
-  const uint8_t fl = t.chip_flags[c];
+  const ChipHdr& H = t.chip_hdr[c];
+  const double e0 = H.env[0], e1 = H.env[1], e2 = H.env[2], e3 = H.env[3];
+  const uint8_t fl = H.flags;
   if (fl & (kChipEmpty | kChipNoGeom)) return false;
-  const double* env = t.chip_env + 4 * c;
-  if (!env_has(env, px, py)) return false;
-  if (fl & kChipRect) return !(px == env[0] || px == env[2] || py == env[1] || py == env[3]);
+  if (!(px >= e0 && px <= e2 && py >= e1 && py <= e3)) return false;
+  if (fl & kChipRect) return !(px == e0 || px == e2 || py == e1 || py == e3);
   if (fl & kChipNoStrips) return chip_locate(t, c, px, py) == kInterior;
-  const uint32_t sb = t.chip_strip[c];
-  const int S = (int)(t.chip_strip[c + 1] - sb);
-  const int s = strip_of(py, t.chip_sy[2 * c], t.chip_sy[2 * c + 1], S);
+  const uint32_t sb = H.strip_base;
+  const int s = strip_of(py, H.y0, H.inv_h, (int)H.n_strips);
   const uint32_t eb = t.strip_edge[sb + s], ee = t.strip_edge[sb + s + 1];
   uint32_t bnd = 0, par = 0;
   for (uint32_t e = eb; e < ee; e++) {
@@ -255,12 +218,10 @@ MGPU_HDI bool chip_contains_strips(const ChipTableView& t, uint32_t c, double px
       if (bits & 2) par ^= rb;
     }
   }
+  // one polygon, one ring (its envelope is the chip's): RayCrossingCounter's verdict
+  if (H.single_ring) return !(bnd & 1) && (par & 1);
   const uint32_t pb = t.chip_part[c], pe = t.chip_part[c + 1];
   const uint32_t r0 = t.part_ring[pb];
-  if (pe - pb == 1 && t.part_ring[pb + 1] - r0 == 1 && !(fl & kChipMulti)) {
-    // one polygon, one ring (its envelope is the chip's): RayCrossingCounter's verdict
-    return !(bnd & 1) && (par & 1);
-  }
   bool is_in = false;
   int n_bnd = 0, single = -1;
   for (uint32_t p = pb; p < pe; p++) {

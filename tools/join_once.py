@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Run the bench workload's join (or cells) kernel a few times -- a short target for
+rocprofv3 PMC passes.  --ablate sets MGPU_ABLATE (1 = no PIP, 2 = no probe)."""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=int, default=100_000_000)
+    ap.add_argument("--res", type=int, default=9)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--ablate", type=int, default=0)
+    ap.add_argument("--cells", action="store_true")
+    a = ap.parse_args()
+    if a.ablate:
+        os.environ["MGPU_ABLATE"] = str(a.ablate)
+    import mosaic_amd as M
+    import bench as B
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    ctx = M.default_context(dev)
+    zones = M.Polygons.from_npz(os.path.join(ROOT, "tests", "golden", "nyc_taxi_zones.npz"))
+    chips = M.tessellate(zones, M.H3IndexSystem(), a.res).upload(ctx)
+    x, y = B.gen_points(a.points, 0, 0x20250314, dev)
+    cap = a.points // 2 + 1024
+    op = torch.empty(cap, dtype=torch.int64, device=dev)
+    oq = torch.empty(cap, dtype=torch.int32, device=dev)
+    ctx.reserve(a.points)
+    for _ in range(a.reps):
+        if a.cells:
+            M.grid_longlatascellid(x, y, a.res)
+        else:
+            M.pip_join(x, y, chips, a.res, out=(op, oq), capacity=cap)
+    torch.cuda.synchronize()
+    print("done", flush=True)
+
+
+if __name__ == "__main__":
+    main()
