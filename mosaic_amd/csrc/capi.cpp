@@ -48,7 +48,7 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // offsets, so a byte copy of the blob on another GPU (RCCL broadcast) is a
 // complete chip table there.
 constexpr uint64_t kBlobMagic = 0x4d4f534149434850ULL;  // "MOSAICHP"
-constexpr int kBlobArrays = 17;
+constexpr int kBlobArrays = 18;
 constexpr uint32_t kBlobVersion = 3;
 struct BlobHeader {
   uint64_t magic;
@@ -59,8 +59,9 @@ struct BlobHeader {
   uint32_t face_mask, pad2;
   double bbox[4];
   double k_res;
+  mgpu::DenseFace dense[20];
 };
-constexpr size_t kBlobHeaderBytes = 256;
+constexpr size_t kBlobHeaderBytes = 1024;
 static_assert(sizeof(BlobHeader) <= kBlobHeaderBytes, "header too large");
 
 mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
@@ -86,6 +87,8 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.edges = (const double*)(base + h.off[14]);
   v.edge_ring = (const uint8_t*)(base + h.off[15]);
   v.chip_hdr = (const mgpu::ChipHdr*)(base + h.off[16]);
+  v.grid = (const uint64_t*)(base + h.off[17]);
+  for (int f = 0; f < 20; f++) v.dense[f] = h.dense[f];
   v.probe_mode = h.probe_mode;
   v.res = h.res;
   v.face_mask = h.face_mask;
@@ -312,7 +315,7 @@ namespace {
 //   [records u64 x (T * tile points + pool)]
 // T = tiles of the largest point batch reserved; pool = overflow records (tiles with
 // more pairs than points), at most the output capacity.
-constexpr size_t kWsCounters = 64;
+constexpr size_t kWsCounters = 128;  // 16 x u64
 
 struct WsLayout {
   size_t count, where, off, recs, total;
@@ -542,6 +545,14 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
     h.single_ring = (pe - pb == 1 && geo.part_ring[pb + 1] - geo.part_ring[pb] == 1 &&
                      !(cflags[c] & mgpu::kChipMulti)) ? 1 : 0;
     h.poly = cpoly[c];
+    h.edge_base = strips.strip_edge[h.strip_base];
+    if (h.n_strips <= mgpu::kHdrStrips) {
+      for (int q = 0; q <= h.n_strips; q++) {
+        const uint32_t rel = strips.strip_edge[h.strip_base + q] - h.edge_base;
+        if (rel > 0xFFFF) return fail(MGPU_E_INTERNAL, "chip %lld: strip offsets exceed 16 bits", (long long)c);
+        h.soff[q] = (uint16_t)rel;
+      }
+    }
   }
   // H3: probe by lattice key when possible (chip_table.h)
   int32_t probe_mode = mgpu::kProbeCellId, lres = -1;
@@ -563,6 +574,51 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
   } else {
     entries = distinct;
     if (index_system == MGPU_H3 && !distinct.empty()) lres = (int32_t)((distinct[0].cell >> 52) & 15);
+  }
+  // dense lattice grid when the chip cells' (a, b) boxes are compact: one load per
+  // point instead of a hash probe sequence (misses -- most points -- included)
+  std::vector<uint64_t> grid;
+  mgpu::DenseFace dense[20];
+  memset(dense, 0, sizeof dense);
+  if (probe_mode == mgpu::kProbeLattice && !entries.empty()) {
+    int64_t amin[20], amax[20], bmin[20], bmax[20];
+    for (int f = 0; f < 20; f++) amin[f] = bmin[f] = INT64_MAX, amax[f] = bmax[f] = INT64_MIN;
+    auto dec = [](uint64_t key, int* f, int64_t* a, int64_t* b) {
+      *f = (int)(key >> 56);
+      *a = (int64_t)((key >> 28) & 0xFFFFFFFULL) - (1 << 27);
+      *b = (int64_t)(key & 0xFFFFFFFULL) - (1 << 27);
+    };
+    for (const auto& e : entries) {
+      int f;
+      int64_t a, b;
+      dec(e.cell, &f, &a, &b);
+      amin[f] = std::min(amin[f], a), amax[f] = std::max(amax[f], a);
+      bmin[f] = std::min(bmin[f], b), bmax[f] = std::max(bmax[f], b);
+    }
+    int64_t total = 0;
+    for (int f = 0; f < 20; f++)
+      if (amax[f] >= amin[f]) total += (amax[f] - amin[f] + 1) * (bmax[f] - bmin[f] + 1);
+    if (total <= std::max<int64_t>(16 * (int64_t)entries.size(), 1 << 20) && total <= (1LL << 26)) {
+      uint32_t base = 0;
+      for (int f = 0; f < 20; f++) {
+        if (amax[f] < amin[f]) continue;
+        dense[f].a0 = (int32_t)amin[f];
+        dense[f].b0 = (int32_t)bmin[f];
+        dense[f].w = (uint32_t)(amax[f] - amin[f] + 1);
+        dense[f].h = (uint32_t)(bmax[f] - bmin[f] + 1);
+        dense[f].base = base;
+        base += dense[f].w * dense[f].h;
+      }
+      grid.assign(base, 0);
+      for (const auto& e : entries) {
+        int f;
+        int64_t a, b;
+        dec(e.cell, &f, &a, &b);
+        grid[dense[f].base + (b - dense[f].b0) * dense[f].w + (a - dense[f].a0)] =
+            (uint64_t)e.first | ((uint64_t)e.count << 32) | ((uint64_t)e.core_mask << 48);
+      }
+      probe_mode = mgpu::kProbeDense;
+    }
   }
   uint32_t cap = 16;
   while (cap < 2 * entries.size()) cap <<= 1;
@@ -602,6 +658,7 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
       {strips.edges.data(), strips.edges.size() * 8, 0},
       {strips.edge_ring.data(), strips.edge_ring.size(), 0},
       {chdr.data(), chdr.size() * sizeof(mgpu::ChipHdr), 0},
+      {grid.data(), grid.size() * 8, 0},
   };
   size_t total = kBlobHeaderBytes;
   BlobHeader hdr{};
@@ -613,6 +670,7 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
   hdr.n_cells = (uint32_t)distinct.size();
   hdr.n_vertices = (int64_t)geo.vtx.size() / 2;
   hdr.probe_mode = probe_mode;
+  memcpy(hdr.dense, dense, sizeof dense);
   hdr.res = lres;
   hdr.face_mask = face_mask;
   for (int k = 0; k < 4; k++) hdr.bbox[k] = bbox[k];
@@ -774,6 +832,13 @@ int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_
   HIP_TRY(hipMemcpyAsync(h, ctx->ws, sizeof h, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   if (out_n_pairs) *out_n_pairs = (int64_t)h[0];
+  if (getenv("MGPU_DEBUG_COUNTERS")) {  // profiling builds (-DMGPU_STATS)
+    unsigned long long d[16] = {0};
+    HIP_TRY(hipMemcpy(d, ctx->ws, sizeof d, hipMemcpyDeviceToHost));
+    fprintf(stderr, "mgpu counters:");
+    for (int k = 0; k < 16; k++) fprintf(stderr, " %llu", d[k]);
+    fprintf(stderr, "\n");
+  }
   if (stats) {
     stats->n_points = n;
     stats->n_pairs = (int64_t)h[0];

@@ -69,9 +69,12 @@ struct alignas(16) HashSlot {
   uint16_t core_mask;
 };
 
-// Everything the join's PIP step needs about one chip, in one 64-byte line (the
-// per-array form above stays for st_contains and the sequential PointLocator).
-struct alignas(64) ChipHdr {
+// Everything the join's PIP step needs about one chip, in 128 bytes (the per-array
+// form above stays for st_contains and the sequential PointLocator).  Chips with at
+// most kHdrStrips strips carry their strip boundaries inline (edge offsets relative
+// to edge_base); others read strip_edge[strip_base + s].
+constexpr int kHdrStrips = 31;
+struct alignas(128) ChipHdr {
   double env[4];        // minx, miny, maxx, maxy
   double y0, inv_h;     // strip_of() parameters
   uint32_t strip_base;  // first strip (index into strip_edge)
@@ -79,9 +82,16 @@ struct alignas(64) ChipHdr {
   uint8_t flags;        // ChipFlags
   uint8_t single_ring;  // one polygon with one ring, not a collection
   int32_t poly;         // polygon id
-  uint32_t pad;
+  uint32_t edge_base;   // first edge record of the chip's strips
+  uint16_t soff[kHdrStrips + 1];  // strip s = edges [edge_base + soff[s], edge_base + soff[s + 1])
 };
-static_assert(sizeof(ChipHdr) == 64, "ChipHdr is one line");
+static_assert(sizeof(ChipHdr) == 128, "ChipHdr is two lines");
+
+struct DenseFace {
+  int32_t a0, b0;
+  uint32_t w, h;
+  uint32_t base;
+};
 
 struct ChipTableView {
   const HashSlot* slots;
@@ -106,14 +116,19 @@ struct ChipTableView {
   const uint8_t* edge_ring;    // ring index of the edge within its chip
   const ChipHdr* chip_hdr;     // [n_chips]
   // H3 probing (index system H3 only)
-  int32_t probe_mode;          // 0: hash keyed by cell id; 1: keyed by (face, i, j) lattice key
+  int32_t probe_mode;          // ProbeMode: hash by cell id / hash by lattice key / dense lattice grid
   int32_t res;                 // resolution of the chip cells (H3), -1 if mixed / unknown
   uint32_t face_mask;          // icosahedron faces a point inside `bbox` can be nearest to
   double bbox[4];              // lon_min, lat_min, lon_max, lat_max (deg): points outside match no chip
   double k_res;                // sqrt7^res / RES0_U_GNOMONIC
+  // kProbeDense: per face f, grid[base + (b - b0) * w + (a - a0)] for the axial
+  // lattice coordinates a = i - k, b = j - k inside [a0, a0 + w) x [b0, b0 + h);
+  // entry = first | count << 32 | core_mask << 48 (count 0: no chip cell there)
+  const uint64_t* grid;
+  DenseFace dense[20];
 };
 
-enum ProbeMode { kProbeCellId = 0, kProbeLattice = 1 };
+enum ProbeMode { kProbeCellId = 0, kProbeLattice = 1, kProbeDense = 2 };
 
 #ifdef __HIPCC__
 #define MGPU_HDI __host__ __device__ __forceinline__

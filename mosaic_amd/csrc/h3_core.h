@@ -390,18 +390,33 @@ constexpr double kDegToRad = 0.017453292519943295769236907684886;
 constexpr double kInvSin60 = 1.1547005383792515290182975610039149112953;
 MGPU_HD double to_radians_fast(double deg) { return deg * kDegToRad; }
 
-MGPU_HD void sincos_tab(double a, double* s, double* c) {
-  double kf = rint(a * 64.0);
-  int k = (int)kf;
-  double d = fma_(kf, -0.015625, a);  // exact (Sterbenz)
-  double d2 = d * d;
-  double sp = fma_(d2, fma_(d2, fma_(d2, 1.0 / 362880.0, -1.0 / 5040.0), 1.0 / 120.0), -1.0 / 6.0);
-  double sd = fma_(d * d2, sp, d);
-  double cp = fma_(d2, fma_(d2, fma_(d2, fma_(d2, -1.0 / 3628800.0, 1.0 / 40320.0), -1.0 / 720.0), 1.0 / 24.0), -0.5);
-  double cd = fma_(d2, cp, 1.0);
-  double sk = H3T_SINCOS64[k + H3T_SC64_BIAS][0], ck = H3T_SINCOS64[k + H3T_SC64_BIAS][1];
-  *s = fma_(sk, cd, ck * sd);
-  *c = fma_(ck, cd, -(sk * sd));
+// sin and cos of |a| <= 3.15 without tables: a = k pi/2 + r (two-part Cody-Waite,
+// |r| <= pi/4 + 1e-15), Taylor series to r^15 / r^16 (truncation < 5e-17), then the
+// quadrant of k.  Absolute error ~3e-16: far inside the tie band.
+MGPU_HD void sincos_fast(double a, double* s, double* c) {
+  const double kf = rint(a * 0.63661977236758134308);
+  const double r0 = fma_(kf, -1.5707963267948965580, a);
+  const double r = fma_(kf, -6.1232339957367658e-17, r0);
+  const double r2 = r * r;
+  double ps = fma_(r2, -7.6471637318198164759e-13, 1.6059043836821614599e-10);
+  ps = fma_(r2, ps, -2.5052108385441718775e-08);
+  ps = fma_(r2, ps, 2.7557319223985890653e-06);
+  ps = fma_(r2, ps, -1.9841269841269841270e-04);
+  ps = fma_(r2, ps, 8.3333333333333333333e-03);
+  ps = fma_(r2, ps, -1.6666666666666666667e-01);
+  const double sr = fma_(r * r2, ps, r);
+  double pc = fma_(r2, 4.7794773323873852974e-14, -1.1470745597729724714e-11);
+  pc = fma_(r2, pc, 2.0876756987868098979e-09);
+  pc = fma_(r2, pc, -2.7557319223985890653e-07);
+  pc = fma_(r2, pc, 2.4801587301587301587e-05);
+  pc = fma_(r2, pc, -1.3888888888888888889e-03);
+  pc = fma_(r2, pc, 4.1666666666666666667e-02);
+  pc = fma_(r2, pc, -0.5);
+  const double cr = fma_(r2, pc, 1.0);
+  const int q = (int)kf & 3;
+  const double ss = (q & 1) ? cr : sr, cc = (q & 1) ? sr : cr;
+  *s = (q & 2) ? -ss : ss;
+  *c = ((q + 1) & 2) ? -cc : cc;
 }
 
 // _hex2dToCoordIJK with the fast path's multiply-by-reciprocal and the decision
@@ -479,12 +494,12 @@ struct FastHex {
 // the tie band)
 MGPU_HD FastHex fast_hex2d(double lat, double lon, int res, double k_res, uint32_t faces) {
   FastHex o;
-  // the sine table spans |angle| <= 202/64 rad: anything else takes the H3 route
+  // sincos_fast's reduction is exact for |angle| <= 3.15: beyond, the H3 route
   const bool in_table = fabs(lat) <= 3.14 && fabs(lon) <= 3.14;
   if (!in_table) lat = lon = 0.0;
   double slat, clat, slon, clon;
-  sincos_tab(lat, &slat, &clat);
-  sincos_tab(lon, &slon, &clon);
+  sincos_fast(lat, &slat, &clat);
+  sincos_fast(lon, &slon, &clon);
   double vx = clon * clat, vy = slon * clat, vz = slat;
   double best = 5.0, second = 5.0;
   int f0 = 0;
@@ -508,10 +523,23 @@ MGPU_HD FastHex fast_hex2d(double lat, double lon, int res, double k_res, uint32
     }
   }
   o.face = f0;
-  const double(*F)[3] = H3T_FACE_FRAME[f0][res & 1];
-  double dc = fma_(vx, F[2][0], fma_(vy, F[2][1], vz * F[2][2]));
-  double da = fma_(vx, F[0][0], fma_(vy, F[0][1], vz * F[0][2]));
-  double db = fma_(vx, F[1][0], fma_(vy, F[1][1], vz * F[1][2]));
+  double dc, da, db;
+#ifdef __HIP_DEVICE_COMPILE__
+  // one face for the whole wave (the usual case): the frame comes in by scalar loads
+  const int fu = __builtin_amdgcn_readfirstlane(f0);
+  if (__all(f0 == fu)) {
+    const double(*F)[3] = H3T_FACE_FRAME[fu][res & 1];
+    dc = fma_(vx, F[2][0], fma_(vy, F[2][1], vz * F[2][2]));
+    da = fma_(vx, F[0][0], fma_(vy, F[0][1], vz * F[0][2]));
+    db = fma_(vx, F[1][0], fma_(vy, F[1][1], vz * F[1][2]));
+  } else
+#endif
+  {
+    const double(*F)[3] = H3T_FACE_FRAME[f0][res & 1];
+    dc = fma_(vx, F[2][0], fma_(vy, F[2][1], vz * F[2][2]));
+    da = fma_(vx, F[0][0], fma_(vy, F[0][1], vz * F[0][2]));
+    db = fma_(vx, F[1][0], fma_(vy, F[1][1], vz * F[1][2]));
+  }
   double q = k_res * recip(dc);
   double x = da * q, y = db * q;
   double margin;

@@ -22,7 +22,8 @@ struct JoinArgs {
   int64_t pool_cap;
   unsigned long long* pool_used;    // zeroed before launch
   unsigned long long* counters;     // [0] pairs [1] near-ties [2] invalid [3] candidates
-  int ablate;                       // profiling only (MGPU_ABLATE): 1 = no PIP (border = miss), 2 = no probe
+  int ablate;                       // profiling only (MGPU_ABLATE): 1 = no PIP (border = miss), 2 = no probe,
+                                    // 3 = no projection either
 };
 
 // pair_emit_kernel: tile records -> ordered (point_id, polygon_id) output

@@ -133,7 +133,7 @@ __device__ __forceinline__ Range probe_range(const ChipTableView& t, uint64_t ke
 
 template <int IS>
 __device__ __forceinline__ Range chip_range(const ChipTableView& t, double px, double py, int res, bool res_match,
-                                            bool* ok, bool* tie) {
+                                            bool* ok, bool* tie, int ablate) {
   *tie = false;
   if (IS == MGPU_BNG) {
     int64_t c;
@@ -144,12 +144,29 @@ __device__ __forceinline__ Range chip_range(const ChipTableView& t, double px, d
   *ok = isfinite(px) && isfinite(py);
   if (!*ok || !res_match) return Range{0, 0, 0};
   const double lat = h3::to_radians_fast(py), lon = h3::to_radians_fast(px);
-  if (t.probe_mode == kProbeLattice) {
+  if (t.probe_mode != kProbeCellId) {
     // outside the chip cells' bounding box no cell can match
     if (!(px >= t.bbox[0] && px <= t.bbox[2] && py >= t.bbox[1] && py <= t.bbox[3])) return Range{0, 0, 0};
     h3::FastHex f = h3::fast_hex2d(lat, lon, res, t.k_res, t.face_mask);
     if (f.tie) h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, tie);
-    return probe_range(t, h3::lattice_key(f.face, f.ijk));
+    if (t.probe_mode == kProbeDense) {
+      const int32_t ga = f.ijk.i - f.ijk.k, gb = f.ijk.j - f.ijk.k;
+      if (ablate == 2) return Range{0, (ga ^ gb) == 0x12345 ? 1u : 0u, 0};  // profiling: projection, no probe
+      DenseFace D;
+      const int fu = __builtin_amdgcn_readfirstlane(f.face);
+      if (__all(f.face == fu)) {
+        D = t.dense[fu];
+      } else {
+        D = t.dense[f.face];
+      }
+      const uint32_t da = (uint32_t)(ga - D.a0), db = (uint32_t)(gb - D.b0);
+      if (da >= D.w || db >= D.h) return Range{0, 0, 0};
+      const uint64_t e = t.grid[D.base + db * D.w + da];
+      return Range{(uint32_t)e, (uint32_t)(e >> 32) & 0xFFFF, (uint32_t)(e >> 48)};
+    }
+    const uint64_t key = h3::lattice_key(f.face, f.ijk);
+    if (ablate == 2) return Range{0, key == 0x123456789ULL ? 1u : 0u, 0};  // profiling: projection, no probe
+    return probe_range(t, key);
   }
   h3::FastHex f = h3::fast_hex2d(lat, lon, res, t.k_res > 0 ? t.k_res : h3::k_of_res(res), kAllFaces);
   if (f.tie) h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, tie);
@@ -235,8 +252,12 @@ __global__ __launch_bounds__(kBlock, MGPU_JOIN_WAVES) void pip_join_kernel(JoinA
 #else
       const double px = a.x[p], py = a.y[p];
 #endif
-      r = chip_range<IS>(t, px, py, a.res, res_match, &ok, &tie);
-      if (a.ablate == 2) r.count = 0;
+      if (a.ablate == 3) {  // profiling: no projection, no probe
+        ok = true;
+        tie = false;
+      } else {
+        r = chip_range<IS>(t, px, py, a.res, res_match, &ok, &tie, a.ablate);
+      }
       any_bad |= !ok;
       any_tie |= tie;
       const uint32_t nj = r.count < (uint32_t)kMaskBits ? r.count : (uint32_t)kMaskBits;
@@ -272,13 +293,29 @@ __global__ __launch_bounds__(kBlock, MGPU_JOIN_WAVES) void pip_join_kernel(JoinA
   if (threadIdx.x == 0 && s_ncand) atomicAdd(&a.counters[3], (unsigned long long)s_ncand);
 
   // ---- phase 2: lane per candidate
+#ifdef MGPU_STATS
+  uint32_t st_edges = 0, st_strip = 0, st_hit = 0;
+#endif
   for (uint32_t c = threadIdx.x; c < ncand; c += kBlock) {
     const uint32_t ch = s_cand_chip[c];
     const uint32_t pj = s_cand_pj[c];
     const int li = pj & 1023;
     const int64_t p = base + li;
+#ifdef MGPU_STATS
+    uint32_t ne = 0xFFFFFFFFu;
+    const bool hit = pip::chip_contains_strips(t, ch, a.x[p], a.y[p], &ne);
+    if (ne != 0xFFFFFFFFu) { st_strip++; st_edges += ne; }
+    st_hit += hit;
+    if (hit) atomicOr(&s_mask[li], 1u << (pj >> 10));
+#else
     if (pip::chip_contains_strips(t, ch, a.x[p], a.y[p])) atomicOr(&s_mask[li], 1u << (pj >> 10));
+#endif
   }
+#ifdef MGPU_STATS
+  atomicAdd(&a.counters[8], (unsigned long long)st_edges);
+  atomicAdd(&a.counters[9], (unsigned long long)st_strip);
+  atomicAdd(&a.counters[10], (unsigned long long)st_hit);
+#endif
   __syncthreads();
 
   // ---- phase 3: lane l owns points 4l .. 4l+3 (input order)

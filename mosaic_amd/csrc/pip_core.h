@@ -197,7 +197,8 @@ MGPU_HDI int chip_locate(const ChipTableView& t, uint32_t c, double px, double p
 // same decision as chip_locate() -- envelope, rectangle shortcut, PointLocator over
 // the rings -- with each ring's RayCrossingCounter run over the edges of the
 // point's strip only.  Chips flagged kChipNoStrips go to chip_locate().
-MGPU_HDI bool chip_contains_strips(const ChipTableView& t, uint32_t c, double px, double py) {
+MGPU_HDI bool chip_contains_strips(const ChipTableView& t, uint32_t c, double px, double py,
+                                   uint32_t* stat_edges = nullptr) {
   const ChipHdr& H = t.chip_hdr[c];
   const double e0 = H.env[0], e1 = H.env[1], e2 = H.env[2], e3 = H.env[3];
   const uint8_t fl = H.flags;
@@ -205,17 +206,46 @@ MGPU_HDI bool chip_contains_strips(const ChipTableView& t, uint32_t c, double px
   if (!(px >= e0 && px <= e2 && py >= e1 && py <= e3)) return false;
   if (fl & kChipRect) return !(px == e0 || px == e2 || py == e1 || py == e3);
   if (fl & kChipNoStrips) return chip_locate(t, c, px, py) == kInterior;
-  const uint32_t sb = H.strip_base;
-  const int s = strip_of(py, H.y0, H.inv_h, (int)H.n_strips);
-  const uint32_t eb = t.strip_edge[sb + s], ee = t.strip_edge[sb + s + 1];
+  const int S = (int)H.n_strips;
+  const int s = strip_of(py, H.y0, H.inv_h, S);
+  uint32_t eb, ee;
+#ifndef MGPU_INLINE_STRIPS
+#define MGPU_INLINE_STRIPS 1
+#endif
+  if (MGPU_INLINE_STRIPS && S <= kHdrStrips) {
+    eb = H.edge_base + H.soff[s];
+    ee = H.edge_base + H.soff[s + 1];
+  } else {
+    eb = t.strip_edge[H.strip_base + s];
+    ee = t.strip_edge[H.strip_base + s + 1];
+  }
+  if (stat_edges) *stat_edges = ee - eb;
   uint32_t bnd = 0, par = 0;
-  for (uint32_t e = eb; e < ee; e++) {
-    const double* E = t.edges + 4 * (size_t)e;
-    const int bits = count_segment(E[0], E[1], E[2], E[3], px, py);
-    if (bits) {
-      const uint32_t rb = 1u << t.edge_ring[e];
-      if (bits & kRingOnSegment) bnd |= rb;
-      if (bits & 2) par ^= rb;
+  const double4* E4 = (const double4*)t.edges;
+  uint32_t e = eb;
+#ifndef MGPU_EDGE_UNROLL
+#define MGPU_EDGE_UNROLL 2
+#endif
+  // two edges per step: both records' loads are in flight together
+  for (; MGPU_EDGE_UNROLL == 2 && e + 1 < ee; e += 2) {
+    const double4 A = E4[e], B = E4[e + 1];
+    const int ba = count_segment(A.x, A.y, A.z, A.w, px, py);
+    const int bb = count_segment(B.x, B.y, B.z, B.w, px, py);
+    if (ba | bb) {
+      const uint32_t ra = 1u << t.edge_ring[e], rb2 = 1u << t.edge_ring[e + 1];
+      if (ba & kRingOnSegment) bnd |= ra;
+      if (ba & 2) par ^= ra;
+      if (bb & kRingOnSegment) bnd |= rb2;
+      if (bb & 2) par ^= rb2;
+    }
+  }
+  for (; e < ee; e++) {
+    const double4 A = E4[e];
+    const int ba = count_segment(A.x, A.y, A.z, A.w, px, py);
+    if (ba) {
+      const uint32_t ra = 1u << t.edge_ring[e];
+      if (ba & kRingOnSegment) bnd |= ra;
+      if (ba & 2) par ^= ra;
     }
   }
   // one polygon, one ring (its envelope is the chip's): RayCrossingCounter's verdict

@@ -5,7 +5,8 @@ Times, on the bench workload (uniform NYC-bbox points x 263 zones, H3 res 9):
   cells      mgpu_points_to_cells alone (H3 geoToH3 of every point, 24 B/pt)
   join       the fused kernel
   join/noPIP border chips counted as misses (MGPU_ABLATE=1)
-  join/noprobe  no chip-table probe, i.e. projection + output protocol only (MGPU_ABLATE=2)
+  join/noprobe  H3 projection, no chip-table probe (MGPU_ABLATE=2)
+  join/noproj   no projection either: point loads + tile protocol only (MGPU_ABLATE=3)
 Prints one JSON object.  Kernel times come from HIP events around the launch.
 """
 import argparse
@@ -63,6 +64,7 @@ def main():
     out["join_ms"], out["pairs"] = t_join(0)
     out["join_nopip_ms"], out["pairs_nopip"] = t_join(1)
     out["join_noprobe_ms"], _ = t_join(2)
+    out["join_noproj_ms"], _ = t_join(3)
     print(json.dumps(out), flush=True)
 
 
