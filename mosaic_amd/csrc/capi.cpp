@@ -311,15 +311,20 @@ struct mgpu_chips {
 namespace {
 
 // Workspace layout (each region 256-byte aligned):
-//   [counters 8 x u64] [tile_count u32 x T] [tile_where u64 x T] [tile_off u64 x T]
+//   [counters 16 x u64] [tile_count u32 x T] [tile_where u64 x T] [tile_off u64 x T]
+//   [dirty tiles u32 x T] [cells near-tie queue u64 x (1 + kTieCap)]
 //   [records u64 x (T * tile points + pool)]
+// counters: [0] pairs [1] route near-ties [2] invalid points [3] candidates
+//           [5] pool records used [6] dirty tiles (u32) [8..] MGPU_STATS
 // T = tiles of the largest point batch reserved; pool = overflow records (tiles with
 // more pairs than points), at most the output capacity.
 constexpr size_t kWsCounters = 128;  // 16 x u64
 
 struct WsLayout {
-  size_t count, where, off, recs, total;
+  size_t count, where, off, dirty, ties, recs, total;
 };
+// near-tie queue of mgpu_points_to_cells (overflow: the fix kernel redoes every point)
+constexpr int64_t kTieCap = 1 << 16;
 
 WsLayout ws_layout(int64_t n_tiles, int64_t pool) {
   WsLayout L;
@@ -327,7 +332,9 @@ WsLayout ws_layout(int64_t n_tiles, int64_t pool) {
   L.count = kWsCounters;
   L.where = align_up(L.count + T * 4, 256);
   L.off = align_up(L.where + T * 8, 256);
-  L.recs = align_up(L.off + T * 8, 256);
+  L.dirty = align_up(L.off + T * 8, 256);
+  L.ties = align_up(L.dirty + T * 4, 256);
+  L.recs = align_up(L.ties + (size_t)(kTieCap + 1) * 8, 256);
   L.total = align_up(L.recs + (T * (size_t)mgpu::join_tile_points() + (size_t)std::max<int64_t>(pool, 0)) * 8, 256);
   return L;
 }
@@ -411,10 +418,13 @@ int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t is, int32_t res, const doubl
   if (n < 0 || (n > 0 && (!x || !y || !out_cell))) return fail(MGPU_E_INVALID_ARG, "bad point arrays");
   if (int32_t st = set_device(ctx->device)) return st;
   hipStream_t s = (hipStream_t)stream;
+  if (int32_t st = ensure_ws(ctx, 1)) return st;
   auto* counters = (unsigned long long*)ctx->ws;
+  auto* ties = (unsigned long long*)((uint8_t*)ctx->ws + ws_layout(1, 0).ties);
   HIP_TRY(hipMemsetAsync(counters, 0, kWsCounters, s));
+  HIP_TRY(hipMemsetAsync(ties, 0, 8, s));
   HIP_TRY(hipEventRecord(ctx->ev0, s));
-  HIP_TRY(mgpu::launch_cells(is, res, x, y, n, out_cell, counters, s));
+  HIP_TRY(mgpu::launch_cells(is, res, x, y, n, out_cell, counters, ties, kTieCap, s));
   HIP_TRY(hipEventRecord(ctx->ev1, s));
   unsigned long long h[8] = {0};
   // invalid coordinates must reach the caller as IllegalArgument / IllegalState,
@@ -783,6 +793,8 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   a.chips = chips->view;
   a.counters = (unsigned long long*)base;
   a.pool_used = a.counters + 5;
+  a.n_dirty = (uint32_t*)(a.counters + 6);
+  a.dirty = (uint32_t*)(base + L.dirty);
   a.pool_cap = pool;
   a.tile_count = (uint32_t*)(base + L.count);
   a.tile_where = (uint64_t*)(base + L.where);

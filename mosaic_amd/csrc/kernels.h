@@ -21,6 +21,8 @@ struct JoinArgs {
   uint64_t* recs;                   // [n_tiles * tile points] slots, then [pool_cap] overflow pool
   int64_t pool_cap;
   unsigned long long* pool_used;    // zeroed before launch
+  uint32_t* dirty;                  // [n_tiles] tiles with a near-tie point (for pip_fix_kernel)
+  uint32_t* n_dirty;                // zeroed before launch
   unsigned long long* counters;     // [0] pairs [1] near-ties [2] invalid [3] candidates
   int ablate;                       // profiling only (MGPU_ABLATE): 1 = no PIP (border = miss), 2 = no probe,
                                     // 3 = no projection either
@@ -39,8 +41,9 @@ struct EmitArgs {
   int32_t* out_poly;
 };
 
+// ties: [0] count, [1 .. tie_cap] point indices (zero ties[0] before launch)
 hipError_t launch_cells(int is, int res, const double* x, const double* y, int64_t n, int64_t* out,
-                        unsigned long long* counters, hipStream_t s);
+                        unsigned long long* counters, unsigned long long* ties, int64_t tie_cap, hipStream_t s);
 int64_t join_tiles(int64_t n);
 int64_t join_tile_points();
 hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s);

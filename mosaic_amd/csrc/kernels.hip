@@ -37,45 +37,71 @@ constexpr uint64_t kNoDst = ~0ULL;
 
 constexpr uint32_t kAllFaces = (1u << 20) - 1;
 
-// H3IndexSystem.pointToIndex: fast closed-form projection, H3 route on near-ties
-__device__ __forceinline__ uint64_t h3_cell(double lon_deg, double lat_deg, int res, double k_res, bool* ok,
-                                           bool* tie) {
-  *tie = false;
-  if (!isfinite(lat_deg) || !isfinite(lon_deg)) {
-    *ok = false;
-    return 0;
-  }
-  *ok = true;
-  h3::FastHex f = h3::fast_hex2d(h3::to_radians_fast(lat_deg), h3::to_radians_fast(lon_deg), res, k_res, kAllFaces);
-  if (f.tie) {
-    h3::route_face_ijk(h3::to_radians(lat_deg), h3::to_radians(lon_deg), res, &f.face, &f.ijk, tie);
-  }
-  return h3::face_ijk_to_h3(f.face, f.ijk, res);
-}
-
 __device__ __forceinline__ void count_wave(unsigned long long* ctr, bool pred) {
   unsigned long long b = __ballot(pred);
   if (b && (threadIdx.x & 63) == (__ffsll((long long)b) - 1)) atomicAdd(ctr, (unsigned long long)__popcll(b));
 }
 
+// The H3 route (h3_core.h route_face_ijk: H3's own formulas, libm calls out of line)
+// is needed for ~1 point in 1e6 -- those whose fast-path decisions fall inside the
+// tie band.  It is never called from the streaming kernels: a call makes the caller
+// allocate the callee-saved VGPRs the route's calls need (84+), which would cap the
+// streaming kernels' occupancy.  They hand the rare points to *_fix kernels instead.
+
+// IndexSystem.pointToIndex over a batch.  H3: fast projection; near-ties are queued
+// (ties[0] = count, ties[1 ..] = point indices) for cells_fix_kernel.
 template <int IS>
 __global__ __launch_bounds__(kBlock) void cells_kernel(const double* __restrict__ x, const double* __restrict__ y,
                                                        int64_t n, int res, int64_t* __restrict__ out,
-                                                       unsigned long long* __restrict__ counters) {
+                                                       unsigned long long* __restrict__ counters,
+                                                       unsigned long long* __restrict__ ties, int64_t tie_cap) {
   const double k_res = h3::k_of_res(res);
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (; i < n; i += stride) {
-    bool ok, tie = false;
+    bool ok;
     int64_t c = 0;
+    const double px = x[i], py = y[i];
     if (IS == MGPU_H3) {
-      c = (int64_t)h3_cell(x[i], y[i], res, k_res, &ok, &tie);
+      ok = isfinite(px) && isfinite(py);
+      if (ok) {
+        const h3::FastHex f = h3::fast_hex2d(h3::to_radians_fast(py), h3::to_radians_fast(px), res, k_res, kAllFaces);
+        if (f.tie) {
+          const unsigned long long q = atomicAdd(&ties[0], 1ull);
+          if ((int64_t)q < tie_cap) ties[1 + q] = (unsigned long long)i;
+        } else {
+          c = (int64_t)h3::face_ijk_to_h3(f.face, f.ijk, res);
+        }
+      }
     } else {
-      ok = bng::point_to_cell(x[i], y[i], res, &c);
+      ok = bng::point_to_cell(px, py, res, &c);
     }
     out[i] = c;
-    count_wave(&counters[1], tie);
     count_wave(&counters[2], !ok);
+  }
+}
+
+// The queued near-ties by the H3 route; if the queue overflowed, every point again
+// (fast path + route where needed).
+__global__ __launch_bounds__(kBlock) void cells_fix_kernel(const double* __restrict__ x, const double* __restrict__ y,
+                                                           int64_t n, int res, int64_t* __restrict__ out,
+                                                           unsigned long long* __restrict__ counters,
+                                                           const unsigned long long* __restrict__ ties,
+                                                           int64_t tie_cap) {
+  const int64_t nt = (int64_t)ties[0];
+  const bool all = nt > tie_cap;
+  const int64_t m = all ? n : nt;
+  const double k_res = h3::k_of_res(res);
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = all ? q : (int64_t)ties[1 + q];
+    const double px = x[i], py = y[i];
+    bool tie = false;
+    if (isfinite(px) && isfinite(py)) {
+      h3::FastHex f = h3::fast_hex2d(h3::to_radians_fast(py), h3::to_radians_fast(px), res, k_res, kAllFaces);
+      if (f.tie) h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, &tie);
+      out[i] = (int64_t)h3::face_ijk_to_h3(f.face, f.ijk, res);
+    }
+    count_wave(&counters[1], tie);
   }
 }
 
@@ -108,7 +134,10 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 //     == polygon-id order), block scan for positions within the tile, records
 //     {point-in-tile, polygon id} staged in LDS and written to the tile's slot as
 //     one contiguous run.
-// Chips past the 32nd of one cell (never seen in practice) are evaluated in phase 3.
+// Tiles with a near-tie point, a cell of more than 32 chips or more than kCandCap
+// candidates are abandoned by the streaming kernel after phase 1 and redone by
+// pip_fix_kernel, which evaluates list overflows on the spot and chips past the
+// 32nd of a cell in phase 3.
 constexpr int kCandCap = 1024;
 constexpr int kOutCap = 2048;
 constexpr int kMaskBits = 32;
@@ -131,7 +160,10 @@ __device__ __forceinline__ Range probe_range(const ChipTableView& t, uint64_t ke
   return Range{0, 0, 0};
 }
 
-template <int IS>
+// The chips of the point's cell.  *ok = false for non-finite coordinates.  *tie: in
+// the fast kernel (SLOW = false), the projection is in its tie band (the tile goes
+// to pip_fix_kernel); in the fix kernel, the H3 route's own near-tie flag (counted).
+template <int IS, bool SLOW>
 __device__ __forceinline__ Range chip_range(const ChipTableView& t, double px, double py, int res, bool res_match,
                                             bool* ok, bool* tie, int ablate) {
   *tie = false;
@@ -148,7 +180,13 @@ __device__ __forceinline__ Range chip_range(const ChipTableView& t, double px, d
     // outside the chip cells' bounding box no cell can match
     if (!(px >= t.bbox[0] && px <= t.bbox[2] && py >= t.bbox[1] && py <= t.bbox[3])) return Range{0, 0, 0};
     h3::FastHex f = h3::fast_hex2d(lat, lon, res, t.k_res, t.face_mask);
-    if (f.tie) h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, tie);
+    if (f.tie) {
+      if (!SLOW) {
+        *tie = true;
+        return Range{0, 0, 0};
+      }
+      h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, tie);
+    }
     if (t.probe_mode == kProbeDense) {
       const int32_t ga = f.ijk.i - f.ijk.k, gb = f.ijk.j - f.ijk.k;
       if (ablate == 2) return Range{0, (ga ^ gb) == 0x12345 ? 1u : 0u, 0};  // profiling: projection, no probe
@@ -169,7 +207,13 @@ __device__ __forceinline__ Range chip_range(const ChipTableView& t, double px, d
     return probe_range(t, key);
   }
   h3::FastHex f = h3::fast_hex2d(lat, lon, res, t.k_res > 0 ? t.k_res : h3::k_of_res(res), kAllFaces);
-  if (f.tie) h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, tie);
+  if (f.tie) {
+    if (!SLOW) {
+      *tie = true;
+      return Range{0, 0, 0};
+    }
+    h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, tie);
+  }
   return probe_range(t, h3::face_ijk_to_h3(f.face, f.ijk, res));
 }
 
@@ -177,11 +221,11 @@ __device__ __forceinline__ bool chip_is_core(const ChipTableView& t, const Range
   return j < 16 ? ((r.core >> j) & 1) : (t.chip_flags[r.first + j] & kChipCore) != 0;
 }
 
-#ifndef MGPU_JOIN_WAVES
-#define MGPU_JOIN_WAVES 1
-#endif
-template <int IS>
-__global__ __launch_bounds__(kBlock, MGPU_JOIN_WAVES) void pip_join_kernel(JoinArgs a) {
+// One tile (see the phase comment above).  SLOW = false: the streaming kernel; a
+// tile with a near-tie point is queued for pip_fix_kernel and abandoned after phase 1.
+// SLOW = true: the fix kernel; near-ties go through the H3 route.
+template <int IS, bool SLOW>
+__device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile) {
   __shared__ uint32_t s_ncand;
   __shared__ uint32_t s_wave_tot[kBlock / 64];
   __shared__ uint32_t s_first[kTile];   // first chip of the point's cell
@@ -196,7 +240,6 @@ __global__ __launch_bounds__(kBlock, MGPU_JOIN_WAVES) void pip_join_kernel(JoinA
 
   if (threadIdx.x == 0) s_ncand = 0;
   __syncthreads();
-  const uint32_t tile = blockIdx.x;
   const ChipTableView& t = a.chips;
   const int64_t base = (int64_t)tile * kTile;
   const bool res_match = a.res_match;
@@ -204,62 +247,36 @@ __global__ __launch_bounds__(kBlock, MGPU_JOIN_WAVES) void pip_join_kernel(JoinA
 
   // ---- phase 1: cells, core matches, candidates
   bool any_tie = false, any_bad = false;
-#ifndef MGPU_PREFETCH
-#define MGPU_PREFETCH 2
-#endif
-#if MGPU_PREFETCH == 1
-  // all of the lane's coordinates are loaded up front: one HBM latency per tile
-  double px_[kItems], py_[kItems];
-#pragma unroll
-  for (int k = 0; k < kItems; k++) {
-    const int64_t p = base + k * kBlock + threadIdx.x;
-    px_[k] = p < a.n ? a.x[p] : 0.0;
-    py_[k] = p < a.n ? a.y[p] : 0.0;
-  }
-#elif MGPU_PREFETCH == 2
   // one item ahead: item k + 1's coordinates load while item k computes
   double nx = 0.0, ny = 0.0;
   if (base + threadIdx.x < a.n) {
     nx = a.x[base + threadIdx.x];
     ny = a.y[base + threadIdx.x];
   }
-#endif
 #pragma unroll 1
   for (int k = 0; k < kItems; k++) {
     const int li = k * kBlock + threadIdx.x;
     const int64_t p = base + li;
     Range r{0, 0, 0};
     uint32_t mask = 0;
-#if MGPU_PREFETCH == 2
-    const double cx = nx, cy = ny;
+    const double px = nx, py = ny;
     if (k + 1 < kItems && p + kBlock < a.n) {
       nx = a.x[p + kBlock];
       ny = a.y[p + kBlock];
     }
-#endif
     if (p < a.n) {
       bool ok, tie;
-#if MGPU_PREFETCH == 1
-      // register-resident pick (a runtime index into px_ would go to scratch)
-      double px = px_[0], py = py_[0];
-#pragma unroll
-      for (int q = 1; q < kItems; q++) {
-        px = k == q ? px_[q] : px;
-        py = k == q ? py_[q] : py;
-      }
-#elif MGPU_PREFETCH == 2
-      const double px = cx, py = cy;
-#else
-      const double px = a.x[p], py = a.y[p];
-#endif
       if (a.ablate == 3) {  // profiling: no projection, no probe
         ok = true;
         tie = false;
       } else {
-        r = chip_range<IS>(t, px, py, a.res, res_match, &ok, &tie, a.ablate);
+        r = chip_range<IS, SLOW>(t, px, py, a.res, res_match, &ok, &tie, a.ablate);
       }
       any_bad |= !ok;
       any_tie |= tie;
+      // the streaming kernel keeps no sequential PIP path (its registers would cap
+      // occupancy): a cell with more than 32 chips sends the tile to pip_fix_kernel
+      if (!SLOW && r.count > (uint32_t)kMaskBits) any_tie = true;
       const uint32_t nj = r.count < (uint32_t)kMaskBits ? r.count : (uint32_t)kMaskBits;
       const uint32_t lowm = nj >= 32 ? 0xFFFFFFFFu : ((1u << nj) - 1);
       uint32_t border = ~r.core & lowm;
@@ -275,6 +292,8 @@ __global__ __launch_bounds__(kBlock, MGPU_JOIN_WAVES) void pip_join_kernel(JoinA
           if (j0 < (uint32_t)kCandCap) {
             s_cand_chip[j0] = r.first + j;
             s_cand_pj[j0] = (uint16_t)(li | (j << 10));
+          } else if (!SLOW) {
+            any_tie = true;  // list full: the fix kernel evaluates such tiles
           } else if (pip::chip_contains_strips(t, r.first + j, px, py)) {
             mask |= 1u << j;  // list full: evaluate here
           }
@@ -286,8 +305,18 @@ __global__ __launch_bounds__(kBlock, MGPU_JOIN_WAVES) void pip_join_kernel(JoinA
     s_cnt[li] = (uint16_t)(r.count > 0xFFFF ? 0xFFFF : r.count);
     s_mask[li] = mask;
   }
-  count_wave(&a.counters[1], any_tie);
   count_wave(&a.counters[2], any_bad);
+  if (SLOW) count_wave(&a.counters[1], any_tie);
+  if (!SLOW && __syncthreads_or(any_tie)) {
+    // a near-tie (or a case only the fix kernel handles): the tile is redone there
+    if (threadIdx.x == 0) {
+      const unsigned int q = atomicAdd(a.n_dirty, 1u);
+      a.dirty[q] = tile;
+      a.tile_count[tile] = 0;
+      a.tile_where[tile] = kNoDst;
+    }
+    return;
+  }
   __syncthreads();
   const uint32_t ncand = s_ncand < (uint32_t)kCandCap ? s_ncand : (uint32_t)kCandCap;
   if (threadIdx.x == 0 && s_ncand) atomicAdd(&a.counters[3], (unsigned long long)s_ncand);
@@ -326,7 +355,7 @@ __global__ __launch_bounds__(kBlock, MGPU_JOIN_WAVES) void pip_join_kernel(JoinA
     const int li = l0 + k;
     mine += __popc(s_mask[li]);
     const uint32_t cnt = s_cnt[li];
-    if (cnt > (uint32_t)kMaskBits) {  // chips past the 32nd of the cell
+    if (SLOW && cnt > (uint32_t)kMaskBits) {  // chips past the 32nd of the cell
       const int64_t p = base + li;
       const Range r{s_first[li], cnt, 0};
       for (uint32_t j = kMaskBits; j < cnt; j++)
@@ -378,7 +407,7 @@ __global__ __launch_bounds__(kBlock, MGPU_JOIN_WAVES) void pip_join_kernel(JoinA
     const uint32_t nj = cnt < (uint32_t)kMaskBits ? cnt : (uint32_t)kMaskBits;
     for (uint32_t j = 0; j < cnt; j++) {
       bool hit;
-      if (j < nj) {
+      if (!SLOW || j < nj) {
         hit = (m >> j) & 1;
       } else {
         const Range r{first, cnt, 0};
@@ -398,6 +427,21 @@ __global__ __launch_bounds__(kBlock, MGPU_JOIN_WAVES) void pip_join_kernel(JoinA
   if (!staged || !rec) return;
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < agg; i += kBlock) rec[i] = ((uint64_t)s_out_li[i] << 32) | (uint32_t)s_out_poly[i];
+}
+
+template <int IS>
+__global__ __launch_bounds__(kBlock) void pip_join_kernel(JoinArgs a) {
+  join_tile<IS, false>(a, blockIdx.x);
+}
+
+// The tiles queued by pip_join_kernel, with the H3 route for their near-ties.
+template <int IS>
+__global__ __launch_bounds__(kBlock) void pip_fix_kernel(JoinArgs a) {
+  const uint32_t nd = *a.n_dirty;
+  for (uint32_t q = blockIdx.x; q < nd; q += gridDim.x) {
+    join_tile<IS, true>(a, a.dirty[q]);
+    __syncthreads();
+  }
 }
 
 // Exclusive scan of the tiles' pair counts (one workgroup; ~1e5 tiles per 1e8
@@ -474,14 +518,18 @@ __global__ __launch_bounds__(kBlock) void st_contains_kernel(ChipTableView t, co
 // ---------------------------------------------------------------- launchers
 
 hipError_t launch_cells(int is, int res, const double* x, const double* y, int64_t n, int64_t* out,
-                        unsigned long long* counters, hipStream_t s) {
+                        unsigned long long* counters, unsigned long long* ties, int64_t tie_cap, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   int64_t blocks = (n + kBlock - 1) / kBlock;
   if (blocks > 256 * 64) blocks = 256 * 64;
-  if (is == MGPU_H3)
-    hipLaunchKernelGGL(cells_kernel<MGPU_H3>, dim3((unsigned)blocks), dim3(kBlock), 0, s, x, y, n, res, out, counters);
-  else
-    hipLaunchKernelGGL(cells_kernel<MGPU_BNG>, dim3((unsigned)blocks), dim3(kBlock), 0, s, x, y, n, res, out, counters);
+  if (is == MGPU_H3) {
+    hipLaunchKernelGGL(cells_kernel<MGPU_H3>, dim3((unsigned)blocks), dim3(kBlock), 0, s, x, y, n, res, out, counters,
+                       ties, tie_cap);
+    hipLaunchKernelGGL(cells_fix_kernel, dim3(256), dim3(kBlock), 0, s, x, y, n, res, out, counters, ties, tie_cap);
+  } else {
+    hipLaunchKernelGGL(cells_kernel<MGPU_BNG>, dim3((unsigned)blocks), dim3(kBlock), 0, s, x, y, n, res, out,
+                       counters, ties, tie_cap);
+  }
   return hipGetLastError();
 }
 
@@ -490,10 +538,13 @@ int64_t join_tile_points() { return kTile; }
 
 hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s) {
   if (a.n_tiles <= 0) return hipSuccess;
-  if (is == MGPU_H3)
+  if (is == MGPU_H3) {
     hipLaunchKernelGGL(pip_join_kernel<MGPU_H3>, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, a);
-  else
+    const unsigned fix_blocks = (unsigned)(a.n_tiles < 512 ? a.n_tiles : 512);
+    hipLaunchKernelGGL(pip_fix_kernel<MGPU_H3>, dim3(fix_blocks), dim3(kBlock), 0, s, a);
+  } else {
     hipLaunchKernelGGL(pip_join_kernel<MGPU_BNG>, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, a);
+  }
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.tile_count, a.n_tiles, e.tile_off,
                      a.counters);
   hipLaunchKernelGGL(pair_emit_kernel, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, e);
