@@ -20,6 +20,7 @@
 #include "chip_table.h"
 #include "h3_core.h"
 #include "kernels.h"
+#include "pip_core.h"
 #include "wkb.h"
 
 namespace {
@@ -290,6 +291,73 @@ void build_strips(int64_t n_chips, std::vector<uint8_t>& cflags, const std::vect
   st.chip_strip[n_chips] = (uint32_t)(st.strip_edge.size() - 1);
 }
 
+// Does segment a-b meet the closed box [x0, x1] x [y0, y1]?  (The callers widen the
+// box by a margin that dwarfs the rounding of this test.)
+bool seg_hits_box(double ax, double ay, double bx, double by, double x0, double y0, double x1, double y1) {
+  if (std::max(ax, bx) < x0 || std::min(ax, bx) > x1 || std::max(ay, by) < y0 || std::min(ay, by) > y1) return false;
+  const double dx = bx - ax, dy = by - ay;
+  const double cx[4] = {x0, x1, x0, x1}, cy[4] = {y0, y0, y1, y1};
+  int pos = 0, neg = 0;
+  for (int k = 0; k < 4; k++) {
+    const double cr = dx * (cy[k] - ay) - dy * (cx[k] - ax);
+    pos += cr > 0;
+    neg += cr < 0;
+  }
+  return !(pos == 4 || neg == 4);
+}
+
+// Classification grid of chip c (chip_table.h ChipHdr): cell state 2 where a widened
+// cell rectangle meets an edge, else the PointLocator's verdict at the cell centre.
+void build_grid(const mgpu::ChipTableView& hv, uint32_t c, const mgpu::wkb::Flat& geo, mgpu::ChipHdr& h) {
+  using namespace mgpu;
+  const double e0 = h.env[0], e1 = h.env[1], e2 = h.env[2], e3 = h.env[3];
+  const double W = e2 - e0, H = e3 - e1;
+  h.sx = W > 0 ? kGrid / W : 0.0;
+  h.sy = H > 0 ? kGrid / H : 0.0;
+  uint8_t st[kGrid][kGrid];
+  memset(st, 0xFF, sizeof st);  // 0xFF: not yet known
+  if (!(W > 0) || !(H > 0)) {
+    for (int gy = 0; gy < kGrid; gy++) h.grid[gy] = 0xAAAAAAAAu;  // all mixed
+    return;
+  }
+  // margin in cell units: far above the rounding of grid_index and of this test
+  const double mag = std::max(std::max(std::fabs(e0), std::fabs(e2)), std::max(std::fabs(e1), std::fabs(e3)));
+  const double ulp = std::nextafter(mag, INFINITY) - mag;
+  const double mu_x = 1e-6 + 64 * ulp * h.sx, mu_y = 1e-6 + 64 * ulp * h.sy;
+  const uint32_t r0 = hv.part_ring[hv.chip_part[c]], r1 = hv.part_ring[hv.chip_part[c + 1]];
+  for (uint32_t r = r0; r < r1; r++) {
+    for (uint32_t i = geo.ring_vtx[r] + 1; i < geo.ring_vtx[r + 1]; i++) {
+      const double ax = geo.vtx[2 * i - 2], ay = geo.vtx[2 * i - 1], bx = geo.vtx[2 * i], by = geo.vtx[2 * i + 1];
+      // candidate cells: the segment's bounding box, one cell of slack each way
+      int gx0 = (int)std::floor((std::min(ax, bx) - e0) * h.sx) - 1, gx1 = (int)std::floor((std::max(ax, bx) - e0) * h.sx) + 1;
+      int gy0 = (int)std::floor((std::min(ay, by) - e1) * h.sy) - 1, gy1 = (int)std::floor((std::max(ay, by) - e1) * h.sy) + 1;
+      gx0 = std::max(gx0, 0), gy0 = std::max(gy0, 0), gx1 = std::min(gx1, kGrid - 1), gy1 = std::min(gy1, kGrid - 1);
+      for (int gy = gy0; gy <= gy1; gy++)
+        for (int gx = gx0; gx <= gx1; gx++) {
+          if (st[gy][gx] == kCellMixed) continue;
+          // cell gx spans [e0 + gx / sx, e0 + (gx + 1) / sx]; the clamped last cell
+          // also takes everything up to the envelope edge
+          const double x0 = e0 + (gx - mu_x) / h.sx, x1 = e0 + (gx + 1 + mu_x) / h.sx;
+          const double y0 = e1 + (gy - mu_y) / h.sy, y1 = e1 + (gy + 1 + mu_y) / h.sy;
+          if (seg_hits_box(ax, ay, bx, by, x0, y0, x1, y1)) st[gy][gx] = kCellMixed;
+        }
+    }
+  }
+  for (int gy = 0; gy < kGrid; gy++) {
+    uint32_t row = 0;
+    for (int gx = 0; gx < kGrid; gx++) {
+      uint32_t v = st[gy][gx];
+      if (v != kCellMixed) {
+        const double cxp = e0 + (gx + 0.5) / h.sx, cyp = e1 + (gy + 0.5) / h.sy;
+        const int loc = pip::chip_locate(hv, c, cxp, cyp);
+        v = loc == pip::kInterior ? kCellIn : (loc == pip::kExterior ? kCellOut : kCellMixed);
+      }
+      row |= v << (2 * gx);
+    }
+    h.grid[gy] = row;
+  }
+}
+
 }  // namespace
 
 struct mgpu_ctx {
@@ -542,26 +610,28 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
   Strips strips;
   build_strips(n_chips, cflags, cpart, cenv, geo, strips);
   std::vector<mgpu::ChipHdr> chdr(n_chips);
-  for (int64_t c = 0; c < n_chips; c++) {
-    mgpu::ChipHdr& h = chdr[c];
-    memset(&h, 0, sizeof h);
-    for (int k = 0; k < 4; k++) h.env[k] = cenv[4 * c + k];
-    h.y0 = strips.chip_sy[2 * c];
-    h.inv_h = strips.chip_sy[2 * c + 1];
-    h.strip_base = strips.chip_strip[c];
-    h.n_strips = (uint16_t)(strips.chip_strip[c + 1] - strips.chip_strip[c]);
-    h.flags = cflags[c];
-    const uint32_t pb = cpart[c], pe = cpart[c + 1];
-    h.single_ring = (pe - pb == 1 && geo.part_ring[pb + 1] - geo.part_ring[pb] == 1 &&
-                     !(cflags[c] & mgpu::kChipMulti)) ? 1 : 0;
-    h.poly = cpoly[c];
-    h.edge_base = strips.strip_edge[h.strip_base];
-    if (h.n_strips <= mgpu::kHdrStrips) {
-      for (int q = 0; q <= h.n_strips; q++) {
-        const uint32_t rel = strips.strip_edge[h.strip_base + q] - h.edge_base;
-        if (rel > 0xFFFF) return fail(MGPU_E_INTERNAL, "chip %lld: strip offsets exceed 16 bits", (long long)c);
-        h.soff[q] = (uint16_t)rel;
-      }
+  {
+    // host view of the flattened geometry for the grid classification
+    mgpu::ChipTableView hv{};
+    hv.chip_flags = cflags.data();
+    hv.chip_part = cpart.data();
+    hv.chip_env = cenv.data();
+    hv.part_ring = geo.part_ring.data();
+    hv.ring_vtx = geo.ring_vtx.data();
+    hv.ring_env = geo.ring_env.data();
+    hv.vtx = geo.vtx.data();
+    for (int64_t c = 0; c < n_chips; c++) {
+      mgpu::ChipHdr& h = chdr[c];
+      memset(&h, 0, sizeof h);
+      for (int k = 0; k < 4; k++) h.env[k] = cenv[4 * c + k];
+      h.inv_h = strips.chip_sy[2 * c + 1];
+      h.strip_base = strips.chip_strip[c];
+      h.n_strips = (uint16_t)(strips.chip_strip[c + 1] - strips.chip_strip[c]);
+      h.flags = cflags[c];
+      const uint32_t pb = cpart[c], pe = cpart[c + 1];
+      h.single_ring = (pe - pb == 1 && geo.part_ring[pb + 1] - geo.part_ring[pb] == 1 &&
+                       !(cflags[c] & mgpu::kChipMulti)) ? 1 : 0;
+      if (h.n_strips) build_grid(hv, (uint32_t)c, geo, h);
     }
   }
   // H3: probe by lattice key when possible (chip_table.h)

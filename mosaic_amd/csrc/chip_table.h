@@ -69,23 +69,38 @@ struct alignas(16) HashSlot {
   uint16_t core_mask;
 };
 
-// Everything the join's PIP step needs about one chip, in 128 bytes (the per-array
-// form above stays for st_contains and the sequential PointLocator).  Chips with at
-// most kHdrStrips strips carry their strip boundaries inline (edge offsets relative
-// to edge_base); others read strip_edge[strip_base + s].
-constexpr int kHdrStrips = 31;
-struct alignas(128) ChipHdr {
+// Everything the join's PIP step needs about one border chip, in two 64-byte lines
+// (the per-array form above stays for st_contains and the sequential PointLocator).
+//
+// Classification grid: the chip envelope cut into kGrid x kGrid cells, cell (gx, gy)
+// = the points whose computed indices gx = (int)((x - minx) * sx), gy likewise
+// (clamped) are gx, gy.  State 1 / 0: every such point is INTERIOR / EXTERIOR, so
+// contains() is decided by one lookup; 2: mixed, use the strip's edges.  A cell is
+// given state 0 / 1 only if its rectangle, widened by a margin far above the index
+// rounding error, meets no chip edge: all its points then lie in one connected
+// component of the plane minus the chip boundary, at a positive distance from it,
+// where JTS's robust PointLocator returns the topological location -- the one it
+// returns for the cell centre (evaluated at upload with the same PointLocator).
+constexpr int kGrid = 16;
+struct alignas(64) ChipHdr {
   double env[4];        // minx, miny, maxx, maxy
-  double y0, inv_h;     // strip_of() parameters
+  double sx, sy;        // grid scales kGrid / width, kGrid / height (0: one cell)
+  double inv_h;         // strip scale S / height (strip_of with y0 = miny)
   uint32_t strip_base;  // first strip (index into strip_edge)
   uint16_t n_strips;
   uint8_t flags;        // ChipFlags
   uint8_t single_ring;  // one polygon with one ring, not a collection
-  int32_t poly;         // polygon id
-  uint32_t edge_base;   // first edge record of the chip's strips
-  uint16_t soff[kHdrStrips + 1];  // strip s = edges [edge_base + soff[s], edge_base + soff[s + 1])
+  uint32_t grid[kGrid]; // row gy: 2 bits per cell gx (0 out, 1 in, 2 mixed)
 };
 static_assert(sizeof(ChipHdr) == 128, "ChipHdr is two lines");
+
+enum GridState { kCellOut = 0, kCellIn = 1, kCellMixed = 2 };
+
+MGPU_HDI_FWD int grid_index(double v, double v0, double scale) {
+  double g = (v - v0) * scale;
+  int i = g < (double)kGrid ? (int)g : kGrid - 1;
+  return i < 0 ? 0 : i;
+}
 
 struct DenseFace {
   int32_t a0, b0;

@@ -139,7 +139,9 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 // pip_fix_kernel, which evaluates list overflows on the spot and chips past the
 // 32nd of a cell in phase 3.
 constexpr int kCandCap = 1024;
+constexpr int kMixCap = 512;    // mixed-cell candidates (phase 2b), after the list in s_buf
 constexpr int kOutCap = 2048;
+static_assert(kCandCap * 6 + kMixCap * 2 <= kOutCap * 6, "phase 1-2 lists fit the staging buffer");
 constexpr int kMaskBits = 32;
 
 // chips of a cell: first, count, core mask (bits < 16)
@@ -226,7 +228,7 @@ __device__ __forceinline__ bool chip_is_core(const ChipTableView& t, const Range
 // SLOW = true: the fix kernel; near-ties go through the H3 route.
 template <int IS, bool SLOW>
 __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile) {
-  __shared__ uint32_t s_ncand;
+  __shared__ uint32_t s_ncand, s_nmix;
   __shared__ uint32_t s_wave_tot[kBlock / 64];
   __shared__ uint32_t s_first[kTile];   // first chip of the point's cell
   __shared__ uint32_t s_mask[kTile];    // bit j: chip first + j matches (j < 32)
@@ -238,7 +240,10 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   int32_t* s_out_poly = (int32_t*)s_buf;                          // [kOutCap]
   uint16_t* s_out_li = (uint16_t*)(s_buf + kOutCap * 4);          // [kOutCap]
 
-  if (threadIdx.x == 0) s_ncand = 0;
+  if (threadIdx.x == 0) {
+    s_ncand = 0;
+    s_nmix = 0;
+  }
   __syncthreads();
   const ChipTableView& t = a.chips;
   const int64_t base = (int64_t)tile * kTile;
@@ -321,29 +326,77 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   const uint32_t ncand = s_ncand < (uint32_t)kCandCap ? s_ncand : (uint32_t)kCandCap;
   if (threadIdx.x == 0 && s_ncand) atomicAdd(&a.counters[3], (unsigned long long)s_ncand);
 
-  // ---- phase 2: lane per candidate
-#ifdef MGPU_STATS
-  uint32_t st_edges = 0, st_strip = 0, st_hit = 0;
-#endif
+  // ---- phase 2: lane per candidate: envelope / rectangle / classification grid.
+  // Candidates in a mixed grid cell (~1 in 8) are listed again and evaluated in
+  // phase 2b, so the strip walk runs once per tile instead of in every wave.
+  uint16_t* s_mix = (uint16_t*)(s_buf + kCandCap * 6);  // [kMixCap] candidate index
+  bool redo = false;
   for (uint32_t c = threadIdx.x; c < ncand; c += kBlock) {
     const uint32_t ch = s_cand_chip[c];
     const uint32_t pj = s_cand_pj[c];
     const int li = pj & 1023;
     const int64_t p = base + li;
-#ifdef MGPU_STATS
-    uint32_t ne = 0xFFFFFFFFu;
-    const bool hit = pip::chip_contains_strips(t, ch, a.x[p], a.y[p], &ne);
-    if (ne != 0xFFFFFFFFu) { st_strip++; st_edges += ne; }
-    st_hit += hit;
+    bool hit;
+    if (a.ablate == 4) {  // profiling: candidate list only
+      hit = (ch ^ pj) == 0x7FFFFFFF;
+    } else {
+      const double px = a.x[p], py = a.y[p];
+      const int q = pip::chip_quick(t, ch, px, py);
+      hit = q == pip::kQuickYes;
+      if (q >= pip::kQuickStrips && a.ablate != 5) {
+        const uint32_t m = atomicAdd(&s_nmix, 1u);
+        if (m < (uint32_t)kMixCap && (SLOW || q == pip::kQuickStrips)) {
+          s_mix[m] = (uint16_t)c;
+        } else if (!SLOW) {
+          redo = true;  // list full / chip without strip index: pip_fix_kernel
+        } else {
+          hit = q == pip::kQuickStrips ? pip::chip_contains_mixed(t, ch, px, py)
+                                       : pip::chip_locate(t, ch, px, py) == pip::kInterior;
+        }
+      }
+    }
     if (hit) atomicOr(&s_mask[li], 1u << (pj >> 10));
-#else
-    if (pip::chip_contains_strips(t, ch, a.x[p], a.y[p])) atomicOr(&s_mask[li], 1u << (pj >> 10));
+  }
+  if (!SLOW && __syncthreads_or(redo)) {
+    if (threadIdx.x == 0) {
+      const unsigned int q = atomicAdd(a.n_dirty, 1u);
+      a.dirty[q] = tile;
+      a.tile_count[tile] = 0;
+      a.tile_where[tile] = kNoDst;
+    }
+    return;
+  }
+  __syncthreads();
+  const uint32_t nmix = s_nmix < (uint32_t)kMixCap ? s_nmix : (uint32_t)kMixCap;
+#ifdef MGPU_STATS
+  uint32_t st_edges = 0;
 #endif
+  for (uint32_t m = threadIdx.x; m < nmix; m += kBlock) {
+    const uint32_t c = s_mix[m];
+    const uint32_t ch = s_cand_chip[c];
+    const uint32_t pj = s_cand_pj[c];
+    const int li = pj & 1023;
+    const int64_t p = base + li;
+    const double px = a.x[p], py = a.y[p];
+    bool hit;
+    if (SLOW && (t.chip_hdr[ch].flags & kChipNoStrips)) {
+      hit = pip::chip_locate(t, ch, px, py) == pip::kInterior;
+    } else {
+#ifdef MGPU_STATS
+      uint32_t ne = 0;
+      hit = pip::chip_contains_mixed(t, ch, px, py, &ne);
+      st_edges += ne;
+#else
+      hit = pip::chip_contains_mixed(t, ch, px, py);
+#endif
+    }
+    if (hit) atomicOr(&s_mask[li], 1u << (pj >> 10));
   }
 #ifdef MGPU_STATS
-  atomicAdd(&a.counters[8], (unsigned long long)st_edges);
-  atomicAdd(&a.counters[9], (unsigned long long)st_strip);
-  atomicAdd(&a.counters[10], (unsigned long long)st_hit);
+  if (threadIdx.x == 0) {
+    atomicAdd(&a.counters[8], (unsigned long long)s_nmix);
+  }
+  atomicAdd(&a.counters[9], (unsigned long long)st_edges);
 #endif
   __syncthreads();
 

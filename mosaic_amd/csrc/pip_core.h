@@ -197,59 +197,59 @@ MGPU_HDI int chip_locate(const ChipTableView& t, uint32_t c, double px, double p
 // same decision as chip_locate() -- envelope, rectangle shortcut, PointLocator over
 // the rings -- with each ring's RayCrossingCounter run over the edges of the
 // point's strip only.  Chips flagged kChipNoStrips go to chip_locate().
-MGPU_HDI bool chip_contains_strips(const ChipTableView& t, uint32_t c, double px, double py,
-                                   uint32_t* stat_edges = nullptr) {
+// The quick part of contains(): flags, envelope, rectangle shortcut and the
+// classification grid.  Returns kQuickNo / kQuickYes, or kQuickStrips (a mixed grid
+// cell: chip_contains_mixed decides) / kQuickSequential (chip without strip index).
+enum QuickVerdict { kQuickNo = 0, kQuickYes = 1, kQuickStrips = 2, kQuickSequential = 3 };
+
+MGPU_HDI int chip_quick(const ChipTableView& t, uint32_t c, double px, double py) {
   const ChipHdr& H = t.chip_hdr[c];
   const double e0 = H.env[0], e1 = H.env[1], e2 = H.env[2], e3 = H.env[3];
   const uint8_t fl = H.flags;
-  if (fl & (kChipEmpty | kChipNoGeom)) return false;
-  if (!(px >= e0 && px <= e2 && py >= e1 && py <= e3)) return false;
-  if (fl & kChipRect) return !(px == e0 || px == e2 || py == e1 || py == e3);
-  if (fl & kChipNoStrips) return chip_locate(t, c, px, py) == kInterior;
-  const int S = (int)H.n_strips;
-  const int s = strip_of(py, H.y0, H.inv_h, S);
-  uint32_t eb, ee;
-#ifndef MGPU_INLINE_STRIPS
-#define MGPU_INLINE_STRIPS 1
-#endif
-  if (MGPU_INLINE_STRIPS && S <= kHdrStrips) {
-    eb = H.edge_base + H.soff[s];
-    ee = H.edge_base + H.soff[s + 1];
-  } else {
-    eb = t.strip_edge[H.strip_base + s];
-    ee = t.strip_edge[H.strip_base + s + 1];
-  }
+  if (fl & (kChipEmpty | kChipNoGeom)) return kQuickNo;
+  if (!(px >= e0 && px <= e2 && py >= e1 && py <= e3)) return kQuickNo;
+  if (fl & kChipRect) return (px == e0 || px == e2 || py == e1 || py == e3) ? kQuickNo : kQuickYes;
+  if (fl & kChipNoStrips) return kQuickSequential;
+  const int gx = grid_index(px, e0, H.sx), gy = grid_index(py, e1, H.sy);
+  const uint32_t st = (H.grid[gy] >> (2 * gx)) & 3;
+  return st == kCellMixed ? kQuickStrips : (st == kCellIn ? kQuickYes : kQuickNo);
+}
+
+// contains() for a point in a mixed grid cell of chip c: RayCrossingCounter over the
+// edges of the point's y-strip (MGPU_EDGE_STEP records in flight per step), then PointLocator
+// over the rings' verdicts.
+MGPU_HDI bool chip_contains_mixed(const ChipTableView& t, uint32_t c, double px, double py,
+                                  uint32_t* stat_edges = nullptr) {
+  const ChipHdr& H = t.chip_hdr[c];
+  const int s = strip_of(py, H.env[1], H.inv_h, (int)H.n_strips);
+  const uint32_t eb = t.strip_edge[H.strip_base + s], ee = t.strip_edge[H.strip_base + s + 1];
   if (stat_edges) *stat_edges = ee - eb;
-  uint32_t bnd = 0, par = 0;
   const double4* E4 = (const double4*)t.edges;
-  uint32_t e = eb;
-#ifndef MGPU_EDGE_UNROLL
-#define MGPU_EDGE_UNROLL 2
+  const bool one_ring = H.single_ring;
+  uint32_t bnd = 0, par = 0;
+#ifndef MGPU_EDGE_STEP
+#define MGPU_EDGE_STEP 2
 #endif
-  // two edges per step: both records' loads are in flight together
-  for (; MGPU_EDGE_UNROLL == 2 && e + 1 < ee; e += 2) {
-    const double4 A = E4[e], B = E4[e + 1];
-    const int ba = count_segment(A.x, A.y, A.z, A.w, px, py);
-    const int bb = count_segment(B.x, B.y, B.z, B.w, px, py);
-    if (ba | bb) {
-      const uint32_t ra = 1u << t.edge_ring[e], rb2 = 1u << t.edge_ring[e + 1];
-      if (ba & kRingOnSegment) bnd |= ra;
-      if (ba & 2) par ^= ra;
-      if (bb & kRingOnSegment) bnd |= rb2;
-      if (bb & 2) par ^= rb2;
-    }
-  }
-  for (; e < ee; e++) {
-    const double4 A = E4[e];
-    const int ba = count_segment(A.x, A.y, A.z, A.w, px, py);
-    if (ba) {
-      const uint32_t ra = 1u << t.edge_ring[e];
-      if (ba & kRingOnSegment) bnd |= ra;
-      if (ba & 2) par ^= ra;
+  for (uint32_t e = eb; e < ee; e += MGPU_EDGE_STEP) {
+    const uint32_t l = ee - 1;
+    int bits[MGPU_EDGE_STEP];
+    double4 R[MGPU_EDGE_STEP];
+#pragma unroll
+    for (int k = 0; k < MGPU_EDGE_STEP; k++) R[k] = E4[e + k < l ? e + k : l];
+#pragma unroll
+    for (int k = 0; k < MGPU_EDGE_STEP; k++)
+      bits[k] = e + k < ee ? count_segment(R[k].x, R[k].y, R[k].z, R[k].w, px, py) : 0;
+#pragma unroll
+    for (int k = 0; k < MGPU_EDGE_STEP; k++) {
+      if (!bits[k]) continue;
+      const uint32_t rb = one_ring ? 1u : 1u << t.edge_ring[e + k];
+      if (bits[k] & kRingOnSegment) bnd |= rb;
+      if (bits[k] & 2) par ^= rb;
     }
   }
   // one polygon, one ring (its envelope is the chip's): RayCrossingCounter's verdict
-  if (H.single_ring) return !(bnd & 1) && (par & 1);
+  if (one_ring) return !(bnd & 1) && (par & 1);
+  const uint8_t fl = H.flags;
   const uint32_t pb = t.chip_part[c], pe = t.chip_part[c + 1];
   const uint32_t r0 = t.part_ring[pb];
   bool is_in = false;
@@ -283,6 +283,17 @@ MGPU_HDI bool chip_contains_strips(const ChipTableView& t, uint32_t c, double px
   if (!(fl & kChipMulti)) return single == kInterior;
   if (n_bnd & 1) return false;
   return n_bnd > 0 || is_in;
+}
+
+// Geometry.contains(point) for sorted chip `c` -- the same decision as chip_locate()
+// (envelope, rectangle shortcut, PointLocator over the rings) through the chip's
+// classification grid and strip index.
+MGPU_HDI bool chip_contains_strips(const ChipTableView& t, uint32_t c, double px, double py,
+                                   uint32_t* stat_edges = nullptr) {
+  const int q = chip_quick(t, c, px, py);
+  if (q == kQuickStrips) return chip_contains_mixed(t, c, px, py, stat_edges);
+  if (q == kQuickSequential) return chip_locate(t, c, px, py) == kInterior;
+  return q == kQuickYes;
 }
 
 }  // namespace pip

@@ -7,6 +7,8 @@ Times, on the bench workload (uniform NYC-bbox points x 263 zones, H3 res 9):
   join/noPIP border chips counted as misses (MGPU_ABLATE=1)
   join/noprobe  H3 projection, no chip-table probe (MGPU_ABLATE=2)
   join/noproj   no projection either: point loads + tile protocol only (MGPU_ABLATE=3)
+  join/listonly candidates listed, none evaluated (MGPU_ABLATE=4)
+  join/envonly  candidates evaluated by the chip envelope only (MGPU_ABLATE=5)
 Prints one JSON object.  Kernel times come from HIP events around the launch.
 """
 import argparse
@@ -65,6 +67,8 @@ def main():
     out["join_nopip_ms"], out["pairs_nopip"] = t_join(1)
     out["join_noprobe_ms"], _ = t_join(2)
     out["join_noproj_ms"], _ = t_join(3)
+    out["join_listonly_ms"], _ = t_join(4)
+    out["join_envonly_ms"], _ = t_join(5)
     print(json.dumps(out), flush=True)
 
 
