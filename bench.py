@@ -12,10 +12,17 @@ Multi-GPU (torchrun, one process per GPU): points are sharded by contiguous id r
 and replicated with one RCCL broadcast, per-rank pair counts are all-gathered (RCCL)
 for the global output offsets.  Time = max over ranks of the barrier-bracketed K steps.
 
-Also reported: the fused kernel's achieved bandwidth against the HBM roofline
-(algorithmic bytes: 16 B per point read + 12 B per output pair written; kernel time
-from HIP events on the launch stream) and a CPU baseline (the oracle's multithreaded
-restatement of the reference path on a bounded sample, rank 0, N=1 only).
+A step is one mgpu_pip_join call: pip_join_kernel (cell id -> chip probe -> is_core
+OR st_contains -> per-tile pair records), pip_fix_kernel (tiles holding an H3 near-tie),
+tile_scan_kernel and pair_emit_kernel (ordered (point_id, polygon_id) output).
+
+Also reported: the dominant kernel's (pip_join_kernel) achieved bandwidth against the
+HBM roofline -- algorithmic bytes per launch = 16 B per point read + 8 B per pair
+record written + 12 B per 1024-point tile, over its average duration
+measured with HIP events on the launch stream -- the HBM bytes the PMC counters saw
+(profiles/pmc_join_traffic.json, when it was measured on this workload), and a CPU
+baseline: the oracle's multithreaded C restatement of the reference path on a
+bounded sample (rank 0, N=1 only).
 """
 import argparse
 import json
@@ -60,7 +67,8 @@ def gen_points(n, begin, seed, dev):
 
 
 def cpu_baseline(chips, res, seed, target_s):
-    """Oracle (CPU restatement of the reference path) on a bounded sample: points/s."""
+    """Oracle (CPU restatement of the reference path) on a bounded sample: points/s.
+    Chunks of up to 20M points until ~target_s seconds of join time are spent."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
@@ -76,13 +84,18 @@ def cpu_baseline(chips, res, seed, target_s):
         return time.perf_counter() - t
 
     n0 = 200_000
-    dt = run(n0)
-    n = int(min(60_000_000, max(n0, n0 * target_s / max(dt, 1e-6))))
-    dt = run(n)
-    return {"value": n / dt, "unit": "points/s", "cores": threads, "kind": "port",
-            "sample": "%d uniform NYC-bbox points x 263 zones, H3 res %d, oracle pip_join (C restatement of "
-                      "H3 geoToH3 + hash join + JTS PointLocator, per-candidate WKB re-parse), %d threads, %.1f s"
-                      % (n, res, threads, dt)}
+    dt0 = run(n0)
+    rate = n0 / max(dt0, 1e-6)
+    total_n, total_t = 0, 0.0
+    while total_t < target_s:
+        n = int(min(20_000_000, max(n0, rate * min(target_s - total_t, 5.0))))
+        total_t += run(n)
+        total_n += n
+    return {"value": total_n / total_t, "unit": "points/s", "cores": threads, "kind": "port",
+            "sample": "%d uniform NYC-bbox points (chunks of <= 20M) x 263 zones, H3 res %d, oracle pip_join "
+                      "(C restatement of H3 geoToH3 + hash join on cell + JTS PointLocator with per-candidate WKB "
+                      "re-parse, as the reference's JVM path does), %d threads, %.1f s"
+                      % (total_n, res, threads, total_t)}
 
 
 def main():
@@ -132,12 +145,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    kms = []
+    kms, sms = [], []
     pairs = 0
     ties = 0
     for _ in range(a.steps):
         r = step()
         kms.append(r.stats["kernel_ms"])
+        sms.append(r.stats["stream_kernel_ms"])
         pairs = len(r)
         ties = r.stats["n_near_ties"]
     torch.cuda.synchronize(dev)
@@ -154,9 +168,11 @@ def main():
         total_pairs = pairs
 
     ms_step = elapsed / a.steps * 1e3
-    kernel_ms = float(np.mean(kms))
-    alg_bytes = 16.0 * n + 12.0 * pairs
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    pipeline_ms = float(np.mean(kms))
+    stream_ms = float(np.mean(sms))
+    tiles = (n + 1023) // 1024
+    alg_bytes = 16.0 * n + 8.0 * pairs + 12.0 * tiles
+    achieved = alg_bytes / (stream_ms * 1e-3) / 1e9
     out = {
         "metric": METRIC,
         "value": world * n / (elapsed / a.steps),
@@ -177,8 +193,9 @@ def main():
                    "parallelism": "points sharded x%d, chip table replicated (RCCL broadcast)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "pip_join_kernel<H3>", "kernel_ms": kernel_ms,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "kernel": "pip_join_kernel<H3>", "kernel_ms": stream_ms,
+                     "alg_bytes_per_launch": alg_bytes, "pipeline_ms": pipeline_ms,
+                     "pipeline_GBps": (alg_bytes + 20.0 * pairs) / (pipeline_ms * 1e-3) / 1e9},
         "pairs_per_gpu": pairs,
         "pairs_total": total_pairs,
         "near_ties": ties,
@@ -192,6 +209,7 @@ def main():
             p = json.load(open(prof))
             if p.get("points") == n and p.get("res") == a.res:
                 out["roofline"]["traffic"] = p["hbm_bytes_per_launch"]
+                out["roofline"]["traffic_source"] = "profiles/pmc_join_traffic.json (%s)" % p.get("round", "?")
         except (ValueError, KeyError):
             pass
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

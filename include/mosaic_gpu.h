@@ -55,7 +55,8 @@ typedef struct mgpu_stats {
                                of a cell edge: the only points where an ulp-level libm
                                difference could change the cell */
     int64_t n_candidates;   /* (point, border chip) PIP evaluations */
-    float kernel_ms;        /* device time of the main kernel (HIP events) */
+    float kernel_ms;        /* device time of the whole call's launches (HIP events) */
+    float stream_kernel_ms; /* of which the streaming join kernel (pip_join_kernel) */
 } mgpu_stats;
 
 const char* mgpu_last_error(void);

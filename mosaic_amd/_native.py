@@ -58,7 +58,8 @@ class CapacityError(MosaicGpuError):
 
 class MgpuStats(ctypes.Structure):
     _fields_ = [("n_points", ctypes.c_int64), ("n_pairs", ctypes.c_int64), ("n_near_ties", ctypes.c_int64),
-                ("n_candidates", ctypes.c_int64), ("kernel_ms", ctypes.c_float)]
+                ("n_candidates", ctypes.c_int64), ("kernel_ms", ctypes.c_float),
+                ("stream_kernel_ms", ctypes.c_float)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

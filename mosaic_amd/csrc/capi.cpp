@@ -365,7 +365,7 @@ struct mgpu_ctx {
   // workspace: tile status words + ticket + counters
   void* ws = nullptr;
   size_t ws_bytes = 0;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
 };
 
 struct mgpu_chips {
@@ -454,6 +454,7 @@ int32_t mgpu_ctx_create(int32_t device_id, mgpu_ctx** out) {
   c->device = device_id;
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
+  HIP_TRY(hipEventCreate(&c->ev2));
   int32_t st = ensure_ws(c, 1);
   if (st) {
     delete c;
@@ -469,6 +470,7 @@ int32_t mgpu_ctx_destroy(mgpu_ctx* ctx) {
   if (ctx->ws) hipFree(ctx->ws);
   if (ctx->ev0) hipEventDestroy(ctx->ev0);
   if (ctx->ev1) hipEventDestroy(ctx->ev1);
+  if (ctx->ev2) hipEventDestroy(ctx->ev2);
   delete ctx;
   return MGPU_OK;
 }
@@ -507,6 +509,7 @@ int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t is, int32_t res, const doubl
     float ms = 0;
     hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
     stats->kernel_ms = ms;
+    stats->stream_kernel_ms = ms;
   }
   if (h[2]) {
     if (is == MGPU_BNG) return fail(MGPU_E_NAN, "NaN coordinates are not supported. (%llu points)", h[2]);
@@ -885,7 +888,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   e.out_poly = out_poly;
   HIP_TRY(hipMemsetAsync(base, 0, kWsCounters, s));
   if (timed) HIP_TRY(hipEventRecord(ctx->ev0, s));
-  HIP_TRY(mgpu::launch_join(is, a, e, s));
+  HIP_TRY(mgpu::launch_join(is, a, e, s, timed ? ctx->ev2 : nullptr));
   if (timed) HIP_TRY(hipEventRecord(ctx->ev1, s));
   return MGPU_OK;
 }
@@ -926,9 +929,11 @@ int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_
     stats->n_pairs = (int64_t)h[0];
     stats->n_near_ties = (int64_t)h[1];
     stats->n_candidates = (int64_t)h[3];
-    float ms = 0;
+    float ms = 0, ms2 = 0;
     hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+    if (n > 0) hipEventElapsedTime(&ms2, ctx->ev0, ctx->ev2);
     stats->kernel_ms = ms;
+    stats->stream_kernel_ms = ms2;
   }
   if (h[2]) {
     if (is == MGPU_BNG) return fail(MGPU_E_NAN, "NaN coordinates are not supported. (%llu points)", h[2]);

@@ -46,7 +46,8 @@ hipError_t launch_cells(int is, int res, const double* x, const double* y, int64
                         unsigned long long* counters, unsigned long long* ties, int64_t tie_cap, hipStream_t s);
 int64_t join_tiles(int64_t n);
 int64_t join_tile_points();
-hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s);
+// `after_stream` (optional) is recorded right after pip_join_kernel
+hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s, hipEvent_t after_stream);
 hipError_t launch_st_contains(const ChipTableView& t, const int64_t* row, const double* x, const double* y, int64_t n,
                               int8_t* out, hipStream_t s);
 

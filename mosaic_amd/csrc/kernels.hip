@@ -589,14 +589,16 @@ hipError_t launch_cells(int is, int res, const double* x, const double* y, int64
 int64_t join_tiles(int64_t n) { return (n + kTile - 1) / kTile; }
 int64_t join_tile_points() { return kTile; }
 
-hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s) {
+hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s, hipEvent_t after_stream) {
   if (a.n_tiles <= 0) return hipSuccess;
   if (is == MGPU_H3) {
     hipLaunchKernelGGL(pip_join_kernel<MGPU_H3>, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, a);
+    if (after_stream) hipEventRecord(after_stream, s);
     const unsigned fix_blocks = (unsigned)(a.n_tiles < 512 ? a.n_tiles : 512);
     hipLaunchKernelGGL(pip_fix_kernel<MGPU_H3>, dim3(fix_blocks), dim3(kBlock), 0, s, a);
   } else {
     hipLaunchKernelGGL(pip_join_kernel<MGPU_BNG>, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, a);
+    if (after_stream) hipEventRecord(after_stream, s);
   }
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.tile_count, a.n_tiles, e.tile_off,
                      a.counters);

@@ -18,6 +18,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--ablate", type=int, default=0)
     ap.add_argument("--cells", action="store_true")
+    ap.add_argument("--bng", action="store_true", help="with --cells: BNG res 4 on eastings/northings "
+                    "(a pure 16 B read + 8 B write stream, used to calibrate FETCH_SIZE / WRITE_SIZE)")
     a = ap.parse_args()
     if a.ablate:
         os.environ["MGPU_ABLATE"] = str(a.ablate)
@@ -33,8 +35,13 @@ def main():
     op = torch.empty(cap, dtype=torch.int64, device=dev)
     oq = torch.empty(cap, dtype=torch.int32, device=dev)
     ctx.reserve(a.points)
+    if a.bng:
+        x = x.mul(0).add_(torch.rand_like(x).mul_(58000.0).add_(503000.0))
+        y = y.mul(0).add_(torch.rand_like(y).mul_(46000.0).add_(155000.0))
     for _ in range(a.reps):
-        if a.cells:
+        if a.cells and a.bng:
+            M.grid_longlatascellid(x, y, 4, index_system=M.BNGIndexSystem())
+        elif a.cells:
             M.grid_longlatascellid(x, y, a.res)
         else:
             M.pip_join(x, y, chips, a.res, out=(op, oq), capacity=cap)

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""gpurun_out/traffic_TAG -> profiles/pmc_join_traffic.json.
+
+FETCH_SIZE / WRITE_SIZE are KB per dispatch (summed over the counter's instances).  On
+gfx950 FETCH_SIZE under-reports wide coalesced reads (MI355X_MICROARCH.md, HBM), and
+other access widths are uncalibrated, so both are calibrated on cells_kernel<BNG>: a
+stream of exactly 16 B read + 8 B written per point with the same 8-byte per-lane
+accesses as the join's point reads and record writes."""
+import collections
+import csv
+import json
+import os
+import sys
+
+d, tag = sys.argv[1], sys.argv[2]
+N = 100_000_000
+
+
+def per_dispatch(sub, kname):
+    tot = collections.defaultdict(float)
+    for r in csv.DictReader(open(os.path.join(d, sub, "run_counter_collection.csv"))):
+        if kname in r["Kernel_Name"]:
+            tot[r["Dispatch_Id"]] += float(r["Counter_Value"])
+    v = sorted(tot.values())
+    return sum(v) / len(v) * 1024.0, len(v)
+
+
+jf, nj = per_dispatch("join_fetch", "pip_join_kernel")
+jw, _ = per_dispatch("join_write", "pip_join_kernel")
+bf, nb = per_dispatch("bng_fetch", "cells_kernel<1>")
+bw, _ = per_dispatch("bng_write", "cells_kernel<1>")
+f_read = bf / (16.0 * N)
+f_write = bw / (8.0 * N)
+out = {
+    "round": tag, "points": N, "res": 9,
+    "join_fetch_bytes_raw": jf, "join_write_bytes_raw": jw, "dispatches": nj,
+    "calib_bng_fetch_bytes_raw": bf, "calib_bng_write_bytes_raw": bw,
+    "calib_read_factor": f_read, "calib_write_factor": f_write,
+    "hbm_read_bytes_per_launch": jf / f_read, "hbm_write_bytes_per_launch": jw / f_write,
+    "hbm_bytes_per_launch": jf / f_read + jw / f_write,
+    "note": "pip_join_kernel<H3>, 1e8 uniform NYC-bbox points, H3 res 9, 263 zones; FETCH_SIZE and WRITE_SIZE "
+            "in separate rocprofv3 --pmc passes, each divided by its factor measured on cells_kernel<BNG> "
+            "(16 B read + 8 B written per point)",
+}
+json.dump(out, open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles",
+                                 "pmc_join_traffic.json"), "w"), indent=1)
+print(json.dumps(out, indent=1))
