@@ -379,7 +379,8 @@ struct mgpu_chips {
 namespace {
 
 // Workspace layout (each region 256-byte aligned):
-//   [counters 16 x u64] [tile_count u32 x T] [tile_where u64 x T] [tile_off u64 x T]
+//   [counters 16 x u64] [tile_count u32 x T] [tile_where u64 x T] [group_off u64 x T/32 (T)]
+//   [group_sum u32 x T/32]
 //   [dirty tiles u32 x T] [cells near-tie queue u64 x (1 + kTieCap)]
 //   [records u64 x (T * tile points + pool)]
 // counters: [0] pairs [1] route near-ties [2] invalid points [3] candidates
@@ -389,7 +390,7 @@ namespace {
 constexpr size_t kWsCounters = 128;  // 16 x u64
 
 struct WsLayout {
-  size_t count, where, off, dirty, ties, recs, total;
+  size_t count, where, off, gsum, dirty, ties, recs, total;
 };
 // near-tie queue of mgpu_points_to_cells (overflow: the fix kernel redoes every point)
 constexpr int64_t kTieCap = 1 << 16;
@@ -400,7 +401,8 @@ WsLayout ws_layout(int64_t n_tiles, int64_t pool) {
   L.count = kWsCounters;
   L.where = align_up(L.count + T * 4, 256);
   L.off = align_up(L.where + T * 8, 256);
-  L.dirty = align_up(L.off + T * 8, 256);
+  L.gsum = align_up(L.off + T * 8, 256);
+  L.dirty = align_up(L.gsum + (T / 32 + 1) * 4, 256);
   L.ties = align_up(L.dirty + T * 4, 256);
   L.recs = align_up(L.ties + (size_t)(kTieCap + 1) * 8, 256);
   L.total = align_up(L.recs + (T * (size_t)mgpu::join_tile_points() + (size_t)std::max<int64_t>(pool, 0)) * 8, 256);
@@ -878,7 +880,8 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   }
   mgpu::EmitArgs e;
   e.tile_count = a.tile_count;
-  e.tile_off = (uint64_t*)(base + L.off);
+  e.group_off = (uint64_t*)(base + L.off);
+  a.group_sum = (uint32_t*)(base + L.gsum);
   e.tile_where = a.tile_where;
   e.recs = a.recs;
   e.point_id = point_id;
@@ -887,6 +890,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   e.out_point = out_point;
   e.out_poly = out_poly;
   HIP_TRY(hipMemsetAsync(base, 0, kWsCounters, s));
+  HIP_TRY(hipMemsetAsync(base + L.gsum, 0, ((size_t)tiles / 32 + 1) * 4, s));
   if (timed) HIP_TRY(hipEventRecord(ctx->ev0, s));
   HIP_TRY(mgpu::launch_join(is, a, e, s, timed ? ctx->ev2 : nullptr));
   if (timed) HIP_TRY(hipEventRecord(ctx->ev1, s));

@@ -17,6 +17,7 @@ struct JoinArgs {
   int res_match;                    // H3: the chips' resolution equals `res` (else nothing can match)
   ChipTableView chips;
   uint32_t* tile_count;             // [n_tiles] pairs of each tile
+  uint32_t* group_sum;              // [n_tiles / 32] pairs per group of 32 tiles, zeroed before launch
   uint64_t* tile_where;             // [n_tiles] first record of the tile in `recs` (~0: dropped)
   uint64_t* recs;                   // [n_tiles * tile points] slots, then [pool_cap] overflow pool
   int64_t pool_cap;
@@ -31,7 +32,7 @@ struct JoinArgs {
 // pair_emit_kernel: tile records -> ordered (point_id, polygon_id) output
 struct EmitArgs {
   const uint32_t* tile_count;
-  uint64_t* tile_off;               // written by the tile scan
+  uint64_t* group_off;              // [n_tiles / 32] written by the tile scan
   const uint64_t* tile_where;
   const uint64_t* recs;
   const int64_t* point_id;

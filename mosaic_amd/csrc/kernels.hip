@@ -32,6 +32,7 @@ constexpr int kItems = 4;
 constexpr int kTile = kBlock * kItems;
 
 constexpr uint64_t kNoDst = ~0ULL;
+constexpr int kScanGroup = 32;  // tiles per first-level scan group (<= 64)
 
 // ---------------------------------------------------------------- point -> cell
 
@@ -253,10 +254,18 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   // ---- phase 1: cells, core matches, candidates
   bool any_tie = false, any_bad = false;
   // one item ahead: item k + 1's coordinates load while item k computes
+#ifndef MGPU_NT_POINTS
+#define MGPU_NT_POINTS 0
+#endif
+#if MGPU_NT_POINTS
+#define MGPU_LDPT(ptr) __builtin_nontemporal_load(ptr)
+#else
+#define MGPU_LDPT(ptr) (*(ptr))
+#endif
   double nx = 0.0, ny = 0.0;
   if (base + threadIdx.x < a.n) {
-    nx = a.x[base + threadIdx.x];
-    ny = a.y[base + threadIdx.x];
+    nx = MGPU_LDPT(&a.x[base + threadIdx.x]);
+    ny = MGPU_LDPT(&a.y[base + threadIdx.x]);
   }
 #pragma unroll 1
   for (int k = 0; k < kItems; k++) {
@@ -266,8 +275,8 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     uint32_t mask = 0;
     const double px = nx, py = ny;
     if (k + 1 < kItems && p + kBlock < a.n) {
-      nx = a.x[p + kBlock];
-      ny = a.y[p + kBlock];
+      nx = MGPU_LDPT(&a.x[p + kBlock]);
+      ny = MGPU_LDPT(&a.y[p + kBlock]);
     }
     if (p < a.n) {
       bool ok, tie;
@@ -439,6 +448,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     }
     a.tile_count[tile] = agg;
     a.tile_where[tile] = dst;
+    if (agg) atomicAdd(&a.group_sum[tile / kScanGroup], agg);
     s_dst = dst;
   }
   const bool staged = agg <= (uint32_t)kOutCap;
@@ -497,46 +507,61 @@ __global__ __launch_bounds__(kBlock) void pip_fix_kernel(JoinArgs a) {
   }
 }
 
-// Exclusive scan of the tiles' pair counts (one workgroup; ~1e5 tiles per 1e8
-// points): tile_off[t] = pairs of tiles < t; counters[0] = total.
+// Output offsets, in two levels: pip_join_kernel / pip_fix_kernel add each tile's pair
+// count to its group of kScanGroup tiles; this one workgroup scans the group sums
+// (~3e3 per 1e8 points, coalesced chunks of 1024) and pair_emit_kernel adds the counts
+// of the tile's predecessors inside its group.  counters[0] = total pairs.
 constexpr int kScanBlock = 1024;
-__global__ __launch_bounds__(kScanBlock) void tile_scan_kernel(const uint32_t* __restrict__ cnt, int64_t n,
-                                                               uint64_t* __restrict__ off,
+__global__ __launch_bounds__(kScanBlock) void tile_scan_kernel(const uint32_t* __restrict__ gsum, int64_t ng,
+                                                               uint64_t* __restrict__ goff,
                                                                unsigned long long* __restrict__ counters) {
   __shared__ unsigned long long s_w[kScanBlock / 64];
-  const int64_t per = (n + kScanBlock - 1) / kScanBlock;
-  const int64_t b = per * threadIdx.x, e = b + per < n ? b + per : n;
-  unsigned long long sum = 0;
-  for (int64_t i = b; i < e; i++) sum += cnt[i];
+  __shared__ unsigned long long s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  unsigned long long incl = sum;
+  for (int64_t b = 0; b < ng; b += kScanBlock) {
+    const int64_t i = b + threadIdx.x;
+    const unsigned long long v = i < ng ? gsum[i] : 0ull;
+    unsigned long long incl = v;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    unsigned long long v = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += v;
+    for (int d = 1; d < 64; d <<= 1) {
+      unsigned long long u = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += u;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    unsigned long long run = s_carry + incl - v, tot = 0;
+    for (int w = 0; w < kScanBlock / 64; w++) {
+      if (w < wave) run += s_w[w];
+      tot += s_w[w];
+    }
+    if (i < ng) goff[i] = run;
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry += tot;
+    __syncthreads();
   }
-  if (lane == 63) s_w[wave] = incl;
-  __syncthreads();
-  unsigned long long run = incl - sum, tot = 0;
-  for (int w = 0; w < kScanBlock / 64; w++) {
-    if (w < wave) run += s_w[w];
-    tot += s_w[w];
-  }
-  for (int64_t i = b; i < e; i++) {
-    off[i] = run;
-    run += cnt[i];
-  }
-  if (threadIdx.x == 0) counters[0] = tot;
+  if (threadIdx.x == 0) counters[0] = s_carry;
 }
 
-// Ordered output: tile t's records -> out[tile_off[t] ...] with point ids.
+// Ordered output: tile t's records -> out[offset of t ...] with point ids.
 __global__ __launch_bounds__(kBlock) void pair_emit_kernel(EmitArgs a) {
+  __shared__ int64_t s_off;
   const int64_t t = blockIdx.x;
   const uint32_t n = a.tile_count[t];
   if (!n) return;
   const uint64_t where = a.tile_where[t];
   if (where == kNoDst) return;  // pool exhausted: the total exceeds the capacity
-  const int64_t off = (int64_t)a.tile_off[t];
+  if (threadIdx.x < 64) {
+    // predecessors inside the tile's scan group
+    const int64_t g0 = t - t % kScanGroup;
+    const int64_t j = g0 + threadIdx.x;
+    unsigned long long v = (threadIdx.x < kScanGroup && j < t) ? a.tile_count[j] : 0u;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    if (threadIdx.x == 0) s_off = (int64_t)(a.group_off[t / kScanGroup] + v);
+  }
+  __syncthreads();
+  const int64_t off = s_off;
   const uint64_t* src = a.recs + where;
   const int64_t base = t * kTile;
   for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
@@ -600,8 +625,8 @@ hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t
     hipLaunchKernelGGL(pip_join_kernel<MGPU_BNG>, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, a);
     if (after_stream) hipEventRecord(after_stream, s);
   }
-  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.tile_count, a.n_tiles, e.tile_off,
-                     a.counters);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.group_sum,
+                     (a.n_tiles + kScanGroup - 1) / kScanGroup, e.group_off, a.counters);
   hipLaunchKernelGGL(pair_emit_kernel, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, e);
   return hipGetLastError();
 }
