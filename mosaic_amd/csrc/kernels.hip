@@ -142,7 +142,11 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 constexpr int kCandCap = 1024;
 constexpr int kMixCap = 512;    // mixed-cell candidates (phase 2b), after the list in s_buf
 constexpr int kOutCap = 2048;
-static_assert(kCandCap * 6 + kMixCap * 2 <= kOutCap * 6, "phase 1-2 lists fit the staging buffer");
+#ifndef MGPU_STASH
+#define MGPU_STASH 512
+#endif
+constexpr int kStash = MGPU_STASH;  // candidates whose coordinates phase 1 leaves in LDS
+static_assert(kCandCap * 2 + kMixCap * 2 + kStash * 16 <= kOutCap * 6, "phase 1-2 lists fit the staging buffer");
 constexpr int kMaskBits = 32;
 
 // chips of a cell: first, count, core mask (bits < 16)
@@ -236,8 +240,11 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   __shared__ uint16_t s_cnt[kTile];     // chips of the point's cell (0: none)
   // phases 1-2: candidate list; phase 3: output staging (same bytes)
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[kOutCap * 6];
-  uint32_t* s_cand_chip = (uint32_t*)s_buf;                       // [kCandCap]
-  uint16_t* s_cand_pj = (uint16_t*)(s_buf + kCandCap * 4);        // [kCandCap] li | j << 10
+  // candidate c = chip s_first[li] + j of point li, s_cand_pj[c] = li | j << 10; the
+  // first kStash candidates also keep the point's coordinates (no re-read in phase 2)
+  double2* s_cand_xy = (double2*)s_buf;                             // [kStash]
+  uint16_t* s_cand_pj = (uint16_t*)(s_buf + kStash * 16);           // [kCandCap]
+  uint16_t* s_mix = (uint16_t*)(s_buf + kStash * 16 + kCandCap * 2);  // [kMixCap] candidate index
   int32_t* s_out_poly = (int32_t*)s_buf;                          // [kOutCap]
   uint16_t* s_out_li = (uint16_t*)(s_buf + kOutCap * 4);          // [kOutCap]
 
@@ -304,8 +311,8 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         for (uint32_t b = border; b; b &= b - 1) {
           const uint32_t j = __builtin_ctz(b);
           if (j0 < (uint32_t)kCandCap) {
-            s_cand_chip[j0] = r.first + j;
             s_cand_pj[j0] = (uint16_t)(li | (j << 10));
+            if (j0 < (uint32_t)kStash) s_cand_xy[j0] = make_double2(px, py);
           } else if (!SLOW) {
             any_tie = true;  // list full: the fix kernel evaluates such tiles
           } else if (pip::chip_contains_strips(t, r.first + j, px, py)) {
@@ -338,18 +345,25 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   // ---- phase 2: lane per candidate: envelope / rectangle / classification grid.
   // Candidates in a mixed grid cell (~1 in 8) are listed again and evaluated in
   // phase 2b, so the strip walk runs once per tile instead of in every wave.
-  uint16_t* s_mix = (uint16_t*)(s_buf + kCandCap * 6);  // [kMixCap] candidate index
   bool redo = false;
   for (uint32_t c = threadIdx.x; c < ncand; c += kBlock) {
-    const uint32_t ch = s_cand_chip[c];
     const uint32_t pj = s_cand_pj[c];
     const int li = pj & 1023;
+    const uint32_t ch = s_first[li] + (pj >> 10);
     const int64_t p = base + li;
     bool hit;
     if (a.ablate == 4) {  // profiling: candidate list only
       hit = (ch ^ pj) == 0x7FFFFFFF;
     } else {
-      const double px = a.x[p], py = a.y[p];
+      double px, py;
+      if (c < (uint32_t)kStash) {
+        const double2 q = s_cand_xy[c];
+        px = q.x;
+        py = q.y;
+      } else {
+        px = a.x[p];
+        py = a.y[p];
+      }
       const int q = pip::chip_quick(t, ch, px, py);
       hit = q == pip::kQuickYes;
       if (q >= pip::kQuickStrips && a.ablate != 5) {
@@ -382,11 +396,19 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #endif
   for (uint32_t m = threadIdx.x; m < nmix; m += kBlock) {
     const uint32_t c = s_mix[m];
-    const uint32_t ch = s_cand_chip[c];
     const uint32_t pj = s_cand_pj[c];
     const int li = pj & 1023;
+    const uint32_t ch = s_first[li] + (pj >> 10);
     const int64_t p = base + li;
-    const double px = a.x[p], py = a.y[p];
+    double px, py;
+    if (c < (uint32_t)kStash) {
+      const double2 q = s_cand_xy[c];
+      px = q.x;
+      py = q.y;
+    } else {
+      px = a.x[p];
+      py = a.y[p];
+    }
     bool hit;
     if (SLOW && (t.chip_hdr[ch].flags & kChipNoStrips)) {
       hit = pip::chip_locate(t, ch, px, py) == pip::kInterior;
