@@ -108,11 +108,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world > 1:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (a.gpus, world))
+    # MGPU_DIST_BACKEND=gloo and more ranks than GPUs: a protocol rehearsal on a
+    # 1-GPU box (never a measurement); the real run is RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("MGPU_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     ctx = M.default_context(dev)
     isys = M.H3IndexSystem()
 
@@ -160,7 +167,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         off, total_pairs, _ = D.global_offsets(pairs, dev)
