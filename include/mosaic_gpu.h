@@ -157,6 +157,15 @@ int32_t mgpu_tess_result_copy(const mgpu_tess* t, int64_t* cell, int32_t* polygo
                               int64_t* wkb_offsets, uint8_t* wkb);
 int32_t mgpu_tess_destroy(mgpu_tess* t);
 
+/* TEST ONLY -- not an interface of the reference.  Builds the chip table on the host
+ * and evaluates st_contains(chip row, point) for n pairs by the join's path (the
+ * classification grid + strip index of the device chip table) and by the sequential
+ * JTS PointLocator; out_* = 1 / 0, -1 for a NULL geometry.  Host pointers; no GPU. */
+int32_t mgpu_test_chip_contains_host(int32_t index_system, int64_t n_chips, const int64_t* cell,
+                                     const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
+                                     const uint8_t* wkb, int64_t n, const int64_t* chip_row, const double* x,
+                                     const double* y, int8_t* out_join_path, int8_t* out_point_locator);
+
 #ifdef __cplusplus
 }
 #endif

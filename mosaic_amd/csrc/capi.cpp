@@ -542,17 +542,19 @@ int32_t mgpu_points_to_cells_host(mgpu_ctx* ctx, int32_t is, int32_t res, const 
 
 // ------------------------------------------------------------------ chips
 
-int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, const int64_t* cell,
-                          const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
-                          const uint8_t* wkb, mgpu_chips** out) {
-  if (!ctx || !out) return fail(MGPU_E_INVALID_ARG, "ctx/out is NULL");
+}  // extern "C"
+
+// The whole chip table as one host blob (header + arrays, chip_table.h); uploaded as
+// is by mgpu_chips_upload, evaluated in place by mgpu_test_chip_contains_host.
+static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
+                          const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb,
+                          std::vector<uint8_t>& host, BlobHeader& hdr_out) {
   if (index_system != MGPU_H3 && index_system != MGPU_BNG)
     return fail(MGPU_E_INVALID_ARG, "unknown index system %d (0 = H3, 1 = BNG)", index_system);
   if (n_chips < 0 || n_chips > (int64_t)std::numeric_limits<int32_t>::max())
     return fail(MGPU_E_INVALID_ARG, "n_chips out of range");
   if (n_chips > 0 && (!cell || !polygon_id || !is_core || !wkb_offsets))
     return fail(MGPU_E_INVALID_ARG, "chip arrays are NULL");
-  if (int32_t st = set_device(ctx->device)) return st;
 
   std::vector<int64_t> order(n_chips);
   for (int64_t i = 0; i < n_chips; i++) order[i] = i;
@@ -765,10 +767,26 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
     hdr.off[k] = total;
     total = align_up(total + std::max<size_t>(parts[k].bytes, 1), 256);
   }
-  std::vector<uint8_t> host(total, 0);
+  host.assign(total, 0);
   memcpy(host.data(), &hdr, sizeof hdr);
   for (auto& p : parts)
     if (p.bytes) memcpy(host.data() + p.off, p.src, p.bytes);
+  hdr_out = hdr;
+  return MGPU_OK;
+}
+
+extern "C" {
+
+int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, const int64_t* cell,
+                          const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
+                          const uint8_t* wkb, mgpu_chips** out) {
+  if (!ctx || !out) return fail(MGPU_E_INVALID_ARG, "ctx/out is NULL");
+  std::vector<uint8_t> host;
+  BlobHeader hdr;
+  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr))
+    return st;
+  if (int32_t st = set_device(ctx->device)) return st;
+  const size_t total = host.size();
   mgpu_chips* ch = new mgpu_chips();
   ch->device = ctx->device;
   hipError_t e1 = hipMalloc(&ch->blob, total);
@@ -985,6 +1003,34 @@ int32_t mgpu_pip_join_host(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, i
   hipFree(dpo);
   if (dpid) hipFree(dpid);
   return st;
+}
+
+// TEST ONLY (not part of the reference's interface): builds the chip table on the
+// host and evaluates st_contains(chip row, point) for n pairs twice -- by the join's
+// path (classification grid + strip index, pip::chip_contains_strips) and by the
+// sequential PointLocator (pip::chip_locate) -- so the CPU test suite can check the
+// grid/strip exactness claims without a GPU.  out_* = 1 / 0 (-1: NULL geometry).
+int32_t mgpu_test_chip_contains_host(int32_t index_system, int64_t n_chips, const int64_t* cell,
+                                     const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
+                                     const uint8_t* wkb, int64_t n, const int64_t* chip_row, const double* x,
+                                     const double* y, int8_t* out_join_path, int8_t* out_point_locator) {
+  std::vector<uint8_t> host;
+  BlobHeader hdr;
+  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr))
+    return st;
+  const mgpu::ChipTableView v = view_from_header(hdr, host.data());
+  for (int64_t i = 0; i < n; i++) {
+    const int64_t r = chip_row[i];
+    if (r < 0 || r >= n_chips) return fail(MGPU_E_INVALID_ARG, "chip row %lld out of range", (long long)r);
+    const uint32_t c = v.row_to_chip[r];
+    if (v.chip_flags[c] & mgpu::kChipNoGeom) {
+      out_join_path[i] = out_point_locator[i] = -1;
+      continue;
+    }
+    out_join_path[i] = mgpu::pip::chip_contains_strips(v, c, x[i], y[i]) ? 1 : 0;
+    out_point_locator[i] = mgpu::pip::chip_locate(v, c, x[i], y[i]) == mgpu::pip::kInterior ? 1 : 0;
+  }
+  return MGPU_OK;
 }
 
 }  // extern "C"
