@@ -27,9 +27,14 @@
 
 namespace mgpu {
 
-constexpr int kBlock = 256;
+// the join's tile: one workgroup of kBlock threads, kItems points per thread
+#ifndef MGPU_BLOCK
+#define MGPU_BLOCK 256
+#endif
+constexpr int kBlock = MGPU_BLOCK;
 constexpr int kItems = 4;
 constexpr int kTile = kBlock * kItems;
+static_assert(kTile <= 1024, "point-in-tile indices are 10 bits");
 
 constexpr uint64_t kNoDst = ~0ULL;
 constexpr int kScanGroup = 32;  // tiles per first-level scan group (<= 64)
@@ -139,11 +144,11 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 // candidates are abandoned by the streaming kernel after phase 1 and redone by
 // pip_fix_kernel, which evaluates list overflows on the spot and chips past the
 // 32nd of a cell in phase 3.
-constexpr int kCandCap = 1024;
-constexpr int kMixCap = 512;    // mixed-cell candidates (phase 2b), after the list in s_buf
-constexpr int kOutCap = 2048;
+constexpr int kCandCap = kTile;
+constexpr int kMixCap = kTile / 2;  // mixed-cell candidates (phase 2b), after the list in s_buf
+constexpr int kOutCap = 2 * kTile;
 #ifndef MGPU_STASH
-#define MGPU_STASH 512
+#define MGPU_STASH (kTile / 2)
 #endif
 constexpr int kStash = MGPU_STASH;  // candidates whose coordinates phase 1 leaves in LDS
 static_assert(kCandCap * 2 + kMixCap * 2 + kStash * 16 <= kOutCap * 6, "phase 1-2 lists fit the staging buffer");
