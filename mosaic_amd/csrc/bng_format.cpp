@@ -10,6 +10,7 @@
 #include <cstring>
 #include <string>
 
+#include "error.h"
 #include "../../include/mosaic_gpu.h"
 #include "bng_core.h"
 
@@ -117,14 +118,14 @@ bool parse_one(const char* s, int64_t len, int64_t* out) {
 extern "C" {
 
 int32_t mgpu_bng_format(const int64_t* cells, int64_t n, char* out, int64_t out_bytes, int64_t* out_offsets) {
-  if (n < 0 || (n > 0 && (!cells || !out_offsets))) return MGPU_E_INVALID_ARG;
+  if (n < 0 || (n > 0 && (!cells || !out_offsets))) return mgpu::set_error(MGPU_E_INVALID_ARG, "bng_format: bad arguments");
   int64_t pos = 0;
   char buf[32];
   out_offsets[0] = 0;
   for (int64_t i = 0; i < n; i++) {
     int len = format_one(cells[i], buf);
-    if (len < 0) return MGPU_E_INVALID_ARG;
-    if (pos + len > out_bytes) return MGPU_E_CAPACITY;
+    if (len < 0) return mgpu::set_error(MGPU_E_INVALID_ARG, "BNG cell id %lld has no string form", (long long)cells[i]);
+    if (pos + len > out_bytes) return mgpu::set_error(MGPU_E_CAPACITY, "bng_format: output buffer too small");
     memcpy(out + pos, buf, len);
     pos += len;
     out_offsets[i + 1] = pos;
@@ -133,9 +134,10 @@ int32_t mgpu_bng_format(const int64_t* cells, int64_t n, char* out, int64_t out_
 }
 
 int32_t mgpu_bng_parse(const char* ids, const int64_t* offsets, int64_t n, int64_t* out_cells) {
-  if (n < 0 || (n > 0 && (!ids || !offsets || !out_cells))) return MGPU_E_INVALID_ARG;
+  if (n < 0 || (n > 0 && (!ids || !offsets || !out_cells))) return mgpu::set_error(MGPU_E_INVALID_ARG, "bng_parse: bad arguments");
   for (int64_t i = 0; i < n; i++)
-    if (!parse_one(ids + offsets[i], offsets[i + 1] - offsets[i], &out_cells[i])) return MGPU_E_INVALID_ARG;
+    if (!parse_one(ids + offsets[i], offsets[i + 1] - offsets[i], &out_cells[i]))
+      return mgpu::set_error(MGPU_E_INVALID_ARG, "not a BNG cell id: %.*s", (int)(offsets[i + 1] - offsets[i]), ids + offsets[i]);
   return MGPU_OK;
 }
 

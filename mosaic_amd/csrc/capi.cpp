@@ -18,6 +18,7 @@
 
 #include "../../include/mosaic_gpu.h"
 #include "chip_table.h"
+#include "error.h"
 #include "h3_core.h"
 #include "kernels.h"
 #include "pip_core.h"
@@ -359,6 +360,18 @@ void build_grid(const mgpu::ChipTableView& hv, uint32_t c, const mgpu::wkb::Flat
 }
 
 }  // namespace
+
+namespace mgpu {
+int32_t set_error(int32_t code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+}  // namespace mgpu
 
 struct mgpu_ctx {
   int device = 0;

@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "../../include/mosaic_gpu.h"
+#include "error.h"
 #include "bng_core.h"
 #include "h3_core.h"
 #include "wkb.h"
@@ -483,8 +484,8 @@ extern "C" {
 int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, const int32_t* polygon_id,
                         const int64_t* poly_part_off, const int64_t* part_ring_off, const int64_t* ring_off,
                         const double* xy, int32_t keep_core_geometries, mgpu_tess** out) {
-  if (!out || n_polys < 0) return MGPU_E_INVALID_ARG;
-  if (mgpu_check_resolution(index_system, res) != MGPU_OK) return MGPU_E_RESOLUTION;
+  if (!out || n_polys < 0) return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellate: bad arguments");
+  if (int32_t st = mgpu_check_resolution(index_system, res)) return st;
   mgpu_tess* t = new mgpu_tess();
   for (int64_t p = 0; p < n_polys; p++) {
     Polygon poly;
@@ -513,14 +514,17 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
           }
       if (!one_face) {
         delete t;
-        return MGPU_E_INVALID_ARG;  // polygon spans icosahedron faces (not supported by this builder)
+        return mgpu::set_error(MGPU_E_INVALID_ARG,
+                               "tessellate: polygon %d spans several icosahedron faces (not supported by this "
+                               "builder; split it first)", polygon_id[p]);
       }
       H3Grid g(face, res);
       tessellate_polygon(g, poly, polygon_id[p], keep_core_geometries != 0, t->chips);
     } else {
       if (res == -1) {
         delete t;
-        return MGPU_E_RESOLUTION;  // 500km ids depend on the easting letter only: no square cells to clip
+        // 500km ids depend on the easting letter only: no square cells to clip
+        return mgpu::set_error(MGPU_E_RESOLUTION, "BNG resolution -1 (500km) cannot be tessellated");
       }
       BngGrid g(res);
       tessellate_polygon(g, poly, polygon_id[p], keep_core_geometries != 0, t->chips);
@@ -531,7 +535,7 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
 }
 
 int32_t mgpu_tess_result_sizes(const mgpu_tess* t, int64_t* n_chips, int64_t* wkb_bytes) {
-  if (!t) return MGPU_E_INVALID_ARG;
+  if (!t) return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellation result is NULL");
   int64_t b = 0;
   for (auto& c : t->chips) b += (int64_t)c.wkb.size();
   if (n_chips) *n_chips = (int64_t)t->chips.size();
@@ -541,7 +545,7 @@ int32_t mgpu_tess_result_sizes(const mgpu_tess* t, int64_t* n_chips, int64_t* wk
 
 int32_t mgpu_tess_result_copy(const mgpu_tess* t, int64_t* cell, int32_t* polygon_id, uint8_t* is_core,
                               int64_t* wkb_offsets, uint8_t* wkb) {
-  if (!t) return MGPU_E_INVALID_ARG;
+  if (!t) return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellation result is NULL");
   int64_t off = 0;
   for (size_t i = 0; i < t->chips.size(); i++) {
     const Chip& c = t->chips[i];
