@@ -311,6 +311,71 @@ MGPU_HD uint64_t face_ijk_to_h3(int face, IJK ijk, int res) {
   return h;
 }
 
+// _faceIjkToH3, restated for throughput (bit-identical to face_ijk_to_h3; checked by
+// tests/test_h3_digits_host.py on every base cell and resolution):
+//  * the walk from `res` to 0 runs in axial coordinates (a, b) = (i - k, j - k), where
+//    up_ap7 / down_ap7 are plain linear maps and no ijk normalisation is needed; the
+//    digit is a 9-entry lookup of the difference to the parent's centre;
+//  * the base-cell rotations permute every 3-bit digit at once with bit-plane logic
+//    (rot60ccw: 1->5->4->6->2->3->1, 0 and 7 fixed) instead of a loop per digit.
+//  Pentagon base cells keep face_ijk_to_h3's digit-by-digit path.
+constexpr uint64_t kDigitPlane = 0x49249249249ULL;  // bit 0 of each of the 15 digit fields
+MGPU_HD uint64_t rotate60ccw_all(uint64_t f) {
+  const uint64_t b0 = f & kDigitPlane, b1 = (f >> 1) & kDigitPlane, b2 = (f >> 2) & kDigitPlane;
+  const uint64_t t = b0 & b1 & b2;
+  const uint64_t n2 = ((~b1 & (b0 | b2)) | t) & kDigitPlane;
+  const uint64_t n1 = ((~b0 & (b1 | b2)) | t) & kDigitPlane;
+  const uint64_t n0 = ((~b2 & (b0 | b1)) | t) & kDigitPlane;
+  return n0 | (n1 << 1) | (n2 << 2);
+}
+
+MGPU_HD uint64_t face_ijk_to_h3_fast(int face, IJK ijk, int res) {
+  uint64_t h = kInit | (1ULL << 59) | ((uint64_t)res << 52);
+  int a = ijk.i - ijk.k, b = ijk.j - ijk.k;
+  uint64_t digits = kInit;  // 15 digits of 7
+  for (int r = res - 1; r >= 0; r--) {
+    int na, nb, ca, cb;
+    if ((r + 1) & 1) {  // Class III child: up_ap7 / down_ap7
+      na = round_div7(3 * a - b);
+      nb = round_div7(a + 2 * b);
+      ca = 2 * na + nb;
+      cb = 3 * nb - na;
+    } else {  // Class II child: up_ap7r / down_ap7r
+      na = round_div7(2 * a + b);
+      nb = round_div7(3 * b - a);
+      ca = 3 * na - nb;
+      cb = na + 2 * nb;
+    }
+    const int da = a - ca + 1, db = b - cb + 1;
+    const int digit = ((unsigned)da < 3u && (unsigned)db < 3u)
+                          ? (int)((0x647205731ULL >> (4 * (da * 3 + db))) & 0xF)
+                          : 7;
+    const int sh = (kMaxRes - (r + 1)) * 3;
+    digits = (digits & ~(7ULL << sh)) | ((uint64_t)digit << sh);
+    a = na;
+    b = nb;
+  }
+  IJK base{a, b, 0};
+  ijk_normalize(base);
+  if (base.i > kMaxFaceCoord || base.j > kMaxFaceCoord || base.k > kMaxFaceCoord) return 0;
+  const unsigned e = H3T_FACE_IJK_BASE_CELLS[face][base.i][base.j][base.k];
+  const int bc = (int)(e & 0xff), rots = (int)(e >> 8);
+  h = (h & ~kInit) | digits | ((uint64_t)bc << 45);
+  if (H3T_BASE_CELL_DATA[bc][4]) {  // pentagon: digit-by-digit rotations
+    if (leading_nonzero(h, res) == 1) {
+      if (H3T_BASE_CELL_DATA[bc][5] == face || H3T_BASE_CELL_DATA[bc][6] == face)
+        h = rotate_cw(h, res);
+      else
+        h = rotate_ccw(h, res);
+    }
+    for (int i = 0; i < rots; i++) h = rotate_pent_ccw(h, res);
+    return h;
+  }
+  uint64_t f = h & kInit;
+  for (int i = 0; i < rots; i++) f = rotate60ccw_all(f);
+  return (h & ~kInit) | f;
+}
+
 // java.lang.Math.toRadians as on the reference's JDK 8 toolchain
 MGPU_HD double to_radians(double deg) { return deg / 180.0 * 3.14159265358979323846; }
 

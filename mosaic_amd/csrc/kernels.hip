@@ -76,7 +76,7 @@ __global__ __launch_bounds__(kBlock) void cells_kernel(const double* __restrict_
           const unsigned long long q = atomicAdd(&ties[0], 1ull);
           if ((int64_t)q < tie_cap) ties[1 + q] = (unsigned long long)i;
         } else {
-          c = (int64_t)h3::face_ijk_to_h3(f.face, f.ijk, res);
+          c = (int64_t)h3::face_ijk_to_h3_fast(f.face, f.ijk, res);
         }
       }
     } else {
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(kBlock) void cells_fix_kernel(const double* __restr
     if (isfinite(px) && isfinite(py)) {
       h3::FastHex f = h3::fast_hex2d(h3::to_radians_fast(py), h3::to_radians_fast(px), res, k_res, kAllFaces);
       if (f.tie) h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, &tie);
-      out[i] = (int64_t)h3::face_ijk_to_h3(f.face, f.ijk, res);
+      out[i] = (int64_t)h3::face_ijk_to_h3_fast(f.face, f.ijk, res);
     }
     count_wave(&counters[1], tie);
   }
@@ -226,7 +226,7 @@ __device__ __forceinline__ Range chip_range(const ChipTableView& t, double px, d
     }
     h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, tie);
   }
-  return probe_range(t, h3::face_ijk_to_h3(f.face, f.ijk, res));
+  return probe_range(t, h3::face_ijk_to_h3_fast(f.face, f.ijk, res));
 }
 
 __device__ __forceinline__ bool chip_is_core(const ChipTableView& t, const Range& r, uint32_t j) {

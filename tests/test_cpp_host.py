@@ -11,10 +11,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "tests", "cpp", "test_host_api")
 
 
-def _run(mode):
-    if not os.path.exists(EXE):
-        pytest.skip("tests/cpp/test_host_api not built (run __graft_entry__.build())")
-    r = subprocess.run([EXE, mode], capture_output=True, text=True, timeout=300)
+def _run(mode, exe=EXE):
+    if not os.path.exists(exe):
+        pytest.skip("%s not built (run __graft_entry__.build())" % exe)
+    r = subprocess.run([exe] + ([mode] if mode else []), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     return r.stdout
 
@@ -26,3 +26,10 @@ def test_cpp_host_cpu():
 @pytest.mark.gpu
 def test_cpp_host_gpu(gpu):
     assert "0 failure" in _run("--gpu")
+
+
+def test_h3_fast_digit_encoding_equals_restatement():
+    """face_ijk_to_h3_fast (axial walk + bit-plane rotations, used by the kernels) ==
+    face_ijk_to_h3 (the _faceIjkToH3 restatement) on 6.4M lattice positions."""
+    out = _run(None, os.path.join(ROOT, "tests", "cpp", "test_h3_digits"))
+    assert "mismatches 0" in out
