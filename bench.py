@@ -47,7 +47,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--points", type=int, default=100_000_000, help="points per GPU")
-    ap.add_argument("--res", type=int, default=9)
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"],
+                    help="BASELINE.json config: c2 (default, the headline), c4 (BNG), c5 (skewed)")
+    ap.add_argument("--res", type=int, default=None, help="default: 9 (c2, c5), 4 (c4)")
     ap.add_argument("--seed", type=int, default=0x20250314)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
@@ -66,20 +68,20 @@ def gen_points(n, begin, seed, dev):
     return x, y
 
 
-def cpu_baseline(chips, res, seed, target_s):
+def cpu_baseline(chips, isys, res, wl, seed, target_s):
     """Oracle (CPU restatement of the reference path) on a bounded sample: points/s.
     Chunks of up to 20M points until ~target_s seconds of join time are spent."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     threads = max(1, min(threads, 64))
-    rng = np.random.default_rng(seed)
+    chunk_seed = [seed]
 
     def run(n):
-        x = rng.uniform(NYC_BBOX[0], NYC_BBOX[2], n)
-        y = rng.uniform(NYC_BBOX[1], NYC_BBOX[3], n)
+        chunk_seed[0] += 1
+        x, y = wl["points_np"](n, chunk_seed[0])
         t = time.perf_counter()
-        O.pip_join(0, res, x, y, chips.cell, chips.polygon_id, chips.is_core, chips.wkb_offsets, chips.wkb,
+        O.pip_join(isys.code, res, x, y, chips.cell, chips.polygon_id, chips.is_core, chips.wkb_offsets, chips.wkb,
                    threads=threads)
         return time.perf_counter() - t
 
@@ -92,10 +94,41 @@ def cpu_baseline(chips, res, seed, target_s):
         total_t += run(n)
         total_n += n
     return {"value": total_n / total_t, "unit": "points/s", "cores": threads, "kind": "port",
-            "sample": "%d uniform NYC-bbox points (chunks of <= 20M) x 263 zones, H3 res %d, oracle pip_join "
-                      "(C restatement of H3 geoToH3 + hash join on cell + JTS PointLocator with per-candidate WKB "
-                      "re-parse, as the reference's JVM path does), %d threads, %.1f s"
-                      % (total_n, res, threads, total_t)}
+            "sample": "%d points (chunks of <= 20M) of the same workload, %s res %d, oracle pip_join "
+                      "(C restatement of the reference's cell id + hash join on cell + JTS PointLocator with "
+                      "per-candidate WKB re-parse, as its JVM path does), %d threads, %.1f s"
+                      % (total_n, isys.name, res, threads, total_t)}
+
+
+def workload(a, W, M):
+    """The config's polygons, index system and point generators (bench_workloads.py)."""
+    if a.config == "c4":
+        a.res = 4 if a.res is None else a.res
+        return {"isys": M.BNGIndexSystem(), "polygons": W.london_districts(),
+                "points": lambda n, begin, dev: W.london_points(n, a.seed * 1000003 + begin, dev),
+                "points_np": lambda n, sd: W.london_points(n, sd),
+                "pairs_per_point": 1.1,
+                "workload": "C4: %d points/GPU uniform in the London BNG extent (0.01 m) x 180 UK-style districts "
+                            "(seeded Voronoi partition, jittered edges), BNG res %d",
+                "data": "synthetic (UPRN-like points; Voronoi districts covering the extent)"}
+    if a.config == "c5":
+        a.res = 9 if a.res is None else a.res
+        P = W.skewed_polygons()
+        return {"isys": M.H3IndexSystem(), "polygons": P,
+                "points": lambda n, begin, dev: W.boundary_points(P, n, a.seed * 1000003 + begin, 0.003, dev),
+                "points_np": lambda n, sd: W.boundary_points(P, n, sd, 0.003),
+                "pairs_per_point": 0.7,
+                "workload": "C5: %d points/GPU, 90%% Gaussian (sigma 0.003 deg) around the boundaries of 4 "
+                            "fractal polygons of 49k vertices, H3 res %d",
+                "data": "synthetic (skewed points near polygon edges; seeded fractal polygons)"}
+    a.res = 9 if a.res is None else a.res
+    return {"isys": M.H3IndexSystem(), "polygons": W.nyc_zones(),
+            "points": lambda n, begin, dev: gen_points(n, begin, a.seed, dev),
+            "points_np": lambda n, sd: (np.random.default_rng(sd).uniform(NYC_BBOX[0], NYC_BBOX[2], n),
+                                        np.random.default_rng(sd + 7).uniform(NYC_BBOX[1], NYC_BBOX[3], n)),
+            "pairs_per_point": 0.5,
+            "workload": "C2: %d points/GPU uniform in NYC bbox x 263 NYC taxi zones, H3 res %d",
+            "data": "synthetic (uniform points in the NYC zone bbox; real NYC taxi-zone polygons from the reference)"}
 
 
 def main():
@@ -121,9 +154,9 @@ def main():
         else:
             dist.init_process_group(backend)
     ctx = M.default_context(dev)
-    isys = M.H3IndexSystem()
-
-    zones = M.Polygons.from_npz(os.path.join(ROOT, "tests", "golden", "nyc_taxi_zones.npz"))
+    import bench_workloads as W
+    wl = workload(a, W, M)
+    isys, zones = wl["isys"], wl["polygons"]
     table = None
     if rank == 0:
         table = M.tessellate(zones, isys, a.res)
@@ -136,14 +169,15 @@ def main():
 
     n = a.points
     begin = rank * n
-    x, y = gen_points(n, begin, a.seed, dev)
-    cap = n // 2 + 1024  # ~36% of uniform bbox points fall in a zone
+    x, y = wl["points"](n, begin, dev)
+    cap = int(n * wl["pairs_per_point"]) + 1024
     out_p = torch.empty(cap, dtype=torch.int64, device=dev)
     out_q = torch.empty(cap, dtype=torch.int32, device=dev)
     ctx.reserve(n)
 
     def step():
-        return M.pip_join(x, y, chips, a.res, point_id_base=begin, out=(out_p, out_q), capacity=cap)
+        return M.pip_join(x, y, chips, a.res, index_system=isys, point_id_base=begin, out=(out_p, out_q),
+                          capacity=cap)
 
     for _ in range(a.warmup):
         r = step()
@@ -192,15 +226,14 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (uniform points in the NYC zone bbox; real NYC taxi-zone polygons from the reference)",
-        "config": {"workload": "C2: %d points/GPU uniform in NYC bbox x 263 NYC taxi zones, H3 res %d"
-                               % (n, a.res),
-                   "points_per_gpu": n, "polygons": len(zones), "chips": info["chips"], "chip_cells": info["cells"],
-                   "index_system": "H3", "resolution": a.res,
+        "data": wl["data"],
+        "config": {"workload": wl["workload"] % (n, a.res),
+                   "points_per_gpu": n, "polygons": len(zones.poly_part_off) - 1, "chips": info["chips"],
+                   "chip_cells": info["cells"], "index_system": isys.name, "resolution": a.res,
                    "parallelism": "points sharded x%d, chip table replicated (RCCL broadcast)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "pip_join_kernel<H3>", "kernel_ms": stream_ms,
+                     "kernel": "pip_join_kernel<%s>" % isys.name, "kernel_ms": stream_ms,
                      "alg_bytes_per_launch": alg_bytes, "pipeline_ms": pipeline_ms,
                      "pipeline_GBps": (alg_bytes + 20.0 * pairs) / (pipeline_ms * 1e-3) / 1e9},
         "pairs_per_gpu": pairs,
@@ -214,7 +247,7 @@ def main():
     if os.path.exists(prof):
         try:
             p = json.load(open(prof))
-            if p.get("points") == n and p.get("res") == a.res:
+            if p.get("points") == n and p.get("res") == a.res and a.config == "c2":
                 out["roofline"]["traffic"] = p["hbm_bytes_per_launch"]
                 out["roofline"]["traffic_source"] = "profiles/pmc_join_traffic.json (%s)" % p.get("round", "?")
         except (ValueError, KeyError):
@@ -222,7 +255,7 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         if table is None:
             table = M.tessellate(zones, isys, a.res)
-        out["cpu_baseline"] = cpu_baseline(table, a.res, a.seed, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(table, isys, a.res, wl, a.seed, a.cpu_seconds)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/mosaic_gpu.h"
+#include "bng_core.h"
 #include "chip_table.h"
 #include "error.h"
 #include "h3_core.h"
@@ -51,7 +52,7 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // complete chip table there.
 constexpr uint64_t kBlobMagic = 0x4d4f534149434850ULL;  // "MOSAICHP"
 constexpr int kBlobArrays = 18;
-constexpr uint32_t kBlobVersion = 3;
+constexpr uint32_t kBlobVersion = 4;
 struct BlobHeader {
   uint64_t magic;
   uint32_t version, hash_mask, max_probe, n_chips, n_cells, pad;
@@ -62,6 +63,8 @@ struct BlobHeader {
   double bbox[4];
   double k_res;
   mgpu::DenseFace dense[20];
+  uint32_t bng_edge, pad3;
+  double bng_inv_edge;
 };
 constexpr size_t kBlobHeaderBytes = 1024;
 static_assert(sizeof(BlobHeader) <= kBlobHeaderBytes, "header too large");
@@ -96,7 +99,76 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.face_mask = h.face_mask;
   for (int k = 0; k < 4; k++) v.bbox[k] = h.bbox[k];
   v.k_res = h.k_res;
+  v.bng_edge = h.bng_edge;
+  v.bng_inv_edge = h.bng_inv_edge;
   return v;
+}
+
+// BNG dense probing.  For one resolution r (nPositions p, BNGIndexSystem.scala:
+// 284-298, encode :540-553) a cell id is 10^(2p+3) + eLetter 10^(2p+1) + nLetter
+// 10^(2p-1) + eBin 10^p + nBin 10 + quadrant with eBin, nBin < 10^(p-1): for whole-metre
+// eastings / northings in [0, 1e7) (letters < 100, ids < 2^53) it is a bijection of
+// (column, row) = (e / edge, n / edge), edge = the cell edge (halved for the quadrant
+// resolutions r <= -2, whose quadrant digit is the column / row parity).  Every chip
+// cell is decoded and re-encoded by point_to_cell at its centre; any cell that does
+// not round-trip (negative coordinates, mixed resolutions, r = -1) keeps the hash.
+bool build_bng_dense(const std::vector<mgpu::HashSlot>& cells, int32_t* res_out, mgpu::DenseFace* D,
+                     uint32_t* edge_out, std::vector<uint64_t>& grid) {
+  if (cells.empty()) return false;
+  auto p10 = [](int k) {
+    int64_t v = 1;
+    while (k-- > 0) v *= 10;
+    return v;
+  };
+  int p = -1;
+  for (int q = 1; q <= 6; q++)
+    if ((int64_t)cells[0].cell >= p10(2 * q + 3) && (int64_t)cells[0].cell < 2 * p10(2 * q + 3)) p = q;
+  if (p < 0) return false;
+  const bool quad = cells[0].cell % 10 != 0;
+  if (quad && p > 5) return false;
+  const int res = quad ? -(p + 1) : p;
+  const int64_t d = p10(6 - p);  // metres per (column, row) of the id's bins
+  const int64_t edge = quad ? d / 2 : d;
+  const int64_t B = p10(p - 1);
+  std::vector<std::pair<int64_t, int64_t>> cr(cells.size());
+  int64_t c0 = INT64_MAX, c1 = INT64_MIN, r0 = INT64_MAX, r1 = INT64_MIN;
+  for (size_t k = 0; k < cells.size(); k++) {
+    const int64_t id = (int64_t)cells[k].cell;
+    int64_t rem = id - p10(2 * p + 3);
+    if (rem < 0 || rem >= p10(2 * p + 3)) return false;
+    const int64_t eL = rem / p10(2 * p + 1);
+    rem %= p10(2 * p + 1);
+    const int64_t nL = rem / p10(2 * p - 1);
+    rem %= p10(2 * p - 1);
+    const int64_t eB = rem / p10(p);
+    rem %= p10(p);
+    const int64_t nB = rem / 10, q = rem % 10;
+    if (eB >= B || nB >= B || (quad ? (q < 1 || q > 4) : q != 0)) return false;
+    int64_t col = eL * B + eB, row = nL * B + nB;
+    if (quad) col = 2 * col + (q == 3 || q == 4), row = 2 * row + (q == 2 || q == 3);
+    int64_t back = 0;
+    mgpu::bng::point_to_cell((col + 0.5) * (double)edge, (row + 0.5) * (double)edge, res, &back);
+    if (back != id || (col + 1) * edge > 10000000 || (row + 1) * edge > 10000000) return false;
+    cr[k] = {col, row};
+    c0 = std::min(c0, col), c1 = std::max(c1, col), r0 = std::min(r0, row), r1 = std::max(r1, row);
+  }
+  const int64_t total = (c1 - c0 + 1) * (r1 - r0 + 1);
+  if (total > std::max<int64_t>(16 * (int64_t)cells.size(), 1 << 20) || total > (1LL << 26)) return false;
+  memset(D, 0, sizeof(mgpu::DenseFace));
+  D->a0 = (int32_t)c0;
+  D->b0 = (int32_t)r0;
+  D->w = (uint32_t)(c1 - c0 + 1);
+  D->h = (uint32_t)(r1 - r0 + 1);
+  D->base = 0;
+  grid.assign((size_t)total, 0);
+  for (size_t k = 0; k < cells.size(); k++) {
+    const mgpu::HashSlot& e = cells[k];
+    grid[(size_t)((cr[k].second - r0) * D->w + (cr[k].first - c0))] =
+        (uint64_t)e.first | ((uint64_t)e.count << 32) | ((uint64_t)e.core_mask << 48);
+  }
+  *res_out = res;
+  *edge_out = (uint32_t)edge;
+  return true;
 }
 
 constexpr double kPi = 3.14159265358979323846;
@@ -720,6 +792,9 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
       probe_mode = mgpu::kProbeDense;
     }
   }
+  uint32_t bng_edge = 0;
+  if (index_system == MGPU_BNG && build_bng_dense(distinct, &lres, &dense[0], &bng_edge, grid))
+    probe_mode = mgpu::kProbeDense;
   uint32_t cap = 16;
   while (cap < 2 * entries.size()) cap <<= 1;
   std::vector<mgpu::HashSlot> slots(cap, mgpu::HashSlot{0, 0, 0, 0});
@@ -774,7 +849,9 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   hdr.res = lres;
   hdr.face_mask = face_mask;
   for (int k = 0; k < 4; k++) hdr.bbox[k] = bbox[k];
-  hdr.k_res = lres >= 0 ? mgpu::h3::k_of_res(lres) : 0.0;
+  hdr.k_res = index_system == MGPU_H3 && lres >= 0 ? mgpu::h3::k_of_res(lres) : 0.0;
+  hdr.bng_edge = bng_edge;
+  hdr.bng_inv_edge = bng_edge ? 1.0 / bng_edge : 0.0;
   for (size_t k = 0; k < parts.size(); k++) {
     parts[k].off = total;
     hdr.off[k] = total;

@@ -130,8 +130,8 @@ struct ChipTableView {
   const double* edges;         // 4 per edge record: p1x, p1y, p2x, p2y (p1 = ring[i], p2 = ring[i-1])
   const uint8_t* edge_ring;    // ring index of the edge within its chip
   const ChipHdr* chip_hdr;     // [n_chips]
-  // H3 probing (index system H3 only)
-  int32_t probe_mode;          // ProbeMode: hash by cell id / hash by lattice key / dense lattice grid
+  // probing (lattice: H3 only; dense grid: H3 lattice or BNG column/row)
+  int32_t probe_mode;          // ProbeMode: hash by cell id / hash by lattice key / dense grid
   int32_t res;                 // resolution of the chip cells (H3), -1 if mixed / unknown
   uint32_t face_mask;          // icosahedron faces a point inside `bbox` can be nearest to
   double bbox[4];              // lon_min, lat_min, lon_max, lat_max (deg): points outside match no chip
@@ -139,8 +139,13 @@ struct ChipTableView {
   // kProbeDense: per face f, grid[base + (b - b0) * w + (a - a0)] for the axial
   // lattice coordinates a = i - k, b = j - k inside [a0, a0 + w) x [b0, b0 + h);
   // entry = first | count << 32 | core_mask << 48 (count 0: no chip cell there)
+  // BNG (kProbeDense): dense[0] spans the chip cells' (column, row) box, column =
+  // easting / bng_edge and row = northing / bng_edge in whole metres (bng_edge = the
+  // cell edge, halved for quadrant resolutions); the same entry format
   const uint64_t* grid;
   DenseFace dense[20];
+  uint32_t bng_edge;
+  double bng_inv_edge;
 };
 
 enum ProbeMode { kProbeCellId = 0, kProbeLattice = 1, kProbeDense = 2 };

@@ -180,9 +180,26 @@ __device__ __forceinline__ Range chip_range(const ChipTableView& t, double px, d
                                             bool* ok, bool* tie, int ablate) {
   *tie = false;
   if (IS == MGPU_BNG) {
-    int64_t c;
-    *ok = bng::point_to_cell(px, py, res, &c);
+    *ok = px == px && py == py;  // pointToIndex rejects NaN only
     if (!*ok || !res_match) return Range{0, 0, 0};
+    const int32_t eI = bng::d2i(px), nI = bng::d2i(py);
+    // whole-metre coordinates in [0, 1e7): the cell id is a bijection of (eI / edge,
+    // nI / edge) (capi.cpp build_bng_dense), so the dense grid replaces id + hash probe
+    if (t.probe_mode == kProbeDense && res == t.res && (uint32_t)eI < 10000000u && (uint32_t)nI < 10000000u) {
+      const uint32_t ed = t.bng_edge;
+      uint32_t col = (uint32_t)((double)eI * t.bng_inv_edge);
+      uint32_t row = (uint32_t)((double)nI * t.bng_inv_edge);
+      col = col * ed > (uint32_t)eI ? col - 1 : ((col + 1) * ed <= (uint32_t)eI ? col + 1 : col);
+      row = row * ed > (uint32_t)nI ? row - 1 : ((row + 1) * ed <= (uint32_t)nI ? row + 1 : row);
+      const DenseFace& D = t.dense[0];
+      const uint32_t da = col - (uint32_t)D.a0, db = row - (uint32_t)D.b0;
+      if (ablate == 2) return Range{0, (da ^ db) == 0x12345 ? 1u : 0u, 0};  // profiling: no probe
+      if (da >= D.w || db >= D.h) return Range{0, 0, 0};
+      const uint64_t e = t.grid[D.base + db * D.w + da];
+      return Range{(uint32_t)e, (uint32_t)(e >> 32) & 0xFFFF, (uint32_t)(e >> 48)};
+    }
+    int64_t c;
+    bng::point_to_cell(px, py, res, &c);
     return probe_range(t, (uint64_t)c);
   }
   *ok = isfinite(px) && isfinite(py);
@@ -643,14 +660,17 @@ int64_t join_tile_points() { return kTile; }
 
 hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s, hipEvent_t after_stream) {
   if (a.n_tiles <= 0) return hipSuccess;
+  // BNG has no near-ties, but its tiles still go dirty on a cell of more than 32
+  // chips, a candidate-list overflow or a chip without a strip index
+  const unsigned fix_blocks = (unsigned)(a.n_tiles < 512 ? a.n_tiles : 512);
   if (is == MGPU_H3) {
     hipLaunchKernelGGL(pip_join_kernel<MGPU_H3>, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, a);
     if (after_stream) hipEventRecord(after_stream, s);
-    const unsigned fix_blocks = (unsigned)(a.n_tiles < 512 ? a.n_tiles : 512);
     hipLaunchKernelGGL(pip_fix_kernel<MGPU_H3>, dim3(fix_blocks), dim3(kBlock), 0, s, a);
   } else {
     hipLaunchKernelGGL(pip_join_kernel<MGPU_BNG>, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, a);
     if (after_stream) hipEventRecord(after_stream, s);
+    hipLaunchKernelGGL(pip_fix_kernel<MGPU_BNG>, dim3(fix_blocks), dim3(kBlock), 0, s, a);
   }
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.group_sum,
                      (a.n_tiles + kScanGroup - 1) / kScanGroup, e.group_off, a.counters);

@@ -225,7 +225,7 @@ def test_pip_join_adversarial_points(gpu, nyc_chips_r9):
 def test_pip_join_bng_equals_oracle(gpu):
     from test_host import _bng_synthetic
     P = _bng_synthetic(seed=21, n=40)
-    for res in (3, 4, -4):
+    for res in (3, 4, -4, -2, -3, -5):
         c = M.tessellate(P, M.BNGIndexSystem(), res)
         rng = np.random.default_rng(res + 50)
         x = np.round(rng.uniform(505000, 560000, 1_000_000), 2)  # 0.01 m granularity like UPRNs
@@ -281,3 +281,78 @@ def test_pip_join_full_size_properties(gpu, nyc_chips_r9):
     gp = (p[mask] // 100).cpu().numpy()
     gq = r.polygon_id[mask].cpu().numpy()
     assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+
+
+# ---------------------------------------------------------------- BASELINE configs C4 / C5
+
+def test_pip_join_c4_london_districts_bng(gpu):
+    """C4 (BNG): UPRN-like points x Voronoi districts covering the London extent."""
+    import bench_workloads as W
+    P = W.london_districts()
+    for res in (3, 4):
+        c = M.tessellate(P, M.BNGIndexSystem(), res)
+        x, y = W.london_points(1_000_000, 40 + res)
+        r = M.pip_join(T(x, gpu), T(y, gpu), c, res, index_system=M.BNGIndexSystem())
+        op, oq = oracle_join(c, x, y, res=res, isys=1)
+        gp, gq = r.numpy()
+        assert np.array_equal(gp, op) and np.array_equal(gq, oq), res
+        assert len(gp) > 0.95 * len(x)  # the districts tile the extent
+
+
+def test_pip_join_c5_skewed_fractal(gpu):
+    """C5: points concentrated on the boundaries of 49k-vertex fractal polygons."""
+    import bench_workloads as W
+    P = W.skewed_polygons()
+    c = M.tessellate(P, M.H3IndexSystem(), 9)
+    x, y = W.boundary_points(P, 400_000, 11, 0.003)
+    r = M.pip_join(T(x, gpu), T(y, gpu), c, 9)
+    op, oq = oracle_join(c, x, y)
+    gp, gq = r.numpy()
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+    assert 0.2 * len(x) < len(gp) < 0.9 * len(x)
+
+
+@pytest.mark.parametrize("isys", ["h3", "bng"])
+def test_pip_join_more_than_32_chips_per_cell(gpu, isys):
+    """40 nested, overlapping polygons: every cell holds 40 chips, past the 32 the
+    streaming kernel keeps in a lane mask, so every tile goes through pip_fix_kernel."""
+    if isys == "h3":
+        base, sc, res, I = (-74.0, 40.7), 0.02, 7, M.H3IndexSystem()
+    else:
+        base, sc, res, I = (530000.0, 180000.0), 3000.0, 3, M.BNGIndexSystem()
+    sq = [(0.0, 0.0), (1.0, 0.0), (1.0, 1.0), (0.0, 1.0), (0.0, 0.0)]
+    polys = [(pid, [[[(base[0] + sc * u * (1 + 0.01 * pid), base[1] + sc * v * (1 + 0.013 * pid))
+                      for u, v in sq]]]) for pid in range(40, 0, -1)]
+    c = M.tessellate(M.Polygons.from_lists(polys), I, res)
+    rng = np.random.default_rng(33)
+    x = base[0] + sc * rng.uniform(-0.1, 1.6, 60_000)
+    y = base[1] + sc * rng.uniform(-0.1, 1.6, 60_000)
+    r = M.pip_join(T(x, gpu), T(y, gpu), c, res, index_system=I)
+    op, oq = oracle_join(c, x, y, res=res, isys=0 if isys == "h3" else 1)
+    gp, gq = r.numpy()
+    assert len(op) > 10 * len(x)
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+
+
+def test_pip_join_bng_near_origin(gpu):
+    """Chips and points around the BNG origin: negative eastings / northings give cell
+    ids outside the (column, row) bijection (the reference's truncating arithmetic), so
+    the dense grid must step aside for them -- chips there disable it, points there
+    take the id + hash route."""
+    I = M.BNGIndexSystem()
+    rng = np.random.default_rng(77)
+    x = np.round(rng.uniform(-3000, 3000, 400_000), 2)
+    y = np.round(rng.uniform(-3000, 3000, 400_000), 2)
+    sq = lambda a, b, c, d: [[[(a, b), (c, b), (c, d), (a, d), (a, b)]]]
+    for polys in ([(1, sq(-1500, -700, 1300, 2100)), (2, sq(-2900, -2900, 2950, 2950))],   # chips at negative cells
+                  [(1, sq(10, 20, 1990, 2500)), (2, sq(300, 300, 2900, 2900))]):         # chips positive only
+        for res in (4, -4, 3):
+            c = M.tessellate(M.Polygons.from_lists(polys), I, res)
+            r = M.pip_join(T(x, gpu), T(y, gpu), c, res, index_system=I)
+            op, oq = oracle_join(c, x, y, res=res, isys=1)
+            gp, gq = r.numpy()
+            assert np.array_equal(gp, op) and np.array_equal(gq, oq), res
+            # a join at another resolution than the chips': no dense grid either
+            r2 = M.pip_join(T(x, gpu), T(y, gpu), c, 5, index_system=I)
+            op2, oq2 = oracle_join(c, x, y, res=5, isys=1)
+            assert np.array_equal(r2.numpy()[0], op2) and np.array_equal(r2.numpy()[1], oq2)

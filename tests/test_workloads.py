@@ -1,0 +1,36 @@
+"""The synthetic workloads of BASELINE.json's configs (bench_workloads.py): shapes and
+tessellation invariants on the CPU; the GPU parity of their joins is in
+test_gpu_parity.py."""
+import os
+import sys
+
+import numpy as np
+
+import mosaic_amd as M
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import bench_workloads as W  # noqa: E402
+import oracle as O  # noqa: E402  (test infrastructure: the checker)
+
+
+def test_london_districts_partition_the_extent():
+    P = W.london_districts()
+    assert len(P.poly_part_off) - 1 > 150
+    c = M.tessellate(P, M.BNGIndexSystem(), 3)
+    x, y = W.london_points(20_000, 3)
+    pts, polys = O.pip_join(1, 3, x, y, c.cell, c.polygon_id, c.is_core, c.wkb_offsets, c.wkb)
+    # every point is in at most one district, and almost all in exactly one
+    assert len(np.unique(pts)) == len(pts)
+    assert len(pts) > 0.97 * len(x)
+
+
+def test_skewed_polygons_shape():
+    P = W.skewed_polygons()
+    assert len(P.poly_part_off) - 1 == 4
+    assert len(P.xy) > 4 * 10_000
+    x, y = W.boundary_points(P, 10_000, 1, 0.003)
+    assert x.shape == (10_000,) and np.isfinite(x).all() and np.isfinite(y).all()
+    c = M.tessellate(P, M.H3IndexSystem(), 9)
+    assert (c.is_core == 0).sum() > 100
