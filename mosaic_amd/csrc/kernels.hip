@@ -175,10 +175,19 @@ __device__ __forceinline__ Range probe_range(const ChipTableView& t, uint64_t ke
 // The chips of the point's cell.  *ok = false for non-finite coordinates.  *tie: in
 // the fast kernel (SLOW = false), the projection is in its tie band (the tile goes
 // to pip_fix_kernel); in the fix kernel, the H3 route's own near-tie flag (counted).
+// A dense-grid probe is left to the caller: *gi = the grid entry to load (the loads of
+// a lane's four points then fly together), else *gi = kNoEntry and the range is final.
+constexpr uint32_t kNoEntry = 0xFFFFFFFFu;
+
+__device__ __forceinline__ Range grid_range(uint64_t e) {
+  return Range{(uint32_t)e, (uint32_t)(e >> 32) & 0xFFFF, (uint32_t)(e >> 48)};
+}
+
 template <int IS, bool SLOW>
-__device__ __forceinline__ Range chip_range(const ChipTableView& t, double px, double py, int res, bool res_match,
-                                            bool* ok, bool* tie, int ablate) {
+__device__ __forceinline__ Range chip_probe(const ChipTableView& t, double px, double py, int res, bool res_match,
+                                            bool* ok, bool* tie, int ablate, uint32_t* gi) {
   *tie = false;
+  *gi = kNoEntry;
   if (IS == MGPU_BNG) {
     *ok = px == px && py == py;  // pointToIndex rejects NaN only
     if (!*ok || !res_match) return Range{0, 0, 0};
@@ -195,8 +204,9 @@ __device__ __forceinline__ Range chip_range(const ChipTableView& t, double px, d
       const uint32_t da = col - (uint32_t)D.a0, db = row - (uint32_t)D.b0;
       if (ablate == 2) return Range{0, (da ^ db) == 0x12345 ? 1u : 0u, 0};  // profiling: no probe
       if (da >= D.w || db >= D.h) return Range{0, 0, 0};
-      const uint64_t e = t.grid[D.base + db * D.w + da];
-      return Range{(uint32_t)e, (uint32_t)(e >> 32) & 0xFFFF, (uint32_t)(e >> 48)};
+      if (ablate == 6) return Range{(da * 7u + db) % t.n_chips, 1, 1};  // profiling: no grid load, one core chip
+      *gi = D.base + db * D.w + da;
+      return Range{0, 0, 0};
     }
     int64_t c;
     bng::point_to_cell(px, py, res, &c);
@@ -228,8 +238,9 @@ __device__ __forceinline__ Range chip_range(const ChipTableView& t, double px, d
       }
       const uint32_t da = (uint32_t)(ga - D.a0), db = (uint32_t)(gb - D.b0);
       if (da >= D.w || db >= D.h) return Range{0, 0, 0};
-      const uint64_t e = t.grid[D.base + db * D.w + da];
-      return Range{(uint32_t)e, (uint32_t)(e >> 32) & 0xFFFF, (uint32_t)(e >> 48)};
+      if (ablate == 6) return Range{(da * 7u + db) % t.n_chips, 1, 1};  // profiling: no grid load, one core chip
+      *gi = D.base + db * D.w + da;
+      return Range{0, 0, 0};
     }
     const uint64_t key = h3::lattice_key(f.face, f.ijk);
     if (ablate == 2) return Range{0, key == 0x123456789ULL ? 1u : 0u, 0};  // profiling: projection, no probe
@@ -248,6 +259,44 @@ __device__ __forceinline__ Range chip_range(const ChipTableView& t, double px, d
 
 __device__ __forceinline__ bool chip_is_core(const ChipTableView& t, const Range& r, uint32_t j) {
   return j < 16 ? ((r.core >> j) & 1) : (t.chip_flags[r.first + j] & kChipCore) != 0;
+}
+
+// Phase 1 for one point: its core chips match at once; every border chip becomes a
+// candidate (chip, point, slot j) in the tile's LDS list (a full list: the fast kernel
+// abandons the tile, the fix kernel evaluates the candidate on the spot).
+template <bool SLOW>
+__device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, const Range& r, double px, double py,
+                                            bool do_pip, bool& any_tie, uint32_t* s_ncand, uint16_t* s_cand_pj,
+                                            double2* s_cand_xy, uint32_t* s_first, uint16_t* s_cnt,
+                                            uint32_t* s_mask) {
+  // the streaming kernel keeps no sequential PIP path (its registers would cap
+  // occupancy): a cell with more than 32 chips sends the tile to pip_fix_kernel
+  if (!SLOW && r.count > (uint32_t)kMaskBits) any_tie = true;
+  const uint32_t nj = r.count < (uint32_t)kMaskBits ? r.count : (uint32_t)kMaskBits;
+  const uint32_t lowm = nj >= 32 ? 0xFFFFFFFFu : ((1u << nj) - 1);
+  uint32_t border = ~r.core & lowm;
+  for (uint32_t j = 16; j < nj; j++)
+    if (t.chip_flags[r.first + j] & kChipCore) border &= ~(1u << j);
+  uint32_t mask = lowm & ~border;
+  if (border && do_pip) {
+    const uint32_t nb = __popc(border);
+    uint32_t j0 = atomicAdd(s_ncand, nb);
+    for (uint32_t b = border; b; b &= b - 1) {
+      const uint32_t j = __builtin_ctz(b);
+      if (j0 < (uint32_t)kCandCap) {
+        s_cand_pj[j0] = (uint16_t)(li | (j << 10));
+        if (j0 < (uint32_t)kStash) s_cand_xy[j0] = make_double2(px, py);
+      } else if (!SLOW) {
+        any_tie = true;  // list full: the fix kernel evaluates such tiles
+      } else if (pip::chip_contains_strips(t, r.first + j, px, py)) {
+        mask |= 1u << j;  // list full: evaluate here
+      }
+      j0++;
+    }
+  }
+  s_first[li] = r.first;
+  s_cnt[li] = (uint16_t)(r.count > 0xFFFF ? 0xFFFF : r.count);
+  s_mask[li] = mask;
 }
 
 // One tile (see the phase comment above).  SLOW = false: the streaming kernel; a
@@ -282,71 +331,81 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 
   // ---- phase 1: cells, core matches, candidates
   bool any_tie = false, any_bad = false;
-  // one item ahead: item k + 1's coordinates load while item k computes
 #ifndef MGPU_NT_POINTS
-#define MGPU_NT_POINTS 0
+#define MGPU_NT_POINTS 1
 #endif
 #if MGPU_NT_POINTS
 #define MGPU_LDPT(ptr) __builtin_nontemporal_load(ptr)
 #else
 #define MGPU_LDPT(ptr) (*(ptr))
 #endif
-  double nx = 0.0, ny = 0.0;
-  if (base + threadIdx.x < a.n) {
-    nx = MGPU_LDPT(&a.x[base + threadIdx.x]);
-    ny = MGPU_LDPT(&a.y[base + threadIdx.x]);
-  }
+  if (IS == MGPU_BNG) {
+    // the cell is a few integer ops: the lane's four points load together, then
+    // their four grid entries (a wave's loads complete in order, so a load issued
+    // behind a point prefetch would wait for it)
+    double bx[kItems], by[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      const int64_t p = base + k * kBlock + threadIdx.x;
+      bx[k] = by[k] = 0.0;
+      if (p < a.n) {
+        bx[k] = MGPU_LDPT(&a.x[p]);
+        by[k] = MGPU_LDPT(&a.y[p]);
+      }
+    }
+    Range r[kItems];
+    uint32_t gi[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      r[k] = Range{0, 0, 0};
+      gi[k] = kNoEntry;
+      if (base + k * kBlock + threadIdx.x < a.n) {
+        bool ok, tie;
+        r[k] = chip_probe<IS, SLOW>(t, bx[k], by[k], a.res, res_match, &ok, &tie, a.ablate, &gi[k]);
+        any_bad |= !ok;
+      }
+    }
+    uint64_t ge[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; k++) ge[k] = gi[k] != kNoEntry ? t.grid[gi[k]] : 0;
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      if (gi[k] != kNoEntry) r[k] = grid_range(ge[k]);
+      phase1_item<SLOW>(t, k * kBlock + threadIdx.x, r[k], bx[k], by[k], do_pip, any_tie, &s_ncand, s_cand_pj,
+                        s_cand_xy, s_first, s_cnt, s_mask);
+    }
+  } else {
+    // one item ahead: item k + 1's coordinates load while item k projects
+    double nx = 0.0, ny = 0.0;
+    if (base + threadIdx.x < a.n) {
+      nx = MGPU_LDPT(&a.x[base + threadIdx.x]);
+      ny = MGPU_LDPT(&a.y[base + threadIdx.x]);
+    }
 #pragma unroll 1
-  for (int k = 0; k < kItems; k++) {
-    const int li = k * kBlock + threadIdx.x;
-    const int64_t p = base + li;
-    Range r{0, 0, 0};
-    uint32_t mask = 0;
-    const double px = nx, py = ny;
-    if (k + 1 < kItems && p + kBlock < a.n) {
-      nx = MGPU_LDPT(&a.x[p + kBlock]);
-      ny = MGPU_LDPT(&a.y[p + kBlock]);
-    }
-    if (p < a.n) {
-      bool ok, tie;
-      if (a.ablate == 3) {  // profiling: no projection, no probe
-        ok = true;
-        tie = false;
-      } else {
-        r = chip_range<IS, SLOW>(t, px, py, a.res, res_match, &ok, &tie, a.ablate);
+    for (int k = 0; k < kItems; k++) {
+      const int li = k * kBlock + threadIdx.x;
+      const int64_t p = base + li;
+      Range r{0, 0, 0};
+      const double px = nx, py = ny;
+      if (k + 1 < kItems && p + kBlock < a.n) {
+        nx = MGPU_LDPT(&a.x[p + kBlock]);
+        ny = MGPU_LDPT(&a.y[p + kBlock]);
       }
-      any_bad |= !ok;
-      any_tie |= tie;
-      // the streaming kernel keeps no sequential PIP path (its registers would cap
-      // occupancy): a cell with more than 32 chips sends the tile to pip_fix_kernel
-      if (!SLOW && r.count > (uint32_t)kMaskBits) any_tie = true;
-      const uint32_t nj = r.count < (uint32_t)kMaskBits ? r.count : (uint32_t)kMaskBits;
-      const uint32_t lowm = nj >= 32 ? 0xFFFFFFFFu : ((1u << nj) - 1);
-      uint32_t border = ~r.core & lowm;
-      for (uint32_t j = 16; j < nj; j++)
-        if (t.chip_flags[r.first + j] & kChipCore) border &= ~(1u << j);
-      mask = lowm & ~border;
-      if (border && do_pip) {
-        const uint32_t nb = __popc(border);
-        const uint32_t c0 = atomicAdd(&s_ncand, nb);
-        uint32_t j0 = c0;
-        for (uint32_t b = border; b; b &= b - 1) {
-          const uint32_t j = __builtin_ctz(b);
-          if (j0 < (uint32_t)kCandCap) {
-            s_cand_pj[j0] = (uint16_t)(li | (j << 10));
-            if (j0 < (uint32_t)kStash) s_cand_xy[j0] = make_double2(px, py);
-          } else if (!SLOW) {
-            any_tie = true;  // list full: the fix kernel evaluates such tiles
-          } else if (pip::chip_contains_strips(t, r.first + j, px, py)) {
-            mask |= 1u << j;  // list full: evaluate here
-          }
-          j0++;
+      if (p < a.n) {
+        bool ok, tie;
+        if (a.ablate == 3) {  // profiling: no projection, no probe
+          ok = true;
+          tie = false;
+        } else {
+          uint32_t gi;
+          r = chip_probe<IS, SLOW>(t, px, py, a.res, res_match, &ok, &tie, a.ablate, &gi);
+          if (gi != kNoEntry) r = grid_range(t.grid[gi]);
         }
+        any_bad |= !ok;
+        any_tie |= tie;
       }
+      phase1_item<SLOW>(t, li, r, px, py, do_pip, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
     }
-    s_first[li] = r.first;
-    s_cnt[li] = (uint16_t)(r.count > 0xFFFF ? 0xFFFF : r.count);
-    s_mask[li] = mask;
   }
   count_wave(&a.counters[2], any_bad);
   if (SLOW) count_wave(&a.counters[1], any_tie);
@@ -533,7 +592,17 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   }
   if (!staged || !rec) return;
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < agg; i += kBlock) rec[i] = ((uint64_t)s_out_li[i] << 32) | (uint32_t)s_out_poly[i];
+#ifndef MGPU_NT_RECS
+#define MGPU_NT_RECS 1
+#endif
+  for (uint32_t i = threadIdx.x; i < agg; i += kBlock) {
+    const uint64_t v = ((uint64_t)s_out_li[i] << 32) | (uint32_t)s_out_poly[i];
+#if MGPU_NT_RECS
+    __builtin_nontemporal_store(v, &rec[i]);
+#else
+    rec[i] = v;
+#endif
+  }
 }
 
 template <int IS>

@@ -9,7 +9,8 @@ Times, on the bench workload (uniform NYC-bbox points x 263 zones, H3 res 9):
   join/noproj   no projection either: point loads + tile protocol only (MGPU_ABLATE=3)
   join/listonly candidates listed, none evaluated (MGPU_ABLATE=4)
   join/envonly  candidates evaluated by the chip envelope only (MGPU_ABLATE=5)
-Prints one JSON object.  Kernel times come from HIP events around the launch.
+  join/nogridload  dense probe replaced by one synthetic core chip (MGPU_ABLATE=6)
+Prints one JSON object.  Times: the streaming kernel (pip_join_kernel), HIP events on its stream.
 """
 import argparse
 import json
@@ -26,7 +27,9 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--points", type=int, default=100_000_000)
-    ap.add_argument("--res", type=int, default=9)
+    ap.add_argument("--res", type=int, default=None)
+    ap.add_argument("--config", choices=["c2", "c4", "c5"], default="c2")
+    ap.add_argument("--seed", type=int, default=0x20250314)
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
     import mosaic_amd as M
@@ -34,19 +37,21 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     ctx = M.default_context(dev)
-    zones = M.Polygons.from_npz(os.path.join(ROOT, "tests", "golden", "nyc_taxi_zones.npz"))
-    chips = M.tessellate(zones, M.H3IndexSystem(), a.res).upload(ctx)
-    x, y = B.gen_points(a.points, 0, 0x20250314, dev)
-    cap = a.points // 2 + 1024
+    import bench_workloads as W
+    wl = B.workload(a, W, M)
+    isys = wl["isys"]
+    chips = M.tessellate(wl["polygons"], isys, a.res).upload(ctx)
+    x, y = wl["points"](a.points, 0, dev)
+    cap = max(int(a.points * wl["pairs_per_point"]), a.points) + 1024
     op = torch.empty(cap, dtype=torch.int64, device=dev)
     oq = torch.empty(cap, dtype=torch.int32, device=dev)
     ctx.reserve(a.points)
-    out = {"points": a.points, "res": a.res}
+    out = {"points": a.points, "res": a.res, "config": a.config}
 
     def t_cells():
         ms = []
         for _ in range(a.reps + 1):
-            _, st = M.grid_longlatascellid(x, y, a.res, stats=True)
+            _, st = M.grid_longlatascellid(x, y, a.res, index_system=isys, stats=True)
             ms.append(st["kernel_ms"])
         return float(np.median(ms[1:]))
 
@@ -57,8 +62,8 @@ def main():
             os.environ.pop("MGPU_ABLATE", None)
         ms = []
         for _ in range(a.reps + 1):
-            r = M.pip_join(x, y, chips, a.res, out=(op, oq), capacity=cap)
-            ms.append(r.stats["kernel_ms"])
+            r = M.pip_join(x, y, chips, a.res, out=(op, oq), capacity=cap, index_system=isys)
+            ms.append(r.stats["stream_kernel_ms"])
         os.environ.pop("MGPU_ABLATE", None)
         return float(np.median(ms[1:])), len(r)
 
@@ -69,6 +74,7 @@ def main():
     out["join_noproj_ms"], _ = t_join(3)
     out["join_listonly_ms"], _ = t_join(4)
     out["join_envonly_ms"], _ = t_join(5)
+    out["join_nogridload_ms"], out["pairs_nogridload"] = t_join(6)
     print(json.dumps(out), flush=True)
 
 

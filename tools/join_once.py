@@ -14,7 +14,9 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--points", type=int, default=100_000_000)
-    ap.add_argument("--res", type=int, default=9)
+    ap.add_argument("--res", type=int, default=None)
+    ap.add_argument("--config", choices=["c2", "c4", "c5"], default="c2")
+    ap.add_argument("--seed", type=int, default=0x20250314)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--ablate", type=int, default=0)
     ap.add_argument("--cells", action="store_true")
@@ -28,10 +30,12 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     ctx = M.default_context(dev)
-    zones = M.Polygons.from_npz(os.path.join(ROOT, "tests", "golden", "nyc_taxi_zones.npz"))
-    chips = M.tessellate(zones, M.H3IndexSystem(), a.res).upload(ctx)
-    x, y = B.gen_points(a.points, 0, 0x20250314, dev)
-    cap = a.points // 2 + 1024
+    import bench_workloads as W
+    wl = B.workload(a, W, M)
+    isys = wl["isys"]
+    chips = M.tessellate(wl["polygons"], isys, a.res).upload(ctx)
+    x, y = wl["points"](a.points, 0, dev)
+    cap = int(a.points * wl["pairs_per_point"]) + 1024
     op = torch.empty(cap, dtype=torch.int64, device=dev)
     oq = torch.empty(cap, dtype=torch.int32, device=dev)
     ctx.reserve(a.points)
@@ -42,9 +46,9 @@ def main():
         if a.cells and a.bng:
             M.grid_longlatascellid(x, y, 4, index_system=M.BNGIndexSystem())
         elif a.cells:
-            M.grid_longlatascellid(x, y, a.res)
+            M.grid_longlatascellid(x, y, a.res, index_system=isys)
         else:
-            M.pip_join(x, y, chips, a.res, out=(op, oq), capacity=cap)
+            M.pip_join(x, y, chips, a.res, out=(op, oq), capacity=cap, index_system=isys)
     torch.cuda.synchronize()
     print("done", flush=True)
 

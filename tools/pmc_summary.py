@@ -8,13 +8,14 @@ import os
 import sys
 
 d = sys.argv[1]
+kern = sys.argv[2] if len(sys.argv) > 2 else "mgpu::"
 for args in sorted(glob.glob(os.path.join(d, "c*.args"))):
     c = os.path.basename(args)[:-5]
     vals = collections.defaultdict(list)
     for f in glob.glob(os.path.join(d, c + "_p*", "run_counter_collection.csv")):
         per = collections.defaultdict(float)
         for r in csv.DictReader(open(f)):
-            if "mgpu::" not in r["Kernel_Name"]:
+            if kern not in r["Kernel_Name"]:
                 continue
             per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
         for (disp, name), v in per.items():
