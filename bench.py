@@ -18,7 +18,7 @@ tile_scan_kernel and pair_emit_kernel (ordered (point_id, polygon_id) output).
 
 Also reported: the dominant kernel's (pip_join_kernel) achieved bandwidth against the
 HBM roofline -- algorithmic bytes per launch = 16 B per point read + 8 B per pair
-record written + 12 B per 1024-point tile, over its average duration
+record written + 12 B per tile (256 points), over its average duration
 measured with HIP events on the launch stream -- the HBM bytes the PMC counters saw
 (profiles/pmc_join_traffic.json, when it was measured on this workload), and a CPU
 baseline: the oracle's multithreaded C restatement of the reference path on a
@@ -211,7 +211,8 @@ def main():
     ms_step = elapsed / a.steps * 1e3
     pipeline_ms = float(np.mean(kms))
     stream_ms = float(np.mean(sms))
-    tiles = (n + 1023) // 1024
+    tp = M._native.lib().mgpu_join_tile_points()
+    tiles = (n + tp - 1) // tp
     alg_bytes = 16.0 * n + 8.0 * pairs + 12.0 * tiles
     achieved = alg_bytes / (stream_ms * 1e-3) / 1e9
     out = {

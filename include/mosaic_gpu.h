@@ -61,6 +61,9 @@ typedef struct mgpu_stats {
 
 const char* mgpu_last_error(void);
 const char* mgpu_version(void);
+/* Points per tile of mgpu_pip_join (its per-tile workspace and statistics; no
+ * reference counterpart). */
+int32_t mgpu_join_tile_points(void);
 
 /* One context per GPU/executor: owns the stream-ordered workspace. */
 int32_t mgpu_ctx_create(int32_t device_id, mgpu_ctx** out);

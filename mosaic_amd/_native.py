@@ -25,7 +25,7 @@ MGPU_BNG = 1
 
 # every symbol include/mosaic_gpu.h declares
 EXPORTS = (
-    "mgpu_last_error", "mgpu_version", "mgpu_ctx_create", "mgpu_ctx_destroy", "mgpu_check_resolution",
+    "mgpu_last_error", "mgpu_version", "mgpu_join_tile_points", "mgpu_ctx_create", "mgpu_ctx_destroy", "mgpu_check_resolution",
     "mgpu_points_to_cells", "mgpu_points_to_cells_host", "mgpu_bng_format", "mgpu_bng_parse",
     "mgpu_chips_upload", "mgpu_chips_destroy", "mgpu_chips_device_blob", "mgpu_chips_from_device_blob",
     "mgpu_chips_info", "mgpu_st_contains", "mgpu_pip_join", "mgpu_pip_join_async", "mgpu_ctx_reserve",
@@ -83,6 +83,7 @@ def lib():
     sig = {
         "mgpu_last_error": (ctypes.c_char_p, []),
         "mgpu_version": (ctypes.c_char_p, []),
+        "mgpu_join_tile_points": (ctypes.c_int32, []),
         "mgpu_ctx_create": (I32, [I32, ctypes.POINTER(P)]),
         "mgpu_ctx_destroy": (I32, [P]),
         "mgpu_check_resolution": (I32, [I32, I32]),

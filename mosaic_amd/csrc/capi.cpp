@@ -468,7 +468,7 @@ namespace {
 //   [group_sum u32 x T/32]
 //   [dirty tiles u32 x T] [cells near-tie queue u64 x (1 + kTieCap)]
 //   [records u64 x (T * tile points + pool)]
-// counters: [0] pairs [1] route near-ties [2] invalid points [3] candidates
+// counters: [0] pairs [1] route near-ties [2] invalid points [3] candidates (tile_scan_kernel)
 //           [5] pool records used [6] dirty tiles (u32) [8..] MGPU_STATS
 // T = tiles of the largest point batch reserved; pool = overflow records (tiles with
 // more pairs than points), at most the output capacity.
@@ -487,7 +487,7 @@ WsLayout ws_layout(int64_t n_tiles, int64_t pool) {
   L.where = align_up(L.count + T * 4, 256);
   L.off = align_up(L.where + T * 8, 256);
   L.gsum = align_up(L.off + T * 8, 256);
-  L.dirty = align_up(L.gsum + (T / 32 + 1) * 4, 256);
+  L.dirty = align_up(L.gsum + 2 * (T / 32 + 1) * 4, 256);  // group pair sums, group candidate sums
   L.ties = align_up(L.dirty + T * 4, 256);
   L.recs = align_up(L.ties + (size_t)(kTieCap + 1) * 8, 256);
   L.total = align_up(L.recs + (T * (size_t)mgpu::join_tile_points() + (size_t)std::max<int64_t>(pool, 0)) * 8, 256);
@@ -528,6 +528,7 @@ extern "C" {
 
 const char* mgpu_last_error(void) { return g_err.c_str(); }
 const char* mgpu_version(void) { return "mosaic-mi355x 0.1.0 (gfx950)"; }
+int32_t mgpu_join_tile_points(void) { return (int32_t)mgpu::join_tile_points(); }
 
 int32_t mgpu_check_resolution(int32_t index_system, int32_t res) { return check_res(index_system, res); }
 
@@ -990,6 +991,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   e.tile_count = a.tile_count;
   e.group_off = (uint64_t*)(base + L.off);
   a.group_sum = (uint32_t*)(base + L.gsum);
+  a.group_cand = a.group_sum + (tiles / 32 + 1);
   e.tile_where = a.tile_where;
   e.recs = a.recs;
   e.point_id = point_id;
@@ -998,7 +1000,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   e.out_point = out_point;
   e.out_poly = out_poly;
   HIP_TRY(hipMemsetAsync(base, 0, kWsCounters, s));
-  HIP_TRY(hipMemsetAsync(base + L.gsum, 0, ((size_t)tiles / 32 + 1) * 4, s));
+  HIP_TRY(hipMemsetAsync(base + L.gsum, 0, 2 * ((size_t)tiles / 32 + 1) * 4, s));
   if (timed) HIP_TRY(hipEventRecord(ctx->ev0, s));
   HIP_TRY(mgpu::launch_join(is, a, e, s, timed ? ctx->ev2 : nullptr));
   if (timed) HIP_TRY(hipEventRecord(ctx->ev1, s));

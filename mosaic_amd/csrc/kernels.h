@@ -18,6 +18,7 @@ struct JoinArgs {
   ChipTableView chips;
   uint32_t* tile_count;             // [n_tiles] pairs of each tile
   uint32_t* group_sum;              // [n_tiles / 32] pairs per group of 32 tiles, zeroed before launch
+  uint32_t* group_cand;             // [n_tiles / 32] border-chip candidates per group (statistics), zeroed
   uint64_t* tile_where;             // [n_tiles] first record of the tile in `recs` (~0: dropped)
   uint64_t* recs;                   // [n_tiles * tile points] slots, then [pool_cap] overflow pool
   int64_t pool_cap;

@@ -8,8 +8,8 @@
 //   st_contains_kernel   st_contains(chip.wkb, point) for explicit pairs
 //
 // Design (DESIGN.md has the roofline analysis): the hot path is one pass over the
-// points plus two light launches.  pip_join_kernel gives each 256-thread workgroup a
-// tile of 1024 consecutive points (4 per lane); the chip table's cell hash and the
+// points plus two light launches.  pip_join_kernel gives each one-wave workgroup a
+// tile of 256 consecutive points (4 per lane; no workgroup barrier waits); the chip table's cell hash and the
 // border chips' strip-indexed edges are small and read-only, so they stay in L2 /
 // Infinity Cache while the point stream flows from HBM.  A tile writes its pairs as
 // compact records into its own slot -- no workgroup ever waits for another --
@@ -29,11 +29,12 @@ namespace mgpu {
 
 // the join's tile: one workgroup of kBlock threads, kItems points per thread
 #ifndef MGPU_BLOCK
-#define MGPU_BLOCK 256
+#define MGPU_BLOCK 64
 #endif
 constexpr int kBlock = MGPU_BLOCK;
 constexpr int kItems = 4;
 constexpr int kTile = kBlock * kItems;
+constexpr int kStreamBlock = 256;  // the per-point kernels (cells, st_contains)
 static_assert(kTile <= 1024, "point-in-tile indices are 10 bits");
 
 constexpr uint64_t kNoDst = ~0ULL;
@@ -57,7 +58,7 @@ __device__ __forceinline__ void count_wave(unsigned long long* ctr, bool pred) {
 // IndexSystem.pointToIndex over a batch.  H3: fast projection; near-ties are queued
 // (ties[0] = count, ties[1 ..] = point indices) for cells_fix_kernel.
 template <int IS>
-__global__ __launch_bounds__(kBlock) void cells_kernel(const double* __restrict__ x, const double* __restrict__ y,
+__global__ __launch_bounds__(kStreamBlock) void cells_kernel(const double* __restrict__ x, const double* __restrict__ y,
                                                        int64_t n, int res, int64_t* __restrict__ out,
                                                        unsigned long long* __restrict__ counters,
                                                        unsigned long long* __restrict__ ties, int64_t tie_cap) {
@@ -89,7 +90,7 @@ __global__ __launch_bounds__(kBlock) void cells_kernel(const double* __restrict_
 
 // The queued near-ties by the H3 route; if the queue overflowed, every point again
 // (fast path + route where needed).
-__global__ __launch_bounds__(kBlock) void cells_fix_kernel(const double* __restrict__ x, const double* __restrict__ y,
+__global__ __launch_bounds__(kStreamBlock) void cells_fix_kernel(const double* __restrict__ x, const double* __restrict__ y,
                                                            int64_t n, int res, int64_t* __restrict__ out,
                                                            unsigned long long* __restrict__ counters,
                                                            const unsigned long long* __restrict__ ties,
@@ -299,6 +300,24 @@ __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, cons
   s_mask[li] = mask;
 }
 
+// Profiling builds (-DMGPU_STAMPS): thread 0 of each tile adds the wall-clock ticks
+// (100 MHz) spent in each phase to counters[10 + phase]: 1 = phase 1, 2 = phase 2,
+// 3 = phase 2b, 4 = phase 3 (output).
+#ifdef MGPU_STAMPS
+#define MGPU_STAMP(ph)                                                              \
+  do {                                                                              \
+    if (threadIdx.x == 0) {                                                         \
+      const uint64_t now = wall_clock64();                                          \
+      if ((ph) > 0) atomicAdd(&a.counters[9 + (ph)], (unsigned long long)(now - st_t)); \
+      st_t = now;                                                                   \
+    }                                                                               \
+  } while (0)
+#else
+#define MGPU_STAMP(ph) \
+  do {             \
+  } while (0)
+#endif
+
 // One tile (see the phase comment above).  SLOW = false: the streaming kernel; a
 // tile with a near-tie point is queued for pip_fix_kernel and abandoned after phase 1.
 // SLOW = true: the fix kernel; near-ties go through the H3 route.
@@ -319,6 +338,9 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   int32_t* s_out_poly = (int32_t*)s_buf;                          // [kOutCap]
   uint16_t* s_out_li = (uint16_t*)(s_buf + kOutCap * 4);          // [kOutCap]
 
+#ifdef MGPU_STAMPS
+  uint64_t st_t = 0;
+#endif
   if (threadIdx.x == 0) {
     s_ncand = 0;
     s_nmix = 0;
@@ -329,6 +351,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   const bool res_match = a.res_match;
   const bool do_pip = a.ablate != 1;
 
+  MGPU_STAMP(0);
   // ---- phase 1: cells, core matches, candidates
   bool any_tie = false, any_bad = false;
 #ifndef MGPU_NT_POINTS
@@ -420,8 +443,10 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     return;
   }
   __syncthreads();
+  MGPU_STAMP(1);
   const uint32_t ncand = s_ncand < (uint32_t)kCandCap ? s_ncand : (uint32_t)kCandCap;
-  if (threadIdx.x == 0 && s_ncand) atomicAdd(&a.counters[3], (unsigned long long)s_ncand);
+  // per scan group, not one global counter: same-address atomics from every tile serialize
+  if (threadIdx.x == 0 && s_ncand) atomicAdd(&a.group_cand[tile / kScanGroup], s_ncand);
 
   // ---- phase 2: lane per candidate: envelope / rectangle / classification grid.
   // Candidates in a mixed grid cell (~1 in 8) are listed again and evaluated in
@@ -471,6 +496,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     return;
   }
   __syncthreads();
+  MGPU_STAMP(2);
   const uint32_t nmix = s_nmix < (uint32_t)kMixCap ? s_nmix : (uint32_t)kMixCap;
 #ifdef MGPU_STATS
   uint32_t st_edges = 0;
@@ -512,6 +538,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #endif
   __syncthreads();
 
+  MGPU_STAMP(3);
   // ---- phase 3: lane l owns points 4l .. 4l+3 (input order)
   const int l0 = threadIdx.x * kItems;
   uint32_t mine = 0;
@@ -590,6 +617,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
       pos++;
     }
   }
+  MGPU_STAMP(4);
   if (!staged || !rec) return;
   __syncthreads();
 #ifndef MGPU_NT_RECS
@@ -603,11 +631,43 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     rec[i] = v;
 #endif
   }
+  MGPU_STAMP(4);
 }
 
+// Persistent (MGPU_PERSIST, default): a grid of resident workgroups walks the tiles,
+// so small tiles cost no workgroup dispatch each.
+#ifndef MGPU_PERSIST
+#define MGPU_PERSIST 0
+#endif
 template <int IS>
 __global__ __launch_bounds__(kBlock) void pip_join_kernel(JoinArgs a) {
+#if MGPU_PERSIST
+  for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    join_tile<IS, false>(a, (uint32_t)tile);
+    __syncthreads();
+  }
+#else
   join_tile<IS, false>(a, blockIdx.x);
+#endif
+}
+
+// resident workgroups of pip_join_kernel<IS> on the device (persistent grid size)
+template <int IS>
+unsigned join_grid(int64_t n_tiles) {
+#if MGPU_PERSIST
+  static int resident[2] = {0, 0};
+  int& r = resident[IS == MGPU_H3 ? 0 : 1];
+  if (!r) {
+    int dev = 0, cus = 0, per = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pip_join_kernel<IS>, kBlock, 0);
+    r = cus * (per > 0 ? per : 1);
+  }
+  return (unsigned)(n_tiles < r ? n_tiles : r);
+#else
+  return (unsigned)n_tiles;
+#endif
 }
 
 // The tiles queued by pip_join_kernel, with the H3 route for their near-ties.
@@ -625,12 +685,17 @@ __global__ __launch_bounds__(kBlock) void pip_fix_kernel(JoinArgs a) {
 // (~3e3 per 1e8 points, coalesced chunks of 1024) and pair_emit_kernel adds the counts
 // of the tile's predecessors inside its group.  counters[0] = total pairs.
 constexpr int kScanBlock = 1024;
-__global__ __launch_bounds__(kScanBlock) void tile_scan_kernel(const uint32_t* __restrict__ gsum, int64_t ng,
+__global__ __launch_bounds__(kScanBlock) void tile_scan_kernel(const uint32_t* __restrict__ gsum,
+                                                               const uint32_t* __restrict__ gcand, int64_t ng,
                                                                uint64_t* __restrict__ goff,
                                                                unsigned long long* __restrict__ counters) {
   __shared__ unsigned long long s_w[kScanBlock / 64];
   __shared__ unsigned long long s_carry;
   if (threadIdx.x == 0) s_carry = 0;
+  unsigned long long cand = 0;
+  for (int64_t i = threadIdx.x; i < ng; i += kScanBlock) cand += gcand[i];
+  cand = wave_sum_u64(cand);
+  if ((threadIdx.x & 63) == 0 && cand) atomicAdd(&counters[3], cand);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int64_t b = 0; b < ng; b += kScanBlock) {
     const int64_t i = b + threadIdx.x;
@@ -656,38 +721,53 @@ __global__ __launch_bounds__(kScanBlock) void tile_scan_kernel(const uint32_t* _
   if (threadIdx.x == 0) counters[0] = s_carry;
 }
 
-// Ordered output: tile t's records -> out[offset of t ...] with point ids.
-__global__ __launch_bounds__(kBlock) void pair_emit_kernel(EmitArgs a) {
+// Ordered output: the records of kEmitTiles consecutive tiles (their output ranges are
+// contiguous) -> out[offset of the first ...] with point ids, as one flat stream over
+// the workgroup's lanes.
+constexpr int kEmitBlock = 256;
+constexpr int kEmitTiles = 4096 / kTile;  // 4 tiles of 1024 points, 16 of 256
+static_assert(kScanGroup % kEmitTiles == 0 && kEmitTiles <= 64, "emit groups inside scan groups");
+__global__ __launch_bounds__(kEmitBlock) void pair_emit_kernel(EmitArgs a, int64_t n_tiles) {
+  __shared__ uint32_t s_pref[kEmitTiles + 1];
+  __shared__ uint64_t s_where[kEmitTiles];
   __shared__ int64_t s_off;
-  const int64_t t = blockIdx.x;
-  const uint32_t n = a.tile_count[t];
-  if (!n) return;
-  const uint64_t where = a.tile_where[t];
-  if (where == kNoDst) return;  // pool exhausted: the total exceeds the capacity
+  const int64_t t0 = (int64_t)blockIdx.x * kEmitTiles;
   if (threadIdx.x < 64) {
-    // predecessors inside the tile's scan group
-    const int64_t g0 = t - t % kScanGroup;
-    const int64_t j = g0 + threadIdx.x;
-    unsigned long long v = (threadIdx.x < kScanGroup && j < t) ? a.tile_count[j] : 0u;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    if (threadIdx.x == 0) s_off = (int64_t)(a.group_off[t / kScanGroup] + v);
+    const int lane = threadIdx.x;
+    // this block's tiles: counts, slots, in-block prefix
+    const int64_t t = t0 + lane;
+    const uint32_t c = (lane < kEmitTiles && t < n_tiles) ? a.tile_count[t] : 0u;
+    if (lane < kEmitTiles) s_where[lane] = t < n_tiles ? a.tile_where[t] : kNoDst;
+    const uint32_t incl = wave_incl_scan(c);
+    if (lane < kEmitTiles) s_pref[lane + 1] = incl;
+    if (lane == 0) s_pref[0] = 0;
+    // predecessors of t0 inside its scan group
+    const int64_t g0 = t0 - t0 % kScanGroup;
+    const int64_t j = g0 + lane;
+    unsigned long long v = (lane < kScanGroup && j < t0) ? a.tile_count[j] : 0u;
+    v = wave_sum_u64(v);
+    if (lane == 0) s_off = (int64_t)(a.group_off[t0 / kScanGroup] + v);
   }
   __syncthreads();
+  const uint32_t total = s_pref[kEmitTiles];
   const int64_t off = s_off;
-  const uint64_t* src = a.recs + where;
-  const int64_t base = t * kTile;
-  for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+  for (uint32_t i = threadIdx.x; i < total; i += kEmitBlock) {
     const int64_t q = off + i;
     if (q >= a.capacity) break;
-    const uint64_t r = src[i];
-    const int64_t p = base + (int64_t)(r >> 32);
+    int k = 0;
+#pragma unroll
+    for (int step = kEmitTiles / 2; step >= 1; step >>= 1)
+      if (s_pref[k + step] <= i) k += step;
+    const uint64_t where = s_where[k];
+    if (where == kNoDst) continue;  // pool exhausted: the total exceeds the capacity
+    const uint64_t r = a.recs[where + (i - s_pref[k])];
+    const int64_t p = (t0 + k) * kTile + (int64_t)(r >> 32);
     a.out_point[q] = a.point_id ? a.point_id[p] : a.id_base + p;
     a.out_poly[q] = (int32_t)(uint32_t)r;
   }
 }
 
-__global__ __launch_bounds__(kBlock) void st_contains_kernel(ChipTableView t, const int64_t* __restrict__ row,
+__global__ __launch_bounds__(kStreamBlock) void st_contains_kernel(ChipTableView t, const int64_t* __restrict__ row,
                                                              const double* __restrict__ x,
                                                              const double* __restrict__ y, int64_t n,
                                                              int8_t* __restrict__ out) {
@@ -711,14 +791,14 @@ __global__ __launch_bounds__(kBlock) void st_contains_kernel(ChipTableView t, co
 hipError_t launch_cells(int is, int res, const double* x, const double* y, int64_t n, int64_t* out,
                         unsigned long long* counters, unsigned long long* ties, int64_t tie_cap, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  int64_t blocks = (n + kBlock - 1) / kBlock;
+  int64_t blocks = (n + kStreamBlock - 1) / kStreamBlock;
   if (blocks > 256 * 64) blocks = 256 * 64;
   if (is == MGPU_H3) {
-    hipLaunchKernelGGL(cells_kernel<MGPU_H3>, dim3((unsigned)blocks), dim3(kBlock), 0, s, x, y, n, res, out, counters,
+    hipLaunchKernelGGL(cells_kernel<MGPU_H3>, dim3((unsigned)blocks), dim3(kStreamBlock), 0, s, x, y, n, res, out, counters,
                        ties, tie_cap);
-    hipLaunchKernelGGL(cells_fix_kernel, dim3(256), dim3(kBlock), 0, s, x, y, n, res, out, counters, ties, tie_cap);
+    hipLaunchKernelGGL(cells_fix_kernel, dim3(256), dim3(kStreamBlock), 0, s, x, y, n, res, out, counters, ties, tie_cap);
   } else {
-    hipLaunchKernelGGL(cells_kernel<MGPU_BNG>, dim3((unsigned)blocks), dim3(kBlock), 0, s, x, y, n, res, out,
+    hipLaunchKernelGGL(cells_kernel<MGPU_BNG>, dim3((unsigned)blocks), dim3(kStreamBlock), 0, s, x, y, n, res, out,
                        counters, ties, tie_cap);
   }
   return hipGetLastError();
@@ -733,24 +813,25 @@ hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t
   // chips, a candidate-list overflow or a chip without a strip index
   const unsigned fix_blocks = (unsigned)(a.n_tiles < 512 ? a.n_tiles : 512);
   if (is == MGPU_H3) {
-    hipLaunchKernelGGL(pip_join_kernel<MGPU_H3>, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(pip_join_kernel<MGPU_H3>, dim3(join_grid<MGPU_H3>(a.n_tiles)), dim3(kBlock), 0, s, a);
     if (after_stream) hipEventRecord(after_stream, s);
     hipLaunchKernelGGL(pip_fix_kernel<MGPU_H3>, dim3(fix_blocks), dim3(kBlock), 0, s, a);
   } else {
-    hipLaunchKernelGGL(pip_join_kernel<MGPU_BNG>, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(pip_join_kernel<MGPU_BNG>, dim3(join_grid<MGPU_BNG>(a.n_tiles)), dim3(kBlock), 0, s, a);
     if (after_stream) hipEventRecord(after_stream, s);
     hipLaunchKernelGGL(pip_fix_kernel<MGPU_BNG>, dim3(fix_blocks), dim3(kBlock), 0, s, a);
   }
-  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.group_sum,
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.group_sum, a.group_cand,
                      (a.n_tiles + kScanGroup - 1) / kScanGroup, e.group_off, a.counters);
-  hipLaunchKernelGGL(pair_emit_kernel, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, e);
+  hipLaunchKernelGGL(pair_emit_kernel, dim3((unsigned)((a.n_tiles + kEmitTiles - 1) / kEmitTiles)),
+                     dim3(kEmitBlock), 0, s, e, a.n_tiles);
   return hipGetLastError();
 }
 
 hipError_t launch_st_contains(const ChipTableView& t, const int64_t* row, const double* x, const double* y, int64_t n,
                               int8_t* out, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(st_contains_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, t, row, x,
+  hipLaunchKernelGGL(st_contains_kernel, dim3((unsigned)((n + kStreamBlock - 1) / kStreamBlock)), dim3(kStreamBlock), 0, s, t, row, x,
                      y, n, out);
   return hipGetLastError();
 }
