@@ -147,9 +147,12 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 // 32nd of a cell in phase 3.
 constexpr int kCandCap = kTile;
 constexpr int kMixCap = kTile / 2;  // mixed-cell candidates (phase 2b), after the list in s_buf
-constexpr int kOutCap = 2 * kTile;
+#ifndef MGPU_OUTCAP
+#define MGPU_OUTCAP 352
+#endif
+constexpr int kOutCap = MGPU_OUTCAP;  // pairs a tile stages in LDS
 #ifndef MGPU_STASH
-#define MGPU_STASH (kTile / 2)
+#define MGPU_STASH 80
 #endif
 constexpr int kStash = MGPU_STASH;  // candidates whose coordinates phase 1 leaves in LDS
 static_assert(kCandCap * 2 + kMixCap * 2 + kStash * 16 <= kOutCap * 6, "phase 1-2 lists fit the staging buffer");
@@ -634,13 +637,24 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   MGPU_STAMP(4);
 }
 
-// Persistent (MGPU_PERSIST, default): a grid of resident workgroups walks the tiles,
-// so small tiles cost no workgroup dispatch each.
+// MGPU_PERSIST=1 (not the default: measured 25% slower): a grid of resident
+// workgroups walks the tiles instead of one workgroup per tile.
 #ifndef MGPU_PERSIST
 #define MGPU_PERSIST 0
 #endif
+// 8 waves per SIMD: the tile's LDS (~4.7 KB) allows 32 workgroups per CU, and the
+// kernel is held to 64 VGPRs (it is latency-bound: the 8th wave measured -7% on C2,
+// -10% on C5)
+#ifndef MGPU_WAVES_PER_EU
+#define MGPU_WAVES_PER_EU 8
+#endif
+#if MGPU_WAVES_PER_EU
+#define MGPU_JOIN_ATTR __attribute__((amdgpu_waves_per_eu(MGPU_WAVES_PER_EU)))
+#else
+#define MGPU_JOIN_ATTR
+#endif
 template <int IS>
-__global__ __launch_bounds__(kBlock) void pip_join_kernel(JoinArgs a) {
+__global__ __launch_bounds__(kBlock) MGPU_JOIN_ATTR void pip_join_kernel(JoinArgs a) {
 #if MGPU_PERSIST
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
     join_tile<IS, false>(a, (uint32_t)tile);
