@@ -41,15 +41,24 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 METRIC = "PIP-join points/sec (H3 res 9) at 1/2/4/8 GPUs + achieved HBM GB/s"
 
 
+def log(msg):
+    """Progress to stderr (setup of the large configs takes a minute)."""
+    print("[bench %.1fs] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+
+
+T_START = time.perf_counter()
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--points", type=int, default=100_000_000, help="points per GPU")
-    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"],
-                    help="BASELINE.json config: c2 (default, the headline), c4 (BNG), c5 (skewed)")
-    ap.add_argument("--res", type=int, default=None, help="default: 9 (c2, c5), 4 (c4)")
+    ap.add_argument("--points", type=int, default=None, help="points per GPU (default 1e8; c3: 1.25e8)")
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"],
+                    help="BASELINE.json config: c2 (default, the headline), c3 (74k tracts, res 10), "
+                         "c4 (BNG), c5 (skewed)")
+    ap.add_argument("--res", type=int, default=None, help="default: 9 (c2, c5), 10 (c3), 4 (c4)")
     ap.add_argument("--seed", type=int, default=0x20250314)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
@@ -102,8 +111,21 @@ def cpu_baseline(chips, isys, res, wl, seed, target_s):
 
 def workload(a, W, M):
     """The config's polygons, index system and point generators (bench_workloads.py)."""
+    if a.config == "c3":
+        a.res = 10 if a.res is None else a.res
+        a.points = 125_000_000 if a.points is None else a.points
+        E = W.TRACT_EXTENT
+        return {"isys": M.H3IndexSystem(), "polygons": W.tract_polygons(),
+                "points": lambda n, begin, dev: W.extent_points(E, n, a.seed * 1000003 + begin, dev),
+                "points_np": lambda n, sd: W.extent_points(E, n, sd),
+                "pairs_per_point": 1.05, "keep_core": False,
+                "workload": "C3: %d points/GPU uniform in lon [-77.5, -73.5] x lat [39.5, 42.5] x 74,000 "
+                            "census-tract-like polygons (seeded Voronoi, jittered shared edges, 17-337 vertices), "
+                            "H3 res %d; chips from grid_tessellateexplode(keepCoreGeometries=false)",
+                "data": "synthetic (uniform points; seeded tract-like Voronoi partition of the extent)"}
     if a.config == "c4":
         a.res = 4 if a.res is None else a.res
+        a.points = 100_000_000 if a.points is None else a.points
         return {"isys": M.BNGIndexSystem(), "polygons": W.london_districts(),
                 "points": lambda n, begin, dev: W.london_points(n, a.seed * 1000003 + begin, dev),
                 "points_np": lambda n, sd: W.london_points(n, sd),
@@ -113,6 +135,7 @@ def workload(a, W, M):
                 "data": "synthetic (UPRN-like points; Voronoi districts covering the extent)"}
     if a.config == "c5":
         a.res = 9 if a.res is None else a.res
+        a.points = 100_000_000 if a.points is None else a.points
         P = W.skewed_polygons()
         return {"isys": M.H3IndexSystem(), "polygons": P,
                 "points": lambda n, begin, dev: W.boundary_points(P, n, a.seed * 1000003 + begin, 0.003, dev),
@@ -122,6 +145,7 @@ def workload(a, W, M):
                             "fractal polygons of 49k vertices, H3 res %d",
                 "data": "synthetic (skewed points near polygon edges; seeded fractal polygons)"}
     a.res = 9 if a.res is None else a.res
+    a.points = 100_000_000 if a.points is None else a.points
     return {"isys": M.H3IndexSystem(), "polygons": W.nyc_zones(),
             "points": lambda n, begin, dev: gen_points(n, begin, a.seed, dev),
             "points_np": lambda n, sd: (np.random.default_rng(sd).uniform(NYC_BBOX[0], NYC_BBOX[2], n),
@@ -157,10 +181,13 @@ def main():
     import bench_workloads as W
     wl = workload(a, W, M)
     isys, zones = wl["isys"], wl["polygons"]
+    log("config %s: %d polygons" % (a.config, len(zones)))
     table = None
     if rank == 0:
-        table = M.tessellate(zones, isys, a.res)
+        table = M.tessellate(zones, isys, a.res, keep_core_geometries=wl.get("keep_core", True))
+        log("tessellated: %d chips" % len(table))
         chips = table.upload(ctx)
+        log("chip table uploaded")
     else:
         chips = None
     if world > 1:
@@ -179,6 +206,7 @@ def main():
         return M.pip_join(x, y, chips, a.res, index_system=isys, point_id_base=begin, out=(out_p, out_q),
                           capacity=cap)
 
+    log("points generated; warmup")
     for _ in range(a.warmup):
         r = step()
     torch.cuda.synchronize(dev)
@@ -255,7 +283,8 @@ def main():
             pass
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         if table is None:
-            table = M.tessellate(zones, isys, a.res)
+            table = M.tessellate(zones, isys, a.res, keep_core_geometries=wl.get("keep_core", True))
+        log("timed; cpu baseline")
         out["cpu_baseline"] = cpu_baseline(table, isys, a.res, wl, a.seed, a.cpu_seconds)
     elif rank == 0:
         out["cpu_baseline"] = None

@@ -132,3 +132,85 @@ def london_points(n, seed, dev=None):
     x = torch.rand(n, dtype=torch.float64, device=dev, generator=g).mul_(x1 - x0).add_(x0).mul_(100).round_().div_(100)
     y = torch.rand(n, dtype=torch.float64, device=dev, generator=g).mul_(y1 - y0).add_(y0).mul_(100).round_().div_(100)
     return x, y
+
+
+# C3: the 1B-point, ~74k-polygon, res-10 join.  Extent: a 4 deg x 3 deg block of the
+# north-eastern US (PA / NJ / NY, one H3 icosahedron face), cut into census-tract-like
+# cells of ~1.6 km^2 on average (urban-tract scale; the real CONUS tract set averages
+# far larger cells, but most tract *boundaries* are urban).
+TRACT_EXTENT = (-77.5, 39.5, -73.5, 42.5)
+N_TRACTS = 74_000
+
+
+def tract_polygons(n_cells=N_TRACTS, extent=TRACT_EXTENT, seed=3, k_lo=2, k_hi=40, amp=0.05):
+    """Seeded Voronoi partition of `extent` into `n_cells` tract-like polygons (ids 1..n)
+    whose shared edges are jittered polylines with k_lo..k_hi interior vertices each
+    (identical in both neighbours), so a tract has ~20-400 vertices."""
+    import mosaic_amd as M
+    from scipy.spatial import Voronoi
+    x0, y0, x1, y1 = extent
+    rng = np.random.default_rng(seed)
+    sites = np.stack([rng.uniform(x0, x1, n_cells), rng.uniform(y0, y1, n_cells)], 1)
+    mir = [sites, sites * [-1, 1] + [2 * x0, 0], sites * [-1, 1] + [2 * x1, 0],
+           sites * [1, -1] + [0, 2 * y0], sites * [1, -1] + [0, 2 * y1]]
+    vor = Voronoi(np.concatenate(mir))
+    V = np.clip(vor.vertices, [x0, y0], [x1, y1])
+    rp = vor.ridge_points
+    rv = np.array([r if len(r) == 2 else [-1, -1] for r in vor.ridge_vertices], dtype=np.int64)
+    keep = ((rp[:, 0] < n_cells) | (rp[:, 1] < n_cells)) & (rv.min(1) >= 0)
+    rp, rv = rp[keep], rv[keep]
+    # a ridge between a site and one of its mirrors lies on the extent border: straight
+    border = (rp[:, 0] % n_cells) == (rp[:, 1] % n_cells)
+    lo, hi = rv.min(1), rv.max(1)
+    k = rng.integers(k_lo, k_hi + 1, len(rv))
+    k[border] = 0
+    # interior points of ridge r, running from V[lo] to V[hi]
+    start = np.zeros(len(rv) + 1, np.int64)
+    start[1:] = np.cumsum(k)
+    rid = np.repeat(np.arange(len(rv)), k)
+    t = (np.arange(start[-1]) - start[rid] + 1) / (k[rid] + 1)
+    a, b = V[lo[rid]], V[hi[rid]]
+    d = b - a
+    nrm = np.stack([-d[:, 1], d[:, 0]], 1)
+    off = rng.uniform(-amp, amp, len(rid)) * np.sin(np.pi * t)
+    P = np.clip(a + t[:, None] * d + off[:, None] * nrm, [x0, y0], [x1, y1])
+    ridge_of = {(int(u), int(v)): i for i, (u, v) in enumerate(zip(lo, hi))}
+    xy, ring_off = [], [0]
+    ids = []
+    for i in range(n_cells):
+        reg = vor.regions[vor.point_region[i]]
+        if -1 in reg or not reg:
+            continue
+        reg = np.array(reg)
+        v = V[reg]
+        c = v.mean(0)
+        reg = reg[np.argsort(np.arctan2(v[:, 1] - c[1], v[:, 0] - c[0]))]
+        pieces = []
+        for j in range(len(reg)):
+            p, q = int(reg[j]), int(reg[(j + 1) % len(reg)])
+            pieces.append(V[p][None, :])
+            r = ridge_of.get((min(p, q), max(p, q)))
+            if r is not None and k[r]:
+                seg = P[start[r]:start[r + 1]]
+                pieces.append(seg if p < q else seg[::-1])
+        pieces.append(V[int(reg[0])][None, :])
+        ring = np.concatenate(pieces)
+        xy.append(ring)
+        ring_off.append(ring_off[-1] + len(ring))
+        ids.append(i + 1)
+    n = len(ids)
+    return M.Polygons(ids, np.arange(n + 1), np.arange(n + 1), ring_off, np.concatenate(xy))
+
+
+def extent_points(extent, n, seed, dev=None):
+    """Points uniform in `extent` (numpy, or torch on `dev`)."""
+    x0, y0, x1, y1 = extent
+    if dev is None:
+        rng = np.random.default_rng(seed)
+        return rng.uniform(x0, x1, n), rng.uniform(y0, y1, n)
+    import torch
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    x = torch.rand(n, dtype=torch.float64, device=dev, generator=g).mul_(x1 - x0).add_(x0)
+    y = torch.rand(n, dtype=torch.float64, device=dev, generator=g).mul_(y1 - y0).add_(y0)
+    return x, y

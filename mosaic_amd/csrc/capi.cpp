@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -22,6 +24,7 @@
 #include "error.h"
 #include "h3_core.h"
 #include "kernels.h"
+#include "parallel.h"
 #include "pip_core.h"
 #include "wkb.h"
 
@@ -195,50 +198,70 @@ bool build_lattice(const std::vector<mgpu::HashSlot>& cells, std::vector<std::pa
   if (res < 5) return false;
   const double rho = 0.3 / pow(H::kSqrt7, res);
   double k_res = H::k_of_res(res);
-  double lat_lo = 1e9, lat_hi = -1e9, lon_lo = 1e9, lon_hi = -1e9;
-  for (size_t ci = 0; ci < cells.size(); ci++) {
-    uint64_t h = cells[ci].cell;
-    if (((h >> 59) & 15) != 1 || (int)((h >> 52) & 15) != res || (h >> 63)) return false;
-    int face, r;
-    H::IJK ijk;
-    if (!H::h3_home_face_ijk(h, &face, &ijk, &r)) return false;
-    double hx, hy, lat, lon;
-    H::ijk_to_hex2d(ijk, &hx, &hy);
-    H::hex2d_to_geo(hx, hy, face, res, &lat, &lon);
-    double v[3] = {cos(lat) * cos(lon), cos(lat) * sin(lon), sin(lat)};
-    double amin = 1e9, ang[20];
-    for (int f = 0; f < 20; f++) {
-      ang[f] = angle_between(v, H3T_FACE_CENTER_POINT[f]);
-      amin = std::min(amin, ang[f]);
-    }
-    bool found_home = false;
-    for (int f = 0; f < 20; f++) {
-      if (ang[f] > amin + 3 * rho) continue;
-      const double(*F)[3] = H3T_FACE_FRAME[f][res & 1];
-      double dc = v[0] * F[2][0] + v[1] * F[2][1] + v[2] * F[2][2];
-      if (dc <= 0.5) continue;
-      double x = k_res * (v[0] * F[0][0] + v[1] * F[0][1] + v[2] * F[0][2]) / dc;
-      double y = k_res * (v[0] * F[1][0] + v[1] * F[1][1] + v[2] * F[1][2]) / dc;
-      double mg;
-      H::IJK c0 = H::hex2d_to_ijk(x, y, &mg);
-      int i0 = c0.i - c0.k, j0 = c0.j - c0.k;
-      for (int di = -3; di <= 3; di++)
-        for (int dj = -3; dj <= 3; dj++) {
-          if (std::abs(di) + std::abs(dj) + std::abs(di - dj) > 6) continue;  // hex distance <= 3
-          H::IJK n{i0 + di, j0 + dj, 0};
-          H::ijk_normalize(n);
-          if (H::face_ijk_to_h3(f, n, res) == h) {
-            keys.push_back({H::lattice_key(f, n), (uint32_t)ci});
-            if (f == face) found_home = true;
+  // cells are independent: per-thread key lists and extents, merged afterwards (the
+  // caller sorts the keys, so the merge order does not matter)
+  const int64_t grain = 4096;
+  const int T = mgpu::parallel_slots((int64_t)cells.size(), grain);
+  std::vector<std::vector<std::pair<uint64_t, uint32_t>>> tkeys(T);
+  std::vector<std::array<double, 4>> text(T, std::array<double, 4>{1e9, -1e9, 1e9, -1e9});
+  std::atomic<bool> bad{false};
+  mgpu::parallel_for((int64_t)cells.size(), grain, [&](int64_t cb, int64_t ce, int t) {
+    auto& tk = tkeys[t];
+    auto& ex = text[t];
+    for (int64_t ci = cb; ci < ce; ci++) {
+      uint64_t h = cells[ci].cell;
+      if (((h >> 59) & 15) != 1 || (int)((h >> 52) & 15) != res || (h >> 63)) {
+        bad = true;
+        return;
+      }
+      int face, r;
+      H::IJK ijk;
+      if (!H::h3_home_face_ijk(h, &face, &ijk, &r)) {
+        bad = true;
+        return;
+      }
+      double hx, hy, lat, lon;
+      H::ijk_to_hex2d(ijk, &hx, &hy);
+      H::hex2d_to_geo(hx, hy, face, res, &lat, &lon);
+      double v[3] = {cos(lat) * cos(lon), cos(lat) * sin(lon), sin(lat)};
+      double amin = 1e9, ang[20];
+      for (int f = 0; f < 20; f++) {
+        ang[f] = angle_between(v, H3T_FACE_CENTER_POINT[f]);
+        amin = std::min(amin, ang[f]);
+      }
+      for (int f = 0; f < 20; f++) {
+        if (ang[f] > amin + 3 * rho) continue;
+        const double(*F)[3] = H3T_FACE_FRAME[f][res & 1];
+        double dc = v[0] * F[2][0] + v[1] * F[2][1] + v[2] * F[2][2];
+        if (dc <= 0.5) continue;
+        double x = k_res * (v[0] * F[0][0] + v[1] * F[0][1] + v[2] * F[0][2]) / dc;
+        double y = k_res * (v[0] * F[1][0] + v[1] * F[1][1] + v[2] * F[1][2]) / dc;
+        double mg;
+        H::IJK c0 = H::hex2d_to_ijk(x, y, &mg);
+        int i0 = c0.i - c0.k, j0 = c0.j - c0.k;
+        for (int di = -3; di <= 3; di++)
+          for (int dj = -3; dj <= 3; dj++) {
+            if (std::abs(di) + std::abs(dj) + std::abs(di - dj) > 6) continue;  // hex distance <= 3
+            H::IJK n{i0 + di, j0 + dj, 0};
+            H::ijk_normalize(n);
+            if (H::face_ijk_to_h3(f, n, res) == h) tk.push_back({H::lattice_key(f, n), (uint32_t)ci});
           }
-        }
+      }
+      double latd = lat * 180 / kPi, lond = lon * 180 / kPi;
+      ex[0] = std::min(ex[0], latd);
+      ex[1] = std::max(ex[1], latd);
+      ex[2] = std::min(ex[2], lond);
+      ex[3] = std::max(ex[3], lond);
     }
-    (void)found_home;
-    double latd = lat * 180 / kPi, lond = lon * 180 / kPi;
-    lat_lo = std::min(lat_lo, latd);
-    lat_hi = std::max(lat_hi, latd);
-    lon_lo = std::min(lon_lo, lond);
-    lon_hi = std::max(lon_hi, lond);
+  });
+  if (bad) return false;
+  double lat_lo = 1e9, lat_hi = -1e9, lon_lo = 1e9, lon_hi = -1e9;
+  for (int t = 0; t < T; t++) {
+    keys.insert(keys.end(), tkeys[t].begin(), tkeys[t].end());
+    lat_lo = std::min(lat_lo, text[t][0]);
+    lat_hi = std::max(lat_hi, text[t][1]);
+    lon_lo = std::min(lon_lo, text[t][2]);
+    lon_hi = std::max(lon_hi, text[t][3]);
   }
   // bounding box of every chip cell (centre +- 2 rho), or the whole sphere
   double m = 2 * rho * 180 / kPi;
@@ -713,7 +736,9 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     hv.ring_vtx = geo.ring_vtx.data();
     hv.ring_env = geo.ring_env.data();
     hv.vtx = geo.vtx.data();
-    for (int64_t c = 0; c < n_chips; c++) {
+    // chips are independent: headers and classification grids in parallel
+    mgpu::parallel_for(n_chips, 1024, [&](int64_t cb, int64_t ce, int) {
+    for (int64_t c = cb; c < ce; c++) {
       mgpu::ChipHdr& h = chdr[c];
       memset(&h, 0, sizeof h);
       for (int k = 0; k < 4; k++) h.env[k] = cenv[4 * c + k];
@@ -726,6 +751,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
                        !(cflags[c] & mgpu::kChipMulti)) ? 1 : 0;
       if (h.n_strips) build_grid(hv, (uint32_t)c, geo, h);
     }
+    });
   }
   // H3: probe by lattice key when possible (chip_table.h)
   int32_t probe_mode = mgpu::kProbeCellId, lres = -1;

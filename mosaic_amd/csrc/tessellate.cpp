@@ -38,6 +38,7 @@
 #include "error.h"
 #include "bng_core.h"
 #include "h3_core.h"
+#include "parallel.h"
 #include "wkb.h"
 
 namespace {
@@ -486,49 +487,63 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
                         const double* xy, int32_t keep_core_geometries, mgpu_tess** out) {
   if (!out || n_polys < 0) return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellate: bad arguments");
   if (int32_t st = mgpu_check_resolution(index_system, res)) return st;
+  if (index_system == MGPU_BNG && res == -1)
+    // 500km ids depend on the easting letter only: no square cells to clip
+    return mgpu::set_error(MGPU_E_RESOLUTION, "BNG resolution -1 (500km) cannot be tessellated");
+  // polygons are independent: tessellate them in parallel into per-polygon chip lists,
+  // then concatenate in input order (the output does not depend on the schedule)
+  std::vector<std::vector<Chip>> per(n_polys);
+  std::vector<uint8_t> multi_face(n_polys, 0);
+  mgpu::parallel_for(n_polys, 64, [&](int64_t pb, int64_t pe, int) {
+    for (int64_t p = pb; p < pe; p++) {
+      Polygon poly;
+      for (int64_t q = poly_part_off[p]; q < poly_part_off[p + 1]; q++) {
+        std::vector<std::vector<Pt>> rings;
+        for (int64_t r = part_ring_off[q]; r < part_ring_off[q + 1]; r++) {
+          std::vector<Pt> ring;
+          for (int64_t v = ring_off[r]; v < ring_off[r + 1]; v++) ring.push_back({xy[2 * v], xy[2 * v + 1]});
+          if (ring.size() >= 2 && (ring.front().x != ring.back().x || ring.front().y != ring.back().y))
+            ring.push_back(ring.front());
+          if (ring.size() >= 4) rings.push_back(std::move(ring));
+          else if (rings.empty()) break;  // degenerate shell: empty part
+        }
+        if (!rings.empty()) poly.parts.push_back(std::move(rings));
+      }
+      if (poly.parts.empty()) continue;
+      if (index_system == MGPU_H3) {
+        int face = -1;
+        bool one_face = true;
+        for (auto& part : poly.parts)
+          for (auto& ring : part)
+            for (auto& pt : ring) {
+              int f = nearest_face(pt.x, pt.y);
+              if (face < 0) face = f;
+              else if (f != face) one_face = false;
+            }
+        if (!one_face) {
+          multi_face[p] = 1;
+          continue;
+        }
+        H3Grid g(face, res);
+        tessellate_polygon(g, poly, polygon_id[p], keep_core_geometries != 0, per[p]);
+      } else {
+        BngGrid g(res);
+        tessellate_polygon(g, poly, polygon_id[p], keep_core_geometries != 0, per[p]);
+      }
+    }
+  });
+  for (int64_t p = 0; p < n_polys; p++)
+    if (multi_face[p])
+      return mgpu::set_error(MGPU_E_INVALID_ARG,
+                             "tessellate: polygon %d spans several icosahedron faces (not supported by this "
+                             "builder; split it first)", polygon_id[p]);
   mgpu_tess* t = new mgpu_tess();
-  for (int64_t p = 0; p < n_polys; p++) {
-    Polygon poly;
-    for (int64_t q = poly_part_off[p]; q < poly_part_off[p + 1]; q++) {
-      std::vector<std::vector<Pt>> rings;
-      for (int64_t r = part_ring_off[q]; r < part_ring_off[q + 1]; r++) {
-        std::vector<Pt> ring;
-        for (int64_t v = ring_off[r]; v < ring_off[r + 1]; v++) ring.push_back({xy[2 * v], xy[2 * v + 1]});
-        if (ring.size() >= 2 && (ring.front().x != ring.back().x || ring.front().y != ring.back().y))
-          ring.push_back(ring.front());
-        if (ring.size() >= 4) rings.push_back(std::move(ring));
-        else if (rings.empty()) break;  // degenerate shell: empty part
-      }
-      if (!rings.empty()) poly.parts.push_back(std::move(rings));
-    }
-    if (poly.parts.empty()) continue;
-    if (index_system == MGPU_H3) {
-      int face = -1;
-      bool one_face = true;
-      for (auto& part : poly.parts)
-        for (auto& ring : part)
-          for (auto& pt : ring) {
-            int f = nearest_face(pt.x, pt.y);
-            if (face < 0) face = f;
-            else if (f != face) one_face = false;
-          }
-      if (!one_face) {
-        delete t;
-        return mgpu::set_error(MGPU_E_INVALID_ARG,
-                               "tessellate: polygon %d spans several icosahedron faces (not supported by this "
-                               "builder; split it first)", polygon_id[p]);
-      }
-      H3Grid g(face, res);
-      tessellate_polygon(g, poly, polygon_id[p], keep_core_geometries != 0, t->chips);
-    } else {
-      if (res == -1) {
-        delete t;
-        // 500km ids depend on the easting letter only: no square cells to clip
-        return mgpu::set_error(MGPU_E_RESOLUTION, "BNG resolution -1 (500km) cannot be tessellated");
-      }
-      BngGrid g(res);
-      tessellate_polygon(g, poly, polygon_id[p], keep_core_geometries != 0, t->chips);
-    }
+  size_t total = 0;
+  for (auto& v : per) total += v.size();
+  t->chips.reserve(total);
+  for (auto& v : per) {
+    for (auto& c : v) t->chips.push_back(std::move(c));
+    std::vector<Chip>().swap(v);
   }
   *out = t;
   return MGPU_OK;

@@ -312,6 +312,21 @@ def test_pip_join_c5_skewed_fractal(gpu):
     assert 0.2 * len(x) < len(gp) < 0.9 * len(x)
 
 
+def test_pip_join_c3_tracts_res10(gpu):
+    """C3's polygons (tract-like Voronoi partition, jittered shared edges) at res 10,
+    on a 3,000-tract block the oracle finishes in seconds: every point in one tract."""
+    import bench_workloads as W
+    E = (-75.0, 40.0, -74.5, 40.4)
+    P = W.tract_polygons(n_cells=3000, extent=E, seed=21)
+    c = M.tessellate(P, M.H3IndexSystem(), 10, keep_core_geometries=False)
+    x, y = W.extent_points(E, 400_000, 12)
+    r = M.pip_join(T(x, gpu), T(y, gpu), c, 10)
+    op, oq = oracle_join(c, x, y, res=10)
+    gp, gq = r.numpy()
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+    assert len(np.unique(gp)) == len(gp) and len(gp) > 0.99 * len(x)
+
+
 @pytest.mark.parametrize("isys", ["h3", "bng"])
 def test_pip_join_more_than_32_chips_per_cell(gpu, isys):
     """40 nested, overlapping polygons: every cell holds 40 chips, past the 32 the

@@ -34,3 +34,17 @@ def test_skewed_polygons_shape():
     assert x.shape == (10_000,) and np.isfinite(x).all() and np.isfinite(y).all()
     c = M.tessellate(P, M.H3IndexSystem(), 9)
     assert (c.is_core == 0).sum() > 100
+
+
+def test_tract_polygons_partition_the_extent():
+    """C3's generator: a Voronoi partition with shared jittered edges -- each point of
+    the extent lies in exactly one tract (checked on a small block at res 9)."""
+    E = (-75.0, 40.0, -74.8, 40.15)
+    P = W.tract_polygons(n_cells=400, extent=E, seed=8)
+    nv = np.diff(P.ring_off)
+    assert len(P) == 400 and nv.min() >= 10 and nv.max() <= 500
+    c = M.tessellate(P, M.H3IndexSystem(), 9, keep_core_geometries=False)
+    x, y = W.extent_points(E, 20_000, 4)
+    pts, polys = O.pip_join(0, 9, x, y, c.cell, c.polygon_id, c.is_core, c.wkb_offsets, c.wkb)
+    assert len(np.unique(pts)) == len(pts)
+    assert len(pts) > 0.99 * len(x)

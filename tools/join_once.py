@@ -15,7 +15,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--points", type=int, default=100_000_000)
     ap.add_argument("--res", type=int, default=None)
-    ap.add_argument("--config", choices=["c2", "c4", "c5"], default="c2")
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2")
     ap.add_argument("--seed", type=int, default=0x20250314)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--ablate", type=int, default=0)
@@ -33,7 +33,7 @@ def main():
     import bench_workloads as W
     wl = B.workload(a, W, M)
     isys = wl["isys"]
-    chips = M.tessellate(wl["polygons"], isys, a.res).upload(ctx)
+    chips = M.tessellate(wl["polygons"], isys, a.res, keep_core_geometries=wl.get("keep_core", True)).upload(ctx)
     x, y = wl["points"](a.points, 0, dev)
     cap = int(a.points * wl["pairs_per_point"]) + 1024
     op = torch.empty(cap, dtype=torch.int64, device=dev)
