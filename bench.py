@@ -272,13 +272,17 @@ def main():
     }
     if os.environ.get("MGPU_ABLATE"):
         out["ablate"] = os.environ["MGPU_ABLATE"]
-    prof = os.path.join(ROOT, "profiles", "pmc_join_traffic.json")
+    name = "pmc_join_traffic.json" if a.config == "c2" else "pmc_join_traffic_%s.json" % a.config
+    prof = os.path.join(ROOT, "profiles", name)
     if os.path.exists(prof):
         try:
             p = json.load(open(prof))
-            if p.get("points") == n and p.get("res") == a.res and a.config == "c2":
-                out["roofline"]["traffic"] = p["hbm_bytes_per_launch"]
-                out["roofline"]["traffic_source"] = "profiles/pmc_join_traffic.json (%s)" % p.get("round", "?")
+            if p.get("res") == a.res and p.get("config", "c2") == a.config and p.get("points"):
+                # measured per launch on p["points"] points of this workload (rocprofv3 PMC
+                # passes, tools/gpu_traffic.sh); scaled to this launch's size if it differs
+                out["roofline"]["traffic"] = p["hbm_bytes_per_launch"] * n / p["points"]
+                out["roofline"]["traffic_source"] = "profiles/%s (%s%s)" % (
+                    name, p.get("round", "?"), "" if p["points"] == n else ", measured on %d points, scaled" % p["points"])
         except (ValueError, KeyError):
             pass
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

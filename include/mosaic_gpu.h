@@ -137,6 +137,17 @@ int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t inde
                             int32_t* out_polygon_id, void* stream);
 int32_t mgpu_ctx_reserve(mgpu_ctx* ctx, int64_t max_points);
 
+/* Parity audit (no reference counterpart): the input positions of the H3 near-tie
+ * points of the last call on `ctx` -- the only points where the device libm could
+ * place a point in a different cell than the reference's H3-Java (glibc) path.
+ * After mgpu_pip_join: the points the H3 route resolved inside its tie band
+ * (mgpu_stats.n_near_ties).  After mgpu_points_to_cells: every point the fast
+ * projection handed to the route (a superset).  Tests recompute exactly these points
+ * with the CPU oracle at full bench sizes.  Unordered; at most 65536 are kept.
+ * Synchronises the device.  MGPU_E_CAPACITY (with *out_n set) if cap is too small
+ * or more than 65536 were found. */
+int32_t mgpu_last_near_ties(mgpu_ctx* ctx, int64_t* out_index, int64_t cap, int64_t* out_n);
+
 /* Host-pointer convenience form of mgpu_pip_join (copies points in, pairs out). */
 int32_t mgpu_pip_join_host(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t index_system, int32_t res,
                            const double* x, const double* y, const int64_t* point_id, int64_t n,

@@ -29,7 +29,7 @@ EXPORTS = (
     "mgpu_points_to_cells", "mgpu_points_to_cells_host", "mgpu_bng_format", "mgpu_bng_parse",
     "mgpu_chips_upload", "mgpu_chips_destroy", "mgpu_chips_device_blob", "mgpu_chips_from_device_blob",
     "mgpu_chips_info", "mgpu_st_contains", "mgpu_pip_join", "mgpu_pip_join_async", "mgpu_ctx_reserve",
-    "mgpu_pip_join_host", "mgpu_tessellate", "mgpu_tess_result_sizes", "mgpu_tess_result_copy",
+    "mgpu_last_near_ties",    "mgpu_pip_join_host", "mgpu_tessellate", "mgpu_tess_result_sizes", "mgpu_tess_result_copy",
     "mgpu_tess_destroy", "mgpu_test_chip_contains_host",
 )
 
@@ -101,6 +101,7 @@ def lib():
                                 ctypes.POINTER(MgpuStats)]),
         "mgpu_pip_join_async": (I32, [P, P, I32, I32, P, P, P, I64, I64, I64, P, P, P, P]),
         "mgpu_ctx_reserve": (I32, [P, I64]),
+        "mgpu_last_near_ties": (I32, [P, P, I64, ctypes.POINTER(I64)]),
         "mgpu_pip_join_host": (I32, [P, P, I32, I32, P, P, P, I64, I64, ctypes.POINTER(I64), P, P]),
         "mgpu_tessellate": (I32, [I32, I32, I64, P, P, P, P, P, I32, ctypes.POINTER(P)]),
         "mgpu_tess_result_sizes": (I32, [P, ctypes.POINTER(I64), ctypes.POINTER(I64)]),

@@ -34,6 +34,16 @@ class GpuContext:
     def reserve(self, max_points):
         N.check(N.lib().mgpu_ctx_reserve(self.handle, int(max_points)))
 
+    def last_near_ties(self):
+        """Sorted input positions of the near-tie points of the last join / cell-id call
+        on this context (mgpu_last_near_ties): the parity audit list."""
+        import numpy as np
+        n = ctypes.c_int64()
+        cap = 1 << 16
+        buf = np.zeros(cap, np.int64)
+        N.check(N.lib().mgpu_last_near_ties(self.handle, buf.ctypes.data, cap, ctypes.byref(n)))
+        return np.sort(buf[:n.value])
+
     def close(self):
         if self.handle:
             N.lib().mgpu_ctx_destroy(self.handle)

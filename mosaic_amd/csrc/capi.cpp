@@ -487,10 +487,10 @@ struct mgpu_chips {
 namespace {
 
 // Workspace layout (each region 256-byte aligned):
-//   [counters 16 x u64] [tile_count u32 x T] [tile_where u64 x T] [group_off u64 x T/32 (T)]
-//   [group_sum u32 x T/32]
-//   [dirty tiles u32 x T] [cells near-tie queue u64 x (1 + kTieCap)]
-//   [records u64 x (T * tile points + pool)]
+//   [counters 16 x u64] [near-tie queue u64 x (1 + kTieCap)] [tile_count u32 x T]
+//   [tile_where u64 x T] [group_off u64 x T/32 (T)] [group_sum u32 x T/32] [dirty tiles u32 x T]
+//   [tile_pend u32 x T] [pending mixed-cell candidates u64 x T * pend cap]
+//   [records u64 x (T * slot records + pool)]
 // counters: [0] pairs [1] route near-ties [2] invalid points [3] candidates (tile_scan_kernel)
 //           [5] pool records used [6] dirty tiles (u32) [8..] MGPU_STATS
 // T = tiles of the largest point batch reserved; pool = overflow records (tiles with
@@ -498,22 +498,26 @@ namespace {
 constexpr size_t kWsCounters = 128;  // 16 x u64
 
 struct WsLayout {
-  size_t count, where, off, gsum, dirty, ties, recs, total;
+  size_t count, where, off, gsum, dirty, ties, tpend, pend, recs, total;
 };
-// near-tie queue of mgpu_points_to_cells (overflow: the fix kernel redoes every point)
+// near-tie queue: mgpu_points_to_cells (overflow: the fix kernel redoes every point) and the
+// join's audit list (mgpu_last_near_ties)
 constexpr int64_t kTieCap = 1 << 16;
 
 WsLayout ws_layout(int64_t n_tiles, int64_t pool) {
   WsLayout L;
   size_t T = (size_t)std::max<int64_t>(n_tiles, 1);
-  L.count = kWsCounters;
+  // the near-tie queue sits at a fixed offset (mgpu_last_near_ties reads it for any size)
+  L.ties = align_up(kWsCounters, 256);
+  L.count = align_up(L.ties + (size_t)(kTieCap + 1) * 8, 256);
   L.where = align_up(L.count + T * 4, 256);
   L.off = align_up(L.where + T * 8, 256);
   L.gsum = align_up(L.off + T * 8, 256);
   L.dirty = align_up(L.gsum + 2 * (T / 32 + 1) * 4, 256);  // group pair sums, group candidate sums
-  L.ties = align_up(L.dirty + T * 4, 256);
-  L.recs = align_up(L.ties + (size_t)(kTieCap + 1) * 8, 256);
-  L.total = align_up(L.recs + (T * (size_t)mgpu::join_tile_points() + (size_t)std::max<int64_t>(pool, 0)) * 8, 256);
+  L.tpend = align_up(L.dirty + T * 4, 256);
+  L.pend = align_up(L.tpend + T * 4, 256);
+  L.recs = align_up(L.pend + T * (size_t)(mgpu::join_pend_cap() * mgpu::join_pend_words()) * 8, 256);
+  L.total = align_up(L.recs + (T * (size_t)mgpu::join_slot_records() + (size_t)std::max<int64_t>(pool, 0)) * 8, 256);
   return L;
 }
 
@@ -589,7 +593,8 @@ int32_t mgpu_ctx_destroy(mgpu_ctx* ctx) {
 int32_t mgpu_ctx_reserve(mgpu_ctx* ctx, int64_t max_points) {
   if (!ctx) return fail(MGPU_E_INVALID_ARG, "ctx is NULL");
   if (int32_t st = set_device(ctx->device)) return st;
-  return ensure_ws(ctx, mgpu::join_tiles(max_points), max_points);
+  const int64_t tiles = mgpu::join_tiles(max_points);
+  return ensure_ws(ctx, tiles, max_points + tiles * mgpu::join_pend_cap());
 }
 
 int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t is, int32_t res, const double* x, const double* y, int64_t n,
@@ -989,7 +994,9 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   int64_t tiles = mgpu::join_tiles(n);
   // pool: the records of tiles with more pairs than points (bounded by the capacity;
   // a total beyond it is reported as MGPU_E_CAPACITY either way)
-  const int64_t pool = capacity;
+  // (+ room for the tentative records of deferred mixed-cell candidates, so exhausting
+  // the pool still implies a total beyond the capacity)
+  const int64_t pool = capacity + tiles * mgpu::join_pend_cap();
   if (int32_t st = ensure_ws(ctx, tiles, pool)) return st;
   auto* base = (uint8_t*)ctx->ws;
   const WsLayout L = ws_layout(tiles, pool);
@@ -1009,12 +1016,15 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   a.tile_count = (uint32_t*)(base + L.count);
   a.tile_where = (uint64_t*)(base + L.where);
   a.recs = (uint64_t*)(base + L.recs);
+  a.tile_pend = (uint32_t*)(base + L.tpend);
+  a.pend = (uint64_t*)(base + L.pend);
   {
     const char* ab = getenv("MGPU_ABLATE");  // profiling switch, never set in production runs
     a.ablate = ab ? atoi(ab) : 0;
   }
   mgpu::EmitArgs e;
   e.tile_count = a.tile_count;
+  e.tile_dead = a.tile_pend;
   e.group_off = (uint64_t*)(base + L.off);
   a.group_sum = (uint32_t*)(base + L.gsum);
   a.group_cand = a.group_sum + (tiles / 32 + 1);
@@ -1025,11 +1035,33 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   e.capacity = capacity;
   e.out_point = out_point;
   e.out_poly = out_poly;
+  a.ties = (unsigned long long*)(base + L.ties);
+  a.tie_cap = kTieCap;
   HIP_TRY(hipMemsetAsync(base, 0, kWsCounters, s));
+  HIP_TRY(hipMemsetAsync(base + L.ties, 0, 8, s));
   HIP_TRY(hipMemsetAsync(base + L.gsum, 0, 2 * ((size_t)tiles / 32 + 1) * 4, s));
   if (timed) HIP_TRY(hipEventRecord(ctx->ev0, s));
   HIP_TRY(mgpu::launch_join(is, a, e, s, timed ? ctx->ev2 : nullptr));
   if (timed) HIP_TRY(hipEventRecord(ctx->ev1, s));
+  return MGPU_OK;
+}
+
+int32_t mgpu_last_near_ties(mgpu_ctx* ctx, int64_t* out_index, int64_t cap, int64_t* out_n) {
+  if (!ctx || !out_n || cap < 0 || (cap > 0 && !out_index)) return fail(MGPU_E_INVALID_ARG, "bad arguments");
+  *out_n = 0;
+  if (!ctx->ws) return MGPU_OK;
+  if (int32_t st = set_device(ctx->device)) return st;
+  // the queue sits at the same offset for every workspace size (ws_layout)
+  const size_t off = ws_layout(1, 0).ties;
+  unsigned long long cnt = 0;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(&cnt, (uint8_t*)ctx->ws + off, 8, hipMemcpyDeviceToHost));
+  const int64_t n = (int64_t)cnt;
+  *out_n = n;
+  if (n > kTieCap) return fail(MGPU_E_CAPACITY, "%lld near-tie points: more than the %lld kept", (long long)n,
+                               (long long)kTieCap);
+  if (n > cap) return fail(MGPU_E_CAPACITY, "%lld near-tie points, capacity %lld", (long long)n, (long long)cap);
+  if (n) HIP_TRY(hipMemcpy(out_index, (uint8_t*)ctx->ws + off + 8, (size_t)n * 8, hipMemcpyDeviceToHost));
   return MGPU_OK;
 }
 

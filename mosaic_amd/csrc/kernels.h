@@ -24,15 +24,20 @@ struct JoinArgs {
   int64_t pool_cap;
   unsigned long long* pool_used;    // zeroed before launch
   uint32_t* dirty;                  // [n_tiles] tiles with a near-tie point (for pip_fix_kernel)
+  uint64_t* pend;                   // [n_tiles * join_pend_cap()] mixed-cell candidates {li << 32 | chip}
+  uint32_t* tile_pend;              // [n_tiles] pending candidates of each tile (pip_resolve_kernel)
   uint32_t* n_dirty;                // zeroed before launch
   unsigned long long* counters;     // [0] pairs [1] near-ties [2] invalid [3] candidates
+  unsigned long long* ties;         // pip_fix_kernel: [0] count, [1 .. tie_cap] input positions of the
+  int64_t tie_cap;                  // near-tie points the H3 route resolved (zero ties[0] before launch)
   int ablate;                       // profiling only (MGPU_ABLATE): 1 = no PIP (border = miss), 2 = no probe,
                                     // 3 = no projection either
 };
 
 // pair_emit_kernel: tile records -> ordered (point_id, polygon_id) output
 struct EmitArgs {
-  const uint32_t* tile_count;
+  const uint32_t* tile_count;       // records of each tile
+  const uint32_t* tile_dead;        // of which dead (pip_resolve_kernel)
   uint64_t* group_off;              // [n_tiles / 32] written by the tile scan
   const uint64_t* tile_where;
   const uint64_t* recs;
@@ -48,6 +53,9 @@ hipError_t launch_cells(int is, int res, const double* x, const double* y, int64
                         unsigned long long* counters, unsigned long long* ties, int64_t tie_cap, hipStream_t s);
 int64_t join_tiles(int64_t n);
 int64_t join_tile_points();
+int64_t join_slot_records();   // records reserved per tile (pairs beyond go to the overflow pool)
+int64_t join_pend_cap();       // pending mixed-cell candidates kept per tile
+int64_t join_pend_words();     // u64 words per pending candidate
 // `after_stream` (optional) is recorded right after pip_join_kernel
 hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s, hipEvent_t after_stream);
 hipError_t launch_st_contains(const ChipTableView& t, const int64_t* row, const double* x, const double* y, int64_t n,

@@ -157,6 +157,19 @@ constexpr int kOutCap = MGPU_OUTCAP;  // pairs a tile stages in LDS
 constexpr int kStash = MGPU_STASH;  // candidates whose coordinates phase 1 leaves in LDS
 static_assert(kCandCap * 2 + kMixCap * 2 + kStash * 16 <= kOutCap * 6, "phase 1-2 lists fit the staging buffer");
 constexpr int kMaskBits = 32;
+// MGPU_DEFER=1: the streaming kernel does not walk mixed-cell candidates itself.  It
+// writes them as tentative pair records (in their sorted place) and lists them, with
+// their record index, in the tile's pending list; pip_resolve_kernel walks every
+// pending candidate of a group of tiles with all lanes busy and marks the misses'
+// records dead; pair_emit_kernel drops dead records.  A tile reserves kSlot records in
+// its slot; more go to the overflow pool.
+#ifndef MGPU_DEFER
+#define MGPU_DEFER 0
+#endif
+constexpr int kSlot = 2 * kTile;
+constexpr uint64_t kDeadRec = ~0ULL;
+// pending entry: x, y (f64 bits), chip | record index << 32, walk info (chip_quick)
+constexpr int kPendWords = 4;
 
 // chips of a cell: first, count, core mask (bits < 16)
 struct Range {
@@ -426,6 +439,10 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
           uint32_t gi;
           r = chip_probe<IS, SLOW>(t, px, py, a.res, res_match, &ok, &tie, a.ablate, &gi);
           if (gi != kNoEntry) r = grid_range(t.grid[gi]);
+          if (SLOW && tie && a.ties) {  // the audit list of mgpu_last_near_ties
+            const unsigned long long q = atomicAdd(&a.ties[0], 1ull);
+            if ((int64_t)q < a.tie_cap) a.ties[1 + q] = (unsigned long long)p;
+          }
         }
         any_bad |= !ok;
         any_tie |= tie;
@@ -442,6 +459,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
       a.dirty[q] = tile;
       a.tile_count[tile] = 0;
       a.tile_where[tile] = kNoDst;
+      a.tile_pend[tile] = 0;
     }
     return;
   }
@@ -473,12 +491,22 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         px = a.x[p];
         py = a.y[p];
       }
-      const int q = pip::chip_quick(t, ch, px, py);
+      uint64_t walk = 0;
+      const int q = pip::chip_quick(t, ch, px, py, (MGPU_DEFER && !SLOW) ? &walk : nullptr);
       hit = q == pip::kQuickYes;
       if (q >= pip::kQuickStrips && a.ablate != 5) {
         const uint32_t m = atomicAdd(&s_nmix, 1u);
         if (m < (uint32_t)kMixCap && (SLOW || q == pip::kQuickStrips)) {
           s_mix[m] = (uint16_t)c;
+          if (MGPU_DEFER && !SLOW) {
+            // tentative match; pip_resolve_kernel walks the strip and decides (the
+            // entry's chip | record index word is written in phase 3)
+            hit = true;
+            uint64_t* pe = a.pend + ((uint64_t)tile * kMixCap + m) * kPendWords;
+            pe[0] = (uint64_t)__double_as_longlong(px);
+            pe[1] = (uint64_t)__double_as_longlong(py);
+            pe[3] = walk;
+          }
         } else if (!SLOW) {
           redo = true;  // list full / chip without strip index: pip_fix_kernel
         } else {
@@ -495,6 +523,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
       a.dirty[q] = tile;
       a.tile_count[tile] = 0;
       a.tile_where[tile] = kNoDst;
+      a.tile_pend[tile] = 0;
     }
     return;
   }
@@ -504,6 +533,9 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #ifdef MGPU_STATS
   uint32_t st_edges = 0;
 #endif
+  // (MGPU_DEFER: the streaming kernel leaves its mixed-cell candidates to
+  // pip_resolve_kernel; they are listed in phase 3, once their record index is known)
+  if (SLOW || !MGPU_DEFER)
   for (uint32_t m = threadIdx.x; m < nmix; m += kBlock) {
     const uint32_t c = s_mix[m];
     const uint32_t pj = s_cand_pj[c];
@@ -569,20 +601,54 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     agg += v;
   }
   const uint32_t excl = wave_off + incl - mine;
+  const uint32_t npend = (MGPU_DEFER && !SLOW) ? nmix : 0u;
+  if (npend && agg > 0xFFFFu) {
+    // record indices of the pending list are 16 bits: the fix kernel redoes the tile
+    if (threadIdx.x == 0) {
+      const unsigned int q = atomicAdd(a.n_dirty, 1u);
+      a.dirty[q] = tile;
+      a.tile_count[tile] = 0;
+      a.tile_where[tile] = kNoDst;
+      a.tile_pend[tile] = 0;
+    }
+    return;
+  }
 
-  // the tile's records go to its own slot (kTile records), or -- when it has more
-  // pairs than points -- to space reserved in the overflow pool
+  // the tile's records go to its own slot (kSlot records), or -- when it has more --
+  // to space reserved in the overflow pool
   __shared__ uint64_t s_dst;
   if (threadIdx.x == 0) {
-    uint64_t dst = (uint64_t)tile * kTile;
-    if (agg > (uint32_t)kTile) {
+    uint64_t dst = (uint64_t)tile * kSlot;
+    if (agg > (uint32_t)kSlot) {
       const unsigned long long off = atomicAdd(a.pool_used, (unsigned long long)agg);
-      dst = off + agg <= (unsigned long long)a.pool_cap ? (uint64_t)a.n_tiles * kTile + off : kNoDst;
+      dst = off + agg <= (unsigned long long)a.pool_cap ? (uint64_t)a.n_tiles * kSlot + off : kNoDst;
     }
     a.tile_count[tile] = agg;
     a.tile_where[tile] = dst;
+    if (!SLOW) a.tile_pend[tile] = npend;
     if (agg) atomicAdd(&a.group_sum[tile / kScanGroup], agg);
     s_dst = dst;
+  }
+  if (!SLOW && MGPU_DEFER && npend) {
+    // pending list: each tentative record's index in the tile (point li's records
+    // start at its exclusive scan position; s_cnt is free once the streaming kernel
+    // has its masks -- it never has chips past the 32nd), the point and the chip
+    uint32_t pos = excl;
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      const int li = l0 + k;
+      s_cnt[li] = (uint16_t)pos;
+      pos += __popc(s_mask[li]);
+    }
+    __syncthreads();
+    uint64_t* pe = a.pend + (uint64_t)tile * kMixCap * kPendWords;
+    for (uint32_t m = threadIdx.x; m < npend; m += kBlock) {
+      const uint32_t pj = s_cand_pj[s_mix[m]];
+      const int li = pj & 1023;
+      const uint32_t j = pj >> 10;
+      const uint32_t ri = s_cnt[li] + __popc(s_mask[li] & ((1u << j) - 1u));
+      pe[m * kPendWords + 2] = (uint64_t)(s_first[li] + j) | ((uint64_t)ri << 32);
+    }
   }
   const bool staged = agg <= (uint32_t)kOutCap;
   __syncthreads();
@@ -595,6 +661,21 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #pragma unroll 1
   for (int k = 0; k < kItems; k++) {
     const int li = l0 + k;
+    if (!SLOW) {
+      // every match (and tentative match) is a mask bit (s_cnt may hold record indices)
+      const uint32_t first = s_first[li];
+      for (uint32_t m = s_mask[li]; m; m &= m - 1) {
+        const int32_t poly = t.chip_poly[first + __builtin_ctz(m)];
+        if (staged) {
+          s_out_poly[pos] = poly;
+          s_out_li[pos] = (uint16_t)li;
+        } else if (rec) {
+          rec[pos] = ((uint64_t)li << 32) | (uint32_t)poly;
+        }
+        pos++;
+      }
+      continue;
+    }
     const uint32_t cnt = s_cnt[li];
     if (!cnt) continue;
     const uint32_t first = s_first[li];
@@ -694,6 +775,61 @@ __global__ __launch_bounds__(kBlock) void pip_fix_kernel(JoinArgs a) {
   }
 }
 
+// The mixed-cell candidates the streaming kernel deferred (MGPU_DEFER): one workgroup
+// per scan group of kScanGroup tiles walks all of the group's pending candidates, one
+// per lane (pip_core.h chip_contains_mixed -- the same exact walk the streaming kernel
+// would have done), and marks the tentative record of every miss dead.  The tile's
+// tile_pend entry becomes its dead-record count and the group's pair sum drops by the
+// misses.  Runs after pip_fix_kernel, before tile_scan_kernel.
+constexpr int kResolveBlock = 512;
+__global__ __launch_bounds__(kResolveBlock) void pip_resolve_kernel(JoinArgs a) {
+  __shared__ uint32_t s_po[kScanGroup + 1];
+  __shared__ uint64_t s_where[kScanGroup];
+  __shared__ uint32_t s_dead[kScanGroup];
+  const int64_t g = blockIdx.x;
+  const int64_t t0 = g * kScanGroup;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int64_t t = t0 + lane;
+    const bool in = lane < kScanGroup && t < a.n_tiles;
+    const uint32_t c = in ? a.tile_pend[t] : 0u;
+    const uint32_t incl = wave_incl_scan(c);
+    if (lane < kScanGroup) {
+      s_po[lane + 1] = incl;
+      s_where[lane] = in && c ? a.tile_where[t] : kNoDst;
+      s_dead[lane] = 0;
+    }
+    if (lane == 0) s_po[0] = 0;
+  }
+  __syncthreads();
+  const uint32_t total = s_po[kScanGroup];
+  if (total == 0) return;
+  const ChipTableView& t = a.chips;
+  for (uint32_t i = threadIdx.x; i < total; i += kResolveBlock) {
+    int k = 0;
+#pragma unroll
+    for (int step = kScanGroup / 2; step >= 1; step >>= 1)
+      if (s_po[k + step] <= i) k += step;
+    const uint64_t* pe = a.pend + ((uint64_t)(t0 + k) * kMixCap + (i - s_po[k])) * kPendWords;
+    const double px = __longlong_as_double((long long)pe[0]), py = __longlong_as_double((long long)pe[1]);
+    const uint64_t w = pe[2], wk = pe[3];
+    if (!pip::chip_contains_strip(t, (uint32_t)w, (uint32_t)wk, ((wk >> 40) & 1) != 0, (uint8_t)(wk >> 32), px, py)) {
+      const uint64_t where = s_where[k];
+      if (where != kNoDst) a.recs[where + (w >> 32)] = kDeadRec;
+      atomicAdd(&s_dead[k], 1u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const bool in = lane < kScanGroup && s_po[lane + 1] > s_po[lane];
+    const uint32_t d = in ? s_dead[lane] : 0u;
+    if (in) a.tile_pend[t0 + lane] = d;
+    const unsigned long long dt = wave_sum_u64(d);
+    if (lane == 0 && dt) a.group_sum[g] -= (uint32_t)dt;
+  }
+}
+
 // Output offsets, in two levels: pip_join_kernel / pip_fix_kernel add each tile's pair
 // count to its group of kScanGroup tiles; this one workgroup scans the group sums
 // (~3e3 per 1e8 points, coalesced chunks of 1024) and pair_emit_kernel adds the counts
@@ -743,41 +879,77 @@ constexpr int kEmitTiles = 4096 / kTile;  // 4 tiles of 1024 points, 16 of 256
 static_assert(kScanGroup % kEmitTiles == 0 && kEmitTiles <= 64, "emit groups inside scan groups");
 __global__ __launch_bounds__(kEmitBlock) void pair_emit_kernel(EmitArgs a, int64_t n_tiles) {
   __shared__ uint32_t s_pref[kEmitTiles + 1];
+  __shared__ uint32_t s_phys[kEmitTiles];
   __shared__ uint64_t s_where[kEmitTiles];
   __shared__ int64_t s_off;
+  __shared__ int s_anydead;
   const int64_t t0 = (int64_t)blockIdx.x * kEmitTiles;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    // this block's tiles: counts, slots, in-block prefix
+    // this block's tiles: live counts (records minus the dead ones pip_resolve_kernel
+    // marked), slots, in-block prefix
     const int64_t t = t0 + lane;
-    const uint32_t c = (lane < kEmitTiles && t < n_tiles) ? a.tile_count[t] : 0u;
-    if (lane < kEmitTiles) s_where[lane] = t < n_tiles ? a.tile_where[t] : kNoDst;
-    const uint32_t incl = wave_incl_scan(c);
+    const bool in = lane < kEmitTiles && t < n_tiles;
+    const uint32_t phys = in ? a.tile_count[t] : 0u;
+    const uint32_t dead = in ? a.tile_dead[t] : 0u;
+    if (lane < kEmitTiles) {
+      s_where[lane] = in ? a.tile_where[t] : kNoDst;
+      s_phys[lane] = phys;
+    }
+    const uint32_t incl = wave_incl_scan(phys - dead);
     if (lane < kEmitTiles) s_pref[lane + 1] = incl;
-    if (lane == 0) s_pref[0] = 0;
+    const bool anyd = __any(dead != 0);
+    if (lane == 0) {
+      s_pref[0] = 0;
+      s_anydead = anyd ? 1 : 0;
+    }
     // predecessors of t0 inside its scan group
     const int64_t g0 = t0 - t0 % kScanGroup;
     const int64_t j = g0 + lane;
-    unsigned long long v = (lane < kScanGroup && j < t0) ? a.tile_count[j] : 0u;
+    unsigned long long v = (lane < kScanGroup && j < t0) ? a.tile_count[j] - a.tile_dead[j] : 0u;
     v = wave_sum_u64(v);
     if (lane == 0) s_off = (int64_t)(a.group_off[t0 / kScanGroup] + v);
   }
   __syncthreads();
-  const uint32_t total = s_pref[kEmitTiles];
   const int64_t off = s_off;
-  for (uint32_t i = threadIdx.x; i < total; i += kEmitBlock) {
-    const int64_t q = off + i;
-    if (q >= a.capacity) break;
-    int k = 0;
+  if (!s_anydead) {
+    const uint32_t total = s_pref[kEmitTiles];
+    for (uint32_t i = threadIdx.x; i < total; i += kEmitBlock) {
+      const int64_t q = off + i;
+      if (q >= a.capacity) break;
+      int k = 0;
 #pragma unroll
-    for (int step = kEmitTiles / 2; step >= 1; step >>= 1)
-      if (s_pref[k + step] <= i) k += step;
+      for (int step = kEmitTiles / 2; step >= 1; step >>= 1)
+        if (s_pref[k + step] <= i) k += step;
+      const uint64_t where = s_where[k];
+      if (where == kNoDst) continue;  // pool exhausted: the total exceeds the capacity
+      const uint64_t r = a.recs[where + (i - s_pref[k])];
+      const int64_t p = (t0 + k) * kTile + (int64_t)(r >> 32);
+      a.out_point[q] = a.point_id ? a.point_id[p] : a.id_base + p;
+      a.out_poly[q] = (int32_t)(uint32_t)r;
+    }
+    return;
+  }
+  // some tile holds dead records: a wave per tile compacts its live records in order
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int k = wave; k < kEmitTiles; k += kEmitBlock / 64) {
     const uint64_t where = s_where[k];
-    if (where == kNoDst) continue;  // pool exhausted: the total exceeds the capacity
-    const uint64_t r = a.recs[where + (i - s_pref[k])];
-    const int64_t p = (t0 + k) * kTile + (int64_t)(r >> 32);
-    a.out_point[q] = a.point_id ? a.point_id[p] : a.id_base + p;
-    a.out_poly[q] = (int32_t)(uint32_t)r;
+    if (where == kNoDst) continue;
+    const uint32_t phys = s_phys[k];
+    int64_t o = off + s_pref[k];
+    for (uint32_t b = 0; b < phys; b += 64) {
+      const uint32_t i = b + lane;
+      const uint64_t r = i < phys ? a.recs[where + i] : kDeadRec;
+      const bool alive = r != kDeadRec;
+      const unsigned long long bal = __ballot(alive);
+      const int64_t q = o + __popcll(bal & ((1ull << lane) - 1ull));
+      if (alive && q < a.capacity) {
+        const int64_t p = (t0 + k) * kTile + (int64_t)(r >> 32);
+        a.out_point[q] = a.point_id ? a.point_id[p] : a.id_base + p;
+        a.out_poly[q] = (int32_t)(uint32_t)r;
+      }
+      o += __popcll(bal);
+    }
   }
 }
 
@@ -820,6 +992,9 @@ hipError_t launch_cells(int is, int res, const double* x, const double* y, int64
 
 int64_t join_tiles(int64_t n) { return (n + kTile - 1) / kTile; }
 int64_t join_tile_points() { return kTile; }
+int64_t join_slot_records() { return kSlot; }
+int64_t join_pend_cap() { return kMixCap; }
+int64_t join_pend_words() { return kPendWords; }
 
 hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s, hipEvent_t after_stream) {
   if (a.n_tiles <= 0) return hipSuccess;
@@ -835,6 +1010,9 @@ hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t
     if (after_stream) hipEventRecord(after_stream, s);
     hipLaunchKernelGGL(pip_fix_kernel<MGPU_BNG>, dim3(fix_blocks), dim3(kBlock), 0, s, a);
   }
+  if (MGPU_DEFER)
+    hipLaunchKernelGGL(pip_resolve_kernel, dim3((unsigned)((a.n_tiles + kScanGroup - 1) / kScanGroup)),
+                       dim3(kResolveBlock), 0, s, a);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.group_sum, a.group_cand,
                      (a.n_tiles + kScanGroup - 1) / kScanGroup, e.group_off, a.counters);
   hipLaunchKernelGGL(pair_emit_kernel, dim3((unsigned)((a.n_tiles + kEmitTiles - 1) / kEmitTiles)),

@@ -202,7 +202,7 @@ MGPU_HDI int chip_locate(const ChipTableView& t, uint32_t c, double px, double p
 // cell: chip_contains_mixed decides) / kQuickSequential (chip without strip index).
 enum QuickVerdict { kQuickNo = 0, kQuickYes = 1, kQuickStrips = 2, kQuickSequential = 3 };
 
-MGPU_HDI int chip_quick(const ChipTableView& t, uint32_t c, double px, double py) {
+MGPU_HDI int chip_quick(const ChipTableView& t, uint32_t c, double px, double py, uint64_t* walk = nullptr) {
   const ChipHdr& H = t.chip_hdr[c];
   const double e0 = H.env[0], e1 = H.env[1], e2 = H.env[2], e3 = H.env[3];
   const uint8_t fl = H.flags;
@@ -212,20 +212,36 @@ MGPU_HDI int chip_quick(const ChipTableView& t, uint32_t c, double px, double py
   if (fl & kChipNoStrips) return kQuickSequential;
   const int gx = grid_index(px, e0, H.sx), gy = grid_index(py, e1, H.sy);
   const uint32_t st = (H.grid[gy] >> (2 * gx)) & 3;
+  if (st == kCellMixed && walk) {
+    // what a deferred walk needs from this header (chip_contains_strip): the point's
+    // strip | flags << 32 | single_ring << 40
+    const uint32_t sidx = H.strip_base + (uint32_t)strip_of(py, e1, H.inv_h, (int)H.n_strips);
+    *walk = (uint64_t)sidx | ((uint64_t)fl << 32) | ((uint64_t)(H.single_ring ? 1 : 0) << 40);
+  }
   return st == kCellMixed ? kQuickStrips : (st == kCellIn ? kQuickYes : kQuickNo);
 }
 
 // contains() for a point in a mixed grid cell of chip c: RayCrossingCounter over the
 // edges of the point's y-strip (MGPU_EDGE_STEP records in flight per step), then PointLocator
 // over the rings' verdicts.
+// The walk proper, given what it needs from the chip header: `strip` = the point's
+// strip (strip_base + strip_of(...)), `one_ring` and the chip flags.  pip_resolve_kernel
+// calls it with the values the streaming kernel already read (no header re-read).
+MGPU_HDI bool chip_contains_strip(const ChipTableView& t, uint32_t c, uint32_t strip, bool one_ring, uint8_t fl,
+                                  double px, double py, uint32_t* stat_edges = nullptr);
+
 MGPU_HDI bool chip_contains_mixed(const ChipTableView& t, uint32_t c, double px, double py,
                                   uint32_t* stat_edges = nullptr) {
   const ChipHdr& H = t.chip_hdr[c];
   const int s = strip_of(py, H.env[1], H.inv_h, (int)H.n_strips);
-  const uint32_t eb = t.strip_edge[H.strip_base + s], ee = t.strip_edge[H.strip_base + s + 1];
+  return chip_contains_strip(t, c, H.strip_base + (uint32_t)s, H.single_ring != 0, H.flags, px, py, stat_edges);
+}
+
+MGPU_HDI bool chip_contains_strip(const ChipTableView& t, uint32_t c, uint32_t strip, bool one_ring, uint8_t fl,
+                                  double px, double py, uint32_t* stat_edges) {
+  const uint32_t eb = t.strip_edge[strip], ee = t.strip_edge[strip + 1];
   if (stat_edges) *stat_edges = ee - eb;
   const double4* E4 = (const double4*)t.edges;
-  const bool one_ring = H.single_ring;
   uint32_t bnd = 0, par = 0;
 #ifndef MGPU_EDGE_STEP
 #define MGPU_EDGE_STEP 2
@@ -249,7 +265,6 @@ MGPU_HDI bool chip_contains_mixed(const ChipTableView& t, uint32_t c, double px,
   }
   // one polygon, one ring (its envelope is the chip's): RayCrossingCounter's verdict
   if (one_ring) return !(bnd & 1) && (par & 1);
-  const uint8_t fl = H.flags;
   const uint32_t pb = t.chip_part[c], pe = t.chip_part[c + 1];
   const uint32_t r0 = t.part_ring[pb];
   bool is_in = false;

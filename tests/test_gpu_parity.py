@@ -281,6 +281,37 @@ def test_pip_join_full_size_properties(gpu, nyc_chips_r9):
     gp = (p[mask] // 100).cpu().numpy()
     gq = r.polygon_id[mask].cpu().numpy()
     assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+    # near-tie audit: the points whose cell an ulp of libm could move, all of them,
+    # recomputed by the oracle (glibc, as H3-Java) -- cells and join pairs
+    ties = M.default_context(gpu).last_near_ties()
+    assert 0 < len(ties) <= 4 * max(1, r.stats["n_near_ties"]) and len(ties) >= r.stats["n_near_ties"]
+    ti = torch.from_numpy(ties).to(gpu)
+    xt, yt = x[ti].cpu().numpy(), y[ti].cpu().numpy()
+    assert np.array_equal(gpu_cells(xt, yt, 9, gpu)[0], O.h3_points_to_cells(xt, yt, 9))
+    op, oq = oracle_join(nyc_chips_r9, xt, yt)
+    sel = torch.isin(p, ti)
+    pos = {int(v): k for k, v in enumerate(ties)}
+    gp = np.array([pos[int(v)] for v in p[sel].cpu().numpy()], dtype=np.int64)
+    gq = r.polygon_id[sel].cpu().numpy()
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+
+
+def test_cells_full_size_near_tie_audit(gpu):
+    """3e7 global points (~8e-4 of them in the fast projection's tie band, within the
+    65536 the audit list keeps): every point the fast projection could not decide (the
+    mgpu_last_near_ties list) gets the oracle's (glibc) cell, at res 9 and 15."""
+    n = 30_000_000
+    g = torch.Generator(device=gpu)
+    g.manual_seed(78)
+    x = torch.rand(n, dtype=torch.float64, device=gpu, generator=g) * 360.0 - 180.0
+    y = torch.rand(n, dtype=torch.float64, device=gpu, generator=g) * 180.0 - 90.0
+    for res in (9, 15):
+        cells = M.grid_longlatascellid(x, y, res)
+        ties = M.default_context(gpu).last_near_ties()
+        assert len(ties) > 0
+        ti = torch.from_numpy(ties).to(gpu)
+        xt, yt = x[ti].cpu().numpy(), y[ti].cpu().numpy()
+        assert np.array_equal(cells[ti].cpu().numpy(), O.h3_points_to_cells(xt, yt, res)), res
 
 
 # ---------------------------------------------------------------- BASELINE configs C4 / C5

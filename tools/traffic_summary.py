@@ -13,7 +13,12 @@ import os
 import sys
 
 d, tag = sys.argv[1], sys.argv[2]
+CFG = sys.argv[3] if len(sys.argv) > 3 else "c2"   # the join_once --config of the join passes
 N = 100_000_000
+DESC = {"c2": ("uniform NYC-bbox points, H3 res 9, 263 zones", 9),
+        "c3": ("uniform points in the C3 extent, H3 res 10, 74k tract-like polygons (9.4M chips)", 10),
+        "c4": ("UPRN-like London points, BNG res 4, 180 districts", 4),
+        "c5": ("skewed points near 4 fractal polygons, H3 res 9", 9)}[CFG]
 
 
 def per_dispatch(sub, kname):
@@ -32,16 +37,17 @@ bw, _ = per_dispatch("bng_write", "cells_kernel<1>")
 f_read = bf / (16.0 * N)
 f_write = bw / (8.0 * N)
 out = {
-    "round": tag, "points": N, "res": 9,
+    "round": tag, "config": CFG, "points": N, "res": DESC[1],
     "join_fetch_bytes_raw": jf, "join_write_bytes_raw": jw, "dispatches": nj,
     "calib_bng_fetch_bytes_raw": bf, "calib_bng_write_bytes_raw": bw,
     "calib_read_factor": f_read, "calib_write_factor": f_write,
     "hbm_read_bytes_per_launch": jf / f_read, "hbm_write_bytes_per_launch": jw / f_write,
     "hbm_bytes_per_launch": jf / f_read + jw / f_write,
-    "note": "pip_join_kernel<H3>, 1e8 uniform NYC-bbox points, H3 res 9, 263 zones; FETCH_SIZE and WRITE_SIZE "
+    "note": "pip_join_kernel, 1e8 " + DESC[0] + "; FETCH_SIZE and WRITE_SIZE "
             "in separate rocprofv3 --pmc passes, each divided by its factor measured on cells_kernel<BNG> "
             "(16 B read + 8 B written per point)",
 }
 json.dump(out, open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles",
-                                 "pmc_join_traffic.json"), "w"), indent=1)
+                                 "pmc_join_traffic.json" if CFG == "c2" else "pmc_join_traffic_%s.json" % CFG), "w"),
+          indent=1)
 print(json.dumps(out, indent=1))
