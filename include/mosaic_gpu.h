@@ -92,6 +92,12 @@ int32_t mgpu_points_to_cells_host(mgpu_ctx* ctx, int32_t index_system, int32_t r
  * capacity of `out` (ids are at most 16 chars). Host pointers. */
 int32_t mgpu_bng_format(const int64_t* cells, int64_t n, char* out, int64_t out_bytes, int64_t* out_offsets);
 int32_t mgpu_bng_parse(const char* ids, const int64_t* offsets, int64_t n, int64_t* out_cells);
+/* Device form of mgpu_bng_format: device pointers, out_offsets[n + 1] device int64.
+ * Synchronises `stream`; *out_total = bytes the ids need.  MGPU_E_INVALID_ARG if an id
+ * has no string form (the reference throws), MGPU_E_CAPACITY if out_bytes is too small
+ * (only the ids that fit are written). */
+int32_t mgpu_bng_format_device(mgpu_ctx* ctx, const int64_t* cells, int64_t n, char* out, int64_t out_bytes,
+                               int64_t* out_offsets, int64_t* out_total, void* stream);
 
 /* Upload a chip table (the rows of grid_tessellateexplode, MosaicExplode.scala:70-83,
  * ChipType.scala:17-29): cell id, owning polygon id, is_core, and the chip WKB

@@ -72,5 +72,105 @@ MGPU_HDB bool point_to_cell(double eastings, double northings, int resolution, i
   return true;
 }
 
+// BNGIndexSystem.format (BNGIndexSystem.scala:119-134) with indexDigits = Long.toString
+// (:440-442): the decimal digits d of the id -> letters letterMap(d(3..4))(d(1..2)) (one
+// letter for the 500 km ids of fewer than 6 digits), then the eastings and northings
+// bins (the digits between position 5 and the last, split in halves), then the
+// quadrant suffix of the last digit.  The string comes back packed little-endian in
+// (lo, hi) (char k = byte k; at most 16 chars); returns the length, or -1 when the id
+// has no string form (non-positive, or a lookup that throws in the reference: fewer
+// than 4 digits, letter indices beyond the map, a quadrant digit above 4).
+// Digit arithmetic in doubles: every id below 2^53 (all BNG ids) is exact, and so is
+// floor(x / 10^k) of a correctly rounded division of two exact integers below 2^53.
+// No per-digit loop and no indexed local arrays (which become register waterfalls on
+// the GPU).  Shared by the host formatter and the device kernels.
+MGPU_HDB void put_char(uint64_t* lo, uint64_t* hi, int pos, uint32_t c) {
+  if (pos < 8) *lo |= (uint64_t)c << (8 * pos);
+  else *hi |= (uint64_t)c << (8 * (pos - 8));
+}
+
+// the digit arithmetic of format_cell_packed, in T = double (exact below 2^53) or
+// uint64_t (ids from 2^53: slower divisions, never a BNG id in practice)
+template <class T>
+MGPU_HDB T fl_div(T a, T b) { return a / b; }
+template <>
+MGPU_HDB double fl_div<double>(double a, double b) { return floor(a / b); }
+
+template <class T>
+MGPU_HDB int format_digits(T x, int max_digits, uint64_t* lo, uint64_t* hi) {
+  T p10[20];
+  p10[0] = (T)1;
+#pragma unroll
+  for (int k = 1; k < 20; k++) p10[k] = p10[k - 1] * (T)10;
+  int n = 1;
+#pragma unroll
+  for (int k = 1; k < 20; k++) n += (k < max_digits && x >= p10[k]) ? 1 : 0;
+  if (n < 4) return -1;  // digits.slice(3, 5) empty: "".toInt throws
+  // 10^j for a data-dependent j without indexing a local array (a register waterfall
+  // on the GPU): an unrolled select
+  auto pow_sel = [&](int j) {
+    T r = (T)1;
+#pragma unroll
+    for (int k = 0; k < 20; k++) r = (k == j) ? p10[k] : r;
+    return r;
+  };
+  const T l5 = n == 4 ? x * (T)10 : fl_div(x, pow_sel(n - 5));  // digits 0..4 (n == 4: d0..d3 then 0)
+  const T t = fl_div(l5, (T)100);
+  const int col = (int)(t - fl_div(t, (T)100) * (T)100);
+  const int row = n == 4 ? (int)((l5 - t * (T)100) / (T)10) : (int)(l5 - t * (T)100);
+  if (row >= 14 || col >= 8) return -1;  // letterMap lookup out of bounds
+  // letterMap (BNGIndexSystem.scala:88-104): rows 0..13 south to north, columns 0..7
+  // west to east; first letter from the 500 km square, second from the 100 km one
+  const uint32_t first = (row < 5) ? (col < 5 ? 'S' : 'T') : (row < 10 ? (col < 5 ? 'N' : 'O') : (col < 5 ? 'H' : 'J'));
+  const uint32_t second = (uint32_t)"VWXYZQRSTULMNOPFGHJKABCDE"[(row % 5) * 5 + (col % 5)];
+  if (n < 6) {
+    *lo = first;
+    return 1;
+  }
+  const T x10 = fl_div(x, (T)10);
+  const int q = (int)(x - x10 * (T)10);
+  if (q > 4) return -1;  // quadrants(q) out of bounds
+  const int clen = n - 6, k = clen / 2;  // digits.drop(5).dropRight(1), split in halves
+  const T pc = pow_sel(clen), pk = pow_sel(k);
+  const T coords = x10 - fl_div(x10, pc) * pc;
+  const uint32_t E = (uint32_t)fl_div(coords, pow_sel(clen - k));
+  const T nn = fl_div(coords, pow_sel(clen - 2 * k));
+  const uint32_t Nb = (uint32_t)(nn - fl_div(nn, pk) * pk);
+  *lo = first | (second << 8);
+  // k <= 6: k digits of E then of N, most significant first
+  uint32_t e = E, m = Nb;
+#pragma unroll
+  for (int i = 5; i >= 0; i--) {
+    if (i < k) {
+      put_char(lo, hi, 2 + i, '0' + e % 10u);
+      put_char(lo, hi, 2 + k + i, '0' + m % 10u);
+      e /= 10u;
+      m /= 10u;
+    }
+  }
+  int len = 2 + 2 * k;
+  if (q) {
+    put_char(lo, hi, len, (q == 1 || q == 4) ? 'S' : 'N');
+    put_char(lo, hi, len + 1, (q == 1 || q == 2) ? 'W' : 'E');
+    len += 2;
+  }
+  return len;
+}
+
+MGPU_HDB int format_cell_packed(int64_t id, uint64_t* lo, uint64_t* hi) {
+  *lo = *hi = 0;
+  if (id <= 0) return -1;
+  if (id < ((int64_t)1 << 53)) return format_digits<double>((double)id, 16, lo, hi);
+  return format_digits<uint64_t>((uint64_t)id, 20, lo, hi);
+}
+
+// the same into chars (host formatter)
+MGPU_HDB int format_cell(int64_t id, char* out) {
+  uint64_t lo, hi;
+  const int len = format_cell_packed(id, &lo, &hi);
+  for (int i = 0; i < len; i++) out[i] = (char)((i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8))) & 0xFF);
+  return len;
+}
+
 }  // namespace bng
 }  // namespace mgpu

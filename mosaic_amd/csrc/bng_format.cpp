@@ -24,37 +24,10 @@ const char* kLetters[14][8] = {
     {"NF", "NG", "NH", "NJ", "NK", "OF", "OG", "OH"}, {"NA", "NB", "NC", "ND", "NE", "OA", "OB", "OC"},
     {"HV", "HW", "HX", "HY", "HZ", "JV", "JW", "JX"}, {"HQ", "HR", "HS", "HT", "HU", "JQ", "JR", "JS"},
     {"HL", "HM", "HN", "HO", "HP", "JL", "JM", "JN"}, {"HF", "HG", "HH", "HJ", "HK", "JF", "JG", "JH"}};
-const char* kQuadrants[5] = {"", "SW", "NW", "NE", "SE"};
+const char* kQuadrants[5] = {"", "SW", "NW", "NE", "SE"};  // parse only
 
-// returns length written (<= 24) or -1 when the id has no BNG string form
-int format_one(int64_t id, char* out) {
-  if (id <= 0) return -1;
-  char d[24];
-  int n = snprintf(d, sizeof d, "%lld", (long long)id);
-  auto num = [&](int a, int b) {  // digits[a, b) as Int
-    int v = 0;
-    for (int i = a; i < b && i < n; i++) v = v * 10 + (d[i] - '0');
-    return v;
-  };
-  if (n < 3) return -1;
-  int row = num(3, 5), col = num(1, 3);
-  if (row >= 14 || col >= 8) return -1;  // letterMap lookup out of bounds
-  if (n < 6) {
-    out[0] = kLetters[row][col][0];
-    return 1;
-  }
-  int q = d[n - 1] - '0';
-  if (q > 4) return -1;
-  int len = 0;
-  out[len++] = kLetters[row][col][0];
-  out[len++] = kLetters[row][col][1];
-  int coords = n - 6;  // digits.drop(5).dropRight(1)
-  int k = coords / 2;
-  for (int i = 0; i < k; i++) out[len++] = d[5 + i];
-  for (int i = 0; i < k; i++) out[len++] = d[5 + k + i];
-  for (const char* s = kQuadrants[q]; *s; s++) out[len++] = *s;
-  return len;
-}
+// the shared host/device formatter (bng_core.h)
+int format_one(int64_t id, char* out) { return mgpu::bng::format_cell(id, out); }
 
 double pow10d(int k) {
   double r = 1;

@@ -972,6 +972,136 @@ __global__ __launch_bounds__(kStreamBlock) void st_contains_kernel(ChipTableView
   out[i] = pip::chip_locate(t, c, x[i], y[i]) == pip::kInterior ? 1 : 0;
 }
 
+// ---------------------------------------------------------------- BNG StringType ids
+// BNGIndexSystem.format (BNGIndexSystem.scala:119-134) over a device column: lengths,
+// a three-kernel scan into offsets, then the characters (bng_core.h format_cell, the
+// same code the host formatter runs).  HBM-bound: 8 B read + ~10 B written per id.
+
+__global__ __launch_bounds__(kStreamBlock) void bng_format_len_kernel(const int64_t* __restrict__ cells, int64_t n,
+                                                                   int64_t* __restrict__ offsets,
+                                                                   unsigned long long* __restrict__ counters) {
+  for (int64_t i = (int64_t)blockIdx.x * kStreamBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kStreamBlock) {
+    uint64_t lo, hi;
+    const int len = bng::format_cell_packed(cells[i], &lo, &hi);
+    offsets[i + 1] = len < 0 ? 0 : len;
+    count_wave(&counters[2], len < 0);
+  }
+}
+
+constexpr int kScan = 1024;
+// inclusive scan of v[0, n) in blocks of kScan; block totals to bsum
+__global__ __launch_bounds__(kScan) void scan_block_kernel(int64_t* __restrict__ v, int64_t n, int64_t* __restrict__ bsum) {
+  __shared__ int64_t s_w[kScan / 64];
+  const int64_t i = (int64_t)blockIdx.x * kScan + threadIdx.x;
+  const int64_t x = i < n ? v[i] : 0;
+  int64_t incl = x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t u = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += u;
+  }
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  int64_t off = 0, tot = 0;
+  for (int w = 0; w < kScan / 64; w++) {
+    if (w < wave) off += s_w[w];
+    tot += s_w[w];
+  }
+  if (i < n) v[i] = incl + off;
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+// exclusive scan of the block totals in place (one workgroup)
+__global__ __launch_bounds__(kScan) void scan_sums_kernel(int64_t* __restrict__ bsum, int64_t nb) {
+  __shared__ int64_t s_w[kScan / 64];
+  __shared__ int64_t s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int64_t b = 0; b < nb; b += kScan) {
+    const int64_t i = b + threadIdx.x;
+    const int64_t x = i < nb ? bsum[i] : 0;
+    int64_t incl = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t u = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += u;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    int64_t run = s_carry + incl - x, tot = 0;
+    for (int w = 0; w < kScan / 64; w++) {
+      if (w < wave) run += s_w[w];
+      tot += s_w[w];
+    }
+    if (i < nb) bsum[i] = run;
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry += tot;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kScan) void scan_add_kernel(int64_t* __restrict__ v, int64_t n, const int64_t* __restrict__ bsum) {
+  const int64_t i = (int64_t)blockIdx.x * kScan + threadIdx.x;
+  if (i < n) v[i] += bsum[blockIdx.x];
+}
+
+// the block's ids are formatted into LDS at their offsets relative to the block's
+// first, then the block's byte range is written with coalesced 4-byte stores (bytes at
+// the unaligned ends)
+__global__ __launch_bounds__(kStreamBlock) void bng_format_write_kernel(const int64_t* __restrict__ cells, int64_t n,
+                                                                     const int64_t* __restrict__ offsets,
+                                                                     char* __restrict__ out, int64_t out_bytes) {
+  __shared__ __attribute__((aligned(16))) char s_c[kStreamBlock * 16 + 8];
+  for (int64_t b0 = (int64_t)blockIdx.x * kStreamBlock; b0 < n; b0 += (int64_t)gridDim.x * kStreamBlock) {
+    const int64_t b1 = b0 + kStreamBlock < n ? b0 + kStreamBlock : n;
+    const int64_t base = offsets[b0];
+    const int64_t end = offsets[b1] < out_bytes ? offsets[b1] : out_bytes;
+    const int64_t i = b0 + threadIdx.x;
+    if (i < b1) {
+      uint64_t lo, hi;
+      const int len = bng::format_cell_packed(cells[i], &lo, &hi);
+      const int64_t o = offsets[i] - base;
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        if (k < len) s_c[o + k] = (char)((k < 8 ? lo >> (8 * k) : hi >> (8 * (k - 8))) & 0xFF);
+    }
+    __syncthreads();
+    // [base, end): head bytes up to 4-byte alignment, words, tail bytes
+    const int64_t a0 = (base + 3) & ~(int64_t)3, a1 = end & ~(int64_t)3;
+    if (a0 >= a1) {
+      for (int64_t q = base + threadIdx.x; q < end; q += kStreamBlock) out[q] = s_c[q - base];
+    } else {
+      if (base + threadIdx.x < a0) out[base + threadIdx.x] = s_c[threadIdx.x];
+      for (int64_t q = a0 + 4 * (int64_t)threadIdx.x; q < a1; q += 4 * kStreamBlock) {
+        const int64_t r = q - base;
+        const uint32_t w = (uint32_t)(uint8_t)s_c[r] | ((uint32_t)(uint8_t)s_c[r + 1] << 8) |
+                           ((uint32_t)(uint8_t)s_c[r + 2] << 16) | ((uint32_t)(uint8_t)s_c[r + 3] << 24);
+        *(uint32_t*)(out + q) = w;
+      }
+      if (a1 + threadIdx.x < end) out[a1 + threadIdx.x] = s_c[a1 + threadIdx.x - base];
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_bng_format(const int64_t* cells, int64_t n, char* out, int64_t out_bytes, int64_t* offsets,
+                             int64_t* bsum, unsigned long long* counters, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(offsets, 0, sizeof(int64_t), s);
+  if (e != hipSuccess || n <= 0) return e;
+  int64_t blocks = (n + kStreamBlock - 1) / kStreamBlock;
+  if (blocks > 256 * 64) blocks = 256 * 64;
+  hipLaunchKernelGGL(bng_format_len_kernel, dim3((unsigned)blocks), dim3(kStreamBlock), 0, s, cells, n, offsets,
+                     counters);
+  const int64_t nb = (n + kScan - 1) / kScan;
+  hipLaunchKernelGGL(scan_block_kernel, dim3((unsigned)nb), dim3(kScan), 0, s, offsets + 1, n, bsum);
+  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScan), 0, s, bsum, nb);
+  hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)nb), dim3(kScan), 0, s, offsets + 1, n, bsum);
+  hipLaunchKernelGGL(bng_format_write_kernel, dim3((unsigned)blocks), dim3(kStreamBlock), 0, s, cells, n, offsets, out,
+                     out_bytes);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- launchers
 
 hipError_t launch_cells(int is, int res, const double* x, const double* y, int64_t n, int64_t* out,

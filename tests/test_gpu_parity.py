@@ -79,6 +79,30 @@ def test_bng_cells_equal_oracle(gpu, res):
     assert np.array_equal(got, ref)
 
 
+def test_bng_format_device_equals_host(gpu):
+    """BNG StringType ids formatted by the HIP kernel == the host formatter == the
+    reference's known answers (TestBNGIndexSystem.scala), at all 12 resolutions."""
+    bng = M.BNGIndexSystem()
+    rng = np.random.default_rng(17)
+    e = rng.uniform(0, 700_000, 100_000)
+    nn = rng.uniform(0, 1_300_000, 100_000)
+    for res in (1, 2, 3, 4, 5, 6, -1, -2, -3, -4, -5, -6):
+        cells = O.bng_points_to_cells(e, nn, res)
+        chars, off = bng.format_device(torch.from_numpy(cells).to(gpu))
+        raw, o = chars.cpu().numpy().tobytes(), off.cpu().numpy()
+        got = [raw[o[i]:o[i + 1]].decode() for i in range(len(cells))]
+        assert got == bng.format_many(cells), res
+    d = json.load(open(os.path.join(GOLDEN, "bng_kats.json")))
+    cells = np.array([O.bng_point_to_index(k["e"], k["n"], k["res"]) for k in d["point_to_index"]], np.int64)
+    chars, off = bng.format_device(torch.from_numpy(cells).to(gpu))
+    raw, o = chars.cpu().numpy().tobytes(), off.cpu().numpy()
+    assert [raw[o[i]:o[i + 1]].decode() for i in range(len(cells))] == [k["str"] for k in d["point_to_index"]]
+    with pytest.raises(M.IllegalArgumentException):
+        bng.format_device(torch.tensor([1051000, -5], dtype=torch.int64, device=gpu))
+    chars, off = bng.format_device(torch.zeros(0, dtype=torch.int64, device=gpu))
+    assert off.cpu().tolist() == [0] and chars.numel() == 0
+
+
 def test_bng_nan_raises(gpu):
     with pytest.raises(M.IllegalStateException):
         gpu_cells([float("nan")], [100.0], 5, gpu, M.BNGIndexSystem())

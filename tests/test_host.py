@@ -144,3 +144,45 @@ def test_tessellation_rejects_unsupported():
         M.tessellate(P, M.BNGIndexSystem(), -1)
     with pytest.raises(M.IllegalStateException):
         M.tessellate(P, M.H3IndexSystem(), 16)
+
+
+# BNGIndexSystem.format restated line by line from BNGIndexSystem.scala:119-134
+# (letterMap :88-104, quadrants :40, indexDigits = Long.toString :440-442); None where
+# the Scala code throws (a lookup out of bounds, "".toInt)
+_BNG_LETTERS = [["SV", "SW", "SX", "SY", "SZ", "TV", "TW", "TX"], ["SQ", "SR", "SS", "ST", "SU", "TQ", "TR", "TS"],
+                ["SL", "SM", "SN", "SO", "SP", "TL", "TM", "TN"], ["SF", "SG", "SH", "SJ", "SK", "TF", "TG", "TH"],
+                ["SA", "SB", "SC", "SD", "SE", "TA", "TB", "TC"], ["NV", "NW", "NX", "NY", "NZ", "OV", "OW", "OX"],
+                ["NQ", "NR", "NS", "NT", "NU", "OQ", "OR", "OS"], ["NL", "NM", "NN", "NO", "NP", "OL", "OM", "ON"],
+                ["NF", "NG", "NH", "NJ", "NK", "OF", "OG", "OH"], ["NA", "NB", "NC", "ND", "NE", "OA", "OB", "OC"],
+                ["HV", "HW", "HX", "HY", "HZ", "JV", "JW", "JX"], ["HQ", "HR", "HS", "HT", "HU", "JQ", "JR", "JS"],
+                ["HL", "HM", "HN", "HO", "HP", "JL", "JM", "JN"], ["HF", "HG", "HH", "HJ", "HK", "JF", "JG", "JH"]]
+_BNG_QUADRANTS = ["", "SW", "NW", "NE", "SE"]
+
+
+def _scala_bng_format(i):
+    d = str(i)
+    try:
+        if len(d) < 6:
+            return _BNG_LETTERS[int(d[3:5])][int(d[1:3])][0]
+        p = _BNG_LETTERS[int(d[3:5])][int(d[1:3])]
+        c = d[5:-1]
+        k = len(c) // 2
+        return p + c[:k] + c[k:2 * k] + _BNG_QUADRANTS[int(d[-1])]
+    except (ValueError, IndexError):
+        return None
+
+
+def test_bng_format_matches_scala_restatement():
+    """The shared (host + device) formatter, bng_core.h format_cell, against the Scala
+    code restated above: random ids over the whole positive int64 range (incl. beyond
+    2^53, where the formatter switches from double to integer digit arithmetic)."""
+    rng = np.random.default_rng(9)
+    ids = np.concatenate([rng.integers(1, 10 ** 16, 20_000), rng.integers(10 ** 16, 2 ** 63 - 1, 5_000, dtype=np.int64),
+                          np.arange(1, 20_000), [2 ** 53 - 1, 2 ** 53, 2 ** 53 + 1, 2 ** 63 - 1]]).astype(np.int64)
+    bng = M.BNGIndexSystem()
+    ok = np.array([_scala_bng_format(int(i)) is not None for i in ids])
+    got = bng.format_many(ids[ok])
+    assert got == [_scala_bng_format(int(i)) for i in ids[ok]]
+    for i in ids[~ok][:200]:
+        with pytest.raises(M.IllegalArgumentException):
+            bng.format(int(i))
