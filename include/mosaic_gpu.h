@@ -92,10 +92,14 @@ int32_t mgpu_points_to_cells_host(mgpu_ctx* ctx, int32_t index_system, int32_t r
  * capacity of `out` (ids are at most 16 chars). Host pointers. */
 int32_t mgpu_bng_format(const int64_t* cells, int64_t n, char* out, int64_t out_bytes, int64_t* out_offsets);
 int32_t mgpu_bng_parse(const char* ids, const int64_t* offsets, int64_t n, int64_t* out_cells);
-/* Device form of mgpu_bng_format: device pointers, out_offsets[n + 1] device int64.
- * Synchronises `stream`; *out_total = bytes the ids need.  MGPU_E_INVALID_ARG if an id
- * has no string form (the reference throws), MGPU_E_CAPACITY if out_bytes is too small
- * (only the ids that fit are written). */
+/* StringType cell ids on the device (IndexSystem.serializeCellId, IndexSystem.scala:61-70):
+ * BNG = BNGIndexSystem.format as above, H3 = h3ToString (lowercase hex, H3IndexSystem
+ * format).  Device pointers, out_offsets[n + 1] device int64.  Synchronises `stream`;
+ * *out_total = bytes the ids need.  MGPU_E_INVALID_ARG if an id has no string form
+ * (the reference throws), MGPU_E_CAPACITY if out_bytes is too small (only the ids
+ * that fit are written).  mgpu_bng_format_device = index_system MGPU_BNG. */
+int32_t mgpu_format_cells_device(mgpu_ctx* ctx, int32_t index_system, const int64_t* cells, int64_t n, char* out,
+                                 int64_t out_bytes, int64_t* out_offsets, int64_t* out_total, void* stream);
 int32_t mgpu_bng_format_device(mgpu_ctx* ctx, const int64_t* cells, int64_t n, char* out, int64_t out_bytes,
                                int64_t* out_offsets, int64_t* out_total, void* stream);
 

@@ -634,19 +634,21 @@ int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t is, int32_t res, const doubl
   return MGPU_OK;
 }
 
-int32_t mgpu_bng_format_device(mgpu_ctx* ctx, const int64_t* cells, int64_t n, char* out, int64_t out_bytes,
-                               int64_t* out_offsets, int64_t* out_total, void* stream) {
+int32_t mgpu_format_cells_device(mgpu_ctx* ctx, int32_t index_system, const int64_t* cells, int64_t n, char* out,
+                                 int64_t out_bytes, int64_t* out_offsets, int64_t* out_total, void* stream) {
   if (!ctx || n < 0 || (n > 0 && (!cells || !out)) || !out_offsets || out_bytes < 0)
-    return fail(MGPU_E_INVALID_ARG, "bng_format_device: bad arguments");
+    return fail(MGPU_E_INVALID_ARG, "format_cells_device: bad arguments");
+  if (index_system != MGPU_H3 && index_system != MGPU_BNG)
+    return fail(MGPU_E_INVALID_ARG, "unknown index system %d (0 = H3, 1 = BNG)", index_system);
   if (int32_t st = set_device(ctx->device)) return st;
   hipStream_t s = (hipStream_t)stream;
-  // block totals of the offset scan live in the workspace's tile_where region (one
-  // int64 per 256 ids there, one per 1024 needed)
+  // per-chunk totals live in the workspace's tile_where region (one int64 per 256 ids
+  // there, one per 4096 needed)
   if (int32_t st = ensure_ws(ctx, mgpu::join_tiles(n))) return st;
   auto* counters = (unsigned long long*)ctx->ws;
-  auto* bsum = (int64_t*)((uint8_t*)ctx->ws + ws_layout(mgpu::join_tiles(n), 0).where);
+  auto* chunk = (int64_t*)((uint8_t*)ctx->ws + ws_layout(mgpu::join_tiles(n), 0).where);
   HIP_TRY(hipMemsetAsync(counters, 0, kWsCounters, s));
-  HIP_TRY(mgpu::launch_bng_format(cells, n, out, out_bytes, out_offsets, bsum, counters, s));
+  HIP_TRY(mgpu::launch_format_cells(index_system, cells, n, out, out_bytes, out_offsets, chunk, counters, s));
   unsigned long long h[4] = {0};
   int64_t total = 0;
   HIP_TRY(hipMemcpyAsync(h, counters, sizeof h, hipMemcpyDeviceToHost, s));
@@ -654,9 +656,14 @@ int32_t mgpu_bng_format_device(mgpu_ctx* ctx, const int64_t* cells, int64_t n, c
   HIP_TRY(hipStreamSynchronize(s));
   if (out_total) *out_total = total;
   if (h[2]) return fail(MGPU_E_INVALID_ARG, "%llu BNG cell ids have no string form", h[2]);
-  if (total > out_bytes) return fail(MGPU_E_CAPACITY, "bng_format_device: %lld bytes needed, %lld given",
+  if (total > out_bytes) return fail(MGPU_E_CAPACITY, "format_cells_device: %lld bytes needed, %lld given",
                                      (long long)total, (long long)out_bytes);
   return MGPU_OK;
+}
+
+int32_t mgpu_bng_format_device(mgpu_ctx* ctx, const int64_t* cells, int64_t n, char* out, int64_t out_bytes,
+                               int64_t* out_offsets, int64_t* out_total, void* stream) {
+  return mgpu_format_cells_device(ctx, MGPU_BNG, cells, n, out, out_bytes, out_offsets, out_total, stream);
 }
 
 int32_t mgpu_points_to_cells_host(mgpu_ctx* ctx, int32_t is, int32_t res, const double* x, const double* y, int64_t n,

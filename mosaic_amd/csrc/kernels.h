@@ -58,9 +58,11 @@ int64_t join_pend_cap();       // pending mixed-cell candidates kept per tile
 int64_t join_pend_words();     // u64 words per pending candidate
 // `after_stream` (optional) is recorded right after pip_join_kernel
 hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s, hipEvent_t after_stream);
-// offsets[n + 1] (device), bsum: scratch of ceil(n / 1024) int64; counters[2] += invalid ids
-hipError_t launch_bng_format(const int64_t* cells, int64_t n, char* out, int64_t out_bytes, int64_t* offsets,
-                             int64_t* bsum, unsigned long long* counters, hipStream_t s);
+// StringType cell ids: offsets[n + 1] (device); chunk: scratch of format_chunks(n) int64;
+// counters[2] += ids without a string form (BNG)
+int64_t format_chunks(int64_t n);
+hipError_t launch_format_cells(int is, const int64_t* cells, int64_t n, char* out, int64_t out_bytes,
+                               int64_t* offsets, int64_t* chunk, unsigned long long* counters, hipStream_t s);
 hipError_t launch_st_contains(const ChipTableView& t, const int64_t* row, const double* x, const double* y, int64_t n,
                               int8_t* out, hipStream_t s);
 

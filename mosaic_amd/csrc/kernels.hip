@@ -972,47 +972,128 @@ __global__ __launch_bounds__(kStreamBlock) void st_contains_kernel(ChipTableView
   out[i] = pip::chip_locate(t, c, x[i], y[i]) == pip::kInterior ? 1 : 0;
 }
 
-// ---------------------------------------------------------------- BNG StringType ids
-// BNGIndexSystem.format (BNGIndexSystem.scala:119-134) over a device column: lengths,
-// a three-kernel scan into offsets, then the characters (bng_core.h format_cell, the
-// same code the host formatter runs).  HBM-bound: 8 B read + ~10 B written per id.
+// ---------------------------------------------------------------- StringType cell ids
+// IndexSystem.serializeCellId for StringType (IndexSystem.scala:61-70): BNG
+// BNGIndexSystem.format (BNGIndexSystem.scala:119-134; bng_core.h format_cell_packed, the
+// code the host formatter runs) and H3 h3ToString (H3IndexSystem.format = Long.toHexString,
+// lowercase, no leading zeros).  Three passes, chunked by kFmtChunk ids per workgroup:
+//   fmt_count_kernel  lengths -> one total per chunk (8 B read per id)
+//   scan_sums_kernel  exclusive scan of the chunk totals
+//   fmt_write_kernel  lengths again, workgroup scan per 256-id slice, offsets (8 B per
+//                     id) and the characters (LDS-staged, coalesced 4-byte stores)
+constexpr int kFmtBlock = 256;
+constexpr int kFmtSlices = 16;
+constexpr int kFmtChunk = kFmtBlock * kFmtSlices;
 
-__global__ __launch_bounds__(kStreamBlock) void bng_format_len_kernel(const int64_t* __restrict__ cells, int64_t n,
-                                                                   int64_t* __restrict__ offsets,
-                                                                   unsigned long long* __restrict__ counters) {
-  for (int64_t i = (int64_t)blockIdx.x * kStreamBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kStreamBlock) {
-    uint64_t lo, hi;
-    const int len = bng::format_cell_packed(cells[i], &lo, &hi);
-    offsets[i + 1] = len < 0 ? 0 : len;
-    count_wave(&counters[2], len < 0);
+template <int IS>
+__device__ __forceinline__ int format_id(int64_t id, uint64_t* lo, uint64_t* hi) {
+  if (IS == MGPU_BNG) return bng::format_cell_packed(id, lo, hi);
+  const uint64_t v = (uint64_t)id;
+  const int nd = v ? (64 - __clzll((long long)v) + 3) / 4 : 1;
+  *lo = *hi = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    if (i < nd) {
+      const uint32_t d = (uint32_t)(v >> (4 * (nd - 1 - i))) & 15u;
+      bng::put_char(lo, hi, i, d < 10 ? '0' + d : 'a' + d - 10);
+    }
+  }
+  return nd;
+}
+
+// workgroup-wide exclusive scan of one value per thread; returns the total too
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t incl = wave_incl_scan(v);
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kFmtBlock / 64; w++) {
+    const uint32_t x = s_w[w];
+    if (w < wave) off += x;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return off + incl - v;
+}
+
+template <int IS>
+__global__ __launch_bounds__(kFmtBlock) void fmt_count_kernel(const int64_t* __restrict__ cells, int64_t n,
+                                                            int64_t* __restrict__ chunk_tot,
+                                                            unsigned long long* __restrict__ counters) {
+  __shared__ uint32_t s_w[kFmtBlock / 64];
+  const int64_t c0 = (int64_t)blockIdx.x * kFmtChunk;
+  uint32_t sum = 0;
+  bool bad = false;
+#pragma unroll 4
+  for (int sl = 0; sl < kFmtSlices; sl++) {
+    const int64_t i = c0 + sl * kFmtBlock + threadIdx.x;
+    if (i < n) {
+      uint64_t lo, hi;
+      const int len = format_id<IS>(cells[i], &lo, &hi);
+      sum += len < 0 ? 0u : (uint32_t)len;
+      bad |= len < 0;
+    }
+  }
+  count_wave(&counters[2], bad);
+  uint32_t tot;
+  block_excl_scan(sum, s_w, &tot);
+  if (threadIdx.x == 0) chunk_tot[blockIdx.x] = tot;
+}
+
+template <int IS>
+__global__ __launch_bounds__(kFmtBlock) void fmt_write_kernel(const int64_t* __restrict__ cells, int64_t n,
+                                                            const int64_t* __restrict__ chunk_off,
+                                                            int64_t* __restrict__ offsets, char* __restrict__ out,
+                                                            int64_t out_bytes) {
+  __shared__ uint32_t s_w[kFmtBlock / 64];
+  __shared__ __attribute__((aligned(16))) char s_c[kFmtBlock * 16 + 8];
+  const int64_t c0 = (int64_t)blockIdx.x * kFmtChunk;
+  int64_t carry = chunk_off[blockIdx.x];
+  for (int sl = 0; sl < kFmtSlices; sl++) {
+    const int64_t s0 = c0 + sl * kFmtBlock;
+    if (s0 >= n) break;
+    const int64_t i = s0 + threadIdx.x;
+    uint64_t lo = 0, hi = 0;
+    int len = 0;
+    if (i < n) {
+      len = format_id<IS>(cells[i], &lo, &hi);
+      if (len < 0) len = 0;
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan((uint32_t)len, s_w, &tot);
+    if (i < n) {
+      offsets[i] = carry + ex;
+      if (i == n - 1) offsets[n] = carry + ex + len;
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        if (k < len) s_c[ex + k] = (char)((k < 8 ? lo >> (8 * k) : hi >> (8 * (k - 8))) & 0xFF);
+    }
+    __syncthreads();
+    // [base, end): head bytes up to 4-byte alignment, words, tail bytes
+    const int64_t base = carry, end = carry + tot < out_bytes ? carry + tot : out_bytes;
+    const int64_t a0 = (base + 3) & ~(int64_t)3, a1 = end & ~(int64_t)3;
+    if (a0 >= a1) {
+      for (int64_t q = base + threadIdx.x; q < end; q += kFmtBlock) out[q] = s_c[q - base];
+    } else {
+      if (base + threadIdx.x < a0) out[base + threadIdx.x] = s_c[threadIdx.x];
+      for (int64_t q = a0 + 4 * (int64_t)threadIdx.x; q < a1; q += 4 * kFmtBlock) {
+        const int64_t r = q - base;
+        const uint32_t w = (uint32_t)(uint8_t)s_c[r] | ((uint32_t)(uint8_t)s_c[r + 1] << 8) |
+                           ((uint32_t)(uint8_t)s_c[r + 2] << 16) | ((uint32_t)(uint8_t)s_c[r + 3] << 24);
+        *(uint32_t*)(out + q) = w;
+      }
+      if (a1 + threadIdx.x < end) out[a1 + threadIdx.x] = s_c[a1 + threadIdx.x - base];
+    }
+    carry += tot;
+    __syncthreads();
   }
 }
 
 constexpr int kScan = 1024;
-// inclusive scan of v[0, n) in blocks of kScan; block totals to bsum
-__global__ __launch_bounds__(kScan) void scan_block_kernel(int64_t* __restrict__ v, int64_t n, int64_t* __restrict__ bsum) {
-  __shared__ int64_t s_w[kScan / 64];
-  const int64_t i = (int64_t)blockIdx.x * kScan + threadIdx.x;
-  const int64_t x = i < n ? v[i] : 0;
-  int64_t incl = x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int64_t u = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += u;
-  }
-  if (lane == 63) s_w[wave] = incl;
-  __syncthreads();
-  int64_t off = 0, tot = 0;
-  for (int w = 0; w < kScan / 64; w++) {
-    if (w < wave) off += s_w[w];
-    tot += s_w[w];
-  }
-  if (i < n) v[i] = incl + off;
-  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
-}
-
-// exclusive scan of the block totals in place (one workgroup)
+// exclusive scan of v[0, nb) in place (one workgroup)
 __global__ __launch_bounds__(kScan) void scan_sums_kernel(int64_t* __restrict__ bsum, int64_t nb) {
   __shared__ int64_t s_w[kScan / 64];
   __shared__ int64_t s_carry;
@@ -1041,64 +1122,24 @@ __global__ __launch_bounds__(kScan) void scan_sums_kernel(int64_t* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(kScan) void scan_add_kernel(int64_t* __restrict__ v, int64_t n, const int64_t* __restrict__ bsum) {
-  const int64_t i = (int64_t)blockIdx.x * kScan + threadIdx.x;
-  if (i < n) v[i] += bsum[blockIdx.x];
-}
+int64_t format_chunks(int64_t n) { return (n + kFmtChunk - 1) / kFmtChunk; }
 
-// the block's ids are formatted into LDS at their offsets relative to the block's
-// first, then the block's byte range is written with coalesced 4-byte stores (bytes at
-// the unaligned ends)
-__global__ __launch_bounds__(kStreamBlock) void bng_format_write_kernel(const int64_t* __restrict__ cells, int64_t n,
-                                                                     const int64_t* __restrict__ offsets,
-                                                                     char* __restrict__ out, int64_t out_bytes) {
-  __shared__ __attribute__((aligned(16))) char s_c[kStreamBlock * 16 + 8];
-  for (int64_t b0 = (int64_t)blockIdx.x * kStreamBlock; b0 < n; b0 += (int64_t)gridDim.x * kStreamBlock) {
-    const int64_t b1 = b0 + kStreamBlock < n ? b0 + kStreamBlock : n;
-    const int64_t base = offsets[b0];
-    const int64_t end = offsets[b1] < out_bytes ? offsets[b1] : out_bytes;
-    const int64_t i = b0 + threadIdx.x;
-    if (i < b1) {
-      uint64_t lo, hi;
-      const int len = bng::format_cell_packed(cells[i], &lo, &hi);
-      const int64_t o = offsets[i] - base;
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-        if (k < len) s_c[o + k] = (char)((k < 8 ? lo >> (8 * k) : hi >> (8 * (k - 8))) & 0xFF);
-    }
-    __syncthreads();
-    // [base, end): head bytes up to 4-byte alignment, words, tail bytes
-    const int64_t a0 = (base + 3) & ~(int64_t)3, a1 = end & ~(int64_t)3;
-    if (a0 >= a1) {
-      for (int64_t q = base + threadIdx.x; q < end; q += kStreamBlock) out[q] = s_c[q - base];
-    } else {
-      if (base + threadIdx.x < a0) out[base + threadIdx.x] = s_c[threadIdx.x];
-      for (int64_t q = a0 + 4 * (int64_t)threadIdx.x; q < a1; q += 4 * kStreamBlock) {
-        const int64_t r = q - base;
-        const uint32_t w = (uint32_t)(uint8_t)s_c[r] | ((uint32_t)(uint8_t)s_c[r + 1] << 8) |
-                           ((uint32_t)(uint8_t)s_c[r + 2] << 16) | ((uint32_t)(uint8_t)s_c[r + 3] << 24);
-        *(uint32_t*)(out + q) = w;
-      }
-      if (a1 + threadIdx.x < end) out[a1 + threadIdx.x] = s_c[a1 + threadIdx.x - base];
-    }
-    __syncthreads();
-  }
-}
-
-hipError_t launch_bng_format(const int64_t* cells, int64_t n, char* out, int64_t out_bytes, int64_t* offsets,
-                             int64_t* bsum, unsigned long long* counters, hipStream_t s) {
+hipError_t launch_format_cells(int is, const int64_t* cells, int64_t n, char* out, int64_t out_bytes,
+                               int64_t* offsets, int64_t* chunk, unsigned long long* counters, hipStream_t s) {
   hipError_t e = hipMemsetAsync(offsets, 0, sizeof(int64_t), s);
   if (e != hipSuccess || n <= 0) return e;
-  int64_t blocks = (n + kStreamBlock - 1) / kStreamBlock;
-  if (blocks > 256 * 64) blocks = 256 * 64;
-  hipLaunchKernelGGL(bng_format_len_kernel, dim3((unsigned)blocks), dim3(kStreamBlock), 0, s, cells, n, offsets,
-                     counters);
-  const int64_t nb = (n + kScan - 1) / kScan;
-  hipLaunchKernelGGL(scan_block_kernel, dim3((unsigned)nb), dim3(kScan), 0, s, offsets + 1, n, bsum);
-  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScan), 0, s, bsum, nb);
-  hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)nb), dim3(kScan), 0, s, offsets + 1, n, bsum);
-  hipLaunchKernelGGL(bng_format_write_kernel, dim3((unsigned)blocks), dim3(kStreamBlock), 0, s, cells, n, offsets, out,
-                     out_bytes);
+  const int64_t nc = format_chunks(n);
+  if (is == MGPU_BNG)
+    hipLaunchKernelGGL(fmt_count_kernel<MGPU_BNG>, dim3((unsigned)nc), dim3(kFmtBlock), 0, s, cells, n, chunk, counters);
+  else
+    hipLaunchKernelGGL(fmt_count_kernel<MGPU_H3>, dim3((unsigned)nc), dim3(kFmtBlock), 0, s, cells, n, chunk, counters);
+  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScan), 0, s, chunk, nc);
+  if (is == MGPU_BNG)
+    hipLaunchKernelGGL(fmt_write_kernel<MGPU_BNG>, dim3((unsigned)nc), dim3(kFmtBlock), 0, s, cells, n, chunk, offsets,
+                       out, out_bytes);
+  else
+    hipLaunchKernelGGL(fmt_write_kernel<MGPU_H3>, dim3((unsigned)nc), dim3(kFmtBlock), 0, s, cells, n, chunk, offsets,
+                       out, out_bytes);
   return hipGetLastError();
 }
 

@@ -42,13 +42,9 @@ def broadcast_chips(chips, ctx, src=0, group=None):
     nbytes = int(size.item())
     buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     if rank == src:
-        # view the blob as a tensor-sized copy source
-        import ctypes
-        from . import _native as N
-        src_t = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        # the broadcast's source: a tensor copy of the library-owned blob
         torch.cuda.synchronize(dev)
-        _copy_device(ptr, src_t.data_ptr(), nbytes)
-        buf.copy_(src_t)
+        _copy_device(ptr, buf.data_ptr(), nbytes)
     if backend == "nccl":
         dist.broadcast(buf, src, group=group)
     else:  # gloo: stage through host memory

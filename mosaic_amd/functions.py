@@ -19,9 +19,22 @@ from .index_system import H3IndexSystem, _check_points
 _H3 = H3IndexSystem()
 
 
-def grid_longlatascellid(lon, lat, resolution, index_system=None, ctx=None, stream=None, stats=False):
-    """Cell id of every (lon, lat) -- (eastings, northings) for BNG."""
-    return (index_system or _H3).points_to_index(lon, lat, resolution, ctx=ctx, stream=stream, stats=stats)
+def grid_longlatascellid(lon, lat, resolution, index_system=None, ctx=None, stream=None, stats=False,
+                         cell_id_type="long"):
+    """Cell id of every (lon, lat) -- (eastings, northings) for BNG.
+
+    cell_id_type "long": an int64 tensor (LongType).  "string": the StringType ids
+    (IndexSystem.serializeCellId -- BNG's default cell id type, BNGIndexSystem.scala:30),
+    formatted on the device: (chars uint8 tensor, offsets int64 tensor of n + 1)."""
+    isys = index_system or _H3
+    out = isys.points_to_index(lon, lat, resolution, ctx=ctx, stream=stream, stats=stats)
+    if cell_id_type == "long":
+        return out
+    if cell_id_type != "string":
+        raise N.IllegalArgumentException(N.MGPU_E_INVALID_ARG, "cell_id_type must be 'long' or 'string'")
+    cells, st = out if stats else (out, None)
+    strs = isys.format_device(cells, ctx=ctx, stream=stream)
+    return (strs, st) if stats else strs
 
 
 def grid_pointascellid(points_xy, resolution, index_system=None, **kw):

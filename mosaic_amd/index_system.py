@@ -92,6 +92,28 @@ class IndexSystem:
         y = torch.tensor([float(lat)], dtype=torch.float64, device=dev)
         return int(self.points_to_index(x, y, resolution, ctx=ctx)[0].item())
 
+    def format_device(self, cells, ctx=None, stream=None):
+        """StringType cell ids of a device int64 column (IndexSystem.serializeCellId,
+        IndexSystem.scala:61-70; mgpu_format_cells_device, HIP): BNG format / H3 hex.
+        Returns (chars: uint8 tensor of the concatenated ids, offsets: int64 tensor of n + 1)."""
+        import ctypes
+        import torch
+        from .context import default_context
+        if cells.dtype != torch.int64 or not cells.is_cuda:
+            raise IllegalArgumentException(N.MGPU_E_INVALID_ARG, "cells must be an int64 device tensor")
+        cells = cells.contiguous()
+        ctx = ctx or default_context(cells.device)
+        n = cells.numel()
+        off = torch.empty(n + 1, dtype=torch.int64, device=cells.device)
+        cap = max(16 * n, 1)  # an id is at most 16 chars
+        out = torch.empty(cap, dtype=torch.uint8, device=cells.device)
+        tot = ctypes.c_int64()
+        s = stream if stream is not None else torch.cuda.current_stream(cells.device).cuda_stream
+        st = N.lib().mgpu_format_cells_device(ctx.handle, self.code, cells.data_ptr(), n, out.data_ptr(), cap,
+                                              off.data_ptr(), ctypes.byref(tot), s)
+        N.check(st, "cell id has no string form")
+        return out[:tot.value], off
+
 
 def _check_points(x, y):
     if x.dtype != y.dtype or str(x.dtype) != "torch.float64":
@@ -181,26 +203,6 @@ class BNGIndexSystem(IndexSystem):
         N.check(st, "BNG cell id has no string form")
         raw = buf.tobytes()
         return [raw[off[i]:off[i + 1]].decode() for i in range(n)]
-
-    def format_device(self, cells, ctx=None, stream=None):
-        """BNGIndexSystem.format over a device int64 column (mgpu_bng_format_device, HIP):
-        returns (chars: uint8 tensor of the concatenated ids, offsets: int64 tensor of n + 1)."""
-        import ctypes
-        import torch
-        from .context import default_context
-        if cells.dtype != torch.int64 or not cells.is_cuda:
-            raise IllegalArgumentException(N.MGPU_E_INVALID_ARG, "cells must be an int64 device tensor")
-        cells = cells.contiguous()
-        ctx = ctx or default_context(cells.device)
-        n = cells.numel()
-        off = torch.empty(n + 1, dtype=torch.int64, device=cells.device)
-        cap = max(16 * n, 1)  # an id is at most 14 chars
-        out = torch.empty(cap, dtype=torch.uint8, device=cells.device)
-        tot = ctypes.c_int64()
-        s = stream if stream is not None else torch.cuda.current_stream(cells.device).cuda_stream
-        N.check(N.lib().mgpu_bng_format_device(ctx.handle, cells.data_ptr(), n, out.data_ptr(), cap, off.data_ptr(),
-                                               ctypes.byref(tot), s), "BNG cell id has no string form")
-        return out[:tot.value], off
 
     def parse_many(self, ids):
         enc = [s.encode() for s in ids]

@@ -103,6 +103,24 @@ def test_bng_format_device_equals_host(gpu):
     assert off.cpu().tolist() == [0] and chars.numel() == 0
 
 
+def test_h3_string_ids_on_gpu(gpu):
+    """grid_longlatascellid with StringType ids: the device H3 formatter == h3ToString
+    (lowercase hex) of the oracle's cells, at res 0, 9 and 15."""
+    rng = np.random.default_rng(31)
+    x, y = rng.uniform(-180, 180, 50_000), rng.uniform(-90, 90, 50_000)
+    for res in (0, 9, 15):
+        chars, off = M.grid_longlatascellid(T(x, gpu), T(y, gpu), res, cell_id_type="string")
+        raw, o = chars.cpu().numpy().tobytes(), off.cpu().numpy()
+        got = [raw[o[i]:o[i + 1]].decode() for i in range(len(x))]
+        assert got == ["%x" % c for c in O.h3_points_to_cells(x, y, res)], res
+    e, nn = rng.uniform(0, 700_000, 1000), rng.uniform(0, 1_300_000, 1000)
+    chars, off = M.grid_longlatascellid(T(e, gpu), T(nn, gpu), 3, index_system=M.BNGIndexSystem(),
+                                        cell_id_type="string")
+    raw, o = chars.cpu().numpy().tobytes(), off.cpu().numpy()
+    assert [raw[o[i]:o[i + 1]].decode() for i in range(1000)] == \
+        M.BNGIndexSystem().format_many(O.bng_points_to_cells(e, nn, 3))
+
+
 def test_bng_nan_raises(gpu):
     with pytest.raises(M.IllegalStateException):
         gpu_cells([float("nan")], [100.0], 5, gpu, M.BNGIndexSystem())
