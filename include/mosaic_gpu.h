@@ -103,6 +103,17 @@ int32_t mgpu_format_cells_device(mgpu_ctx* ctx, int32_t index_system, const int6
 int32_t mgpu_bng_format_device(mgpu_ctx* ctx, const int64_t* cells, int64_t n, char* out, int64_t out_bytes,
                                int64_t* out_offsets, int64_t* out_total, void* stream);
 
+/* IndexSystem.kRing / kLoop over a device column of cells (grid_cellkring /
+ * grid_cellkloop: expressions/index/CellKRing.scala:68, CellKLoop.scala:63) --
+ * BNGIndexSystem.kRing / kLoop, BNGIndexSystem.scala:221-252 (the cell, then loops
+ * 1..k; a loop = pointToIndex of the 8k corners around the cell, kept when isValid),
+ * in the reference's order.  BNG only (H3 returns MGPU_E_INVALID_ARG).  Cell i's list
+ * is out_cells[out_offsets[i] .. out_offsets[i + 1]); device pointers; *out_total =
+ * entries needed (MGPU_E_CAPACITY when above `capacity`).  0 <= k <= 1024. */
+int32_t mgpu_grid_kring(mgpu_ctx* ctx, int32_t index_system, const int64_t* cells, int64_t n, int32_t k,
+                        int32_t loop_only, int64_t* out_cells, int64_t capacity, int64_t* out_offsets,
+                        int64_t* out_total, void* stream);
+
 /* Upload a chip table (the rows of grid_tessellateexplode, MosaicExplode.scala:70-83,
  * ChipType.scala:17-29): cell id, owning polygon id, is_core, and the chip WKB
  * (big- or little-endian, Polygon / MultiPolygon / GeometryCollection of those;

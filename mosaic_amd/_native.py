@@ -27,7 +27,7 @@ MGPU_BNG = 1
 EXPORTS = (
     "mgpu_last_error", "mgpu_version", "mgpu_join_tile_points", "mgpu_ctx_create", "mgpu_ctx_destroy", "mgpu_check_resolution",
     "mgpu_points_to_cells", "mgpu_points_to_cells_host", "mgpu_bng_format", "mgpu_bng_parse",
-    "mgpu_bng_format_device", "mgpu_format_cells_device",
+    "mgpu_bng_format_device", "mgpu_format_cells_device", "mgpu_grid_kring",
     "mgpu_chips_upload", "mgpu_chips_destroy", "mgpu_chips_device_blob", "mgpu_chips_from_device_blob",
     "mgpu_chips_info", "mgpu_st_contains", "mgpu_pip_join", "mgpu_pip_join_async", "mgpu_ctx_reserve",
     "mgpu_last_near_ties",    "mgpu_pip_join_host", "mgpu_tessellate", "mgpu_tess_result_sizes", "mgpu_tess_result_copy",
@@ -93,6 +93,7 @@ def lib():
         "mgpu_bng_format": (I32, [P, I64, P, I64, P]),
         "mgpu_bng_format_device": (I32, [P, P, I64, P, I64, P, ctypes.POINTER(I64), P]),
         "mgpu_format_cells_device": (I32, [P, I32, P, I64, P, I64, P, ctypes.POINTER(I64), P]),
+        "mgpu_grid_kring": (I32, [P, I32, P, I64, I32, I32, P, I64, P, ctypes.POINTER(I64), P]),
         "mgpu_bng_parse": (I32, [P, P, I64, P]),
         "mgpu_chips_upload": (I32, [P, I32, I64, P, P, P, P, P, ctypes.POINTER(P)]),
         "mgpu_chips_destroy": (I32, [P]),

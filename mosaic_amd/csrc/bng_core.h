@@ -172,5 +172,101 @@ MGPU_HDB int format_cell(int64_t id, char* out) {
   return len;
 }
 
+// BNGIndexSystem.getEdgeSize(resolution) (BNGIndexSystem.scala:163-170, sizeMap :64-79)
+MGPU_HDB int32_t edge_of_res(int r) {
+  switch (r) {
+    case 1: return 100000;
+    case -1: return 500000;
+    case 2: return 10000;
+    case -2: return 50000;
+    case 3: return 1000;
+    case -3: return 5000;
+    case 4: return 100;
+    case -4: return 500;
+    case 5: return 10;
+    case -5: return 50;
+    case 6: return 1;
+    case -6: return 5;
+    default: return 0;
+  }
+}
+
+// getResolution(digits), getX / getY (the cell's south-west corner) and the letter
+// indices isValid checks (BNGIndexSystem.scala:261-270, 451-506), for an id below 2^53
+// (doubles exact).  Returns false where the Scala code would throw ("".toInt on an id
+// of fewer than 4 digits) or for a non-positive id.  The Int arithmetic wraps as on
+// the JVM.
+MGPU_HDB bool cell_corner(int64_t id, int* res, int32_t* edge, int32_t* x, int32_t* y, int* x_letter, int* y_letter) {
+  if (id <= 0 || id >= ((int64_t)1 << 53)) return false;
+  const double v = (double)id;
+  double p10[17];
+  p10[0] = 1.0;
+#pragma unroll
+  for (int k = 1; k < 17; k++) p10[k] = p10[k - 1] * 10.0;
+  int n = 1;
+#pragma unroll
+  for (int k = 1; k < 16; k++) n += v >= p10[k] ? 1 : 0;
+  if (n < 4) return false;
+  auto pw = [&](int j) {
+    double r = 1.0;
+#pragma unroll
+    for (int k = 0; k < 17; k++) r = (k == j) ? p10[k] : r;
+    return r;
+  };
+  // digits [a, b) of the id as a number (b <= n)
+  auto slice = [&](int a, int b) {
+    const double hi = floor(v / pw(n - b));
+    const double m = pw(b - a);
+    return hi - floor(hi / m) * m;
+  };
+  const int q = (int)slice(n - 1, n);
+  const int r = n < 6 ? -1 : (q > 0 ? -((n - 6) / 2 + 2) : (n - 6) / 2 + 1);
+  const int32_t e = edge_of_res(r);
+  if (!e) return false;
+  const int k = (n - 6) / 2;  // JVM Int division (n = 4: -1, the bin slices are empty)
+  const int kk = k > 0 ? k : 0;
+  const int b_end = n < 5 ? n : 5;
+  const double A = slice(1, 3), B = slice(3, b_end);
+  const double xv = A * pw(kk) + (kk ? slice(5, 5 + kk) : 0.0);
+  const double yv = B * pw(kk) + (kk ? slice(5 + kk, 5 + 2 * kk) : 0.0);
+  const uint32_t adj = (uint32_t)(q > 0 ? 2 * e : e);
+  *x = (int32_t)((uint32_t)(int32_t)xv * adj + (uint32_t)((q == 3 || q == 4) ? e : 0));
+  *y = (int32_t)((uint32_t)(int32_t)yv * adj + (uint32_t)((q == 2 || q == 3) ? e : 0));
+  *res = r;
+  *edge = e;
+  *x_letter = (int)B;  // isValid's xLetterIndex = digits.slice(3, 5)
+  *y_letter = (int)A;  // yLetterIndex = digits.slice(1, 3)
+  return true;
+}
+
+// BNGIndexSystem.isValid (BNGIndexSystem.scala:261-270): 1 / 0, or -1 where the Scala
+// code throws (NumberFormatException from "".toInt on an id of fewer than 4 digits;
+// a non-positive id, whose digits are not digits, is treated the same)
+MGPU_HDB int valid_state(int64_t id) {
+  int r, xl, yl;
+  int32_t e, x, y;
+  if (!cell_corner(id, &r, &e, &x, &y, &xl, &yl)) return -1;
+  return (x >= 0 && x <= 700000 && y >= 0 && y <= 1300000 && xl < 14 && yl < 8) ? 1 : 0;
+}
+
+// Position c of kLoop(index, k)'s candidate list (BNGIndexSystem.scala:233-246): the
+// bottom, right, top and left sides, 2k corners each, as (x, y) in metres.
+MGPU_HDB void kloop_xy(int32_t x, int32_t y, int32_t e, int k, int c, int32_t* px, int32_t* py) {
+  const int side = c / (2 * k), t = c % (2 * k);
+  if (side == 0) {
+    *px = x + (t - k) * e;
+    *py = y - k * e;
+  } else if (side == 1) {
+    *px = x + k * e;
+    *py = y + (t - k) * e;
+  } else if (side == 2) {
+    *px = x + (k - t) * e;
+    *py = y + k * e;
+  } else {
+    *px = x - k * e;
+    *py = y + (k - t) * e;
+  }
+}
+
 }  // namespace bng
 }  // namespace mgpu

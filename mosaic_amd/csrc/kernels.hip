@@ -1122,7 +1122,116 @@ __global__ __launch_bounds__(kScan) void scan_sums_kernel(int64_t* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------- BNG kRing / kLoop
+// BNGIndexSystem.kRing / kLoop (BNGIndexSystem.scala:221-252) over a device column of
+// cells (grid_cellkring / grid_cellkloop, expressions/index/CellKRing.scala:68,
+// CellKLoop.scala:63): the candidates of every loop are pointToIndex of the corners
+// around the cell's south-west corner (bng_core.h kloop_xy), kept when isValid; kRing =
+// the cell, then loops 1..k.  Same three-pass layout as the string ids: counts per
+// chunk, chunk scan, then per 256-cell slice a workgroup scan, offsets and the ids.
+// one loop's kept ids (-1: a candidate's isValid throws in the reference)
+__device__ __forceinline__ int64_t bng_loop(int r, int32_t e, int32_t x, int32_t y, int k, int64_t* out) {
+  int64_t m = 0;
+  for (int c = 0; c < 8 * k; c++) {
+    int32_t px, py;
+    bng::kloop_xy(x, y, e, k, c, &px, &py);
+    int64_t nb = 0;
+    bng::point_to_cell((double)px, (double)py, r, &nb);
+    const int v = bng::valid_state(nb);
+    if (v < 0) return -1;
+    if (v) {
+      if (out) out[m] = nb;
+      m++;
+    }
+  }
+  return m;
+}
+
+// entries of one cell's list (-1: the reference throws -- the id is no BNG cell, or
+// a loop candidate cannot be parsed by isValid)
+__device__ __forceinline__ int64_t bng_kring(int64_t id, int k, bool loop_only, int64_t* out) {
+  int r, xl, yl;
+  int32_t e, x, y;
+  if (!bng::cell_corner(id, &r, &e, &x, &y, &xl, &yl)) return -1;
+  if (loop_only) return bng_loop(r, e, x, y, k, out);
+  int64_t m = 1;
+  if (out) out[0] = id;
+  for (int j = 1; j <= k; j++) {
+    const int64_t l = bng_loop(r, e, x, y, j, out ? out + m : nullptr);
+    if (l < 0) return -1;
+    m += l;
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(kFmtBlock) void kring_count_kernel(const int64_t* __restrict__ cells, int64_t n, int k,
+                                                              int loop_only, int64_t* __restrict__ chunk_tot,
+                                                              unsigned long long* __restrict__ counters) {
+  __shared__ unsigned long long s_w[kFmtBlock / 64];
+  const int64_t c0 = (int64_t)blockIdx.x * kFmtChunk;
+  unsigned long long sum = 0;
+  bool bad = false;
+  for (int sl = 0; sl < kFmtSlices; sl++) {
+    const int64_t i = c0 + sl * kFmtBlock + threadIdx.x;
+    if (i < n) {
+      const int64_t m = bng_kring(cells[i], k, loop_only != 0, nullptr);
+      sum += m < 0 ? 0ull : (unsigned long long)m;
+      bad |= m < 0;
+    }
+  }
+  count_wave(&counters[2], bad);
+  sum = wave_sum_u64(sum);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kFmtBlock / 64; w++) t += s_w[w];
+    chunk_tot[blockIdx.x] = (int64_t)t;
+  }
+}
+
+__global__ __launch_bounds__(kFmtBlock) void kring_write_kernel(const int64_t* __restrict__ cells, int64_t n, int k,
+                                                              int loop_only, const int64_t* __restrict__ chunk_off,
+                                                              int64_t* __restrict__ offsets, int64_t* __restrict__ out,
+                                                              int64_t capacity) {
+  __shared__ uint32_t s_w[kFmtBlock / 64];
+  const int64_t c0 = (int64_t)blockIdx.x * kFmtChunk;
+  int64_t carry = chunk_off[blockIdx.x];
+  for (int sl = 0; sl < kFmtSlices; sl++) {
+    const int64_t s0 = c0 + sl * kFmtBlock;
+    if (s0 >= n) break;
+    const int64_t i = s0 + threadIdx.x;
+    int64_t m = 0;
+    if (i < n) {
+      m = bng_kring(cells[i], k, loop_only != 0, nullptr);
+      if (m < 0) m = 0;
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan((uint32_t)m, s_w, &tot);
+    if (i < n) {
+      const int64_t o = carry + ex;
+      offsets[i] = o;
+      if (i == n - 1) offsets[n] = o + m;
+      if (m && o + m <= capacity) bng_kring(cells[i], k, loop_only != 0, out + o);
+    }
+    carry += tot;
+  }
+}
+
 int64_t format_chunks(int64_t n) { return (n + kFmtChunk - 1) / kFmtChunk; }
+
+hipError_t launch_bng_kring(const int64_t* cells, int64_t n, int k, int loop_only, int64_t* out, int64_t capacity,
+                            int64_t* offsets, int64_t* chunk, unsigned long long* counters, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(offsets, 0, sizeof(int64_t), s);
+  if (e != hipSuccess || n <= 0) return e;
+  const int64_t nc = format_chunks(n);
+  hipLaunchKernelGGL(kring_count_kernel, dim3((unsigned)nc), dim3(kFmtBlock), 0, s, cells, n, k, loop_only, chunk,
+                     counters);
+  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScan), 0, s, chunk, nc);
+  hipLaunchKernelGGL(kring_write_kernel, dim3((unsigned)nc), dim3(kFmtBlock), 0, s, cells, n, k, loop_only, chunk,
+                     offsets, out, capacity);
+  return hipGetLastError();
+}
 
 hipError_t launch_format_cells(int is, const int64_t* cells, int64_t n, char* out, int64_t out_bytes,
                                int64_t* offsets, int64_t* chunk, unsigned long long* counters, hipStream_t s) {

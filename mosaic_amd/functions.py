@@ -47,6 +47,37 @@ def grid_pointascellid(points_xy, resolution, index_system=None, **kw):
     return grid_longlatascellid(x, y, resolution, index_system=index_system, **kw)
 
 
+def grid_cellkring(cells, k, index_system, loop_only=False, ctx=None, stream=None):
+    """grid_cellkring / grid_cellkloop (CellKRing.scala:68, CellKLoop.scala:63 ->
+    IndexSystem.kRing / kLoop) over a device int64 column, on the GPU (BNG).  Returns
+    (ids int64 tensor, offsets int64 tensor of n + 1): cell i's list is
+    ids[offsets[i]:offsets[i + 1]], in the reference's order."""
+    import ctypes
+    import torch
+    from .context import default_context
+    if cells.dtype != torch.int64 or not cells.is_cuda:
+        raise N.IllegalArgumentException(N.MGPU_E_INVALID_ARG, "cells must be an int64 device tensor")
+    cells = cells.contiguous()
+    ctx = ctx or default_context(cells.device)
+    n = cells.numel()
+    k = int(k)
+    per = 8 * k if loop_only else 1 + 4 * k * (k + 1)
+    cap = max(n * per, 1)
+    out = torch.empty(cap, dtype=torch.int64, device=cells.device)
+    off = torch.empty(n + 1, dtype=torch.int64, device=cells.device)
+    tot = ctypes.c_int64()
+    s = stream if stream is not None else torch.cuda.current_stream(cells.device).cuda_stream
+    N.check(N.lib().mgpu_grid_kring(ctx.handle, index_system.code, cells.data_ptr(), n, k, 1 if loop_only else 0,
+                                    out.data_ptr(), cap, off.data_ptr(), ctypes.byref(tot), s),
+            required=tot.value)
+    return out[:tot.value], off
+
+
+def grid_cellkloop(cells, k, index_system, ctx=None, stream=None):
+    """grid_cellkloop (CellKLoop.scala:63 -> IndexSystem.kLoop) on the GPU (BNG)."""
+    return grid_cellkring(cells, k, index_system, loop_only=True, ctx=ctx, stream=stream)
+
+
 def grid_tessellateexplode(polygons, resolution, keep_core_geometries=True, index_system=None):
     """Chip rows (is_core, index_id, wkb) of every polygon -> ChipTable (host columns)."""
     return tessellate(polygons, index_system or _H3, resolution, keep_core_geometries)

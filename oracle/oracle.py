@@ -136,3 +136,74 @@ def pip_join(index_system, res, x, y, chip_cell, chip_poly, chip_core, wkb_offse
     cnt2 = L.orc_pip_join(*args, _ptr(pts, _i64p), _ptr(polys, _i32p), cnt, nt)
     assert cnt2 == cnt
     return pts[:cnt], polys[:cnt]
+
+
+# ---------------------------------------------------------------- BNG kRing / kLoop
+# Pure-Python restatement (small cases only) of BNGIndexSystem.kRing / kLoop
+# (src/main/scala/com/databricks/labs/mosaic/core/index/BNGIndexSystem.scala:221-252)
+# with the helpers they call: indexDigits (:440-442), getResolution(digits) (:451-464),
+# getX / getY (:477-506), getEdgeSize (:163-170, sizeMap :64-79), isValid (:261-270).
+# pointToIndex is the C restatement above.  Scala Int division truncates toward zero.
+
+BNG_EDGE = {1: 100000, -1: 500000, 2: 10000, -2: 50000, 3: 1000, -3: 5000,
+            4: 100, -4: 500, 5: 10, -5: 50, 6: 1, -6: 5}
+
+
+def _jdiv(a, b):
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b > 0) else -q
+
+
+def _digits_int(ds):
+    return int("".join(str(d) for d in ds))  # "".toInt throws -> ValueError
+
+
+def bng_resolution_of_digits(d):
+    if len(d) < 6:
+        return -1
+    k = _jdiv(len(d) - 6, 2)
+    return -(k + 2) if d[-1] > 0 else k + 1
+
+
+def _bng_k(d):
+    k = _jdiv(len(d) - 6, 2)
+    return k
+
+
+def bng_get_x(d, e):
+    k = _bng_k(d)
+    xs = d[1:3] + (d[5:5 + k] if k > 0 else [])
+    q = d[-1]
+    return _digits_int(xs) * (2 * e if q > 0 else e) + (e if q in (3, 4) else 0)
+
+
+def bng_get_y(d, e):
+    k = _bng_k(d)
+    ys = d[3:5] + (d[5 + k:5 + 2 * k] if k > 0 else [])
+    q = d[-1]
+    return _digits_int(ys) * (2 * e if q > 0 else e) + (e if q in (2, 3) else 0)
+
+
+def bng_is_valid(i):
+    d = [int(c) for c in str(int(i))]
+    xl, yl = _digits_int(d[3:5]), _digits_int(d[1:3])
+    e = BNG_EDGE[bng_resolution_of_digits(d)]
+    x, y = bng_get_x(d, e), bng_get_y(d, e)
+    return 0 <= x <= 700000 and 0 <= y <= 1300000 and xl < 14 and yl < 8
+
+
+def bng_k_loop(i, k):
+    d = [int(c) for c in str(int(i))]
+    r = bng_resolution_of_digits(d)
+    e = BNG_EDGE[r]
+    x, y = bng_get_x(d, e), bng_get_y(d, e)
+    pts = ([(x + (c - k) * e, y - k * e) for c in range(2 * k)] + [(x + k * e, y + (c - k) * e) for c in range(2 * k)] +
+           [(x + (k - c) * e, y + k * e) for c in range(2 * k)] + [(x - k * e, y + (k - c) * e) for c in range(2 * k)])
+    out = [bng_point_to_index(float(px), float(py), r) for px, py in pts]
+    return [c for c in out if bng_is_valid(c)]
+
+
+def bng_k_ring(i, n):
+    if n == 1:
+        return [int(i)] + bng_k_loop(i, 1)
+    return [int(i)] + [c for j in range(1, n + 1) for c in bng_k_loop(i, j)]

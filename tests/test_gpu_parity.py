@@ -121,6 +121,39 @@ def test_h3_string_ids_on_gpu(gpu):
         M.BNGIndexSystem().format_many(O.bng_points_to_cells(e, nn, 3))
 
 
+@pytest.mark.parametrize("res", [1, 2, 3, 4, 5, 6, -1, -2, -3, -4, -5, -6])
+def test_bng_kring_kloop_equal_oracle(gpu, res):
+    """grid_cellkring / grid_cellkloop on the GPU == the oracle's restatement of
+    BNGIndexSystem.kRing / kLoop (BNGIndexSystem.scala:221-252), lists in order, for
+    cells all over the grid (the edges of the 700 km x 1300 km extent included, where
+    isValid drops candidates)."""
+    rng = np.random.default_rng(400 + abs(res) + (res < 0))
+    e = np.concatenate([rng.uniform(0, 700_000, 300), [0.5, 699_999.0, 350_000.0, 1.0]])
+    nn = np.concatenate([rng.uniform(0, 1_300_000, 300), [0.5, 1_299_999.0, 0.5, 1_299_999.0]])
+    cells = O.bng_points_to_cells(e, nn, res)
+    I = M.BNGIndexSystem()
+    for k in (0, 1, 2, 3):
+        for loop in (False, True):
+            refs, ok = [], []
+            for c in cells:
+                try:
+                    refs.append(O.bng_k_loop(int(c), k) if loop else O.bng_k_ring(int(c), k))
+                    ok.append(True)
+                except ValueError:  # the reference throws (NumberFormatException)
+                    ok.append(False)
+            ok = np.array(ok)
+            good = cells[ok]
+            ids, off = M.grid_cellkring(torch.from_numpy(good).to(gpu), k, I, loop_only=loop)
+            ids, off = ids.cpu().numpy(), off.cpu().numpy()
+            for i, c in enumerate(good):
+                assert list(ids[off[i]:off[i + 1]]) == refs[i], (res, k, loop, int(c))
+            if (~ok).any():
+                with pytest.raises(M.IllegalArgumentException):
+                    M.grid_cellkring(torch.from_numpy(cells[~ok]).to(gpu), k, I, loop_only=loop)
+    with pytest.raises(M.IllegalArgumentException):
+        M.grid_cellkring(torch.tensor([617733151092113407], dtype=torch.int64, device=gpu), 1, M.H3IndexSystem())
+
+
 def test_bng_nan_raises(gpu):
     with pytest.raises(M.IllegalStateException):
         gpu_cells([float("nan")], [100.0], 5, gpu, M.BNGIndexSystem())

@@ -104,3 +104,23 @@ def test_pip_end_to_end_kats(nyc_chips_r9):
         assert set(got[i]) <= set(k["objectids"]) and len(got[i]) == 1, (k, got.get(i))
         if k["cell_r9"] is not None:
             assert O.h3_point_to_index(k["lon"], k["lat"], 9) == k["cell_r9"]
+
+
+def test_bng_kring_restatement_known_answers():
+    """The oracle's kRing / kLoop restatement on hand-checked cases: a 1 km cell in the
+    middle of TQ has 8 neighbours in its first loop and 16 in the second, all valid;
+    the SV square's south-west corner cell loses the candidates west / south of the grid."""
+    c = O.bng_point_to_index(530500.0, 180500.0, 3)
+    l1, l2 = O.bng_k_loop(c, 1), O.bng_k_loop(c, 2)
+    assert len(l1) == 8 and len(l2) == 16 and len(set(l1 + l2)) == 24 and c not in l1 + l2
+    assert O.bng_k_ring(c, 2) == [c] + l1 + l2
+    # the first loop starts at the south-west corner neighbour and runs east along the bottom
+    assert l1[0] == O.bng_point_to_index(529500.0, 179500.0, 3)
+    assert l1[1] == O.bng_point_to_index(530500.0, 179500.0, 3)
+    # at the grid's south-west corner some candidates are dropped; the reference's
+    # truncating arithmetic folds others (negative eastings) onto in-grid ids, kept
+    corner = O.bng_point_to_index(0.5, 0.5, 3)
+    lc = O.bng_k_loop(corner, 1)
+    assert len(lc) < 8
+    assert {O.bng_point_to_index(1000.0, 0.0, 3), O.bng_point_to_index(1000.0, 1000.0, 3),
+            O.bng_point_to_index(0.0, 1000.0, 3)} <= set(lc)

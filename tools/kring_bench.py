@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Throughput of grid_cellkring / grid_cellkloop on the device (mgpu_grid_kring, BNG):
+2e7 res-4 cells of C4's UPRN-like London points, k = 1 and 2 (rings) and 2 (loop).
+HIP events around the call; one JSON line.  Algorithmic bytes: 8 B read per cell in
+each of the two passes + 8 B offset + 8 B per id written."""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import bench_workloads as W
+    import mosaic_amd as M
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n = 20_000_000
+    I = M.BNGIndexSystem()
+    x, y = W.london_points(n, 9, dev)
+    cells = I.points_to_index(x, y, 4)
+    del x, y
+    out = {"what": "mgpu_grid_kring, BNG res 4 cells of C4 points", "cells": n}
+    for k, loop in ((1, False), (2, False), (2, True)):
+        for _ in range(2):
+            ids, off = M.grid_cellkring(cells, k, I, loop_only=loop)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(3):
+            ids, off = M.grid_cellkring(cells, k, I, loop_only=loop)
+        b.record()
+        torch.cuda.synchronize(dev)
+        ms = a.elapsed_time(b) / 3
+        alg = 24.0 * n + 8.0 * ids.numel()
+        out["%s%d" % ("loop" if loop else "ring", k)] = {"ms": ms, "ids": int(ids.numel()),
+                                                        "cells_per_s": n / (ms * 1e-3),
+                                                        "alg_GBps": alg / (ms * 1e-3) / 1e9}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
