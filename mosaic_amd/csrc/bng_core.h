@@ -12,8 +12,10 @@
 
 #ifdef __HIPCC__
 #define MGPU_HDB __host__ __device__ __forceinline__
+#define MGPU_UNROLL _Pragma("unroll")
 #else
 #define MGPU_HDB inline
+#define MGPU_UNROLL
 #endif
 
 namespace mgpu {
@@ -100,17 +102,17 @@ template <class T>
 MGPU_HDB int format_digits(T x, int max_digits, uint64_t* lo, uint64_t* hi) {
   T p10[20];
   p10[0] = (T)1;
-#pragma unroll
+MGPU_UNROLL
   for (int k = 1; k < 20; k++) p10[k] = p10[k - 1] * (T)10;
   int n = 1;
-#pragma unroll
+MGPU_UNROLL
   for (int k = 1; k < 20; k++) n += (k < max_digits && x >= p10[k]) ? 1 : 0;
   if (n < 4) return -1;  // digits.slice(3, 5) empty: "".toInt throws
   // 10^j for a data-dependent j without indexing a local array (a register waterfall
   // on the GPU): an unrolled select
   auto pow_sel = [&](int j) {
     T r = (T)1;
-#pragma unroll
+MGPU_UNROLL
     for (int k = 0; k < 20; k++) r = (k == j) ? p10[k] : r;
     return r;
   };
@@ -139,7 +141,7 @@ MGPU_HDB int format_digits(T x, int max_digits, uint64_t* lo, uint64_t* hi) {
   *lo = first | (second << 8);
   // k <= 6: k digits of E then of N, most significant first
   uint32_t e = E, m = Nb;
-#pragma unroll
+MGPU_UNROLL
   for (int i = 5; i >= 0; i--) {
     if (i < k) {
       put_char(lo, hi, 2 + i, '0' + e % 10u);
@@ -201,15 +203,15 @@ MGPU_HDB bool cell_corner(int64_t id, int* res, int32_t* edge, int32_t* x, int32
   const double v = (double)id;
   double p10[17];
   p10[0] = 1.0;
-#pragma unroll
+MGPU_UNROLL
   for (int k = 1; k < 17; k++) p10[k] = p10[k - 1] * 10.0;
   int n = 1;
-#pragma unroll
+MGPU_UNROLL
   for (int k = 1; k < 16; k++) n += v >= p10[k] ? 1 : 0;
   if (n < 4) return false;
   auto pw = [&](int j) {
     double r = 1.0;
-#pragma unroll
+MGPU_UNROLL
     for (int k = 0; k < 17; k++) r = (k == j) ? p10[k] : r;
     return r;
   };

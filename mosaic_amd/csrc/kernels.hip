@@ -871,6 +871,10 @@ __global__ __launch_bounds__(kScanBlock) void tile_scan_kernel(const uint32_t* _
   if (threadIdx.x == 0) counters[0] = s_carry;
 }
 
+// MGPU_NT_OUT=1: nontemporal stores of the output pairs (A/B switch)
+#ifndef MGPU_NT_OUT
+#define MGPU_NT_OUT 0
+#endif
 // Ordered output: the records of kEmitTiles consecutive tiles (their output ranges are
 // contiguous) -> out[offset of the first ...] with point ids, as one flat stream over
 // the workgroup's lanes.
@@ -925,8 +929,13 @@ __global__ __launch_bounds__(kEmitBlock) void pair_emit_kernel(EmitArgs a, int64
       if (where == kNoDst) continue;  // pool exhausted: the total exceeds the capacity
       const uint64_t r = a.recs[where + (i - s_pref[k])];
       const int64_t p = (t0 + k) * kTile + (int64_t)(r >> 32);
+#if MGPU_NT_OUT
+      __builtin_nontemporal_store(a.point_id ? a.point_id[p] : a.id_base + p, &a.out_point[q]);
+      __builtin_nontemporal_store((int32_t)(uint32_t)r, &a.out_poly[q]);
+#else
       a.out_point[q] = a.point_id ? a.point_id[p] : a.id_base + p;
       a.out_poly[q] = (int32_t)(uint32_t)r;
+#endif
     }
     return;
   }
