@@ -40,6 +40,7 @@ extern "C" {
 #define MGPU_E_CAPACITY -5          /* output arrays too small; the required count is returned */
 #define MGPU_E_DEVICE -6            /* HIP runtime error */
 #define MGPU_E_INTERNAL -7          /* kernel protocol failure (look-back timeout) */
+#define MGPU_E_UNSUPPORTED -8       /* input outside what the device path builds (H3 kRing near pentagons) */
 
 #define MGPU_H3 0
 #define MGPU_BNG 1
@@ -107,7 +108,9 @@ int32_t mgpu_bng_format_device(mgpu_ctx* ctx, const int64_t* cells, int64_t n, c
  * grid_cellkloop: expressions/index/CellKRing.scala:68, CellKLoop.scala:63) --
  * BNGIndexSystem.kRing / kLoop, BNGIndexSystem.scala:221-252 (the cell, then loops
  * 1..k; a loop = pointToIndex of the 8k corners around the cell, kept when isValid),
- * in the reference's order.  BNG only (H3 returns MGPU_E_INVALID_ARG).  Cell i's list
+ * in the reference's order.  H3: H3IndexSystem.kRing / kLoop, H3IndexSystem.scala:
+ * 182-205 (H3 v3.7 kRing spiral / hexRing order); a cell whose walk reaches one of the
+ * 12 pentagon base cells returns MGPU_E_UNSUPPORTED (not built on the device).  Cell i's list
  * is out_cells[out_offsets[i] .. out_offsets[i + 1]); device pointers; *out_total =
  * entries needed (MGPU_E_CAPACITY when above `capacity`).  0 <= k <= 1024. */
 int32_t mgpu_grid_kring(mgpu_ctx* ctx, int32_t index_system, const int64_t* cells, int64_t n, int32_t k,

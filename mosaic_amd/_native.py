@@ -19,6 +19,7 @@ MGPU_E_WKB = -4
 MGPU_E_CAPACITY = -5
 MGPU_E_DEVICE = -6
 MGPU_E_INTERNAL = -7
+MGPU_E_UNSUPPORTED = -8
 
 MGPU_H3 = 0
 MGPU_BNG = 1

@@ -666,8 +666,8 @@ int32_t mgpu_grid_kring(mgpu_ctx* ctx, int32_t index_system, const int64_t* cell
                         int64_t* out_total, void* stream) {
   if (!ctx || n < 0 || (n > 0 && !cells) || !out_offsets || capacity < 0 || (capacity > 0 && !out_cells))
     return fail(MGPU_E_INVALID_ARG, "grid_kring: bad arguments");
-  if (index_system != MGPU_BNG)
-    return fail(MGPU_E_INVALID_ARG, "grid_kring on the device: BNG only (H3 kRing is not built here)");
+  if (index_system != MGPU_BNG && index_system != MGPU_H3)
+    return fail(MGPU_E_INVALID_ARG, "grid_kring: unknown index system %d", index_system);
   if (k < 0 || k > 1024) return fail(MGPU_E_INVALID_ARG, "grid_kring: k must be in [0, 1024]");
   if (int32_t st = set_device(ctx->device)) return st;
   hipStream_t s = (hipStream_t)stream;
@@ -675,16 +675,22 @@ int32_t mgpu_grid_kring(mgpu_ctx* ctx, int32_t index_system, const int64_t* cell
   auto* counters = (unsigned long long*)ctx->ws;
   auto* chunk = (int64_t*)((uint8_t*)ctx->ws + ws_layout(mgpu::join_tiles(n), 0).where);
   HIP_TRY(hipMemsetAsync(counters, 0, kWsCounters, s));
-  HIP_TRY(mgpu::launch_bng_kring(cells, n, k, loop_only, out_cells, capacity, out_offsets, chunk, counters, s));
+  HIP_TRY(mgpu::launch_cell_kring(index_system, cells, n, k, loop_only, out_cells, capacity, out_offsets, chunk,
+                                   counters, s));
   unsigned long long h[4] = {0};
   int64_t total = 0;
   HIP_TRY(hipMemcpyAsync(h, counters, sizeof h, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(&total, out_offsets + n, sizeof total, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   if (out_total) *out_total = total;
+  if (h[2] && index_system == MGPU_H3)
+    return fail(MGPU_E_INVALID_ARG, "%llu cells are not H3 cell ids", h[2]);
   if (h[2])
     return fail(MGPU_E_INVALID_ARG, "%llu cells are not BNG cells or reach ids BNGIndexSystem.isValid cannot parse "
                 "(NumberFormatException in the reference)", h[2]);
+  if (h[3])
+    return fail(MGPU_E_UNSUPPORTED, "grid_kring: %llu H3 cells reach a pentagon base cell within k = %d "
+                "(pentagon neighbourhoods are not built on the device)", h[3], k);
   if (total > capacity)
     return fail(MGPU_E_CAPACITY, "grid_kring: %lld ids, capacity %lld", (long long)total, (long long)capacity);
   return MGPU_OK;

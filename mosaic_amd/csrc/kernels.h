@@ -64,7 +64,7 @@ int64_t format_chunks(int64_t n);
 hipError_t launch_format_cells(int is, const int64_t* cells, int64_t n, char* out, int64_t out_bytes,
                                int64_t* offsets, int64_t* chunk, unsigned long long* counters, hipStream_t s);
 // BNG kRing / kLoop lists: out[offsets[i] .. offsets[i + 1]) (written when within capacity)
-hipError_t launch_bng_kring(const int64_t* cells, int64_t n, int k, int loop_only, int64_t* out, int64_t capacity,
+hipError_t launch_cell_kring(int is, const int64_t* cells, int64_t n, int k, int loop_only, int64_t* out, int64_t capacity,
                             int64_t* offsets, int64_t* chunk, unsigned long long* counters, hipStream_t s);
 hipError_t launch_st_contains(const ChipTableView& t, const int64_t* row, const double* x, const double* y, int64_t n,
                               int8_t* out, hipStream_t s);

@@ -23,6 +23,7 @@
 #include "h3_core.h"
 #include "bng_core.h"
 #include "pip_core.h"
+#include "h3_ring.h"
 #include "kernels.h"
 
 namespace mgpu {
@@ -1173,22 +1174,34 @@ __device__ __forceinline__ int64_t bng_kring(int64_t id, int k, bool loop_only, 
   return m;
 }
 
-__global__ __launch_bounds__(kFmtBlock) void kring_count_kernel(const int64_t* __restrict__ cells, int64_t n, int k,
+// one cell's list for either index system: H3 kRing / hexRing (h3_ring.h) or BNG.
+// -1: not a cell of the system (BNG: or isValid throws); -2: H3 walk reaches a
+// pentagon base cell (outside this version's scope)
+__device__ __forceinline__ int64_t cell_kring(int is, int64_t id, int k, bool loop_only, int64_t* out) {
+  if (is == MGPU_BNG) return bng_kring(id, k, loop_only, out);
+  if (!h3ring::valid_cell((uint64_t)id)) return -1;
+  const int64_t m = loop_only ? h3ring::hex_ring((uint64_t)id, k, out) : h3ring::kring((uint64_t)id, k, out);
+  return m < 0 ? -2 : m;
+}
+
+__global__ __launch_bounds__(kFmtBlock) void kring_count_kernel(int is, const int64_t* __restrict__ cells, int64_t n, int k,
                                                               int loop_only, int64_t* __restrict__ chunk_tot,
                                                               unsigned long long* __restrict__ counters) {
   __shared__ unsigned long long s_w[kFmtBlock / 64];
   const int64_t c0 = (int64_t)blockIdx.x * kFmtChunk;
   unsigned long long sum = 0;
-  bool bad = false;
+  bool bad = false, unsup = false;
   for (int sl = 0; sl < kFmtSlices; sl++) {
     const int64_t i = c0 + sl * kFmtBlock + threadIdx.x;
     if (i < n) {
-      const int64_t m = bng_kring(cells[i], k, loop_only != 0, nullptr);
+      const int64_t m = cell_kring(is, cells[i], k, loop_only != 0, nullptr);
       sum += m < 0 ? 0ull : (unsigned long long)m;
-      bad |= m < 0;
+      bad |= m == -1;
+      unsup |= m == -2;
     }
   }
   count_wave(&counters[2], bad);
+  count_wave(&counters[3], unsup);
   sum = wave_sum_u64(sum);
   if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = sum;
   __syncthreads();
@@ -1199,7 +1212,7 @@ __global__ __launch_bounds__(kFmtBlock) void kring_count_kernel(const int64_t* _
   }
 }
 
-__global__ __launch_bounds__(kFmtBlock) void kring_write_kernel(const int64_t* __restrict__ cells, int64_t n, int k,
+__global__ __launch_bounds__(kFmtBlock) void kring_write_kernel(int is, const int64_t* __restrict__ cells, int64_t n, int k,
                                                               int loop_only, const int64_t* __restrict__ chunk_off,
                                                               int64_t* __restrict__ offsets, int64_t* __restrict__ out,
                                                               int64_t capacity) {
@@ -1212,7 +1225,7 @@ __global__ __launch_bounds__(kFmtBlock) void kring_write_kernel(const int64_t* _
     const int64_t i = s0 + threadIdx.x;
     int64_t m = 0;
     if (i < n) {
-      m = bng_kring(cells[i], k, loop_only != 0, nullptr);
+      m = cell_kring(is, cells[i], k, loop_only != 0, nullptr);
       if (m < 0) m = 0;
     }
     uint32_t tot;
@@ -1221,7 +1234,7 @@ __global__ __launch_bounds__(kFmtBlock) void kring_write_kernel(const int64_t* _
       const int64_t o = carry + ex;
       offsets[i] = o;
       if (i == n - 1) offsets[n] = o + m;
-      if (m && o + m <= capacity) bng_kring(cells[i], k, loop_only != 0, out + o);
+      if (m && o + m <= capacity) cell_kring(is, cells[i], k, loop_only != 0, out + o);
     }
     carry += tot;
   }
@@ -1229,15 +1242,15 @@ __global__ __launch_bounds__(kFmtBlock) void kring_write_kernel(const int64_t* _
 
 int64_t format_chunks(int64_t n) { return (n + kFmtChunk - 1) / kFmtChunk; }
 
-hipError_t launch_bng_kring(const int64_t* cells, int64_t n, int k, int loop_only, int64_t* out, int64_t capacity,
+hipError_t launch_cell_kring(int is, const int64_t* cells, int64_t n, int k, int loop_only, int64_t* out, int64_t capacity,
                             int64_t* offsets, int64_t* chunk, unsigned long long* counters, hipStream_t s) {
   hipError_t e = hipMemsetAsync(offsets, 0, sizeof(int64_t), s);
   if (e != hipSuccess || n <= 0) return e;
   const int64_t nc = format_chunks(n);
-  hipLaunchKernelGGL(kring_count_kernel, dim3((unsigned)nc), dim3(kFmtBlock), 0, s, cells, n, k, loop_only, chunk,
+  hipLaunchKernelGGL(kring_count_kernel, dim3((unsigned)nc), dim3(kFmtBlock), 0, s, is, cells, n, k, loop_only, chunk,
                      counters);
   hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScan), 0, s, chunk, nc);
-  hipLaunchKernelGGL(kring_write_kernel, dim3((unsigned)nc), dim3(kFmtBlock), 0, s, cells, n, k, loop_only, chunk,
+  hipLaunchKernelGGL(kring_write_kernel, dim3((unsigned)nc), dim3(kFmtBlock), 0, s, is, cells, n, k, loop_only, chunk,
                      offsets, out, capacity);
   return hipGetLastError();
 }

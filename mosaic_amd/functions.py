@@ -49,7 +49,8 @@ def grid_pointascellid(points_xy, resolution, index_system=None, **kw):
 
 def grid_cellkring(cells, k, index_system, loop_only=False, ctx=None, stream=None):
     """grid_cellkring / grid_cellkloop (CellKRing.scala:68, CellKLoop.scala:63 ->
-    IndexSystem.kRing / kLoop) over a device int64 column, on the GPU (BNG).  Returns
+    IndexSystem.kRing / kLoop) over a device int64 column, on the GPU (BNG; H3 away
+    from the 12 pentagon base cells, else MosaicGpuError MGPU_E_UNSUPPORTED).  Returns
     (ids int64 tensor, offsets int64 tensor of n + 1): cell i's list is
     ids[offsets[i]:offsets[i + 1]], in the reference's order."""
     import ctypes
@@ -61,7 +62,7 @@ def grid_cellkring(cells, k, index_system, loop_only=False, ctx=None, stream=Non
     ctx = ctx or default_context(cells.device)
     n = cells.numel()
     k = int(k)
-    per = 8 * k if loop_only else 1 + 4 * k * (k + 1)
+    per = max(8 * k, 1) if loop_only else 1 + 4 * k * (k + 1)  # H3 hexRing(0) = [cell]
     cap = max(n * per, 1)
     out = torch.empty(cap, dtype=torch.int64, device=cells.device)
     off = torch.empty(n + 1, dtype=torch.int64, device=cells.device)
@@ -74,7 +75,7 @@ def grid_cellkring(cells, k, index_system, loop_only=False, ctx=None, stream=Non
 
 
 def grid_cellkloop(cells, k, index_system, ctx=None, stream=None):
-    """grid_cellkloop (CellKLoop.scala:63 -> IndexSystem.kLoop) on the GPU (BNG)."""
+    """grid_cellkloop (CellKLoop.scala:63 -> IndexSystem.kLoop) on the GPU (BNG, H3)."""
     return grid_cellkring(cells, k, index_system, loop_only=True, ctx=ctx, stream=stream)
 
 

@@ -19,6 +19,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
+#include <stdlib.h>
 #include <pthread.h>
 
 #include "oracle.h"
@@ -296,4 +297,204 @@ void orc_h3_points_to_cells(const double* lon, const double* lat, int64_t n, int
         pthread_create(&th[t], 0, h3_worker, &jobs[t]);
     }
     for (int t = 0; t < nthreads; t++) pthread_join(th[t], 0);
+}
+
+/* ------------------------------------------------------------------ kRing / hexRing
+ * H3IndexSystem.kRing / kLoop (H3IndexSystem.scala:182-205) call H3-Java 3.7.0
+ * kRing(h, k) = nonzero entries, in array order, of H3 C kRing's maxKringSize(k)
+ * array, and hexRing(h, k), which throws PentagonEncounteredException when the C call
+ * reports failure.  Restated from H3 v3.7 algos.c: h3NeighborRotations,
+ * hexRangeDistances (spiral; fails on pentagons), the _kRingInternal fallback (the
+ * output array is an open-addressing hash set keyed by h % maxIdx), hexRing.
+ * Tables: h3_neighbors.inc (tools/gen_h3_neighbors.py). */
+#include "h3_neighbors.inc"
+
+#define H3_RES(h) ((int)(((h) >> 52) & 15))
+#define H3_BASE(h) ((int)(((h) >> 45) & 127))
+#define H3_SET_BASE(h, b) ((h) = ((h) & ~(127ULL << 45)) | ((uint64_t)(b) << 45))
+
+static const int DIRECTIONS[6] = {2, 3, 1, 5, 4, 6}; /* J, JK, K, IK, I, IJ */
+#define NEXT_RING_DIRECTION 4                      /* I */
+
+static int isBaseCellPentagon(int b) { return H3T_BASE_CELL_DATA[b][4]; }
+static int isBaseCellPolarPentagon(int b) { return b == 4 || b == 117; }
+static int baseCellIsCwOffset(int b, int face) {
+    return H3T_BASE_CELL_DATA[b][5] == face || H3T_BASE_CELL_DATA[b][6] == face;
+}
+static int isResClassIII(int r) { return r % 2; }
+
+static int h3IsPentagon(uint64_t h) {
+    return isBaseCellPentagon(H3_BASE(h)) && leadingNonZeroDigit(h, H3_RES(h)) == 0;
+}
+
+uint64_t orc_h3_neighbor_rotations(uint64_t origin, int dir, int* rotations) {
+    uint64_t out = origin;
+    const int res = H3_RES(out);
+    for (int i = 0; i < *rotations; i++) dir = rotate60ccw(dir);
+    int newRotations = 0;
+    const int oldBaseCell = H3_BASE(out);
+    const int oldLeadingDigit = leadingNonZeroDigit(out, res);
+    int r = res - 1;
+    for (;;) {
+        if (r == -1) {
+            H3_SET_BASE(out, H3T_BASE_CELL_NEIGHBORS[oldBaseCell][dir]);
+            newRotations = H3T_BASE_CELL_NEIGHBOR_ROTS[oldBaseCell][dir];
+            if (H3_BASE(out) == H3T_INVALID_BASE_CELL) {
+                /* the deleted K vertex at the base-cell level: this edge borders a
+                   different neighbour */
+                H3_SET_BASE(out, H3T_BASE_CELL_NEIGHBORS[oldBaseCell][5]);
+                newRotations = H3T_BASE_CELL_NEIGHBOR_ROTS[oldBaseCell][5];
+                out = h3Rotate60ccw(out, res);
+                *rotations = *rotations + 1;
+            }
+            break;
+        } else {
+            const int oldDigit = GET_DIGIT(out, r + 1);
+            int nextDir;
+            if (isResClassIII(r + 1)) {
+                SET_DIGIT(out, r + 1, H3T_NEW_DIGIT_II[oldDigit][dir]);
+                nextDir = H3T_NEW_ADJUSTMENT_II[oldDigit][dir];
+            } else {
+                SET_DIGIT(out, r + 1, H3T_NEW_DIGIT_III[oldDigit][dir]);
+                nextDir = H3T_NEW_ADJUSTMENT_III[oldDigit][dir];
+            }
+            if (nextDir != 0) {
+                dir = nextDir;
+                r--;
+            } else {
+                break;
+            }
+        }
+    }
+    const int newBaseCell = H3_BASE(out);
+    if (isBaseCellPentagon(newBaseCell)) {
+        int alreadyAdjustedKSubsequence = 0;
+        if (leadingNonZeroDigit(out, res) == 1) {
+            if (oldBaseCell != newBaseCell) {
+                /* traversed into the deleted K subsequence of a pentagon base cell */
+                if (baseCellIsCwOffset(newBaseCell, H3T_BASE_CELL_DATA[oldBaseCell][0]))
+                    out = h3Rotate60cw(out, res);
+                else
+                    out = h3Rotate60ccw(out, res);
+                alreadyAdjustedKSubsequence = 1;
+            } else {
+                /* into the deleted K subsequence from within the same pentagon */
+                if (oldLeadingDigit == 0) {
+                    return 0; /* undefined: the K direction is deleted from here */
+                } else if (oldLeadingDigit == 3) {
+                    out = h3Rotate60ccw(out, res);
+                    *rotations = *rotations + 1;
+                } else if (oldLeadingDigit == 5) {
+                    out = h3Rotate60cw(out, res);
+                    *rotations = *rotations + 5;
+                } else {
+                    return 0;
+                }
+            }
+        }
+        for (int i = 0; i < newRotations; i++) out = h3RotatePent60ccw(out, res);
+        if (oldBaseCell != newBaseCell) {
+            if (isBaseCellPolarPentagon(newBaseCell)) {
+                if (oldBaseCell != 118 && oldBaseCell != 8 && leadingNonZeroDigit(out, res) != 3)
+                    *rotations = *rotations + 1;
+            } else if (leadingNonZeroDigit(out, res) == 5 && !alreadyAdjustedKSubsequence) {
+                *rotations = *rotations + 1;
+            }
+        }
+    } else {
+        for (int i = 0; i < newRotations; i++) out = h3Rotate60ccw(out, res);
+    }
+    *rotations = (*rotations + newRotations) % 6;
+    return out;
+}
+
+int64_t orc_h3_max_kring_size(int k) { return 3 * (int64_t)k * (k + 1) + 1; }
+
+/* hexRangeDistances: 0 = success, 1 = pentagon encountered, 2 = pentagon distortion */
+static int hexRange(uint64_t origin, int k, uint64_t* out) {
+    int64_t idx = 0;
+    int currentK = 0, direction = 0, i = 0, rotations = 0;
+    out[idx++] = origin;
+    if (h3IsPentagon(origin)) return 1;
+    while (currentK < k) {
+        if (direction == 0 && i == 0) {
+            origin = orc_h3_neighbor_rotations(origin, NEXT_RING_DIRECTION, &rotations);
+            if (origin == 0) return 2;
+            if (h3IsPentagon(origin)) return 1;
+        }
+        origin = orc_h3_neighbor_rotations(origin, DIRECTIONS[direction], &rotations);
+        if (origin == 0) return 2;
+        out[idx++] = origin;
+        i++;
+        if (i == currentK + 1) {
+            i = 0;
+            direction++;
+            if (direction == 6) {
+                direction = 0;
+                currentK++;
+            }
+        }
+        if (h3IsPentagon(origin)) return 1;
+    }
+    return 0;
+}
+
+static void kRingInternal(uint64_t origin, int k, uint64_t* out, int* distances, int64_t maxIdx, int curK) {
+    if (origin == 0) return;
+    int64_t off = (int64_t)(origin % (uint64_t)maxIdx), probes = 0;
+    while (out[off] != 0 && out[off] != origin) {
+        off = (off + 1) % maxIdx;
+        if (++probes >= maxIdx) return; /* full (H3 would spin): only reachable with bad tables */
+    }
+    if (out[off] == origin && distances[off] <= curK) return;
+    out[off] = origin;
+    distances[off] = curK;
+    if (curK >= k) return;
+    for (int i = 0; i < 6; i++) {
+        int rotations = 0;
+        kRingInternal(orc_h3_neighbor_rotations(origin, DIRECTIONS[i], &rotations), k, out, distances, maxIdx,
+                      curK + 1);
+    }
+}
+
+/* H3 C kRing into out[maxKringSize(k)] (zeros = empty slots); returns 1 when the
+   hexRange spiral failed and the hash-set fallback produced the array */
+int orc_h3_kring_raw(uint64_t origin, int k, uint64_t* out) {
+    const int64_t maxIdx = orc_h3_max_kring_size(k);
+    memset(out, 0, (size_t)maxIdx * sizeof(uint64_t));
+    if (hexRange(origin, k, out) == 0) return 0;
+    memset(out, 0, (size_t)maxIdx * sizeof(uint64_t));
+    int* distances = (int*)calloc((size_t)maxIdx, sizeof(int));
+    kRingInternal(origin, k, out, distances, maxIdx, 0);
+    free(distances);
+    return 1;
+}
+
+/* H3 C hexRing: 0 = success (6k entries, 1 for k = 0), 1 = pentagon / distortion */
+int orc_h3_hex_ring(uint64_t origin, int k, uint64_t* out) {
+    if (k == 0) {
+        out[0] = origin;
+        return 0;
+    }
+    int64_t idx = 0;
+    int rotations = 0;
+    if (h3IsPentagon(origin)) return 1;
+    for (int ring = 0; ring < k; ring++) {
+        origin = orc_h3_neighbor_rotations(origin, NEXT_RING_DIRECTION, &rotations);
+        if (origin == 0) return 1;
+        if (h3IsPentagon(origin)) return 1;
+    }
+    const uint64_t lastIndex = origin;
+    out[idx++] = origin;
+    for (int direction = 0; direction < 6; direction++) {
+        for (int pos = 0; pos < k; pos++) {
+            origin = orc_h3_neighbor_rotations(origin, DIRECTIONS[direction], &rotations);
+            if (origin == 0) return 1;
+            if (pos != k - 1 || direction != 5) {
+                out[idx++] = origin;
+                if (h3IsPentagon(origin)) return 1;
+            }
+        }
+    }
+    return lastIndex != origin;
 }

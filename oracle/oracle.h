@@ -68,3 +68,9 @@ int64_t orc_pip_join(int index_system, int res, int jdk,
 }
 #endif
 #endif
+
+/* H3 kRing / hexRing (H3IndexSystem.scala:182-205 -> H3-Java 3.7.0 -> H3 C v3.7 algos.c) */
+uint64_t orc_h3_neighbor_rotations(uint64_t origin, int dir, int* rotations);
+int64_t orc_h3_max_kring_size(int k);
+int orc_h3_kring_raw(uint64_t origin, int k, uint64_t* out);
+int orc_h3_hex_ring(uint64_t origin, int k, uint64_t* out);

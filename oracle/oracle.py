@@ -207,3 +207,78 @@ def bng_k_ring(i, n):
     if n == 1:
         return [int(i)] + bng_k_loop(i, 1)
     return [int(i)] + [c for j in range(1, n + 1) for c in bng_k_loop(i, j)]
+
+
+# ---------------------------------------------------------------- H3 kRing / kLoop
+# H3IndexSystem.kRing / kLoop (src/main/scala/com/databricks/labs/mosaic/core/index/
+# H3IndexSystem.scala:182-205) over H3-Java 3.7.0 (kRing = nonzero entries of the C
+# array in order; hexRing throws PentagonEncounteredException on failure) and the C
+# restatement of H3 v3.7 algos.c in h3_oracle.c.
+
+class PentagonEncountered(Exception):
+    pass
+
+
+def _h3_kring_lib():
+    L = lib()
+    if not getattr(L, "_kring_bound", False):
+        L.orc_h3_max_kring_size.restype = ctypes.c_int64
+        L.orc_h3_max_kring_size.argtypes = [ctypes.c_int]
+        L.orc_h3_kring_raw.restype = ctypes.c_int
+        L.orc_h3_kring_raw.argtypes = [ctypes.c_uint64, ctypes.c_int, _u64p]
+        L.orc_h3_hex_ring.restype = ctypes.c_int
+        L.orc_h3_hex_ring.argtypes = [ctypes.c_uint64, ctypes.c_int, _u64p]
+        L.orc_h3_neighbor_rotations.restype = ctypes.c_uint64
+        L.orc_h3_neighbor_rotations.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        L._kring_bound = True
+    return L
+
+
+def h3_k_ring(h, k):
+    """H3Core.kRing(h, k) as H3-Java returns it (H3IndexSystem.scala:182-184)."""
+    L = _h3_kring_lib()
+    buf = np.zeros(L.orc_h3_max_kring_size(k), dtype=np.uint64)
+    L.orc_h3_kring_raw(int(h), int(k), _ptr(buf, _u64p))
+    return [int(v) for v in buf if v != 0]
+
+
+def h3_hex_ring(h, k):
+    """H3Core.hexRing(h, k); raises PentagonEncountered where H3-Java throws."""
+    L = _h3_kring_lib()
+    buf = np.zeros(max(1, 6 * k), dtype=np.uint64)
+    if L.orc_h3_hex_ring(int(h), int(k), _ptr(buf, _u64p)) != 0:
+        raise PentagonEncountered()
+    return [int(v) for v in buf if v != 0]
+
+
+def _i32(v):
+    v &= 0xFFFFFFFF
+    return v - (1 << 32) if v & 0x80000000 else v
+
+
+def scala_hashset_key(v):
+    """Iteration rank of a java.lang.Long in a Scala 2.12 immutable.HashSet (the trie is
+    indexed by 5-bit chunks of improve(##), lowest chunk first).  ## of a boxed Long
+    is BoxesRunTime.hashFromLong: the int value if it fits, else Long.hashCode."""
+    v &= 0xFFFFFFFFFFFFFFFF
+    sv = v - (1 << 64) if v >> 63 else v
+    hc = sv if -(1 << 31) <= sv < (1 << 31) else _i32(v ^ (v >> 32))
+    h = _i32(hc + ~_i32(hc << 9))
+    h = _i32(h ^ ((h & 0xFFFFFFFF) >> 14))
+    h = _i32(h + _i32(h << 4))
+    h = _i32(h ^ ((h & 0xFFFFFFFF) >> 10))
+    u = h & 0xFFFFFFFF
+    return tuple((u >> s) & 31 for s in range(0, 32, 5))
+
+
+def h3_k_loop(h, n):
+    """H3IndexSystem.kLoop(h, n) (H3IndexSystem.scala:194-205): hexRing, or where it
+    throws, kRing(n).toSet diff kRing(n - 1).toSet, in Scala 2.12 HashSet order."""
+    if int(h) < 0:
+        raise ValueError("requirement failed")
+    try:
+        return h3_hex_ring(h, n)
+    except PentagonEncountered:
+        a = h3_k_ring(h, n)
+        b = set(h3_k_ring(h, n - 1))
+        return sorted(set(a) - b, key=scala_hashset_key)

@@ -150,8 +150,52 @@ def test_bng_kring_kloop_equal_oracle(gpu, res):
             if (~ok).any():
                 with pytest.raises(M.IllegalArgumentException):
                     M.grid_cellkring(torch.from_numpy(cells[~ok]).to(gpu), k, I, loop_only=loop)
+
+
+H3_PENTAGON_BASE_CELLS = {4, 14, 24, 38, 49, 58, 63, 72, 83, 97, 107, 117}
+
+
+@pytest.mark.parametrize("res", [1, 2, 3, 5, 7, 9, 11, 13, 15])
+def test_h3_kring_kloop_equal_oracle(gpu, res):
+    """grid_cellkring / grid_cellkloop for H3 on the GPU == the oracle's restatement of
+    H3IndexSystem.kRing / kLoop (H3IndexSystem.scala:182-205 -> H3 v3.7 kRing spiral /
+    hexRing), lists in order, on global cells whose k-neighbourhood stays among
+    hexagon base cells (the device's scope; base-cell crossings included).  Cells
+    reaching a pentagon base cell raise MosaicGpuError (MGPU_E_UNSUPPORTED); ids that
+    are no H3 cell raise IllegalArgumentException."""
+    rng = np.random.default_rng(900 + res)
+    lon = rng.uniform(-180, 180, 600)
+    lat = np.degrees(np.arcsin(rng.uniform(-1, 1, 600)))
+    cells = O.h3_points_to_cells(lon, lat, res).astype(np.int64)
+    I = M.H3IndexSystem()
+    for k in (0, 1, 2, 4):
+        inside = np.array([all(((x >> 45) & 127) not in H3_PENTAGON_BASE_CELLS for x in O.h3_k_ring(int(c), k + 1))
+                           for c in cells])
+        good = cells[inside]
+        if len(good) == 0:  # res 1, k = 4: every neighbourhood reaches a pentagon base cell
+            continue
+        for loop in (False, True):
+            refs = [O.h3_k_loop(int(c), k) if loop else O.h3_k_ring(int(c), k) for c in good]
+            ids, off = M.grid_cellkring(torch.from_numpy(good).to(gpu), k, I, loop_only=loop)
+            ids, off = ids.cpu().numpy(), off.cpu().numpy()
+            for i, c in enumerate(good):
+                assert [int(v) for v in ids[off[i]:off[i + 1]]] == refs[i], (res, k, loop, hex(int(c)))
+    pent = np.array([((int(c) >> 45) & 127) in H3_PENTAGON_BASE_CELLS for c in cells])
+    if pent.any():  # a cell of a pentagon base cell: outside the device path's scope
+        with pytest.raises(M.MosaicGpuError):
+            M.grid_cellkring(torch.from_numpy(cells[pent][:1]).to(gpu), 1, I)
     with pytest.raises(M.IllegalArgumentException):
-        M.grid_cellkring(torch.tensor([617733151092113407], dtype=torch.int64, device=gpu), 1, M.H3IndexSystem())
+        M.grid_cellkring(torch.tensor([1051200030000], dtype=torch.int64, device=gpu), 1, I)
+
+
+def test_h3_kring_doc_known_answer(gpu):
+    """docs/source/api/spatial-indexing.rst:776-784 (grid_cellkringexplode of
+    613177664827555839, k = 2): the first four ids of the reference's output."""
+    ids, off = M.grid_cellkring(torch.tensor([613177664827555839], dtype=torch.int64, device=gpu), 2,
+                                M.H3IndexSystem())
+    got = [int(v) for v in ids.cpu().numpy()]
+    assert len(got) == 19 and len(set(got)) == 19
+    assert got[:4] == [613177664827555839, 613177664825458687, 613177664831750143, 613177664884178943]
 
 
 def test_bng_nan_raises(gpu):

@@ -124,3 +124,37 @@ def test_bng_kring_restatement_known_answers():
     assert len(lc) < 8
     assert {O.bng_point_to_index(1000.0, 0.0, 3), O.bng_point_to_index(1000.0, 1000.0, 3),
             O.bng_point_to_index(0.0, 1000.0, 3)} <= set(lc)
+
+
+def test_h3_kring_restatement_doc_known_answer():
+    """The oracle's H3 kRing (H3IndexSystem.scala:182-184 -> H3 v3.7 kRing) against the
+    reference's documented output (docs/source/api/spatial-indexing.rst:776-784):
+    grid_cellkringexplode(613177664827555839, 2) starts with these four ids."""
+    r = O.h3_k_ring(613177664827555839, 2)
+    assert len(r) == 19 and len(set(r)) == 19
+    assert r[:4] == [613177664827555839, 613177664825458687, 613177664831750143, 613177664884178943]
+
+
+def test_h3_neighbor_tables_consistent_away_from_pentagons():
+    """Derived base-cell neighbour tables (tools/gen_h3_neighbors.py): at every
+    resolution, cells whose 2-neighbourhood stays among hexagon base cells have 19
+    distinct kRing(2) ids, mutual kRing(1) adjacency, and hexRing(2) == kRing(2)'s
+    outer 12 (same cyclic order, started at the cell two steps in I).  (Neighbourhoods of the 10 non-polar pentagon base cells are
+    not yet consistent in the restatement; the device path refuses them.)"""
+    pent = {4, 14, 24, 38, 49, 58, 63, 72, 83, 97, 107, 117}
+    rng = np.random.default_rng(7)
+    tested = 0
+    for res in range(1, 16):
+        lon = rng.uniform(-180, 180, 60)
+        lat = np.degrees(np.arcsin(rng.uniform(-1, 1, 60)))
+        for c in O.h3_points_to_cells(lon, lat, res):
+            c = int(c)
+            if any(((x >> 45) & 127) in pent for x in O.h3_k_ring(c, 3)):
+                continue
+            tested += 1
+            r1, r2 = O.h3_k_ring(c, 1), O.h3_k_ring(c, 2)
+            assert len(r2) == 19 and len(set(r2)) == 19 and r2[:7] == r1
+            for nb in r1[1:]:
+                assert c in O.h3_k_ring(nb, 1)
+            assert O.h3_k_loop(c, 2) == [r2[-1]] + r2[7:-1]  # hexRing starts at the I-I cell
+    assert tested > 600
