@@ -114,6 +114,27 @@ class IndexSystem:
         N.check(st, "cell id has no string form")
         return out[:tot.value], off
 
+    def k_ring(self, index, n):
+        """IndexSystem.kRing(index, n) (H3IndexSystem.scala:182-184, BNGIndexSystem.scala:
+        221-226): the list of ids, in the reference's order, on the device."""
+        import torch
+        from .context import default_context
+        from .functions import grid_cellkring
+        ctx = default_context()
+        ids, _ = grid_cellkring(torch.tensor([int(index)], dtype=torch.int64, device=ctx.device), n, self, ctx=ctx)
+        return [int(v) for v in ids.cpu().tolist()]
+
+    def k_loop(self, index, n):
+        """IndexSystem.kLoop(index, n) (H3IndexSystem.scala:194-205, BNGIndexSystem.scala:
+        239-252) on the device."""
+        import torch
+        from .context import default_context
+        from .functions import grid_cellkring
+        ctx = default_context()
+        ids, _ = grid_cellkring(torch.tensor([int(index)], dtype=torch.int64, device=ctx.device), n, self,
+                                loop_only=True, ctx=ctx)
+        return [int(v) for v in ids.cpu().tolist()]
+
 
 def _check_points(x, y):
     if x.dtype != y.dtype or str(x.dtype) != "torch.float64":

@@ -188,6 +188,17 @@ def test_h3_kring_kloop_equal_oracle(gpu, res):
         M.grid_cellkring(torch.tensor([1051200030000], dtype=torch.int64, device=gpu), 1, I)
 
 
+def test_index_system_scalar_k_ring_k_loop(gpu):
+    """IndexSystem.kRing / kLoop (scalar surface of the mirror) == the oracle, H3 and BNG."""
+    import numpy as np
+    h = 613177664827555839
+    assert M.H3IndexSystem().k_ring(h, 2) == O.h3_k_ring(h, 2)
+    assert M.H3IndexSystem().k_loop(h, 3) == O.h3_k_loop(h, 3)
+    b = int(O.bng_points_to_cells(np.array([530_123.0]), np.array([180_456.0]), 3)[0])
+    assert M.BNGIndexSystem().k_ring(b, 2) == O.bng_k_ring(b, 2)
+    assert M.BNGIndexSystem().k_loop(b, 2) == O.bng_k_loop(b, 2)
+
+
 def test_h3_kring_doc_known_answer(gpu):
     """docs/source/api/spatial-indexing.rst:776-784 (grid_cellkringexplode of
     613177664827555839, k = 2): the first four ids of the reference's output."""
