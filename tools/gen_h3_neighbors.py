@@ -99,8 +99,8 @@ def frame_rotation(b, d, n, home, cen):
     in n's home-face hex2d frame pointing back at b from angle THETA[d] + 180 + 60 rot.
     Exact for hexagon targets (it reproduces all 659 in-face faceIjkBaseCells entries);
     a pentagon target's frame is cut (its deleted K sector), so the fraction is
-    rounded up for the ten non-polar pentagons and down for the two polar ones -- the
-    rule that reproduces all 25 in-face hexagon -> pentagon entries."""
+    rounded down -- the rule that reproduces all 25 in-face hexagon -> pentagon
+    entries."""
     hf, hijk = home[n]
     _, blat, blon = cen[b]
     x, y = T.geo_to_hex2d_res0(blat, blon, hf)
@@ -109,10 +109,26 @@ def frame_rotation(b, d, n, home, cen):
     q = (phi - THETA[d] - 180.0) / 60.0
     q -= 6.0 * math.floor(q / 6.0)
     if n in T.PENTAGONS:
-        r = math.floor(q + 1e-9) if T.PENT_CW_OFFSET[n] == (-1, -1) else math.ceil(q - 1e-9)
+        r = math.floor(q + 1e-9)
         return int(r) % 6, 0.0
     r = round(q)
     return int(r) % 6, abs(q - r)
+
+
+def shared_face_rotation(b, n, bc_of, rot):
+    """Rotation from hexagon b's frame into pentagon n's frame read off a face g that
+    holds both: faceIjkBaseCells gives g -> b and g -> n, so b -> n = rot(g->n) -
+    rot(g->b).  A pentagon's frame is cut, so the measurement must come from the
+    faceIjkBaseCells convention, not from geometry; every shared face must agree."""
+    vals = set()
+    for (g, i, j, k), c in bc_of.items():
+        if c != n:
+            continue
+        for (g2, i2, j2, k2), c2 in bc_of.items():
+            if g2 == g and c2 == b:
+                vals.add((rot[(g, i, j, k)] - rot[(g2, i2, j2, k2)]) % 6)
+    assert len(vals) == 1, ("hexagon -> pentagon rotation ambiguous", b, n, vals)
+    return vals.pop()
 
 
 def pentagon_labels(b, home, bc_of, cen):
@@ -158,8 +174,9 @@ def neighbors(home, bc_of, rot, cen):
                 n = bc_of[key]
                 if lab is not None:
                     assert lab[d] == n, ("pentagon label disagrees with the in-face step", b, d)
-                r, res = frame_rotation(b, d, n, home, cen)
-                assert r == rot[key], ("frame rotation disagrees with faceIjkBaseCells", b, d, n, r, rot[key])
+                if n not in T.PENTAGONS:
+                    r, res = frame_rotation(b, d, n, home, cen)
+                    assert r == rot[key], ("frame rotation disagrees with faceIjkBaseCells", b, d, n, r, rot[key])
                 nb[b][d], nr[b][d] = n, rot[key]
                 continue
             if lab is not None:
@@ -171,8 +188,11 @@ def neighbors(home, bc_of, rot, cen):
                 dist = sorted((float(np.linalg.norm(cen[c][0] - v)), c) for c in range(122))
                 assert dist[0][0] < 0.5 * dist[1][0], ("ambiguous overage neighbour", b, d)
                 n = dist[0][1]
-            r, res = frame_rotation(b, d, n, home, cen)
-            worst = max(worst, res)
+            if n in T.PENTAGONS and lab is None:
+                r = shared_face_rotation(b, n, bc_of, rot)
+            else:
+                r, res = frame_rotation(b, d, n, home, cen)
+                worst = max(worst, res)
             nb[b][d], nr[b][d] = n, r
     return nb, nr, worst
 

@@ -401,6 +401,16 @@ def pentagon_rotations(b, home_face, cen, cands):
             for s in range(5, step, -1):
                 r = (r + edge_rot(cyc[(s - 1) % 5], cyc[s % 5])) % 6
         out[f] = (-r) % 6
+    if not polar:
+        # The clockwise unfolding gives the non-polar pentagon's five faces 0, 0/1, 3
+        # and 4 (two published per pentagon at most); H3's frame takes 3 for the face the
+        # unfolding puts at 4.  Found by tools/h3_pentagon_search (walk-vs-geometry
+        # consistency): with 4 every non-polar pentagon has 17-19 res-2 neighbour walks
+        # that disagree with the cells' sampled geometry, with 3 none does (170 walks
+        # each), and every published entry is unchanged.
+        for f in out:
+            if out[f] == 4:
+                out[f] = 3
     return out
 
 
