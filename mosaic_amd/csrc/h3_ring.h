@@ -11,7 +11,7 @@
 // C-ABI call fails loudly (MGPU_E_UNSUPPORTED); the reference's pentagon handling
 // (the K-subsequence rotations, the _kRingInternal hash-set fallback, Mosaic's
 // kLoop set-difference fallback) is restated in the oracle only
-// (oracle/h3_oracle.c), whose non-polar pentagon crossings are not yet consistent.
+// (oracle/h3_oracle.c); walks next to the south polar pentagon are not yet consistent there.
 #pragma once
 #include <stdint.h>
 
