@@ -136,7 +136,9 @@ int32_t mgpu_chips_info(const mgpu_chips* chips, int64_t* n_chips, int64_t* n_ce
 
 /* st_contains(chip.wkb, point) for explicit (chip row, point) pairs
  * (ST_Contains.scala:21-44 -> MosaicGeometryJTS.contains, MosaicGeometryJTS.scala:197).
- * out[i] = 1 / 0, or -1 when the chip's geometry is NULL.  Device pointers. */
+ * out[i] = 1 / 0, or -1 when the chip's geometry is NULL.  Device pointers.
+ * Synchronises `stream`: a chip row outside [0, n_chips) fails the call with
+ * MGPU_E_INVALID_ARG (its out[i] is -2). */
 int32_t mgpu_st_contains(mgpu_ctx* ctx, const mgpu_chips* chips, const int64_t* chip_row,
                          const double* x, const double* y, int64_t n, int8_t* out, void* stream);
 
@@ -151,6 +153,15 @@ int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t index_syst
                       const double* x, const double* y, const int64_t* point_id, int64_t point_id_base,
                       int64_t n, int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id,
                       int32_t* out_polygon_id, void* stream, mgpu_stats* stats);
+
+/* After mgpu_pip_join returned MGPU_E_CAPACITY (*out_n_pairs = the count): write all
+ * pairs of that join into larger output arrays without redoing it -- the join's pair
+ * records stay in the context until its next call.  (Only when the workspace's overflow
+ * pool had to drop records -- tiles with more pairs than points beyond the capacity --
+ * is the join redone, from the same, unchanged, input arrays.)  Synchronises `stream`;
+ * MGPU_E_INVALID_ARG if no join was kept, MGPU_E_CAPACITY if capacity is still short. */
+int32_t mgpu_pip_join_fetch(mgpu_ctx* ctx, int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id,
+                            int32_t* out_polygon_id, void* stream);
 
 /* Asynchronous form: the pair count is left in device memory (*d_n_pairs, one
  * int64) and nothing synchronises -- graph-capturable once mgpu_ctx_reserve has
@@ -203,6 +214,17 @@ int32_t mgpu_test_chip_contains_host(int32_t index_system, int64_t n_chips, cons
                                      const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
                                      const uint8_t* wkb, int64_t n, const int64_t* chip_row, const double* x,
                                      const double* y, int8_t* out_join_path, int8_t* out_point_locator);
+
+/* TEST ONLY -- not an interface of the reference.  Builds the chip table on the host and
+ * looks n points up in its pixel index (the pre-resolved answers of the streaming join,
+ * chip_table.h): out_kind 0 = no match, 1 = pure pixel (matches = sorted chips
+ * out_first + j for the bits j of out_mask), 2 = full path, 3 = invalid coordinate,
+ * 4 = no pixel index for this table/resolution; out_chip_poly[n_chips] = polygon id of
+ * each sorted chip.  Host pointers; no GPU. */
+int32_t mgpu_test_raster_host(int32_t index_system, int32_t res, int64_t n_chips, const int64_t* cell,
+                              const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
+                              const uint8_t* wkb, int64_t n, const double* x, const double* y, int8_t* out_kind,
+                              uint32_t* out_first, uint32_t* out_mask, int32_t* out_chip_poly);
 
 #ifdef __cplusplus
 }

@@ -32,7 +32,7 @@ EXPORTS = (
     "mgpu_chips_upload", "mgpu_chips_destroy", "mgpu_chips_device_blob", "mgpu_chips_from_device_blob",
     "mgpu_chips_info", "mgpu_st_contains", "mgpu_pip_join", "mgpu_pip_join_async", "mgpu_ctx_reserve",
     "mgpu_last_near_ties",    "mgpu_pip_join_host", "mgpu_tessellate", "mgpu_tess_result_sizes", "mgpu_tess_result_copy",
-    "mgpu_tess_destroy", "mgpu_test_chip_contains_host",
+    "mgpu_tess_destroy", "mgpu_test_chip_contains_host", "mgpu_test_raster_host", "mgpu_pip_join_fetch",
 )
 
 
@@ -113,6 +113,8 @@ def lib():
         "mgpu_tess_result_copy": (I32, [P, P, P, P, P, P]),
         "mgpu_tess_destroy": (I32, [P]),
         "mgpu_test_chip_contains_host": (I32, [I32, I64, P, P, P, P, P, I64, P, P, P, P, P]),
+        "mgpu_pip_join_fetch": (I32, [P, I64, ctypes.POINTER(I64), P, P, P]),
+        "mgpu_test_raster_host": (I32, [I32, I32, I64, P, P, P, P, P, I64, P, P, P, P, P, P]),
     }
     for name, (rt, args) in sig.items():
         f = getattr(L, name)

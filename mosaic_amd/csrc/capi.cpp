@@ -26,6 +26,7 @@
 #include "kernels.h"
 #include "parallel.h"
 #include "pip_core.h"
+#include "raster.h"
 #include "wkb.h"
 
 namespace {
@@ -54,11 +55,12 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // offsets, so a byte copy of the blob on another GPU (RCCL broadcast) is a
 // complete chip table there.
 constexpr uint64_t kBlobMagic = 0x4d4f534149434850ULL;  // "MOSAICHP"
-constexpr int kBlobArrays = 18;
-constexpr uint32_t kBlobVersion = 4;
+constexpr int kBlobArrays = 20;
+constexpr uint32_t kBlobVersion = 5;
 struct BlobHeader {
   uint64_t magic;
-  uint32_t version, hash_mask, max_probe, n_chips, n_cells, pad;
+  uint32_t version, hash_mask, max_probe, n_chips, n_cells;
+  int32_t index_system;  // MGPU_H3 / MGPU_BNG: the system the chip cells belong to
   int64_t n_vertices;
   uint64_t off[kBlobArrays];
   int32_t probe_mode, res;
@@ -68,6 +70,10 @@ struct BlobHeader {
   mgpu::DenseFace dense[20];
   uint32_t bng_edge, pad3;
   double bng_inv_edge;
+  int32_t raster_mode;
+  uint32_t raster_nx, raster_ny, raster_pix;
+  int32_t raster_px0, raster_py0;
+  double raster_x0, raster_y0, raster_inv_dx, raster_inv_dy;
 };
 constexpr size_t kBlobHeaderBytes = 1024;
 static_assert(sizeof(BlobHeader) <= kBlobHeaderBytes, "header too large");
@@ -104,6 +110,18 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.k_res = h.k_res;
   v.bng_edge = h.bng_edge;
   v.bng_inv_edge = h.bng_inv_edge;
+  v.raster_mode = h.raster_mode;
+  v.raster_nx = h.raster_nx;
+  v.raster_ny = h.raster_ny;
+  v.raster_pix = h.raster_pix;
+  v.raster_px0 = h.raster_px0;
+  v.raster_py0 = h.raster_py0;
+  v.raster_x0 = h.raster_x0;
+  v.raster_y0 = h.raster_y0;
+  v.raster_inv_dx = h.raster_inv_dx;
+  v.raster_inv_dy = h.raster_inv_dy;
+  v.raster = (const uint16_t*)(base + h.off[18]);
+  v.raster_cls = (const uint64_t*)(base + h.off[19]);
   return v;
 }
 
@@ -454,6 +472,300 @@ void build_grid(const mgpu::ChipTableView& hv, uint32_t c, const mgpu::wkb::Flat
   }
 }
 
+// ------------------------------------------------------------------ pixel index
+// (chip_table.h "Pixel index").  A pixel gets a class only when its answer is the same
+// for every point in it, by a certificate with margins that dwarf rounding:
+//  1. one chip cell: H3 -- the four corners of the (widened) pixel are nearest to the
+//     same icosahedron face with a squared-chord gap above delta_f, and take the same
+//     decision path of _hex2dToCoordIJK (same (m1, m2), same branch outcomes, same
+//     quadrant signs) with every compared quantity at least delta_h from its
+//     threshold.  Each path's region is an intersection of half-planes of the face's
+//     gnomonic plane (the face choice likewise: v.(c_g - c_f) >= 0 per face g), hence
+//     convex; the pixel's image there lies within the sagitta of its parallels of the
+//     corners' hull (meridians are straight lines), and delta_h, delta_f are taken 8x
+//     above that bound -- so every point of the pixel takes the corners' cell, in exact
+//     arithmetic and in the reference's (its error is ~1e-12 of a hex unit).  BNG --
+//     pixels tile the cells exactly (the pixel edge divides the cell edge, whole metres).
+//  2. each chip of that cell: core -> match; else no chip edge meets the widened pixel
+//     (seg_hits_box, the classification grid's test), so all its points lie in one
+//     component of the plane minus the chip boundary, where JTS's PointLocator returns
+//     the verdict of the pixel centre (interior -> match).
+// Anything else is kPixMixed and takes the full path in the kernel.
+struct Raster {
+  int32_t mode = mgpu::kRasterNone;
+  uint32_t nx = 0, ny = 0, pix = 0;
+  int32_t px0 = 0, py0 = 0;
+  double x0 = 0, y0 = 0, inv_dx = 0, inv_dy = 0;
+  std::vector<uint16_t> cells;
+  std::vector<uint64_t> cls;
+  int64_t n_pure = 0;
+};
+
+constexpr int64_t kPixAnswerMixed = -1;
+
+// the matches of every point in the widened pixel [x0, x1] x [y0, y1] among the chips
+// of grid entry `e` (first | count << 32 | core_mask << 48): a mask, or kPixAnswerMixed
+int64_t pixel_answer(const mgpu::ChipTableView& hv, uint64_t e, double x0, double y0, double x1, double y1) {
+  using namespace mgpu;
+  const uint32_t first = (uint32_t)e, count = (uint32_t)(e >> 32) & 0xFFFF;
+  if (count == 0) return 0;
+  if (count > 32) return kPixAnswerMixed;
+  uint64_t mask = 0;
+  for (uint32_t j = 0; j < count; j++) {
+    const uint32_t c = first + j;
+    const uint8_t fl = hv.chip_flags[c];
+    if (fl & kChipCore) {
+      mask |= 1ull << j;
+      continue;
+    }
+    if (fl & (kChipEmpty | kChipNoGeom)) continue;
+    const double* env = hv.chip_env + 4 * c;
+    if (x1 < env[0] || x0 > env[2] || y1 < env[1] || y0 > env[3]) continue;  // outside the envelope
+    for (uint32_t p = hv.chip_part[c]; p < hv.chip_part[c + 1]; p++)
+      for (uint32_t r = hv.part_ring[p]; r < hv.part_ring[p + 1]; r++)
+        for (uint32_t i = hv.ring_vtx[r] + 1; i < hv.ring_vtx[r + 1]; i++)
+          if (seg_hits_box(hv.vtx[2 * i - 2], hv.vtx[2 * i - 1], hv.vtx[2 * i], hv.vtx[2 * i + 1], x0, y0, x1, y1))
+            return kPixAnswerMixed;
+    const int loc = pip::chip_locate(hv, c, 0.5 * (x0 + x1), 0.5 * (y0 + y1));
+    if (loc == pip::kBoundary) return kPixAnswerMixed;
+    if (loc == pip::kInterior) mask |= 1ull << j;
+  }
+  return (int64_t)mask;
+}
+
+// One corner of an H3 pixel: nearest face (and the squared-chord gap to the next),
+// hex2d position on that face.
+struct Corner {
+  int face = -1;
+  double gap = 0, x = 0, y = 0;
+  bool ok = false;
+};
+
+Corner h3_corner(double lond, double latd, int res, double k_res) {
+  namespace H = mgpu::h3;
+  Corner o;
+  const double lat = H::to_radians_fast(latd), lon = H::to_radians_fast(lond);
+  double slat, clat, slon, clon;
+  H::sincos_fast(lat, &slat, &clat);
+  H::sincos_fast(lon, &slon, &clon);
+  const double vx = clon * clat, vy = slon * clat, vz = slat;
+  double best = 5.0, second = 5.0;
+  for (int f = 0; f < 20; f++) {
+    const double dx = H3T_FACE_CENTER_POINT[f][0] - vx, dy = H3T_FACE_CENTER_POINT[f][1] - vy,
+                 dz = H3T_FACE_CENTER_POINT[f][2] - vz;
+    const double s = dx * dx + dy * dy + dz * dz;
+    if (s < best) {
+      second = best;
+      best = s;
+      o.face = f;
+    } else if (s < second) {
+      second = s;
+    }
+  }
+  o.gap = second - best;
+  const double(*F)[3] = H3T_FACE_FRAME[o.face][res & 1];
+  const double dc = vx * F[2][0] + vy * F[2][1] + vz * F[2][2];
+  if (!(dc > 0.5)) return o;
+  o.x = k_res * (vx * F[0][0] + vy * F[0][1] + vz * F[0][2]) / dc;
+  o.y = k_res * (vx * F[1][0] + vy * F[1][1] + vz * F[1][2]) / dc;
+  o.ok = std::fabs(o.x) < 1e8 && std::fabs(o.y) < 1e8;
+  return o;
+}
+
+// Does the hexagon of axial lattice position (a, b) -- H3's _hex2dToCoordIJK rounds to
+// the nearest lattice centre (checked by tests/cpp), so a cell is the hexagon of
+// apothem 1/2 around (a - b/2, b sin60) -- come within `d` of the convex quad q?
+// (separating axes: the hexagon's three edge normals and the quad's four)
+bool hex_meets_quad(int64_t a, int64_t b, const double q[4][2], double d) {
+  const double cx = (double)a - 0.5 * (double)b, cy = (double)b * mgpu::h3::kSin60;
+  const double R = 0.57735026918962576451;  // circumradius
+  double hv[6][2];
+  for (int k = 0; k < 6; k++) {
+    const double t = (30.0 + 60.0 * k) * kPi / 180.0;
+    hv[k][0] = cx + R * std::cos(t);
+    hv[k][1] = cy + R * std::sin(t);
+  }
+  auto separated = [&](double nx, double ny) {
+    double h0 = 1e300, h1 = -1e300, q0 = 1e300, q1 = -1e300;
+    for (int k = 0; k < 6; k++) {
+      const double v = hv[k][0] * nx + hv[k][1] * ny;
+      h0 = std::min(h0, v), h1 = std::max(h1, v);
+    }
+    for (int k = 0; k < 4; k++) {
+      const double v = q[k][0] * nx + q[k][1] * ny;
+      q0 = std::min(q0, v), q1 = std::max(q1, v);
+    }
+    return h1 + d < q0 || q1 + d < h0;
+  };
+  for (int k = 0; k < 3; k++) {
+    const double t = 60.0 * k * kPi / 180.0;
+    if (separated(std::cos(t), std::sin(t))) return false;
+  }
+  for (int k = 0; k < 4; k++) {
+    const double ex = q[(k + 1) % 4][0] - q[k][0], ey = q[(k + 1) % 4][1] - q[k][1];
+    const double l = std::hypot(ex, ey);
+    if (l > 0 && separated(-ey / l, ex / l)) return false;
+  }
+  return true;
+}
+
+// pixel budget and size: MGPU_RASTER=0 disables the index; MGPU_RASTER_F = pixel edge
+// as a fraction of the cell edge (default 1/4)
+double raster_fraction() {
+  const char* s = getenv("MGPU_RASTER_F");
+  const double f = s ? atof(s) : 0.25;
+  return f > 0.01 && f <= 1.0 ? f : 0.25;
+}
+bool raster_enabled() {
+  const char* s = getenv("MGPU_RASTER");
+  return !(s && atoi(s) == 0);
+}
+constexpr int64_t kRasterMaxPixels = 1LL << 24;
+
+// classes: per-pixel answers (first | mask << 32, 0 = empty, ~0 = mixed) -> u16 classes
+bool raster_classes(const std::vector<uint64_t>& ans, Raster& R) {
+  R.cells.assign(ans.size(), mgpu::kPixMixed);
+  R.cls.assign(1, 0);  // class 0 = empty
+  std::vector<std::pair<uint64_t, uint32_t>> keyed;
+  keyed.reserve(ans.size());
+  for (size_t i = 0; i < ans.size(); i++) {
+    if (ans[i] == ~0ULL) continue;
+    if ((ans[i] >> 32) == 0) {
+      R.cells[i] = mgpu::kPixEmpty;
+      R.n_pure++;
+      continue;
+    }
+    keyed.push_back({ans[i], (uint32_t)i});
+  }
+  std::sort(keyed.begin(), keyed.end());
+  for (size_t k = 0; k < keyed.size(); k++) {
+    if (k == 0 || keyed[k].first != keyed[k - 1].first) {
+      if (R.cls.size() >= mgpu::kPixMixed) break;  // out of classes: the rest stay mixed
+      R.cls.push_back(keyed[k].first);
+    }
+    R.cells[keyed[k].second] = (uint16_t)(R.cls.size() - 1);
+    R.n_pure++;
+  }
+  return true;
+}
+
+bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const double bbox[4],
+                     const mgpu::DenseFace* dense, const std::vector<uint64_t>& grid, Raster& R) {
+  if (!raster_enabled() || res < 5 || !(bbox[2] - bbox[0] < 360.0) || grid.empty()) return false;
+  const double W = bbox[2] - bbox[0], Hh = bbox[3] - bbox[1];
+  if (!(W > 0) || !(Hh > 0)) return false;
+  const double edge_deg = 1107.712591 / std::pow(mgpu::h3::kSqrt7, res) / 111.195;  // mean cell edge
+  const double latc = std::max(std::fabs(bbox[1]), std::fabs(bbox[3]));
+  if (latc > 80.0) return false;
+  double dyp = raster_fraction() * edge_deg, dxp = dyp / std::cos(latc * kPi / 180.0);
+  double nxd = std::ceil(W / dxp), nyd = std::ceil(Hh / dyp);
+  if (nxd * nyd > (double)kRasterMaxPixels) {
+    const double s = std::sqrt(nxd * nyd / (double)kRasterMaxPixels) * 1.01;
+    dxp *= s, dyp *= s;
+    nxd = std::ceil(W / dxp), nyd = std::ceil(Hh / dyp);
+  }
+  if (dyp > 0.6 * edge_deg) return false;  // pixels as large as cells are rarely pure
+  R.mode = mgpu::kRasterLonLat;
+  R.nx = (uint32_t)nxd, R.ny = (uint32_t)nyd;
+  R.x0 = bbox[0], R.y0 = bbox[1];
+  R.inv_dx = 1.0 / dxp, R.inv_dy = 1.0 / dyp;
+  const double sx = 1.0 / R.inv_dx, sy = 1.0 / R.inv_dy;  // the pixel size the kernel's index implies
+  const double mag = std::max(std::max(std::fabs(bbox[0]), std::fabs(bbox[2])), std::max(std::fabs(bbox[1]), std::fabs(bbox[3])));
+  const double ulp = std::nextafter(mag, INFINITY) - mag;
+  const double mux = 1e-6 * sx + 64 * ulp, muy = 1e-6 * sy + 64 * ulp;
+  std::vector<uint64_t> ans((size_t)R.nx * R.ny, ~0ULL);
+  mgpu::parallel_for((int64_t)R.ny, 4, [&](int64_t yb, int64_t ye, int) {
+    std::vector<int32_t> polys, ref;
+    for (int64_t iy = yb; iy < ye; iy++)
+      for (uint32_t ix = 0; ix < R.nx; ix++) {
+        double xa = R.x0 + ix * sx - mux, xb = R.x0 + (ix + 1) * sx + mux;
+        double ya = R.y0 + iy * sy - muy, yb2 = R.y0 + (iy + 1) * sy + muy;
+        if (ix == R.nx - 1) xb = std::max(xb, bbox[2] + mux);  // the last pixel takes the clamped points
+        if (iy == (int64_t)R.ny - 1) yb2 = std::max(yb2, bbox[3] + muy);
+        // quad corners in order around the pixel
+        const Corner c[4] = {h3_corner(xa, ya, res, k_res), h3_corner(xb, ya, res, k_res), h3_corner(xb, yb2, res, k_res),
+                             h3_corner(xa, yb2, res, k_res)};
+        double q[4][2], L = 0;
+        for (int p = 0; p < 4; p++) q[p][0] = c[p].x, q[p][1] = c[p].y;
+        for (int p = 0; p < 4; p++)
+          for (int r = p + 1; r < 4; r++) L = std::max(L, std::hypot(q[p][0] - q[r][0], q[p][1] - q[r][1]));
+        const double ang = std::hypot(xb - xa, yb2 - ya) * kPi / 180.0;  // angular diagonal bound (rad)
+        const double d_face = 1e-12 + 8.0 * ang * ang;
+        const double d_hex = 1e-9 * (1.0 + std::fabs(q[0][0]) + std::fabs(q[0][1])) + 8.0 * L * L / k_res;
+        bool ok = L < 0.5;
+        for (int p = 0; p < 4 && ok; p++) ok = c[p].ok && c[p].face == c[0].face && c[p].gap > d_face;
+        if (!ok) continue;
+        double mg;
+        const mgpu::h3::IJK h0 = mgpu::h3::hex2d_to_ijk_fast(q[0][0], q[0][1], &mg);
+        const int64_t a0 = h0.i - h0.k, b0 = h0.j - h0.k;
+        // every cell a point of the pixel can take is h0 or a neighbour (L < 1/2) whose
+        // hexagon meets the quad; all must give the same polygon list
+        static const int da[7] = {0, 1, -1, 0, 0, 1, -1}, db[7] = {0, 0, 0, 1, -1, 1, -1};
+        const mgpu::DenseFace& D = dense[c[0].face];
+        bool first = true, pure = true;
+        uint64_t cls = 0;
+        for (int k = 0; k < 7 && pure; k++) {
+          const int64_t a = a0 + da[k], b = b0 + db[k];
+          if (!hex_meets_quad(a, b, q, d_hex)) continue;
+          const uint64_t ua = (uint64_t)(a - D.a0), ub = (uint64_t)(b - D.b0);
+          const uint64_t e = (ua < D.w && ub < D.h) ? grid[D.base + ub * D.w + ua] : 0;
+          const int64_t m = pixel_answer(hv, e, xa, ya, xb, yb2);
+          if (m == kPixAnswerMixed) {
+            pure = false;
+            break;
+          }
+          polys.clear();
+          for (uint64_t bits = (uint64_t)m; bits; bits &= bits - 1) polys.push_back(hv.chip_poly[(uint32_t)e + __builtin_ctzll(bits)]);
+          if (first) {
+            ref = polys;
+            cls = m ? ((uint32_t)e | ((uint64_t)m << 32)) : 0;
+            first = false;
+          } else if (polys != ref) {
+            pure = false;
+          }
+        }
+        if (pure && !first) ans[(size_t)iy * R.nx + ix] = cls;
+      }
+  });
+  return raster_classes(ans, R);
+}
+
+bool build_raster_bng(const mgpu::ChipTableView& hv, const mgpu::DenseFace& D, uint32_t edge,
+                      const std::vector<uint64_t>& grid, Raster& R) {
+  if (!raster_enabled() || edge == 0 || grid.empty()) return false;
+  // pixels per cell edge: the largest k <= 1 / fraction dividing the edge, within budget
+  int kpc = (int)std::floor(1.0 / raster_fraction() + 1e-9);
+  for (; kpc > 1; kpc--)
+    if (edge % kpc == 0 && (double)D.w * kpc * D.h * kpc <= (double)kRasterMaxPixels) break;
+  if (kpc < 2) return false;
+  R.mode = mgpu::kRasterBng;
+  R.pix = edge / kpc;
+  R.nx = D.w * kpc, R.ny = D.h * kpc;
+  R.px0 = D.a0 * kpc, R.py0 = D.b0 * kpc;
+  R.inv_dx = R.inv_dy = 1.0 / R.pix;
+  const double mu = 1e-6 * R.pix + 64 * (std::nextafter(1e7, INFINITY) - 1e7);
+  // BNG pixels hold the match mask itself (the kernel has the cell's grid entry anyway)
+  R.cells.assign((size_t)R.nx * R.ny, mgpu::kPixMixed);
+  R.cls.assign(1, 0);
+  std::atomic<int64_t> pure{0};
+  mgpu::parallel_for((int64_t)R.ny, 8, [&](int64_t yb, int64_t ye, int) {
+    int64_t np = 0;
+    for (int64_t iy = yb; iy < ye; iy++)
+      for (uint32_t ix = 0; ix < R.nx; ix++) {
+        const uint64_t e = grid[D.base + (size_t)(iy / kpc) * D.w + ix / kpc];
+        const double xa = (double)(R.px0 + (int64_t)ix) * R.pix - mu, xb = (double)(R.px0 + (int64_t)ix + 1) * R.pix + mu;
+        const double ya = (double)(R.py0 + iy) * R.pix - mu, yb2 = (double)(R.py0 + iy + 1) * R.pix + mu;
+        const int64_t m = pixel_answer(hv, e, xa, ya, xb, yb2);
+        if (m == kPixAnswerMixed || m >= (int64_t)mgpu::kPixMixed) continue;
+        R.cells[(size_t)iy * R.nx + ix] = (uint16_t)m;
+        np++;
+      }
+    pure += np;
+  });
+  R.n_pure = pure;
+  return true;
+}
+
 }  // namespace
 
 namespace mgpu {
@@ -474,10 +786,23 @@ struct mgpu_ctx {
   void* ws = nullptr;
   size_t ws_bytes = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  // the last mgpu_pip_join on this context, whose pair records stay in the workspace
+  // until the next call (mgpu_pip_join_fetch)
+  struct {
+    bool valid = false, pool_ok = false;
+    const mgpu_chips* chips = nullptr;
+    int32_t is = 0, res = 0;
+    const double *x = nullptr, *y = nullptr;
+    const int64_t* point_id = nullptr;
+    int64_t id_base = 0, n = 0, total = 0;
+    mgpu::EmitArgs emit{};
+    int64_t n_tiles = 0;
+  } last;
 };
 
 struct mgpu_chips {
   int device = 0;
+  int32_t index_system = MGPU_H3;
   void* blob = nullptr;
   size_t bytes = 0;
   mgpu::ChipTableView view{};
@@ -522,6 +847,7 @@ WsLayout ws_layout(int64_t n_tiles, int64_t pool) {
 }
 
 int32_t ensure_ws(mgpu_ctx* ctx, int64_t n_tiles, int64_t pool = 0) {
+  ctx->last.valid = false;  // every call that uses the workspace ends the last join's lifetime
   size_t need = ws_layout(n_tiles, pool).total;
   if (need <= ctx->ws_bytes) return MGPU_OK;
   if (ctx->ws) HIP_TRY(hipFree(ctx->ws));
@@ -894,6 +1220,23 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   uint32_t bng_edge = 0;
   if (index_system == MGPU_BNG && build_bng_dense(distinct, &lres, &dense[0], &bng_edge, grid))
     probe_mode = mgpu::kProbeDense;
+  // pixel index over the dense grid (chip_table.h, build_raster_*)
+  Raster raster;
+  if (probe_mode == mgpu::kProbeDense) {
+    mgpu::ChipTableView hv{};
+    hv.chip_poly = cpoly.data();
+    hv.chip_flags = cflags.data();
+    hv.chip_part = cpart.data();
+    hv.chip_env = cenv.data();
+    hv.part_ring = geo.part_ring.data();
+    hv.ring_vtx = geo.ring_vtx.data();
+    hv.ring_env = geo.ring_env.data();
+    hv.vtx = geo.vtx.data();
+    bool ok = index_system == MGPU_H3
+                  ? build_raster_h3(hv, lres, mgpu::h3::k_of_res(lres), bbox, dense, grid, raster)
+                  : build_raster_bng(hv, dense[0], bng_edge, grid, raster);
+    if (!ok) raster = Raster{};
+  }
   uint32_t cap = 16;
   while (cap < 2 * entries.size()) cap <<= 1;
   std::vector<mgpu::HashSlot> slots(cap, mgpu::HashSlot{0, 0, 0, 0});
@@ -933,6 +1276,8 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
       {strips.edge_ring.data(), strips.edge_ring.size(), 0},
       {chdr.data(), chdr.size() * sizeof(mgpu::ChipHdr), 0},
       {grid.data(), grid.size() * 8, 0},
+      {raster.cells.data(), raster.cells.size() * 2, 0},
+      {raster.cls.data(), raster.cls.size() * 8, 0},
   };
   size_t total = kBlobHeaderBytes;
   BlobHeader hdr{};
@@ -951,6 +1296,20 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   hdr.k_res = index_system == MGPU_H3 && lres >= 0 ? mgpu::h3::k_of_res(lres) : 0.0;
   hdr.bng_edge = bng_edge;
   hdr.bng_inv_edge = bng_edge ? 1.0 / bng_edge : 0.0;
+  hdr.index_system = index_system;
+  hdr.raster_mode = raster.mode;
+  hdr.raster_nx = raster.nx;
+  hdr.raster_ny = raster.ny;
+  hdr.raster_pix = raster.pix;
+  hdr.raster_px0 = raster.px0;
+  hdr.raster_py0 = raster.py0;
+  hdr.raster_x0 = raster.x0;
+  hdr.raster_y0 = raster.y0;
+  hdr.raster_inv_dx = raster.inv_dx;
+  hdr.raster_inv_dy = raster.inv_dy;
+  if (getenv("MGPU_RASTER_REPORT"))
+    fprintf(stderr, "mgpu raster: mode %d, %u x %u pixels, %zu classes, %.1f%% pure\n", raster.mode, raster.nx, raster.ny,
+            raster.cls.size(), raster.cells.empty() ? 0.0 : 100.0 * raster.n_pure / raster.cells.size());
   for (size_t k = 0; k < parts.size(); k++) {
     parts[k].off = total;
     hdr.off[k] = total;
@@ -990,6 +1349,7 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
     return fail(MGPU_E_DEVICE, "hipMemcpy: %s", hipGetErrorString(e2));
   }
   ch->bytes = total;
+  ch->index_system = hdr.index_system;
   ch->view = view_from_header(hdr, (uint8_t*)ch->blob);
   ch->n_vertices = hdr.n_vertices;
   *out = ch;
@@ -1033,6 +1393,7 @@ int32_t mgpu_chips_from_device_blob(mgpu_ctx* ctx, const void* device_ptr, int64
   HIP_TRY(hipMalloc(&ch->blob, bytes));
   HIP_TRY(hipMemcpy(ch->blob, device_ptr, bytes, hipMemcpyDeviceToDevice));
   ch->bytes = bytes;
+  ch->index_system = hdr.index_system;
   ch->view = view_from_header(hdr, (uint8_t*)ch->blob);
   ch->n_vertices = hdr.n_vertices;
   *out = ch;
@@ -1044,7 +1405,18 @@ int32_t mgpu_st_contains(mgpu_ctx* ctx, const mgpu_chips* chips, const int64_t* 
   if (!ctx || !chips) return fail(MGPU_E_INVALID_ARG, "ctx/chips is NULL");
   if (n < 0 || (n > 0 && (!chip_row || !x || !y || !out))) return fail(MGPU_E_INVALID_ARG, "bad arrays");
   if (int32_t st = set_device(ctx->device)) return st;
-  HIP_TRY(mgpu::launch_st_contains(chips->view, chip_row, x, y, n, out, (hipStream_t)stream));
+  if (chips->device != ctx->device)
+    return fail(MGPU_E_INVALID_ARG, "chip table lives on device %d, context on device %d", chips->device, ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (int32_t st = ensure_ws(ctx, 1)) return st;
+  auto* counters = (unsigned long long*)ctx->ws;
+  HIP_TRY(hipMemsetAsync(counters, 0, kWsCounters, s));
+  HIP_TRY(mgpu::launch_st_contains(chips->view, chip_row, x, y, n, out, counters, s));
+  unsigned long long h[4] = {0};
+  HIP_TRY(hipMemcpyAsync(h, counters, sizeof h, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (h[2])
+    return fail(MGPU_E_INVALID_ARG, "st_contains: %llu chip rows outside [0, %u)", h[2], chips->view.n_chips);
   return MGPU_OK;
 }
 
@@ -1055,6 +1427,10 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
                          int64_t* out_point, int32_t* out_poly, hipStream_t s, bool timed) {
   if (!ctx || !chips) return fail(MGPU_E_INVALID_ARG, "ctx/chips is NULL");
   if (int32_t r = check_res(is, res)) return r;
+  if (chips->index_system != is)
+    return fail(MGPU_E_INVALID_ARG, "chip table built for index system %d, join asked for %d", chips->index_system, is);
+  if (chips->device != ctx->device)
+    return fail(MGPU_E_INVALID_ARG, "chip table lives on device %d, context on device %d", chips->device, ctx->device);
   if (n < 0 || (n > 0 && (!x || !y))) return fail(MGPU_E_INVALID_ARG, "bad point arrays");
   if (capacity < 0 || (capacity > 0 && (!out_point || !out_poly))) return fail(MGPU_E_INVALID_ARG, "bad output arrays");
   if (int32_t st = set_device(ctx->device)) return st;
@@ -1110,6 +1486,20 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   if (timed) HIP_TRY(hipEventRecord(ctx->ev0, s));
   HIP_TRY(mgpu::launch_join(is, a, e, s, timed ? ctx->ev2 : nullptr));
   if (timed) HIP_TRY(hipEventRecord(ctx->ev1, s));
+  auto& L2 = ctx->last;
+  L2.chips = chips;
+  L2.is = is;
+  L2.res = res;
+  L2.x = x;
+  L2.y = y;
+  L2.point_id = point_id;
+  L2.id_base = id_base;
+  L2.n = n;
+  L2.emit = e;
+  L2.n_tiles = tiles;
+  L2.pool_ok = false;
+  L2.total = -1;
+  L2.valid = true;
   return MGPU_OK;
 }
 
@@ -1174,12 +1564,44 @@ int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_
     stats->kernel_ms = ms;
     stats->stream_kernel_ms = ms2;
   }
+  // pool records used (counters[5]) within the pool: every record is still in the
+  // workspace, so a larger output can be written by mgpu_pip_join_fetch alone
+  ctx->last.total = (int64_t)h[0];
+  ctx->last.pool_ok = (int64_t)h[5] <= capacity + ctx->last.n_tiles * mgpu::join_pend_cap();
   if (h[2]) {
+    ctx->last.valid = false;
     if (is == MGPU_BNG) return fail(MGPU_E_NAN, "NaN coordinates are not supported. (%llu points)", h[2]);
     return fail(MGPU_E_INVALID_ARG, "Latitude or longitude were invalid. (%llu points)", h[2]);
   }
   if ((int64_t)h[0] > capacity)
     return fail(MGPU_E_CAPACITY, "%lld pairs do not fit capacity %lld", (long long)h[0], (long long)capacity);
+  return MGPU_OK;
+}
+
+int32_t mgpu_pip_join_fetch(mgpu_ctx* ctx, int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id,
+                            int32_t* out_polygon_id, void* stream) {
+  if (!ctx) return fail(MGPU_E_INVALID_ARG, "ctx is NULL");
+  auto& L = ctx->last;
+  if (!L.valid || L.total < 0) return fail(MGPU_E_INVALID_ARG, "pip_join_fetch: no completed join on this context");
+  if (out_n_pairs) *out_n_pairs = L.total;
+  if (capacity < L.total)
+    return fail(MGPU_E_CAPACITY, "%lld pairs do not fit capacity %lld", (long long)L.total, (long long)capacity);
+  if (L.total > 0 && (!out_point_id || !out_polygon_id)) return fail(MGPU_E_INVALID_ARG, "bad output arrays");
+  if (int32_t st = set_device(ctx->device)) return st;
+  hipStream_t s = (hipStream_t)stream;
+  if (!L.pool_ok) {
+    // the overflow pool had dropped records: redo the join with a pool that holds them
+    const auto c = L;
+    int64_t cnt = 0;
+    return mgpu_pip_join(ctx, c.chips, c.is, c.res, c.x, c.y, c.point_id, c.id_base, c.n, capacity, out_n_pairs ? out_n_pairs : &cnt,
+                         out_point_id, out_polygon_id, stream, nullptr);
+  }
+  mgpu::EmitArgs e = L.emit;
+  e.capacity = capacity;
+  e.out_point = out_point_id;
+  e.out_poly = out_polygon_id;
+  HIP_TRY(mgpu::launch_emit(e, L.n_tiles, s));
+  HIP_TRY(hipStreamSynchronize(s));
   return MGPU_OK;
 }
 
@@ -1246,6 +1668,57 @@ int32_t mgpu_test_chip_contains_host(int32_t index_system, int64_t n_chips, cons
     }
     out_join_path[i] = mgpu::pip::chip_contains_strips(v, c, x[i], y[i]) ? 1 : 0;
     out_point_locator[i] = mgpu::pip::chip_locate(v, c, x[i], y[i]) == mgpu::pip::kInterior ? 1 : 0;
+  }
+  return MGPU_OK;
+}
+
+// TEST ONLY (no reference counterpart): builds the chip table on the host and looks up
+// n points in its pixel index exactly as the streaming join kernel does (raster.h), so
+// the CPU suite can check every pure pixel's answer against the oracle.  Per point:
+// out_kind 0 = no match possible (empty pixel / outside the box), 1 = pure pixel (its
+// matches are the sorted chips out_first + j for the bits j of out_mask), 2 = mixed
+// (full path), 3 = invalid coordinate, 4 = the table has no pixel index.
+// out_chip_poly[n_chips] = the polygon id of each sorted chip.  Host pointers; no GPU.
+int32_t mgpu_test_raster_host(int32_t index_system, int32_t res, int64_t n_chips, const int64_t* cell,
+                              const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
+                              const uint8_t* wkb, int64_t n, const double* x, const double* y, int8_t* out_kind,
+                              uint32_t* out_first, uint32_t* out_mask, int32_t* out_chip_poly) {
+  std::vector<uint8_t> host;
+  BlobHeader hdr;
+  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr))
+    return st;
+  const mgpu::ChipTableView v = view_from_header(hdr, host.data());
+  for (int64_t c = 0; c < n_chips; c++) out_chip_poly[c] = v.chip_poly[c];
+  const bool usable = v.raster_mode != mgpu::kRasterNone && (index_system == MGPU_H3 ? v.res == res : v.res == res);
+  for (int64_t i = 0; i < n; i++) {
+    out_first[i] = out_mask[i] = 0;
+    if (!usable) {
+      out_kind[i] = 4;
+      continue;
+    }
+    bool ok = true;
+    uint32_t gi = 0;
+    const uint32_t ri = index_system == MGPU_H3 ? mgpu::raster_index<MGPU_H3>(v, x[i], y[i], &ok, &gi)
+                                                : mgpu::raster_index<MGPU_BNG>(v, x[i], y[i], &ok, &gi);
+    if (!ok) {
+      out_kind[i] = 3;
+      continue;
+    }
+    if (ri == mgpu::kRasterFull) {
+      out_kind[i] = 2;
+      continue;
+    }
+    const uint32_t cl = ri == mgpu::kNoPixel ? mgpu::kPixEmpty : v.raster[ri];
+    if (cl == mgpu::kPixMixed) {
+      out_kind[i] = 2;
+      continue;
+    }
+    uint64_t ce = 0;
+    if (cl != mgpu::kPixEmpty)
+      ce = index_system == MGPU_BNG ? ((uint64_t)(uint32_t)v.grid[gi] | ((uint64_t)cl << 32)) : v.raster_cls[cl];
+    out_kind[i] = ce ? 1 : 0;
+    out_first[i] = (uint32_t)ce;
+    out_mask[i] = (uint32_t)(ce >> 32);
   }
   return MGPU_OK;
 }

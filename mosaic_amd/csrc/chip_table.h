@@ -146,7 +146,29 @@ struct ChipTableView {
   DenseFace dense[20];
   uint32_t bng_edge;
   double bng_inv_edge;
+  // Pixel index (kRaster*, capi.cpp build_raster): a raster of the chip cells' box in the
+  // point coordinates whose pixel p holds a class: kPixEmpty (no point of the pixel has a
+  // match), kPixMixed (the streaming kernel projects and tests the point), or k >= 1 =
+  // raster_cls[k] = first chip | match mask << 32 -- every point of the pixel lies in
+  // ONE chip cell (certified at build time, with margins, for the whole pixel) and in the
+  // interior / exterior of each of its chips (no chip edge meets the pixel), so its
+  // matches are the chips first + j for the mask bits j.
+  //   H3: pixel (ix, iy) = ((lon - x0) * inv_dx, (lat - y0) * inv_dy) truncated, clamped
+  //       to the last pixel (the raster spans `bbox`);
+  //   BNG: pixel = (easting / pix, northing / pix) in whole metres, minus (px0, py0); pix
+  //       divides the cell edge, so every pixel lies in one cell.
+  int32_t raster_mode;         // kRasterNone / kRasterLonLat / kRasterBng
+  uint32_t raster_nx, raster_ny;
+  uint32_t raster_pix;         // BNG pixel edge (metres)
+  int32_t raster_px0, raster_py0;
+  double raster_x0, raster_y0, raster_inv_dx, raster_inv_dy;
+  const uint16_t* raster;      // [ny * nx] classes
+  const uint64_t* raster_cls;  // [classes]
 };
+
+enum RasterMode { kRasterNone = 0, kRasterLonLat = 1, kRasterBng = 2 };
+constexpr uint16_t kPixEmpty = 0;
+constexpr uint16_t kPixMixed = 0xFFFF;
 
 enum ProbeMode { kProbeCellId = 0, kProbeLattice = 1, kProbeDense = 2 };
 

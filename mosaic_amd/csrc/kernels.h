@@ -58,6 +58,8 @@ int64_t join_pend_cap();       // pending mixed-cell candidates kept per tile
 int64_t join_pend_words();     // u64 words per pending candidate
 // `after_stream` (optional) is recorded right after pip_join_kernel
 hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s, hipEvent_t after_stream);
+// pair_emit_kernel alone, over the records a join left in the workspace
+hipError_t launch_emit(const EmitArgs& e, int64_t n_tiles, hipStream_t s);
 // StringType cell ids: offsets[n + 1] (device); chunk: scratch of format_chunks(n) int64;
 // counters[2] += ids without a string form (BNG)
 int64_t format_chunks(int64_t n);
@@ -66,7 +68,8 @@ hipError_t launch_format_cells(int is, const int64_t* cells, int64_t n, char* ou
 // BNG kRing / kLoop lists: out[offsets[i] .. offsets[i + 1]) (written when within capacity)
 hipError_t launch_cell_kring(int is, const int64_t* cells, int64_t n, int k, int loop_only, int64_t* out, int64_t capacity,
                             int64_t* offsets, int64_t* chunk, unsigned long long* counters, hipStream_t s);
+// counters[2] += chip rows outside [0, n_chips) (their out is -2)
 hipError_t launch_st_contains(const ChipTableView& t, const int64_t* row, const double* x, const double* y, int64_t n,
-                              int8_t* out, hipStream_t s);
+                              int8_t* out, unsigned long long* counters, hipStream_t s);
 
 }  // namespace mgpu

@@ -25,6 +25,7 @@
 #include "pip_core.h"
 #include "h3_ring.h"
 #include "kernels.h"
+#include "raster.h"
 
 namespace mgpu {
 
@@ -313,9 +314,12 @@ __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, cons
     }
   }
   s_first[li] = r.first;
-  s_cnt[li] = (uint16_t)(r.count > 0xFFFF ? 0xFFFF : r.count);
+  // (the streaming kernel reads no counts: its s_cnt doubles as the raster's list)
+  if (SLOW || MGPU_DEFER) s_cnt[li] = (uint16_t)(r.count > 0xFFFF ? 0xFFFF : r.count);
   s_mask[li] = mask;
 }
+
+
 
 // Profiling builds (-DMGPU_STAMPS): thread 0 of each tile adds the wall-clock ticks
 // (100 MHz) spent in each phase to counters[10 + phase]: 1 = phase 1, 2 = phase 2,
@@ -379,7 +383,88 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #else
 #define MGPU_LDPT(ptr) (*(ptr))
 #endif
-  if (IS == MGPU_BNG) {
+  if (!SLOW && kBlock == 64 && t.raster_mode != kRasterNone && a.ablate == 0 && res_match &&
+      (IS == MGPU_H3 || a.res == t.res)) {
+    // pass A: the lane's four points load together, then their pixels' classes: a
+    // pure pixel's matches are final (no projection, no candidates); the rest are
+    // listed (s_cnt is free in the streaming kernel) for pass B
+    const int lane = threadIdx.x;
+    double bx[kItems], by[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      const int64_t p = base + k * kBlock + lane;
+      bx[k] = by[k] = 0.0;
+      if (p < a.n) {
+        bx[k] = MGPU_LDPT(&a.x[p]);
+        by[k] = MGPU_LDPT(&a.y[p]);
+      }
+    }
+    uint32_t ri[kItems], gix[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      ri[k] = kNoPixel;
+      gix[k] = 0;
+      if (base + k * kBlock + lane < a.n) {
+        bool ok;
+        ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &gix[k]);
+        any_bad |= !ok;
+      }
+    }
+    uint32_t cl[kItems];
+    uint64_t ge[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      cl[k] = ri[k] < kRasterFull ? (uint32_t)t.raster[ri[k]] : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
+      if (IS == MGPU_BNG) ge[k] = ri[k] < kRasterFull ? t.grid[gix[k]] : 0ull;  // (independent of the pixel load)
+    }
+    uint64_t ce[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      if (IS == MGPU_BNG)  // the pixel holds the mask of the cell's chips
+        ce[k] = (cl[k] != kPixEmpty && cl[k] != kPixMixed) ? ((uint64_t)(uint32_t)ge[k] | ((uint64_t)cl[k] << 32)) : 0ull;
+      else
+        ce[k] = (cl[k] != kPixEmpty && cl[k] != kPixMixed) ? t.raster_cls[cl[k]] : 0ull;
+    }
+    uint16_t* s_list = s_cnt;
+    uint32_t nlist = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      const int li = k * kBlock + lane;
+      const bool mixed = cl[k] == kPixMixed;
+      if (!mixed) {
+        s_first[li] = (uint32_t)ce[k];
+        s_mask[li] = (uint32_t)(ce[k] >> 32);
+      }
+      const unsigned long long bal = __ballot(mixed);
+      if (mixed) s_list[nlist + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)li;
+      nlist += (uint32_t)__popcll(bal);
+    }
+    __syncthreads();
+    // pass B: the listed points, 64 at a time with every lane busy (coordinates from
+    // the owning lane's registers)
+    for (uint32_t q0 = 0; q0 < nlist; q0 += kBlock) {
+      const uint32_t q = q0 + lane;
+      const int li = q < nlist ? (int)s_list[q] : 0;
+      const int owner = li & 63, kk = li >> 6;
+      double px = 0.0, py = 0.0;
+#pragma unroll
+      for (int k = 0; k < kItems; k++) {
+        const double vx = __shfl(bx[k], owner, 64), vy = __shfl(by[k], owner, 64);
+        if (kk == k) {
+          px = vx;
+          py = vy;
+        }
+      }
+      if (q < nlist) {
+        bool ok, tie;
+        uint32_t gi;
+        Range r = chip_probe<IS, SLOW>(t, px, py, a.res, res_match, &ok, &tie, a.ablate, &gi);
+        if (gi != kNoEntry) r = grid_range(t.grid[gi]);
+        any_tie |= tie;
+        phase1_item<SLOW>(t, li, r, px, py, do_pip, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
+      }
+    }
+  } else if (IS == MGPU_BNG) {
     // the cell is a few integer ops: the lane's four points load together, then
     // their four grid entries (a wave's loads complete in order, so a load issued
     // behind a point prefetch would wait for it)
@@ -966,11 +1051,14 @@ __global__ __launch_bounds__(kEmitBlock) void pair_emit_kernel(EmitArgs a, int64
 __global__ __launch_bounds__(kStreamBlock) void st_contains_kernel(ChipTableView t, const int64_t* __restrict__ row,
                                                              const double* __restrict__ x,
                                                              const double* __restrict__ y, int64_t n,
-                                                             int8_t* __restrict__ out) {
+                                                             int8_t* __restrict__ out,
+                                                             unsigned long long* __restrict__ counters) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = i < n ? row[i] : 0;
+  const bool bad = i < n && (r < 0 || r >= (int64_t)t.n_chips);
+  count_wave(&counters[2], bad);  // the call fails with MGPU_E_INVALID_ARG
   if (i >= n) return;
-  int64_t r = row[i];
-  if (r < 0 || r >= (int64_t)t.n_chips) {
+  if (bad) {
     out[i] = -2;
     return;
   }
@@ -1322,11 +1410,18 @@ hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t
   return hipGetLastError();
 }
 
+hipError_t launch_emit(const EmitArgs& e, int64_t n_tiles, hipStream_t s) {
+  if (n_tiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pair_emit_kernel, dim3((unsigned)((n_tiles + kEmitTiles - 1) / kEmitTiles)), dim3(kEmitBlock), 0, s, e,
+                     n_tiles);
+  return hipGetLastError();
+}
+
 hipError_t launch_st_contains(const ChipTableView& t, const int64_t* row, const double* x, const double* y, int64_t n,
-                              int8_t* out, hipStream_t s) {
+                              int8_t* out, unsigned long long* counters, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(st_contains_kernel, dim3((unsigned)((n + kStreamBlock - 1) / kStreamBlock)), dim3(kStreamBlock), 0, s, t, row, x,
-                     y, n, out);
+                     y, n, out, counters);
   return hipGetLastError();
 }
 

@@ -120,7 +120,8 @@ def pip_join(x, y, chips, resolution, index_system=None, point_id=None, point_id
 
     Returns a JoinResult with int64 point ids and int32 polygon ids ordered by input
     position then polygon id.  ``capacity`` bounds the output (default: n + 1/8 n
-    headroom, grown and re-run once if exceeded)."""
+    headroom; when the pairs do not fit, arrays of the exact count are allocated and
+    filled from the join's kept records by mgpu_pip_join_fetch -- the join is not redone)."""
     import torch
     isys = index_system or _H3
     res = isys.get_resolution(resolution)
@@ -130,31 +131,34 @@ def pip_join(x, y, chips, resolution, index_system=None, point_id=None, point_id
         chips = chips.upload()
     _check_points(x, y)
     n = x.numel()
+    if chips.ctx.device != x.device:
+        raise N.IllegalArgumentException(N.MGPU_E_INVALID_ARG, "chip table on %s, points on %s" % (chips.ctx.device, x.device))
     pid_ptr = None
     if point_id is not None:
         if point_id.dtype != torch.int64 or point_id.numel() != n or point_id.device != x.device:
             raise N.IllegalArgumentException(N.MGPU_E_INVALID_ARG, "point_id must be int64 on the points' device")
-        pid_ptr = point_id.contiguous().data_ptr()
+        point_id = point_id.contiguous()  # kept alive (bound here) until the call returns
+        pid_ptr = point_id.data_ptr()
     s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
-    cap = int(capacity if capacity is not None else max(16, n + n // 8))
-    for attempt in range(2):
-        if out is not None and attempt == 0:
-            op, oq = out
-            cap = min(op.numel(), oq.numel())
-        else:
-            op = torch.empty(cap, dtype=torch.int64, device=x.device)
-            oq = torch.empty(cap, dtype=torch.int32, device=x.device)
-        import ctypes
-        cnt = ctypes.c_int64()
-        st = N.MgpuStats()
-        status = N.lib().mgpu_pip_join(chips.ctx.handle, chips.handle, isys.code, res, x.data_ptr(), y.data_ptr(),
-                                       pid_ptr, int(point_id_base), n, cap, ctypes.byref(cnt), op.data_ptr(),
-                                       oq.data_ptr(), s, st)
-        if status == N.MGPU_E_CAPACITY and capacity is None and attempt == 0:
-            cap = int(cnt.value)
-            out = None
-            continue
-        N.check(status, required=cnt.value)
-        m = int(cnt.value)
-        return JoinResult(op[:m], oq[:m], st.as_dict())
-    raise AssertionError("unreachable")
+    import ctypes
+    if out is not None:
+        op, oq = out
+        cap = min(op.numel(), oq.numel())
+    else:
+        cap = int(capacity if capacity is not None else max(16, n + n // 8))
+        op = torch.empty(cap, dtype=torch.int64, device=x.device)
+        oq = torch.empty(cap, dtype=torch.int32, device=x.device)
+    cnt = ctypes.c_int64()
+    st = N.MgpuStats()
+    status = N.lib().mgpu_pip_join(chips.ctx.handle, chips.handle, isys.code, res, x.data_ptr(), y.data_ptr(),
+                                   pid_ptr, int(point_id_base), n, cap, ctypes.byref(cnt), op.data_ptr(),
+                                   oq.data_ptr(), s, st)
+    if status == N.MGPU_E_CAPACITY and capacity is None and out is None:
+        # the join's records are kept: write them into arrays of the exact size
+        cap = int(cnt.value)
+        op = torch.empty(cap, dtype=torch.int64, device=x.device)
+        oq = torch.empty(cap, dtype=torch.int32, device=x.device)
+        status = N.lib().mgpu_pip_join_fetch(chips.ctx.handle, cap, ctypes.byref(cnt), op.data_ptr(), oq.data_ptr(), s)
+    N.check(status, required=cnt.value)
+    m = int(cnt.value)
+    return JoinResult(op[:m], oq[:m], st.as_dict())

@@ -532,3 +532,56 @@ def test_pip_join_bng_near_origin(gpu):
             r2 = M.pip_join(T(x, gpu), T(y, gpu), c, 5, index_system=I)
             op2, oq2 = oracle_join(c, x, y, res=5, isys=1)
             assert np.array_equal(r2.numpy()[0], op2) and np.array_equal(r2.numpy()[1], oq2)
+
+
+# ---------------------------------------------------------------- round 2 additions
+
+def test_pip_join_strided_point_ids(gpu, nyc_chips_r9):
+    """A non-contiguous point_id column (a strided view) joins like its contiguous copy."""
+    x, y = nyc_points(200_000, 31)
+    ids_all = torch.arange(400_000, dtype=torch.int64, device=gpu) * 3 + 5
+    ids = ids_all[::2]
+    assert not ids.is_contiguous()
+    r = M.pip_join(T(x, gpu), T(y, gpu), nyc_chips_r9, 9, point_id=ids)
+    op, oq = oracle_join(nyc_chips_r9, x, y)
+    gp, gq = r.numpy()
+    assert np.array_equal(gp, ids.cpu().numpy()[op]) and np.array_equal(gq, oq)
+
+
+def test_st_contains_bad_row_raises(gpu, nyc_chips_r9):
+    d = nyc_chips_r9.upload()
+    rows = torch.tensor([0, len(nyc_chips_r9), 1], dtype=torch.int64, device=gpu)
+    with pytest.raises(M.IllegalArgumentException):
+        M.st_contains(d, rows, T([-73.9, -73.9, -73.9], gpu), T([40.7, 40.7, 40.7], gpu))
+
+
+def test_join_rejects_chips_of_another_index_system(gpu, nyc_chips_r9):
+    d = nyc_chips_r9.upload()  # H3 chips
+    x, y = nyc_points(1000, 32)
+    with pytest.raises(M.IllegalArgumentException):
+        M.pip_join(T(x, gpu), T(y, gpu), d, 4, index_system=M.BNGIndexSystem())
+
+
+def test_pixel_index_on_off_identical(gpu, nyc_chips_r9):
+    """The join answers identically with and without the chip table's pixel index
+    (MGPU_RASTER=0 at upload builds the table without it), on uniform and adversarial
+    points, H3 (NYC r9) and BNG (London districts r4)."""
+    import bench_workloads as W
+    cases = [(nyc_chips_r9, 9, M.H3IndexSystem(), nyc_points(2_000_000, 33))]
+    ax, ay = adversarial_points(nyc_chips_r9)
+    cases.append((nyc_chips_r9, 9, M.H3IndexSystem(), (ax, ay)))
+    cb = M.tessellate(W.london_districts(), M.BNGIndexSystem(), 4)
+    cases.append((cb, 4, M.BNGIndexSystem(), W.london_points(2_000_000, 34)))
+    for c, res, isys, (x, y) in cases:
+        os.environ["MGPU_RASTER"] = "0"
+        try:
+            d0 = c.upload()
+        finally:
+            del os.environ["MGPU_RASTER"]
+        d1 = c.upload()
+        a = M.pip_join(T(x, gpu), T(y, gpu), d0, res, index_system=isys).numpy()
+        b = M.pip_join(T(x, gpu), T(y, gpu), d1, res, index_system=isys).numpy()
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+        if len(x) <= 300_000:
+            op, oq = oracle_join(c, x, y, res=res, isys=isys.code)
+            assert np.array_equal(b[0], op) and np.array_equal(b[1], oq)

@@ -1,0 +1,17 @@
+#!/bin/bash
+# One GPU iteration: parity suite, then join timings with the pixel index off / on
+# (tools/ab_time.py), each step under its own limit: tools/gpu_check.sh TAG [CONFIGS]
+set -o pipefail
+TAG=${1:-x}
+CFGS=${2:-c2,c4,c5}
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1
+rc=$?
+tail -3 gpurun_out/pytest_gpu_$TAG.log
+[ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" gpurun_out/pytest_gpu_$TAG.log | head -20; exit $rc; }
+MGPU_RASTER=0 timeout -k 10 300 python3 -u tools/ab_time.py --configs $CFGS > gpurun_out/ab_${TAG}_off.json 2> gpurun_out/ab_${TAG}_off.err &&
+MGPU_RASTER=1 timeout -k 10 300 python3 -u tools/ab_time.py --configs $CFGS > gpurun_out/ab_${TAG}_on.json 2> gpurun_out/ab_${TAG}_on.err
+rc=$?
+echo "== raster off"; cat gpurun_out/ab_${TAG}_off.json
+echo "== raster on"; cat gpurun_out/ab_${TAG}_on.json
+exit $rc
