@@ -10,7 +10,10 @@ is_core OR st_contains -> ordered pair output) over the GPU's resident points.
 Multi-GPU (torchrun, one process per GPU): points are sharded by contiguous id range
 (weak scaling: the per-GPU point count is fixed), the chip table is built on rank 0
 and replicated with one RCCL broadcast, per-rank pair counts are all-gathered (RCCL)
-for the global output offsets.  Time = max over ranks of the barrier-bracketed K steps.
+for the global output offsets -- both through the C ABI (mgpu_comm_init,
+mgpu_chips_broadcast, mgpu_pair_offsets; mosaic_amd/csrc/comm.cpp).  torch.distributed
+(gloo) is only the control plane: the RCCL unique id, the barriers and the max over
+ranks of the barrier-bracketed K steps.
 
 A step is one mgpu_pip_join call: pip_join_kernel (cell id -> chip probe -> is_core
 OR st_contains -> per-tile pair records), pip_fix_kernel (tiles holding an H3 near-tie),
@@ -166,18 +169,18 @@ def main():
     if a.gpus != world and world > 1:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (a.gpus, world))
     # MGPU_DIST_BACKEND=gloo and more ranks than GPUs: a protocol rehearsal on a
-    # 1-GPU box (never a measurement); the real run is RCCL ("nccl"), one rank per GPU
-    backend = os.environ.get("MGPU_DIST_BACKEND", "nccl")
+    # 1-GPU box (never a measurement: the chip blob and the counts travel over gloo);
+    # the real run is RCCL through the C ABI, one rank per GPU
+    rehearsal = os.environ.get("MGPU_DIST_BACKEND", "rccl") == "gloo"
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")  # control plane only
     ctx = M.default_context(dev)
+    if world > 1 and not rehearsal:
+        D.init_comm(ctx)
     import bench_workloads as W
     wl = workload(a, W, M)
     isys, zones = wl["isys"], wl["polygons"]
@@ -190,8 +193,11 @@ def main():
         log("chip table uploaded")
     else:
         chips = None
-    if world > 1:
+    if world > 1 and not rehearsal:
         chips = D.broadcast_chips(chips, ctx)
+    elif world > 1:
+        blob = D.broadcast_host_blob(D.host_blob(table) if rank == 0 else None, 0)
+        chips = chips if rank == 0 else D.upload_host_blob(blob, ctx)
     info = chips.info()
 
     n = a.points
@@ -229,10 +235,13 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        off, total_pairs, _ = D.global_offsets(pairs, dev)
+        if rehearsal:
+            off, total_pairs, _ = D.gather_offsets_host(pairs)
+        else:
+            off, total_pairs, _ = D.global_offsets(pairs, ctx)
     else:
         total_pairs = pairs
 

@@ -57,8 +57,17 @@ typedef struct mgpu_stats {
                                difference could change the cell */
     int64_t n_candidates;   /* (point, border chip) PIP evaluations */
     float kernel_ms;        /* device time of the whole call's launches (HIP events) */
-    float stream_kernel_ms; /* of which the streaming join kernel (pip_join_kernel) */
+    float stream_kernel_ms; /* of which the streaming kernel over all points (pip_join_kernel,
+                               or classify_kernel in the split pipeline) */
+    float mixed_kernel_ms;  /* split pipeline: pip_mixed_kernel + pip_mixed_fix_kernel */
+    float emit_kernel_ms;   /* split pipeline: tile_scan_kernel + split_emit_kernel */
+    int32_t pipeline;       /* MGPU_PIPELINE_FUSED or MGPU_PIPELINE_SPLIT */
+    int32_t pad;
 } mgpu_stats;
+/* the join's two pipelines: one fused kernel per tile of points, or -- for a
+ * chip table with a pixel index -- classify all points, resolve the mixed ones, emit */
+#define MGPU_PIPELINE_FUSED 0
+#define MGPU_PIPELINE_SPLIT 1
 
 const char* mgpu_last_error(void);
 const char* mgpu_version(void);
@@ -66,7 +75,8 @@ const char* mgpu_version(void);
  * reference counterpart). */
 int32_t mgpu_join_tile_points(void);
 
-/* One context per GPU/executor: owns the stream-ordered workspace. */
+/* One context per GPU/executor: owns the stream-ordered workspace (and, after
+ * mgpu_comm_init, the RCCL communicator; destroyed with the context). */
 int32_t mgpu_ctx_create(int32_t device_id, mgpu_ctx** out);
 int32_t mgpu_ctx_destroy(mgpu_ctx* ctx);
 
@@ -133,6 +143,43 @@ int32_t mgpu_chips_destroy(mgpu_chips* chips);
 int32_t mgpu_chips_device_blob(const mgpu_chips* chips, void** device_ptr, int64_t* bytes);
 int32_t mgpu_chips_from_device_blob(mgpu_ctx* ctx, const void* device_ptr, int64_t bytes, mgpu_chips** out);
 int32_t mgpu_chips_info(const mgpu_chips* chips, int64_t* n_chips, int64_t* n_cells, int64_t* n_vertices);
+
+/* The chip table as one self-describing host blob (what mgpu_chips_upload uploads): a
+ * JVM driver can build it once and ship the bytes to its executors, which upload them
+ * with mgpu_chips_upload_blob.  Free with mgpu_host_free.  mgpu_host_blob_info checks a
+ * received blob (magic, version, size, offsets) and reports its contents.  Host only. */
+int32_t mgpu_chips_host_blob(int32_t index_system, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
+                             const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb, uint8_t** out,
+                             int64_t* bytes);
+int32_t mgpu_host_free(void* p);
+int32_t mgpu_host_blob_info(const void* host_blob, int64_t bytes, int32_t* index_system, int64_t* n_chips,
+                            int64_t* n_cells, int64_t* n_vertices);
+int32_t mgpu_chips_upload_blob(mgpu_ctx* ctx, const void* host_blob, int64_t bytes, mgpu_chips** out);
+
+/* Multi-GPU (one process per GPU): points are sharded by contiguous id range,
+ * the chip table is replicated.  The reference's scale-out is Spark's broadcast of the
+ * chip side to every executor (BroadcastHashJoin in the plan of notebooks/examples/python/
+ * Quickstart/QuickstartNotebook.ipynb:1835); here each GPU's context owns an RCCL
+ * communicator:
+ *   mgpu_comm_unique_id  one rank creates the id (ncclGetUniqueId) and ships its
+ *                        MGPU_COMM_ID_BYTES to every rank out of band (the JVM driver's
+ *                        broadcast; torch.distributed's store in mosaic_amd/dist.py);
+ *   mgpu_comm_init       every rank joins (ncclCommInitRank; blocks until all have);
+ *   mgpu_chips_broadcast the root's chip table is replicated into a new allocation on
+ *                        every other rank by one RCCL broadcast of the blob (plus one of
+ *                        its 1 KiB header to size it); *out = the replica (NULL on root);
+ *   mgpu_pair_offsets    RCCL all-gather of the per-rank pair counts: this rank's offset
+ *                        in the globally ordered output, the total, and (optionally)
+ *                        out_counts[world].
+ * The collectives are enqueued on `stream` and complete before the calls return. */
+#define MGPU_COMM_ID_BYTES 128
+int32_t mgpu_comm_unique_id(uint8_t* out_id);
+int32_t mgpu_comm_init(mgpu_ctx* ctx, const uint8_t* unique_id, int32_t rank, int32_t world);
+int32_t mgpu_comm_info(mgpu_ctx* ctx, int32_t* rank, int32_t* world);
+int32_t mgpu_comm_destroy(mgpu_ctx* ctx);
+int32_t mgpu_chips_broadcast(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t root, mgpu_chips** out, void* stream);
+int32_t mgpu_pair_offsets(mgpu_ctx* ctx, int64_t local_pairs, int64_t* out_offset, int64_t* out_total,
+                          int64_t* out_counts, void* stream);
 
 /* st_contains(chip.wkb, point) for explicit (chip row, point) pairs
  * (ST_Contains.scala:21-44 -> MosaicGeometryJTS.contains, MosaicGeometryJTS.scala:197).
@@ -214,6 +261,12 @@ int32_t mgpu_test_chip_contains_host(int32_t index_system, int64_t n_chips, cons
                                      const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
                                      const uint8_t* wkb, int64_t n, const int64_t* chip_row, const double* x,
                                      const double* y, int8_t* out_join_path, int8_t* out_point_locator);
+
+/* TEST ONLY -- st_contains(chip row, point) evaluated on a HOST blob (the join's
+ * classification grid + strip path), to check on the CPU that a shipped blob is a
+ * complete chip table.  out = 1 / 0, -1 NULL geometry.  Host pointers; no GPU. */
+int32_t mgpu_test_blob_contains_host(const void* host_blob, int64_t bytes, int64_t n, const int64_t* chip_row,
+                                     const double* x, const double* y, int8_t* out);
 
 /* TEST ONLY -- not an interface of the reference.  Builds the chip table on the host and
  * looks n points up in its pixel index (the pre-resolved answers of the streaming join,

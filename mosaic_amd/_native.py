@@ -33,7 +33,13 @@ EXPORTS = (
     "mgpu_chips_info", "mgpu_st_contains", "mgpu_pip_join", "mgpu_pip_join_async", "mgpu_ctx_reserve",
     "mgpu_last_near_ties",    "mgpu_pip_join_host", "mgpu_tessellate", "mgpu_tess_result_sizes", "mgpu_tess_result_copy",
     "mgpu_tess_destroy", "mgpu_test_chip_contains_host", "mgpu_test_raster_host", "mgpu_pip_join_fetch",
+    "mgpu_chips_host_blob", "mgpu_host_free", "mgpu_host_blob_info", "mgpu_chips_upload_blob",
+    "mgpu_comm_unique_id", "mgpu_comm_init", "mgpu_comm_info", "mgpu_comm_destroy", "mgpu_chips_broadcast",
+    "mgpu_pair_offsets", "mgpu_test_blob_contains_host",
 )
+MGPU_COMM_ID_BYTES = 128
+MGPU_PIPELINE_FUSED = 0
+MGPU_PIPELINE_SPLIT = 1
 
 
 class MosaicGpuError(RuntimeError):
@@ -61,7 +67,8 @@ class CapacityError(MosaicGpuError):
 class MgpuStats(ctypes.Structure):
     _fields_ = [("n_points", ctypes.c_int64), ("n_pairs", ctypes.c_int64), ("n_near_ties", ctypes.c_int64),
                 ("n_candidates", ctypes.c_int64), ("kernel_ms", ctypes.c_float),
-                ("stream_kernel_ms", ctypes.c_float)]
+                ("stream_kernel_ms", ctypes.c_float), ("mixed_kernel_ms", ctypes.c_float),
+                ("emit_kernel_ms", ctypes.c_float), ("pipeline", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -115,6 +122,18 @@ def lib():
         "mgpu_test_chip_contains_host": (I32, [I32, I64, P, P, P, P, P, I64, P, P, P, P, P]),
         "mgpu_pip_join_fetch": (I32, [P, I64, ctypes.POINTER(I64), P, P, P]),
         "mgpu_test_raster_host": (I32, [I32, I32, I64, P, P, P, P, P, I64, P, P, P, P, P, P]),
+        "mgpu_chips_host_blob": (I32, [I32, I64, P, P, P, P, P, ctypes.POINTER(P), ctypes.POINTER(I64)]),
+        "mgpu_host_free": (I32, [P]),
+        "mgpu_host_blob_info": (I32, [P, I64, ctypes.POINTER(I32), ctypes.POINTER(I64), ctypes.POINTER(I64),
+                                      ctypes.POINTER(I64)]),
+        "mgpu_chips_upload_blob": (I32, [P, P, I64, ctypes.POINTER(P)]),
+        "mgpu_comm_unique_id": (I32, [P]),
+        "mgpu_comm_init": (I32, [P, P, I32, I32]),
+        "mgpu_comm_info": (I32, [P, ctypes.POINTER(I32), ctypes.POINTER(I32)]),
+        "mgpu_comm_destroy": (I32, [P]),
+        "mgpu_chips_broadcast": (I32, [P, P, I32, ctypes.POINTER(P), P]),
+        "mgpu_pair_offsets": (I32, [P, I64, ctypes.POINTER(I64), ctypes.POINTER(I64), P, P]),
+        "mgpu_test_blob_contains_host": (I32, [P, I64, I64, P, P, P, P]),
     }
     for name, (rt, args) in sig.items():
         f = getattr(L, name)

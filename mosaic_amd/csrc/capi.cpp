@@ -28,6 +28,7 @@
 #include "pip_core.h"
 #include "raster.h"
 #include "wkb.h"
+#include "capi_internal.h"
 
 namespace {
 
@@ -74,6 +75,9 @@ struct BlobHeader {
   uint32_t raster_nx, raster_ny, raster_pix;
   int32_t raster_px0, raster_py0;
   double raster_x0, raster_y0, raster_inv_dx, raster_inv_dy;
+  uint64_t blob_bytes;  // the whole blob (header included)
+  uint32_t max_cell_chips, pad4;
+  uint32_t raster_pc[4];
 };
 constexpr size_t kBlobHeaderBytes = 1024;
 static_assert(sizeof(BlobHeader) <= kBlobHeaderBytes, "header too large");
@@ -110,6 +114,7 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.k_res = h.k_res;
   v.bng_edge = h.bng_edge;
   v.bng_inv_edge = h.bng_inv_edge;
+  v.max_cell_chips = h.max_cell_chips;
   v.raster_mode = h.raster_mode;
   v.raster_nx = h.raster_nx;
   v.raster_ny = h.raster_ny;
@@ -120,6 +125,7 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.raster_y0 = h.raster_y0;
   v.raster_inv_dx = h.raster_inv_dx;
   v.raster_inv_dy = h.raster_inv_dy;
+  for (int k = 0; k < 4; k++) v.raster_pc[k] = h.raster_pc[k];
   v.raster = (const uint16_t*)(base + h.off[18]);
   v.raster_cls = (const uint64_t*)(base + h.off[19]);
   return v;
@@ -498,6 +504,7 @@ struct Raster {
   double x0 = 0, y0 = 0, inv_dx = 0, inv_dy = 0;
   std::vector<uint16_t> cells;
   std::vector<uint64_t> cls;
+  uint32_t pc[4] = {0, 0, 0, 0};
   int64_t n_pure = 0;
 };
 
@@ -637,7 +644,13 @@ bool raster_classes(const std::vector<uint64_t>& ans, Raster& R) {
     }
     keyed.push_back({ans[i], (uint32_t)i});
   }
-  std::sort(keyed.begin(), keyed.end());
+  // classes ordered by their number of matches, so a class id tells its pair count
+  // (pc[k]: the first class with more than k + 1 matches)
+  auto pc = [](uint64_t v) { return __builtin_popcountll(v >> 32); };
+  std::sort(keyed.begin(), keyed.end(), [&](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) {
+    const int x = pc(a.first), y = pc(b.first);
+    return x != y ? x < y : a < b;
+  });
   for (size_t k = 0; k < keyed.size(); k++) {
     if (k == 0 || keyed[k].first != keyed[k - 1].first) {
       if (R.cls.size() >= mgpu::kPixMixed) break;  // out of classes: the rest stay mixed
@@ -645,6 +658,11 @@ bool raster_classes(const std::vector<uint64_t>& ans, Raster& R) {
     }
     R.cells[keyed[k].second] = (uint16_t)(R.cls.size() - 1);
     R.n_pure++;
+  }
+  for (int k = 0; k < 4; k++) {
+    uint32_t c = 1;
+    while (c < R.cls.size() && pc(R.cls[c]) <= k + 1) c++;
+    R.pc[k] = c;
   }
   return true;
 }
@@ -780,35 +798,6 @@ int32_t set_error(int32_t code, const char* fmt, ...) {
 }
 }  // namespace mgpu
 
-struct mgpu_ctx {
-  int device = 0;
-  // workspace: tile status words + ticket + counters
-  void* ws = nullptr;
-  size_t ws_bytes = 0;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
-  // the last mgpu_pip_join on this context, whose pair records stay in the workspace
-  // until the next call (mgpu_pip_join_fetch)
-  struct {
-    bool valid = false, pool_ok = false;
-    const mgpu_chips* chips = nullptr;
-    int32_t is = 0, res = 0;
-    const double *x = nullptr, *y = nullptr;
-    const int64_t* point_id = nullptr;
-    int64_t id_base = 0, n = 0, total = 0;
-    mgpu::EmitArgs emit{};
-    int64_t n_tiles = 0;
-  } last;
-};
-
-struct mgpu_chips {
-  int device = 0;
-  int32_t index_system = MGPU_H3;
-  void* blob = nullptr;
-  size_t bytes = 0;
-  mgpu::ChipTableView view{};
-  int64_t n_vertices = 0;
-};
-
 namespace {
 
 // Workspace layout (each region 256-byte aligned):
@@ -839,7 +828,7 @@ WsLayout ws_layout(int64_t n_tiles, int64_t pool) {
   L.off = align_up(L.where + T * 8, 256);
   L.gsum = align_up(L.off + T * 8, 256);
   L.dirty = align_up(L.gsum + 2 * (T / 32 + 1) * 4, 256);  // group pair sums, group candidate sums
-  L.tpend = align_up(L.dirty + T * 4, 256);
+  L.tpend = align_up(L.dirty + T * 4 * 4, 256);  // (the split pipeline's mixed tiles: 64 points)
   L.pend = align_up(L.tpend + T * 4, 256);
   L.recs = align_up(L.pend + T * (size_t)(mgpu::join_pend_cap() * mgpu::join_pend_words()) * 8, 256);
   L.total = align_up(L.recs + (T * (size_t)mgpu::join_slot_records() + (size_t)std::max<int64_t>(pool, 0)) * 8, 256);
@@ -896,6 +885,7 @@ int32_t mgpu_ctx_create(int32_t device_id, mgpu_ctx** out) {
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
   HIP_TRY(hipEventCreate(&c->ev2));
+  HIP_TRY(hipEventCreate(&c->ev3));
   int32_t st = ensure_ws(c, 1);
   if (st) {
     delete c;
@@ -907,11 +897,14 @@ int32_t mgpu_ctx_create(int32_t device_id, mgpu_ctx** out) {
 
 int32_t mgpu_ctx_destroy(mgpu_ctx* ctx) {
   if (!ctx) return MGPU_OK;
+  mgpu_comm_destroy(ctx);
   hipSetDevice(ctx->device);
+  if (ctx->split_ws) hipFree(ctx->split_ws);
   if (ctx->ws) hipFree(ctx->ws);
   if (ctx->ev0) hipEventDestroy(ctx->ev0);
   if (ctx->ev1) hipEventDestroy(ctx->ev1);
   if (ctx->ev2) hipEventDestroy(ctx->ev2);
+  if (ctx->ev3) hipEventDestroy(ctx->ev3);
   delete ctx;
   return MGPU_OK;
 }
@@ -1297,6 +1290,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   hdr.bng_edge = bng_edge;
   hdr.bng_inv_edge = bng_edge ? 1.0 / bng_edge : 0.0;
   hdr.index_system = index_system;
+  for (const auto& d : distinct) hdr.max_cell_chips = std::max<uint32_t>(hdr.max_cell_chips, d.count);
   hdr.raster_mode = raster.mode;
   hdr.raster_nx = raster.nx;
   hdr.raster_ny = raster.ny;
@@ -1307,6 +1301,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   hdr.raster_y0 = raster.y0;
   hdr.raster_inv_dx = raster.inv_dx;
   hdr.raster_inv_dy = raster.inv_dy;
+  for (int k = 0; k < 4; k++) hdr.raster_pc[k] = raster.pc[k];
   if (getenv("MGPU_RASTER_REPORT"))
     fprintf(stderr, "mgpu raster: mode %d, %u x %u pixels, %zu classes, %.1f%% pure\n", raster.mode, raster.nx, raster.ny,
             raster.cls.size(), raster.cells.empty() ? 0.0 : 100.0 * raster.n_pure / raster.cells.size());
@@ -1315,6 +1310,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     hdr.off[k] = total;
     total = align_up(total + std::max<size_t>(parts[k].bytes, 1), 256);
   }
+  hdr.blob_bytes = total;
   host.assign(total, 0);
   memcpy(host.data(), &hdr, sizeof hdr);
   for (auto& p : parts)
@@ -1323,7 +1319,91 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   return MGPU_OK;
 }
 
+// A blob header read back from memory: magic, version, sizes and array offsets checked.
+static int32_t check_header(const BlobHeader& hdr, int64_t bytes) {
+  if (hdr.magic != kBlobMagic || hdr.version != kBlobVersion) return fail(MGPU_E_INVALID_ARG, "not a chip-table blob");
+  if ((int64_t)hdr.blob_bytes != bytes) return fail(MGPU_E_INVALID_ARG, "chip-table blob of %lld bytes, header says %llu",
+                                                    (long long)bytes, (unsigned long long)hdr.blob_bytes);
+  for (int k = 0; k < kBlobArrays; k++)
+    if (hdr.off[k] < kBlobHeaderBytes || hdr.off[k] >= (uint64_t)bytes) return fail(MGPU_E_INVALID_ARG, "corrupt chip-table blob");
+  if (hdr.index_system != MGPU_H3 && hdr.index_system != MGPU_BNG) return fail(MGPU_E_INVALID_ARG, "corrupt chip-table blob");
+  return MGPU_OK;
+}
+
+namespace mgpu {
+int64_t blob_bytes_of_header(const void* header) {
+  BlobHeader h;
+  memcpy(&h, header, sizeof h);
+  if (h.magic != kBlobMagic || h.version != kBlobVersion) return 0;
+  return (int64_t)h.blob_bytes;
+}
+
+int32_t adopt_device_blob(mgpu_ctx* ctx, void* dev_blob, int64_t bytes, mgpu_chips** out) {
+  BlobHeader hdr;
+  HIP_TRY(hipMemcpy(&hdr, dev_blob, sizeof hdr, hipMemcpyDeviceToHost));
+  if (int32_t st = check_header(hdr, bytes)) return st;
+  mgpu_chips* ch = new mgpu_chips();
+  ch->device = ctx->device;
+  ch->blob = dev_blob;
+  ch->bytes = (size_t)bytes;
+  ch->index_system = hdr.index_system;
+  ch->view = view_from_header(hdr, (uint8_t*)ch->blob);
+  ch->n_vertices = hdr.n_vertices;
+  *out = ch;
+  return MGPU_OK;
+}
+}  // namespace mgpu
+
 extern "C" {
+
+int32_t mgpu_chips_host_blob(int32_t index_system, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
+                             const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb, uint8_t** out,
+                             int64_t* bytes) {
+  if (!out || !bytes) return fail(MGPU_E_INVALID_ARG, "out/bytes is NULL");
+  std::vector<uint8_t> host;
+  BlobHeader hdr;
+  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr)) return st;
+  uint8_t* p = (uint8_t*)malloc(host.size());
+  if (!p) return fail(MGPU_E_INTERNAL, "out of host memory (%zu bytes)", host.size());
+  memcpy(p, host.data(), host.size());
+  *out = p;
+  *bytes = (int64_t)host.size();
+  return MGPU_OK;
+}
+
+int32_t mgpu_host_free(void* p) {
+  free(p);
+  return MGPU_OK;
+}
+
+int32_t mgpu_host_blob_info(const void* host_blob, int64_t bytes, int32_t* index_system, int64_t* n_chips,
+                            int64_t* n_cells, int64_t* n_vertices) {
+  if (!host_blob || bytes < (int64_t)kBlobHeaderBytes) return fail(MGPU_E_INVALID_ARG, "blob too small");
+  BlobHeader hdr;
+  memcpy(&hdr, host_blob, sizeof hdr);
+  if (int32_t st = check_header(hdr, bytes)) return st;
+  if (index_system) *index_system = hdr.index_system;
+  if (n_chips) *n_chips = hdr.n_chips;
+  if (n_cells) *n_cells = hdr.n_cells;
+  if (n_vertices) *n_vertices = hdr.n_vertices;
+  return MGPU_OK;
+}
+
+int32_t mgpu_chips_upload_blob(mgpu_ctx* ctx, const void* host_blob, int64_t bytes, mgpu_chips** out) {
+  if (!ctx || !out) return fail(MGPU_E_INVALID_ARG, "ctx/out is NULL");
+  if (int32_t st = mgpu_host_blob_info(host_blob, bytes, nullptr, nullptr, nullptr, nullptr)) return st;
+  if (int32_t st = set_device(ctx->device)) return st;
+  void* d = nullptr;
+  HIP_TRY(hipMalloc(&d, (size_t)bytes));
+  hipError_t e = hipMemcpy(d, host_blob, (size_t)bytes, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    hipFree(d);
+    return fail(MGPU_E_DEVICE, "hipMemcpy: %s", hipGetErrorString(e));
+  }
+  int32_t st = mgpu::adopt_device_blob(ctx, d, bytes, out);
+  if (st) hipFree(d);
+  return st;
+}
 
 int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, const int64_t* cell,
                           const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
@@ -1333,27 +1413,7 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
   BlobHeader hdr;
   if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr))
     return st;
-  if (int32_t st = set_device(ctx->device)) return st;
-  const size_t total = host.size();
-  mgpu_chips* ch = new mgpu_chips();
-  ch->device = ctx->device;
-  hipError_t e1 = hipMalloc(&ch->blob, total);
-  if (e1 != hipSuccess) {
-    delete ch;
-    return fail(MGPU_E_DEVICE, "hipMalloc(%zu): %s", total, hipGetErrorString(e1));
-  }
-  hipError_t e2 = hipMemcpy(ch->blob, host.data(), total, hipMemcpyHostToDevice);
-  if (e2 != hipSuccess) {
-    hipFree(ch->blob);
-    delete ch;
-    return fail(MGPU_E_DEVICE, "hipMemcpy: %s", hipGetErrorString(e2));
-  }
-  ch->bytes = total;
-  ch->index_system = hdr.index_system;
-  ch->view = view_from_header(hdr, (uint8_t*)ch->blob);
-  ch->n_vertices = hdr.n_vertices;
-  *out = ch;
-  return MGPU_OK;
+  return mgpu_chips_upload_blob(ctx, host.data(), (int64_t)host.size(), out);
 }
 
 int32_t mgpu_chips_destroy(mgpu_chips* chips) {
@@ -1385,19 +1445,17 @@ int32_t mgpu_chips_from_device_blob(mgpu_ctx* ctx, const void* device_ptr, int64
   if (bytes < (int64_t)kBlobHeaderBytes) return fail(MGPU_E_INVALID_ARG, "blob too small");
   BlobHeader hdr;
   HIP_TRY(hipMemcpy(&hdr, device_ptr, sizeof hdr, hipMemcpyDeviceToHost));
-  if (hdr.magic != kBlobMagic || hdr.version != kBlobVersion) return fail(MGPU_E_INVALID_ARG, "not a chip-table blob");
-  for (int k = 0; k < kBlobArrays; k++)
-    if (hdr.off[k] >= (uint64_t)bytes) return fail(MGPU_E_INVALID_ARG, "corrupt chip-table blob");
-  mgpu_chips* ch = new mgpu_chips();
-  ch->device = ctx->device;
-  HIP_TRY(hipMalloc(&ch->blob, bytes));
-  HIP_TRY(hipMemcpy(ch->blob, device_ptr, bytes, hipMemcpyDeviceToDevice));
-  ch->bytes = bytes;
-  ch->index_system = hdr.index_system;
-  ch->view = view_from_header(hdr, (uint8_t*)ch->blob);
-  ch->n_vertices = hdr.n_vertices;
-  *out = ch;
-  return MGPU_OK;
+  if (int32_t st = check_header(hdr, bytes)) return st;
+  void* d = nullptr;
+  HIP_TRY(hipMalloc(&d, bytes));
+  hipError_t e = hipMemcpy(d, device_ptr, bytes, hipMemcpyDeviceToDevice);
+  if (e != hipSuccess) {
+    hipFree(d);
+    return fail(MGPU_E_DEVICE, "hipMemcpy: %s", hipGetErrorString(e));
+  }
+  int32_t st = mgpu::adopt_device_blob(ctx, d, bytes, out);
+  if (st) hipFree(d);
+  return st;
 }
 
 int32_t mgpu_st_contains(mgpu_ctx* ctx, const mgpu_chips* chips, const int64_t* chip_row, const double* x,
@@ -1482,11 +1540,60 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   a.tie_cap = kTieCap;
   HIP_TRY(hipMemsetAsync(base, 0, kWsCounters, s));
   HIP_TRY(hipMemsetAsync(base + L.ties, 0, 8, s));
-  HIP_TRY(hipMemsetAsync(base + L.gsum, 0, 2 * ((size_t)tiles / 32 + 1) * 4, s));
+  // the split pipeline (kernels.h SplitArgs) when the chip table has a pixel index for
+  // this resolution and no cell holds more than 32 chips (MGPU_SPLIT=0: always fused)
+  const char* sp = getenv("MGPU_SPLIT");
+  const bool split = !(sp && atoi(sp) == 0) && n > 0 && chips->view.raster_mode != mgpu::kRasterNone && a.res_match &&
+                     (is == MGPU_H3 || res == chips->view.res) && chips->view.max_cell_chips <= 32 &&
+                     (a.ablate == 0 || a.ablate >= 10);  // (>= 10: split-pipeline profiling switches)
+  mgpu::SplitArgs sa{};
+  if (split) {
+    const int64_t nc = mgpu::split_chunks(n), C = mgpu::split_chunk();
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+      const size_t o = off;
+      off = align_up(off + bytes, 256);
+      return o;
+    };
+    const size_t o_codes = carve((size_t)nc * C * 4), o_idx = carve((size_t)nc * C * 2), o_res = carve((size_t)nc * C * 8);
+    const size_t o_pairs = carve(nc * 4), o_mixed = carve(nc * 4), o_cand = carve(nc * 4), o_off = carve(nc * 8);
+    if (off > ctx->split_bytes) {
+      if (ctx->split_ws) HIP_TRY(hipFree(ctx->split_ws));
+      ctx->split_ws = nullptr;
+      ctx->split_bytes = 0;
+      HIP_TRY(hipMalloc(&ctx->split_ws, off));
+      ctx->split_bytes = off;
+    }
+    auto* sb = (uint8_t*)ctx->split_ws;
+    sa.codes = sb + o_codes;
+    sa.mixed_idx = (uint16_t*)(sb + o_idx);
+    sa.chunk_pairs = (uint32_t*)(sb + o_pairs);
+    sa.chunk_mixed = (uint32_t*)(sb + o_mixed);
+    sa.chunk_off = (uint64_t*)(sb + o_off);
+    a.group_sum = sa.chunk_pairs;
+    a.group_cand = (uint32_t*)(sb + o_cand);
+    a.mixed_idx = sa.mixed_idx;
+    a.mixed_res = (uint64_t*)(sb + o_res);
+    a.chunk_mixed = sa.chunk_mixed;
+    sa.point_id = point_id;
+    sa.id_base = id_base;
+    sa.capacity = capacity;
+    sa.out_point = out_point;
+    sa.out_poly = out_poly;
+    sa.j = a;
+    HIP_TRY(hipMemsetAsync(a.group_cand, 0, nc * 4, s));
+  } else {
+    HIP_TRY(hipMemsetAsync(base + L.gsum, 0, 2 * ((size_t)tiles / 32 + 1) * 4, s));
+  }
   if (timed) HIP_TRY(hipEventRecord(ctx->ev0, s));
-  HIP_TRY(mgpu::launch_join(is, a, e, s, timed ? ctx->ev2 : nullptr));
+  if (split)
+    HIP_TRY(mgpu::launch_split(is, sa, s, timed ? ctx->ev2 : nullptr, timed ? ctx->ev3 : nullptr));
+  else
+    HIP_TRY(mgpu::launch_join(is, a, e, s, timed ? ctx->ev2 : nullptr));
   if (timed) HIP_TRY(hipEventRecord(ctx->ev1, s));
   auto& L2 = ctx->last;
+  L2.split = split;
+  L2.sargs = sa;
   L2.chips = chips;
   L2.is = is;
   L2.res = res;
@@ -1563,11 +1670,20 @@ int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_
     if (n > 0) hipEventElapsedTime(&ms2, ctx->ev0, ctx->ev2);
     stats->kernel_ms = ms;
     stats->stream_kernel_ms = ms2;
+    stats->mixed_kernel_ms = stats->emit_kernel_ms = 0;
+    if (ctx->last.split && n > 0) {
+      float m3 = 0;
+      hipEventElapsedTime(&m3, ctx->ev0, ctx->ev3);
+      stats->mixed_kernel_ms = m3 - ms2;
+      stats->emit_kernel_ms = ms - m3;
+    }
+    stats->pipeline = ctx->last.split ? MGPU_PIPELINE_SPLIT : MGPU_PIPELINE_FUSED;
   }
   // pool records used (counters[5]) within the pool: every record is still in the
-  // workspace, so a larger output can be written by mgpu_pip_join_fetch alone
+  // workspace, so a larger output can be written by mgpu_pip_join_fetch alone (the split
+  // pipeline keeps its codes and mixed answers: always)
   ctx->last.total = (int64_t)h[0];
-  ctx->last.pool_ok = (int64_t)h[5] <= capacity + ctx->last.n_tiles * mgpu::join_pend_cap();
+  ctx->last.pool_ok = ctx->last.split || (int64_t)h[5] <= capacity + ctx->last.n_tiles * mgpu::join_pend_cap();
   if (h[2]) {
     ctx->last.valid = false;
     if (is == MGPU_BNG) return fail(MGPU_E_NAN, "NaN coordinates are not supported. (%llu points)", h[2]);
@@ -1595,6 +1711,15 @@ int32_t mgpu_pip_join_fetch(mgpu_ctx* ctx, int64_t capacity, int64_t* out_n_pair
     int64_t cnt = 0;
     return mgpu_pip_join(ctx, c.chips, c.is, c.res, c.x, c.y, c.point_id, c.id_base, c.n, capacity, out_n_pairs ? out_n_pairs : &cnt,
                          out_point_id, out_polygon_id, stream, nullptr);
+  }
+  if (L.split) {
+    mgpu::SplitArgs sa = L.sargs;
+    sa.capacity = capacity;
+    sa.out_point = out_point_id;
+    sa.out_poly = out_polygon_id;
+    HIP_TRY(mgpu::launch_split_emit(L.is, sa, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return MGPU_OK;
   }
   mgpu::EmitArgs e = L.emit;
   e.capacity = capacity;
@@ -1719,6 +1844,21 @@ int32_t mgpu_test_raster_host(int32_t index_system, int32_t res, int64_t n_chips
     out_kind[i] = ce ? 1 : 0;
     out_first[i] = (uint32_t)ce;
     out_mask[i] = (uint32_t)(ce >> 32);
+  }
+  return MGPU_OK;
+}
+
+int32_t mgpu_test_blob_contains_host(const void* host_blob, int64_t bytes, int64_t n, const int64_t* chip_row,
+                                     const double* x, const double* y, int8_t* out) {
+  if (int32_t st = mgpu_host_blob_info(host_blob, bytes, nullptr, nullptr, nullptr, nullptr)) return st;
+  BlobHeader hdr;
+  memcpy(&hdr, host_blob, sizeof hdr);
+  const mgpu::ChipTableView v = view_from_header(hdr, (uint8_t*)host_blob);
+  for (int64_t i = 0; i < n; i++) {
+    const int64_t r = chip_row[i];
+    if (r < 0 || r >= (int64_t)v.n_chips) return fail(MGPU_E_INVALID_ARG, "chip row %lld out of range", (long long)r);
+    const uint32_t c = v.row_to_chip[r];
+    out[i] = (v.chip_flags[c] & mgpu::kChipNoGeom) ? -1 : (mgpu::pip::chip_contains_strips(v, c, x[i], y[i]) ? 1 : 0);
   }
   return MGPU_OK;
 }

@@ -1,0 +1,52 @@
+// Internal: the C-ABI handle types and the helpers capi.cpp shares with comm.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mosaic_gpu.h"
+#include "chip_table.h"
+#include "kernels.h"
+
+struct mgpu_ctx {
+  int device = 0;
+  // workspace: tile status words + ticket + counters
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
+  void* comm = nullptr;  // comm.cpp CommState: the RCCL communicator (mgpu_comm_init)
+  // the split pipeline's per-point buffers (codes, mixed lists and answers), grown on demand
+  void* split_ws = nullptr;
+  size_t split_bytes = 0;
+  // the last mgpu_pip_join on this context, whose pair records stay in the workspace
+  // until the next call (mgpu_pip_join_fetch)
+  struct {
+    bool valid = false, pool_ok = false;
+    const mgpu_chips* chips = nullptr;
+    int32_t is = 0, res = 0;
+    const double *x = nullptr, *y = nullptr;
+    const int64_t* point_id = nullptr;
+    int64_t id_base = 0, n = 0, total = 0;
+    mgpu::EmitArgs emit{};
+    int64_t n_tiles = 0;
+    bool split = false;
+    mgpu::SplitArgs sargs{};
+  } last;
+};
+
+struct mgpu_chips {
+  int device = 0;
+  int32_t index_system = MGPU_H3;
+  void* blob = nullptr;
+  size_t bytes = 0;
+  mgpu::ChipTableView view{};
+  int64_t n_vertices = 0;
+};
+
+namespace mgpu {
+int32_t set_error(int32_t code, const char* fmt, ...);
+// Size of the whole chip-table blob from its 1 KiB header (host copy); 0 if not a blob.
+int64_t blob_bytes_of_header(const void* header);
+constexpr int64_t kBlobHeaderSize = 1024;
+// Take ownership of a device allocation holding a complete blob (no copy).
+int32_t adopt_device_blob(mgpu_ctx* ctx, void* dev_blob, int64_t bytes, mgpu_chips** out);
+}  // namespace mgpu

@@ -157,11 +157,14 @@ struct ChipTableView {
   //       to the last pixel (the raster spans `bbox`);
   //   BNG: pixel = (easting / pix, northing / pix) in whole metres, minus (px0, py0); pix
   //       divides the cell edge, so every pixel lies in one cell.
+  uint32_t max_cell_chips;     // chips of the fullest cell
   int32_t raster_mode;         // kRasterNone / kRasterLonLat / kRasterBng
   uint32_t raster_nx, raster_ny;
   uint32_t raster_pix;         // BNG pixel edge (metres)
   int32_t raster_px0, raster_py0;
   double raster_x0, raster_y0, raster_inv_dx, raster_inv_dy;
+  uint32_t raster_pc[4];       // lonlat: classes are ordered by match count; class c has k + 1
+                               // matches for raster_pc[k - 1] <= c < raster_pc[k] (k < 4)
   const uint16_t* raster;      // [ny * nx] classes
   const uint64_t* raster_cls;  // [classes]
 };

@@ -32,7 +32,39 @@ struct JoinArgs {
   int64_t tie_cap;                  // near-tie points the H3 route resolved (zero ties[0] before launch)
   int ablate;                       // profiling only (MGPU_ABLATE): 1 = no PIP (border = miss), 2 = no probe,
                                     // 3 = no projection either
+  // split pipeline (launch_split): the mixed points of chunk c are the chunk's listed
+  // points c * split_chunk() + mixed_idx[c * split_chunk() + m], m < chunk_mixed[c]; their
+  // answers (first chip | match mask << 32) go to mixed_res at the same list position;
+  // group_sum / group_cand are then per chunk
+  const uint16_t* mixed_idx;
+  uint64_t* mixed_res;
+  const uint32_t* chunk_mixed;
 };
+
+// The split pipeline (a chip table with a pixel index and at most 32 chips per cell):
+//   classify_kernel   per point: pixel class -> code (pure answer or "mixed"); per chunk of
+//                     split_chunk() points the pure pairs and the ordered list of mixed points
+//   pip_mixed_kernel  the mixed points, tiles of join_tile_points() gathered from the lists
+//                     (+ pip_mixed_fix_kernel for tiles holding an H3 near-tie)
+//   tile_scan_kernel  chunk pair counts -> output offsets
+//   split_emit_kernel codes + mixed answers -> ordered (point_id, polygon_id) pairs
+struct SplitArgs {
+  JoinArgs j;                       // points, chips, counters, dirty list, mixed lists
+  void* codes;                      // [n] u16 (H3: pixel class) / u32 (BNG: first << 8 | mask)
+  uint32_t* chunk_pairs;            // [chunks] (= j.group_sum)
+  uint32_t* chunk_mixed;            // [chunks]
+  uint16_t* mixed_idx;              // [chunks * split_chunk()]
+  uint64_t* chunk_off;              // [chunks] written by the scan
+  const int64_t* point_id;
+  int64_t id_base;
+  int64_t capacity;
+  int64_t* out_point;
+  int32_t* out_poly;
+};
+int64_t split_chunk();
+int64_t split_chunks(int64_t n);
+hipError_t launch_split(int is, const SplitArgs& a, hipStream_t s, hipEvent_t after_classify, hipEvent_t after_mixed);
+hipError_t launch_split_emit(int is, const SplitArgs& a, hipStream_t s);
 
 // pair_emit_kernel: tile records -> ordered (point_id, polygon_id) output
 struct EmitArgs {

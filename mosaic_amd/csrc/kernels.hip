@@ -283,7 +283,7 @@ __device__ __forceinline__ bool chip_is_core(const ChipTableView& t, const Range
 // Phase 1 for one point: its core chips match at once; every border chip becomes a
 // candidate (chip, point, slot j) in the tile's LDS list (a full list: the fast kernel
 // abandons the tile, the fix kernel evaluates the candidate on the spot).
-template <bool SLOW>
+template <bool SLOW, int CAND_CAP = kCandCap>
 __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, const Range& r, double px, double py,
                                             bool do_pip, bool& any_tie, uint32_t* s_ncand, uint16_t* s_cand_pj,
                                             double2* s_cand_xy, uint32_t* s_first, uint16_t* s_cnt,
@@ -302,7 +302,7 @@ __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, cons
     uint32_t j0 = atomicAdd(s_ncand, nb);
     for (uint32_t b = border; b; b &= b - 1) {
       const uint32_t j = __builtin_ctz(b);
-      if (j0 < (uint32_t)kCandCap) {
+      if (j0 < (uint32_t)CAND_CAP) {
         s_cand_pj[j0] = (uint16_t)(li | (j << 10));
         if (j0 < (uint32_t)kStash) s_cand_xy[j0] = make_double2(px, py);
       } else if (!SLOW) {
@@ -322,8 +322,8 @@ __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, cons
 
 
 // Profiling builds (-DMGPU_STAMPS): thread 0 of each tile adds the wall-clock ticks
-// (100 MHz) spent in each phase to counters[10 + phase]: 1 = phase 1, 2 = phase 2,
-// 3 = phase 2b, 4 = phase 3 (output).
+// (100 MHz) spent in each phase to counters[9 + phase]: 1 = phase 1 (with a pixel index:
+// its pass B), 2 = phase 2, 3 = phase 2b, 4 = phase 3 (output), 5 = pixel-index pass A.
 #ifdef MGPU_STAMPS
 #define MGPU_STAMP(ph)                                                              \
   do {                                                                              \
@@ -339,10 +339,23 @@ __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, cons
   } while (0)
 #endif
 
+// the split pipeline's chunk (classify_kernel / split_emit_kernel workgroup): its points
+// and at most kChunkTiles tiles of mixed points.  A mixed tile holds kGTile points; mixed
+// points lie near chip edges, with ~2 border-chip candidates each, so its candidate
+// lists are longer (kGCandCap, kGMixCap).
+constexpr int kChunk = 4096;
+constexpr int kGTile = kTile;
+constexpr int kChunkTiles = kChunk / kGTile;
+constexpr int kGCandCap = 3 * kTile;
+constexpr int kGMixCap = kTile;
+
 // One tile (see the phase comment above).  SLOW = false: the streaming kernel; a
 // tile with a near-tie point is queued for pip_fix_kernel and abandoned after phase 1.
 // SLOW = true: the fix kernel; near-ties go through the H3 route.
-template <int IS, bool SLOW>
+// G = true: the split pipeline's mixed points -- tile = chunk * kChunkTiles + t covers
+// list positions [t * kTile, ...) of the chunk's mixed list; the phases are the same,
+// the result is each point's (first chip, match mask) in mixed_res (no pair records).
+template <int IS, bool SLOW, bool G = false>
 __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile) {
   __shared__ uint32_t s_ncand, s_nmix;
   __shared__ uint32_t s_wave_tot[kBlock / 64];
@@ -350,14 +363,31 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   __shared__ uint32_t s_mask[kTile];    // bit j: chip first + j matches (j < 32)
   __shared__ uint16_t s_cnt[kTile];     // chips of the point's cell (0: none)
   // phases 1-2: candidate list; phase 3: output staging (same bytes)
-  __shared__ __attribute__((aligned(16))) uint8_t s_buf[kOutCap * 6];
+  constexpr int kCap = G ? kGCandCap : kCandCap, kMix = G ? kGMixCap : kMixCap;
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[G ? kStash * 16 + kGCandCap * 2 + kGMixCap * 2 : kOutCap * 6];
   // candidate c = chip s_first[li] + j of point li, s_cand_pj[c] = li | j << 10; the
   // first kStash candidates also keep the point's coordinates (no re-read in phase 2)
   double2* s_cand_xy = (double2*)s_buf;                             // [kStash]
   uint16_t* s_cand_pj = (uint16_t*)(s_buf + kStash * 16);           // [kCandCap]
-  uint16_t* s_mix = (uint16_t*)(s_buf + kStash * 16 + kCandCap * 2);  // [kMixCap] candidate index
+  uint16_t* s_mix = (uint16_t*)(s_buf + kStash * 16 + kCap * 2);  // [kMix] candidate index
   int32_t* s_out_poly = (int32_t*)s_buf;                          // [kOutCap]
   uint16_t* s_out_li = (uint16_t*)(s_buf + kOutCap * 4);          // [kOutCap]
+  __shared__ uint16_t s_gidx[G ? kTile : 1];  // G: the point's index within its chunk
+
+  // G: the tile's slice of its chunk's mixed list
+  const uint32_t chunk = G ? tile / kChunkTiles : 0u;
+  const int64_t gbase = (int64_t)chunk * kChunk;         // first point of the chunk
+  const int64_t lbase = gbase + (int64_t)(tile % kChunkTiles) * kGTile;  // first list position
+  uint32_t gcount = 0;
+  if (G) {
+    const uint32_t nm = a.chunk_mixed[chunk], t0 = (tile % kChunkTiles) * kGTile;
+    if (nm <= t0) return;
+    gcount = nm - t0 < (uint32_t)kGTile ? nm - t0 : (uint32_t)kGTile;
+    for (uint32_t li = threadIdx.x; li < (uint32_t)kTile; li += kBlock)
+      s_gidx[li] = li < gcount ? a.mixed_idx[lbase + li] : (uint16_t)0;
+  }
+#define MGPU_PT(li) (G ? gbase + (int64_t)s_gidx[li] : (int64_t)tile * kTile + (li))
+#define MGPU_VALID(li) (G ? (uint32_t)(li) < gcount : (int64_t)tile * kTile + (li) < a.n)
 
 #ifdef MGPU_STAMPS
   uint64_t st_t = 0;
@@ -383,7 +413,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #else
 #define MGPU_LDPT(ptr) (*(ptr))
 #endif
-  if (!SLOW && kBlock == 64 && t.raster_mode != kRasterNone && a.ablate == 0 && res_match &&
+  if (!G && !SLOW && kBlock == 64 && t.raster_mode != kRasterNone && a.ablate == 0 && res_match &&
       (IS == MGPU_H3 || a.res == t.res)) {
     // pass A: the lane's four points load together, then their pixels' classes: a
     // pure pixel's matches are final (no projection, no candidates); the rest are
@@ -440,6 +470,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
       nlist += (uint32_t)__popcll(bal);
     }
     __syncthreads();
+    MGPU_STAMP(5);  // (profiling: pass A)
     // pass B: the listed points, 64 at a time with every lane busy (coordinates from
     // the owning lane's registers)
     for (uint32_t q0 = 0; q0 < nlist; q0 += kBlock) {
@@ -461,7 +492,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         Range r = chip_probe<IS, SLOW>(t, px, py, a.res, res_match, &ok, &tie, a.ablate, &gi);
         if (gi != kNoEntry) r = grid_range(t.grid[gi]);
         any_tie |= tie;
-        phase1_item<SLOW>(t, li, r, px, py, do_pip, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
+        phase1_item<SLOW, kCap>(t, li, r, px, py, do_pip, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
       }
     }
   } else if (IS == MGPU_BNG) {
@@ -471,9 +502,10 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     double bx[kItems], by[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
-      const int64_t p = base + k * kBlock + threadIdx.x;
+      const int li = k * kBlock + threadIdx.x;
       bx[k] = by[k] = 0.0;
-      if (p < a.n) {
+      if (MGPU_VALID(li)) {
+        const int64_t p = MGPU_PT(li);
         bx[k] = MGPU_LDPT(&a.x[p]);
         by[k] = MGPU_LDPT(&a.y[p]);
       }
@@ -484,7 +516,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     for (int k = 0; k < kItems; k++) {
       r[k] = Range{0, 0, 0};
       gi[k] = kNoEntry;
-      if (base + k * kBlock + threadIdx.x < a.n) {
+      if (MGPU_VALID(k * kBlock + threadIdx.x)) {
         bool ok, tie;
         r[k] = chip_probe<IS, SLOW>(t, bx[k], by[k], a.res, res_match, &ok, &tie, a.ablate, &gi[k]);
         any_bad |= !ok;
@@ -496,27 +528,27 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
       if (gi[k] != kNoEntry) r[k] = grid_range(ge[k]);
-      phase1_item<SLOW>(t, k * kBlock + threadIdx.x, r[k], bx[k], by[k], do_pip, any_tie, &s_ncand, s_cand_pj,
+      phase1_item<SLOW, kCap>(t, k * kBlock + threadIdx.x, r[k], bx[k], by[k], do_pip, any_tie, &s_ncand, s_cand_pj,
                         s_cand_xy, s_first, s_cnt, s_mask);
     }
   } else {
     // one item ahead: item k + 1's coordinates load while item k projects
     double nx = 0.0, ny = 0.0;
-    if (base + threadIdx.x < a.n) {
-      nx = MGPU_LDPT(&a.x[base + threadIdx.x]);
-      ny = MGPU_LDPT(&a.y[base + threadIdx.x]);
+    if (MGPU_VALID(threadIdx.x)) {
+      nx = MGPU_LDPT(&a.x[MGPU_PT(threadIdx.x)]);
+      ny = MGPU_LDPT(&a.y[MGPU_PT(threadIdx.x)]);
     }
 #pragma unroll 1
     for (int k = 0; k < kItems; k++) {
       const int li = k * kBlock + threadIdx.x;
-      const int64_t p = base + li;
+      const int64_t p = MGPU_PT(li);
       Range r{0, 0, 0};
       const double px = nx, py = ny;
-      if (k + 1 < kItems && p + kBlock < a.n) {
-        nx = MGPU_LDPT(&a.x[p + kBlock]);
-        ny = MGPU_LDPT(&a.y[p + kBlock]);
+      if (k + 1 < kItems && MGPU_VALID(li + kBlock)) {
+        nx = MGPU_LDPT(&a.x[MGPU_PT(li + kBlock)]);
+        ny = MGPU_LDPT(&a.y[MGPU_PT(li + kBlock)]);
       }
-      if (p < a.n) {
+      if (MGPU_VALID(li)) {
         bool ok, tie;
         if (a.ablate == 3) {  // profiling: no projection, no probe
           ok = true;
@@ -533,7 +565,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         any_bad |= !ok;
         any_tie |= tie;
       }
-      phase1_item<SLOW>(t, li, r, px, py, do_pip, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
+      phase1_item<SLOW, kCap>(t, li, r, px, py, do_pip, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
     }
   }
   count_wave(&a.counters[2], any_bad);
@@ -543,17 +575,19 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     if (threadIdx.x == 0) {
       const unsigned int q = atomicAdd(a.n_dirty, 1u);
       a.dirty[q] = tile;
-      a.tile_count[tile] = 0;
-      a.tile_where[tile] = kNoDst;
-      a.tile_pend[tile] = 0;
+      if (!G) {
+        a.tile_count[tile] = 0;
+        a.tile_where[tile] = kNoDst;
+        a.tile_pend[tile] = 0;
+      }
     }
     return;
   }
   __syncthreads();
   MGPU_STAMP(1);
-  const uint32_t ncand = s_ncand < (uint32_t)kCandCap ? s_ncand : (uint32_t)kCandCap;
+  const uint32_t ncand = s_ncand < (uint32_t)kCap ? s_ncand : (uint32_t)kCap;
   // per scan group, not one global counter: same-address atomics from every tile serialize
-  if (threadIdx.x == 0 && s_ncand) atomicAdd(&a.group_cand[tile / kScanGroup], s_ncand);
+  if (threadIdx.x == 0 && s_ncand) atomicAdd(&a.group_cand[G ? chunk : tile / kScanGroup], s_ncand);
 
   // ---- phase 2: lane per candidate: envelope / rectangle / classification grid.
   // Candidates in a mixed grid cell (~1 in 8) are listed again and evaluated in
@@ -563,7 +597,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     const uint32_t pj = s_cand_pj[c];
     const int li = pj & 1023;
     const uint32_t ch = s_first[li] + (pj >> 10);
-    const int64_t p = base + li;
+    const int64_t p = MGPU_PT(li);
     bool hit;
     if (a.ablate == 4) {  // profiling: candidate list only
       hit = (ch ^ pj) == 0x7FFFFFFF;
@@ -582,7 +616,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
       hit = q == pip::kQuickYes;
       if (q >= pip::kQuickStrips && a.ablate != 5) {
         const uint32_t m = atomicAdd(&s_nmix, 1u);
-        if (m < (uint32_t)kMixCap && (SLOW || q == pip::kQuickStrips)) {
+        if (m < (uint32_t)kMix && (SLOW || q == pip::kQuickStrips)) {
           s_mix[m] = (uint16_t)c;
           if (MGPU_DEFER && !SLOW) {
             // tentative match; pip_resolve_kernel walks the strip and decides (the
@@ -607,15 +641,17 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     if (threadIdx.x == 0) {
       const unsigned int q = atomicAdd(a.n_dirty, 1u);
       a.dirty[q] = tile;
-      a.tile_count[tile] = 0;
-      a.tile_where[tile] = kNoDst;
-      a.tile_pend[tile] = 0;
+      if (!G) {
+        a.tile_count[tile] = 0;
+        a.tile_where[tile] = kNoDst;
+        a.tile_pend[tile] = 0;
+      }
     }
     return;
   }
   __syncthreads();
   MGPU_STAMP(2);
-  const uint32_t nmix = s_nmix < (uint32_t)kMixCap ? s_nmix : (uint32_t)kMixCap;
+  const uint32_t nmix = s_nmix < (uint32_t)kMix ? s_nmix : (uint32_t)kMix;
 #ifdef MGPU_STATS
   uint32_t st_edges = 0;
 #endif
@@ -627,7 +663,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     const uint32_t pj = s_cand_pj[c];
     const int li = pj & 1023;
     const uint32_t ch = s_first[li] + (pj >> 10);
-    const int64_t p = base + li;
+    const int64_t p = MGPU_PT(li);
     double px, py;
     if (c < (uint32_t)kStash) {
       const double2 q = s_cand_xy[c];
@@ -660,6 +696,18 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   __syncthreads();
 
   MGPU_STAMP(3);
+  if (G) {
+    // the split pipeline: each listed point's answer, and the chunk's pair count
+    uint32_t mine = 0;
+    for (uint32_t li = threadIdx.x; li < gcount; li += kBlock) {
+      const uint32_t m = s_mask[li];
+      a.mixed_res[lbase + li] = (uint64_t)s_first[li] | ((uint64_t)m << 32);
+      mine += __popc(m);
+    }
+    const unsigned long long tot = wave_sum_u64(mine);
+    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&a.group_sum[chunk], (uint32_t)tot);
+    return;
+  }
   // ---- phase 3: lane l owns points 4l .. 4l+3 (input order)
   const int l0 = threadIdx.x * kItems;
   uint32_t mine = 0;
@@ -669,7 +717,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     mine += __popc(s_mask[li]);
     const uint32_t cnt = s_cnt[li];
     if (SLOW && cnt > (uint32_t)kMaskBits) {  // chips past the 32nd of the cell
-      const int64_t p = base + li;
+      const int64_t p = MGPU_PT(li);
       const Range r{s_first[li], cnt, 0};
       for (uint32_t j = kMaskBits; j < cnt; j++)
         mine += (chip_is_core(t, r, j) || (do_pip && pip::chip_contains_strips(t, r.first + j, a.x[p], a.y[p]))) ? 1 : 0;
@@ -693,9 +741,11 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     if (threadIdx.x == 0) {
       const unsigned int q = atomicAdd(a.n_dirty, 1u);
       a.dirty[q] = tile;
-      a.tile_count[tile] = 0;
-      a.tile_where[tile] = kNoDst;
-      a.tile_pend[tile] = 0;
+      if (!G) {
+        a.tile_count[tile] = 0;
+        a.tile_where[tile] = kNoDst;
+        a.tile_pend[tile] = 0;
+      }
     }
     return;
   }
@@ -765,7 +815,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     const uint32_t cnt = s_cnt[li];
     if (!cnt) continue;
     const uint32_t first = s_first[li];
-    const int64_t p = base + li;
+    const int64_t p = MGPU_PT(li);
     uint32_t m = s_mask[li];
     const uint32_t nj = cnt < (uint32_t)kMaskBits ? cnt : (uint32_t)kMaskBits;
     for (uint32_t j = 0; j < cnt; j++) {
@@ -858,6 +908,228 @@ __global__ __launch_bounds__(kBlock) void pip_fix_kernel(JoinArgs a) {
   for (uint32_t q = blockIdx.x; q < nd; q += gridDim.x) {
     join_tile<IS, true>(a, a.dirty[q]);
     __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- split pipeline
+// (kernels.h SplitArgs).  A chip table with a pixel index answers most points from their
+// pixel; the fused kernel still pays a tile's full phase structure (and its memory round
+// trips) for them.  The split pipeline streams instead: classify_kernel touches every
+// point once (16 B read, one pixel load, a 2- or 4-byte code written), the few mixed
+// points go through join_tile's phases gathered into full tiles, and split_emit_kernel
+// writes the ordered pairs from the codes.
+constexpr int kClsBlock = 256;
+constexpr int kClsItems = kChunk / kClsBlock;  // points per thread
+constexpr int kClsBatch = 8;                   // of which in flight together
+static_assert(kClsItems * (kClsBlock / 64) == 64, "one wave scans a chunk's ballots");
+constexpr uint32_t kCodeMixed32 = 0xFFFFFFFFu;
+
+template <int IS>
+struct CodeOf {
+  using T = uint16_t;  // H3: the pixel class (kPixMixed: mixed)
+};
+template <>
+struct CodeOf<MGPU_BNG> {
+  using T = uint32_t;  // BNG: first chip << 8 | match mask (0: none, ~0: mixed)
+};
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+template <int IS>
+__global__ __launch_bounds__(kClsBlock) void classify_kernel(SplitArgs sa) {
+  using Code = typename CodeOf<IS>::T;
+  const JoinArgs& a = sa.j;
+  const ChipTableView& t = a.chips;
+  __shared__ unsigned long long s_bal[64];  // [item][wave]: the wave's mixed points
+  __shared__ uint32_t s_pos[64];
+  __shared__ uint32_t s_red[kClsBlock / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  Code* codes = (Code*)sa.codes;
+  uint32_t pairs = 0, mixed_bits = 0;
+  bool any_bad = false;
+  for (int b = 0; b < kClsItems; b += kClsBatch) {
+    double bx[kClsBatch], by[kClsBatch];
+#pragma unroll
+    for (int k = 0; k < kClsBatch; k++) {
+      const int64_t p = c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x;
+      bx[k] = by[k] = 0.0;
+      if (p < a.n) {
+        bx[k] = __builtin_nontemporal_load(&a.x[p]);
+        by[k] = __builtin_nontemporal_load(&a.y[p]);
+      }
+    }
+    uint32_t ri[kClsBatch], gix[kClsBatch];
+#pragma unroll
+    for (int k = 0; k < kClsBatch; k++) {
+      ri[k] = kNoPixel;
+      gix[k] = 0;
+      if (c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x < a.n) {
+        bool ok;
+        ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &gix[k]);
+        any_bad |= !ok;
+        if (a.ablate == 11) ri[k] = bx[k] == 12345.0 ? 0u : kNoPixel;  // profiling: no pixel loads
+      }
+    }
+    uint32_t cl[kClsBatch];
+    uint64_t ge[kClsBatch];
+#pragma unroll
+    for (int k = 0; k < kClsBatch; k++) {
+      cl[k] = ri[k] < kRasterFull ? (uint32_t)t.raster[ri[k]] : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
+      ge[k] = (IS == MGPU_BNG && ri[k] < kRasterFull) ? t.grid[gix[k]] : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < kClsBatch; k++) {
+      const int64_t p = c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x;
+      const bool valid = p < a.n;
+      bool mixed = cl[k] == kPixMixed;
+      Code code;
+      if (IS == MGPU_H3) {
+        code = (Code)cl[k];
+        if (!mixed && cl[k] != kPixEmpty) {
+          const uint32_t c = cl[k];  // the class id gives the match count (raster_pc)
+          pairs += c < t.raster_pc[0] ? 1u : c < t.raster_pc[1] ? 2u : c < t.raster_pc[2] ? 3u : c < t.raster_pc[3] ? 4u
+                   : (uint32_t)__popc((uint32_t)(t.raster_cls[c] >> 32));
+        }
+      } else {
+        const uint32_t first = (uint32_t)ge[k], m = cl[k];
+        if (!mixed && m && !(m < 256u && first < (1u << 24))) mixed = true;  // no room in the code
+        code = (Code)(mixed ? kCodeMixed32 : (m ? (first << 8) | m : 0u));
+        if (!mixed) pairs += __popc(m);
+      }
+      if (valid && a.ablate != 12) codes[p] = code;  // (12: profiling, no code stores)
+      mixed = mixed && valid;
+      const unsigned long long bal = __ballot(mixed);
+      if (lane == 0) s_bal[(b + k) * (kClsBlock / 64) + wave] = bal;
+      if (mixed) mixed_bits |= 1u << (b + k);
+    }
+  }
+  count_wave(&a.counters[2], any_bad);
+  const uint32_t wp = wave_sum_u32(pairs);
+  if (lane == 0) s_red[wave] = wp;
+  __syncthreads();
+  // mixed points ranked in point order (item-major, then wave, then lane)
+  if (wave == 0) {
+    const uint32_t v = (uint32_t)__popcll(s_bal[lane]);
+    const uint32_t incl = wave_incl_scan(v);
+    s_pos[lane] = incl - v;
+    if (lane == 63) sa.chunk_mixed[blockIdx.x] = incl;
+    if (lane == 0) {
+      uint32_t tp = 0;
+      for (int w = 0; w < kClsBlock / 64; w++) tp += s_red[w];
+      sa.chunk_pairs[blockIdx.x] = tp;
+    }
+  }
+  __syncthreads();
+  for (uint32_t m = mixed_bits; m; m &= m - 1) {
+    const int it = __builtin_ctz(m);
+    const int e = it * (kClsBlock / 64) + wave;
+    const uint32_t r = s_pos[e] + (uint32_t)__popcll(s_bal[e] & ((1ull << lane) - 1ull));
+    sa.mixed_idx[c0 + r] = (uint16_t)(it * kClsBlock + threadIdx.x);
+  }
+}
+
+// the mixed points of one chunk per workgroup, a tile of kTile at a time
+template <int IS>
+__global__ __launch_bounds__(kBlock) MGPU_JOIN_ATTR void pip_mixed_kernel(JoinArgs a) {
+  const uint32_t nm = a.chunk_mixed[blockIdx.x];
+  for (uint32_t t = 0; t * kGTile < nm; t++) {
+    join_tile<IS, false, true>(a, blockIdx.x * kChunkTiles + t);
+    __syncthreads();
+  }
+}
+
+template <int IS>
+__global__ __launch_bounds__(kBlock) void pip_mixed_fix_kernel(JoinArgs a) {
+  const uint32_t nd = *a.n_dirty;
+  for (uint32_t q = blockIdx.x; q < nd; q += gridDim.x) {
+    join_tile<IS, true, true>(a, a.dirty[q]);
+    __syncthreads();
+  }
+}
+
+// Ordered output.  Thread i handles the points c0 + 256 k + i (k = 0 .. 15, as
+// classify_kernel): the mixed points' list positions come from the same ballots, and per
+// k one workgroup scan places the pairs of 256 consecutive points -- consecutive lanes
+// write consecutive pairs.
+template <int IS>
+__global__ __launch_bounds__(kClsBlock) void split_emit_kernel(SplitArgs sa) {
+  using Code = typename CodeOf<IS>::T;
+  const JoinArgs& a = sa.j;
+  const ChipTableView& t = a.chips;
+  __shared__ unsigned long long s_bal[64];
+  __shared__ uint32_t s_pos[64];
+  __shared__ uint32_t s_w[2][kClsBlock / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  const Code* codes = (const Code*)sa.codes;
+  const Code kMixed = IS == MGPU_H3 ? (Code)kPixMixed : (Code)kCodeMixed32;
+  Code cd[kClsItems];
+#pragma unroll
+  for (int k = 0; k < kClsItems; k++) {
+    const int64_t p = c0 + (int64_t)k * kClsBlock + threadIdx.x;
+    cd[k] = p < a.n ? codes[p] : (Code)0;
+  }
+#pragma unroll
+  for (int k = 0; k < kClsItems; k++) {
+    const unsigned long long bal = __ballot(cd[k] == kMixed);
+    if (lane == 0) s_bal[k * (kClsBlock / 64) + wave] = bal;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const uint32_t v = (uint32_t)__popcll(s_bal[lane]);
+    s_pos[lane] = wave_incl_scan(v) - v;
+  }
+  __syncthreads();
+  uint64_t run = sa.chunk_off[blockIdx.x];
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  // every answer's load in flight at once (mixed answers, class table)
+  uint64_t vv[kClsItems];
+#pragma unroll
+  for (int k = 0; k < kClsItems; k++) {
+    uint64_t v = 0;
+    if (cd[k] == kMixed) {
+      const int e = k * (kClsBlock / 64) + wave;
+      v = a.mixed_res[c0 + s_pos[e] + (uint32_t)__popcll(s_bal[e] & lt)];
+    } else if (cd[k] != 0) {
+      if (IS == MGPU_H3)
+        v = t.raster_cls[(uint32_t)cd[k]];
+      else
+        v = (uint64_t)((uint32_t)cd[k] >> 8) | ((uint64_t)((uint32_t)cd[k] & 0xFFu) << 32);
+    }
+    vv[k] = v;
+  }
+#pragma unroll
+  for (int k = 0; k < kClsItems; k++) {
+    const int64_t p = c0 + (int64_t)k * kClsBlock + threadIdx.x;
+    const uint64_t v = vv[k];
+    const uint32_t first = (uint32_t)v, mask = (uint32_t)(v >> 32), cnt = __popc(mask);
+    const uint32_t incl = wave_incl_scan(cnt);
+    if (lane == 63) s_w[k & 1][wave] = incl;
+    __syncthreads();
+    uint64_t q = run + incl - cnt;
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < kClsBlock / 64; w++) {
+      const uint32_t x = s_w[k & 1][w];
+      if (w < wave) q += x;
+      tot += x;
+    }
+    run += tot;
+    if (mask) {
+      const int64_t pid = sa.point_id ? sa.point_id[p] : sa.id_base + p;
+      for (uint32_t m = mask; m; m &= m - 1) {
+        if ((int64_t)q < sa.capacity) {
+          sa.out_point[q] = pid;
+          sa.out_poly[q] = t.chip_poly[first + __builtin_ctz(m)];
+        }
+        q++;
+      }
+    }
   }
 }
 
@@ -1407,6 +1679,43 @@ hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t
                      (a.n_tiles + kScanGroup - 1) / kScanGroup, e.group_off, a.counters);
   hipLaunchKernelGGL(pair_emit_kernel, dim3((unsigned)((a.n_tiles + kEmitTiles - 1) / kEmitTiles)),
                      dim3(kEmitBlock), 0, s, e, a.n_tiles);
+  return hipGetLastError();
+}
+
+int64_t split_chunk() { return kChunk; }
+int64_t split_chunks(int64_t n) { return (n + kChunk - 1) / kChunk; }
+
+template <int IS>
+static void launch_split_t(const SplitArgs& a, hipStream_t s, hipEvent_t after_classify, hipEvent_t after_mixed) {
+  const int64_t nc = split_chunks(a.j.n);
+  hipLaunchKernelGGL(classify_kernel<IS>, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
+  if (after_classify) hipEventRecord(after_classify, s);
+  hipLaunchKernelGGL(pip_mixed_kernel<IS>, dim3((unsigned)nc), dim3(kBlock), 0, s, a.j);
+  const int64_t fix = nc * kChunkTiles < 512 ? nc * kChunkTiles : 512;
+  hipLaunchKernelGGL(pip_mixed_fix_kernel<IS>, dim3((unsigned)fix), dim3(kBlock), 0, s, a.j);
+  if (after_mixed) hipEventRecord(after_mixed, s);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.chunk_pairs, a.j.group_cand, nc,
+                     a.chunk_off, a.j.counters);
+  hipLaunchKernelGGL(split_emit_kernel<IS>, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
+}
+
+hipError_t launch_split(int is, const SplitArgs& a, hipStream_t s, hipEvent_t after_classify, hipEvent_t after_mixed) {
+  if (a.j.n <= 0) return hipSuccess;
+  if (is == MGPU_H3)
+    launch_split_t<MGPU_H3>(a, s, after_classify, after_mixed);
+  else
+    launch_split_t<MGPU_BNG>(a, s, after_classify, after_mixed);
+  return hipGetLastError();
+}
+
+// only the ordered output of a split join already computed (mgpu_pip_join_fetch)
+hipError_t launch_split_emit(int is, const SplitArgs& a, hipStream_t s) {
+  if (a.j.n <= 0) return hipSuccess;
+  const int64_t nc = split_chunks(a.j.n);
+  if (is == MGPU_H3)
+    hipLaunchKernelGGL(split_emit_kernel<MGPU_H3>, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL(split_emit_kernel<MGPU_BNG>, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
   return hipGetLastError();
 }
 

@@ -1,19 +1,28 @@
 """Multi-GPU point-in-polygon join: points sharded, chip table replicated.
 
 The reference scales this path with Spark data parallelism: the chip side is
-broadcast (BroadcastHashJoin) or both sides shuffled (SortMergeJoin), SURVEY §3.D.
-On one MI355X node the MI355X-native plan is:
+broadcast to the executors (BroadcastHashJoin) or both sides shuffled, SURVEY §3.D.
+On one MI355X node the MI355X-native plan, all of it behind the C ABI
+(include/mosaic_gpu.h "Multi-GPU", mosaic_amd/csrc/comm.cpp):
   * points are independent -> contiguous point-id ranges per GPU, no shuffle;
-  * the chip table is built once (rank 0) and replicated as ONE device blob with
-    a single RCCL broadcast over xGMI (the blob is self-describing, see
-    mosaic_amd/csrc/capi.cpp BlobHeader);
-  * per-GPU pair counts are combined with one RCCL all_gather to give every rank
-    its global output offset (the only exchange step on the path).
+  * every rank's context joins one RCCL communicator (mgpu_comm_init); the unique id
+    travels through torch.distributed's control plane (any backend, gloo is enough);
+  * the chip table is built once (rank 0) and replicated with mgpu_chips_broadcast:
+    one RCCL broadcast of the self-describing blob straight into each receiving
+    allocation (its 1 KiB header first, to size it);
+  * per-GPU pair counts are combined with mgpu_pair_offsets (one RCCL all-gather) to give
+    every rank its global output offset -- the only exchange step on the path.
 Concatenating the shards in rank order is then globally ordered by point id.
-One process per GPU; the torch.distributed backend "nccl" is RCCL on ROCm.
+
+For a host that ships chip tables itself (a JVM driver broadcasting bytes to its
+executors), the same blob exists in host memory: host_blob / blob_info /
+upload_host_blob (mgpu_chips_host_blob, mgpu_host_blob_info, mgpu_chips_upload_blob).
 """
+import ctypes
+
 import numpy as np
 
+from . import _native as N
 from .chips import DeviceChips
 
 
@@ -24,58 +33,119 @@ def shard_range(n_total, rank, world):
     return begin, begin + base + (1 if rank < extra else 0)
 
 
-def broadcast_chips(chips, ctx, src=0, group=None):
-    """Replicate rank `src`'s uploaded chip table to every rank (one broadcast).
+# ---------------------------------------------------------------- RCCL (native)
 
-    `chips` is a DeviceChips on `src` (ignored elsewhere).  Returns a DeviceChips on
-    every rank."""
-    import torch
+def init_comm(ctx, group=None):
+    """Join ctx to the job's RCCL communicator: rank 0 creates the unique id
+    (mgpu_comm_unique_id), torch.distributed carries it to every rank, each rank calls
+    mgpu_comm_init (which blocks until all ranks have joined)."""
     import torch.distributed as dist
-    rank = dist.get_rank(group)
-    dev = ctx.device
-    backend = dist.get_backend(group)
-    size = torch.zeros(1, dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
-    if rank == src:
-        ptr, nbytes = chips.device_blob()
-        size[0] = nbytes
-    dist.broadcast(size, src, group=group)
-    nbytes = int(size.item())
-    buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    if rank == src:
-        # the broadcast's source: a tensor copy of the library-owned blob
-        torch.cuda.synchronize(dev)
-        _copy_device(ptr, buf.data_ptr(), nbytes)
-    if backend == "nccl":
-        dist.broadcast(buf, src, group=group)
-    else:  # gloo: stage through host memory
-        host = buf.cpu()
-        dist.broadcast(host, src, group=group)
-        buf.copy_(host.to(dev))
-    if rank == src:
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    uid = (ctypes.c_uint8 * N.MGPU_COMM_ID_BYTES)()
+    if rank == 0:
+        N.check(N.lib().mgpu_comm_unique_id(uid))
+    obj = [bytes(uid)]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    buf = (ctypes.c_uint8 * N.MGPU_COMM_ID_BYTES).from_buffer_copy(obj[0])
+    N.check(N.lib().mgpu_comm_init(ctx.handle, buf, rank, world))
+
+
+def comm_info(ctx):
+    r, w = ctypes.c_int32(), ctypes.c_int32()
+    N.check(N.lib().mgpu_comm_info(ctx.handle, ctypes.byref(r), ctypes.byref(w)))
+    return r.value, w.value
+
+
+def broadcast_chips(chips, ctx, root=0, stream=None):
+    """Replicate rank `root`'s uploaded chip table to every rank (mgpu_chips_broadcast:
+    one RCCL broadcast into the receiving allocation).  `chips` is a DeviceChips on
+    `root` (ignored elsewhere); returns a DeviceChips on every rank."""
+    import torch
+    rank, _ = comm_info(ctx)
+    s = stream if stream is not None else torch.cuda.current_stream(ctx.device).cuda_stream
+    out = ctypes.c_void_p()
+    src = chips.handle if (rank == root and chips is not None) else None
+    N.check(N.lib().mgpu_chips_broadcast(ctx.handle, src, int(root), ctypes.byref(out), s))
+    if rank == root:
         return chips
-    torch.cuda.synchronize(dev)
-    return DeviceChips.from_device_blob(ctx, buf.data_ptr(), nbytes)
+    return DeviceChips(None, ctx, handle=out)
 
 
-def _copy_device(src_ptr, dst_ptr, nbytes):
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
-    hip.hipMemcpy.restype = ctypes.c_int
-    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    st = hip.hipMemcpy(ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src_ptr), ctypes.c_size_t(nbytes), 3)
-    if st != 0:
-        raise RuntimeError("hipMemcpy device->device failed (%d)" % st)
+def global_offsets(local_count, ctx, stream=None):
+    """mgpu_pair_offsets (RCCL all-gather): (this rank's offset, total, per-rank counts)."""
+    import torch
+    _, world = comm_info(ctx)
+    s = stream if stream is not None else torch.cuda.current_stream(ctx.device).cuda_stream
+    off, tot = ctypes.c_int64(), ctypes.c_int64()
+    counts = np.zeros(world, dtype=np.int64)
+    N.check(N.lib().mgpu_pair_offsets(ctx.handle, int(local_count), ctypes.byref(off), ctypes.byref(tot),
+                                      counts.ctypes.data, s))
+    return off.value, tot.value, counts
 
 
-def global_offsets(local_count, device=None, group=None):
-    """All-gather the per-rank pair counts; return (this rank's offset, total, counts)."""
+# ---------------------------------------------------------------- host blobs
+
+def host_blob(table):
+    """The chip table as one self-describing host blob (bytes), no GPU needed."""
+    p = ctypes.c_void_p()
+    nb = ctypes.c_int64()
+    wkb = table.wkb if table.wkb.size else np.zeros(1, np.uint8)
+    N.check(N.lib().mgpu_chips_host_blob(table.index_system, len(table), table.cell.ctypes.data,
+                                         table.polygon_id.ctypes.data, table.is_core.ctypes.data,
+                                         table.wkb_offsets.ctypes.data, wkb.ctypes.data, ctypes.byref(p),
+                                         ctypes.byref(nb)))
+    try:
+        return ctypes.string_at(p.value, nb.value)
+    finally:
+        N.lib().mgpu_host_free(p)
+
+
+def blob_info(blob):
+    """Check a received blob (magic, version, size, offsets); its contents."""
+    isys, a, b, c = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    N.check(N.lib().mgpu_host_blob_info(blob, len(blob), ctypes.byref(isys), ctypes.byref(a), ctypes.byref(b),
+                                        ctypes.byref(c)))
+    return {"index_system": isys.value, "chips": a.value, "cells": b.value, "vertices": c.value}
+
+
+def upload_host_blob(blob, ctx):
+    h = ctypes.c_void_p()
+    N.check(N.lib().mgpu_chips_upload_blob(ctx.handle, blob, len(blob), ctypes.byref(h)))
+    return DeviceChips(None, ctx, handle=h)
+
+
+def broadcast_host_blob(blob, src=0, group=None):
+    """Control-plane replication of a host blob (torch.distributed, e.g. gloo): what a
+    host without RCCL (or a JVM driver) does instead of mgpu_chips_broadcast."""
     import torch
     import torch.distributed as dist
-    world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    dev = device if (device is not None and dist.get_backend(group) == "nccl") else "cpu"
-    mine = torch.tensor([int(local_count)], dtype=torch.int64, device=dev)
-    allc = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    size = torch.tensor([len(blob) if rank == src else 0], dtype=torch.int64)
+    dist.broadcast(size, src, group=group)
+    buf = torch.frombuffer(bytearray(blob), dtype=torch.uint8) if rank == src else \
+        torch.empty(int(size.item()), dtype=torch.uint8)
+    dist.broadcast(buf, src, group=group)
+    return bytes(buf.numpy().tobytes())
+
+
+def gather_offsets_host(local_count, group=None):
+    """The all-gather of mgpu_pair_offsets on the control plane (CPU protocol tests)."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    mine = torch.tensor([int(local_count)], dtype=torch.int64)
+    allc = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(allc, mine, group=group)
     counts = np.array([int(c.item()) for c in allc], dtype=np.int64)
     return int(counts[:rank].sum()), int(counts.sum()), counts
+
+
+def blob_contains(blob, rows, x, y):
+    """st_contains of (chip row, point) pairs evaluated on a host blob (test aid)."""
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    out = np.empty(len(rows), np.int8)
+    N.check(N.lib().mgpu_test_blob_contains_host(blob, len(blob), len(rows), rows.ctypes.data, x.ctypes.data,
+                                                  y.ctypes.data, out.ctypes.data))
+    return out

@@ -380,8 +380,10 @@ def test_chip_blob_roundtrip(gpu, nyc_chips_r9):
     d = nyc_chips_r9.upload()
     ptr, nbytes = d.device_blob()
     buf = torch.empty(nbytes, dtype=torch.uint8, device=gpu)
-    from mosaic_amd.dist import _copy_device
-    _copy_device(ptr, buf.data_ptr(), nbytes)
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    assert hip.hipMemcpy(buf.data_ptr(), ptr, nbytes, 3) == 0  # device to device
     d2 = M.DeviceChips.from_device_blob(d.ctx, buf.data_ptr(), nbytes)
     del buf
     x, y = nyc_points(200_000, 5)
@@ -580,8 +582,46 @@ def test_pixel_index_on_off_identical(gpu, nyc_chips_r9):
             del os.environ["MGPU_RASTER"]
         d1 = c.upload()
         a = M.pip_join(T(x, gpu), T(y, gpu), d0, res, index_system=isys).numpy()
-        b = M.pip_join(T(x, gpu), T(y, gpu), d1, res, index_system=isys).numpy()
+        rb = M.pip_join(T(x, gpu), T(y, gpu), d1, res, index_system=isys)
+        b = rb.numpy()
+        assert rb.stats["pipeline"] == 1  # the split pipeline (classify / mixed / emit)
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
-        if len(x) <= 300_000:
-            op, oq = oracle_join(c, x, y, res=res, isys=isys.code)
-            assert np.array_equal(b[0], op) and np.array_equal(b[1], oq)
+        os.environ["MGPU_SPLIT"] = "0"  # the fused kernel's own pixel-index pass
+        try:
+            rf = M.pip_join(T(x, gpu), T(y, gpu), d1, res, index_system=isys)
+        finally:
+            del os.environ["MGPU_SPLIT"]
+        assert rf.stats["pipeline"] == 0
+        f = rf.numpy()
+        assert np.array_equal(a[0], f[0]) and np.array_equal(a[1], f[1])
+    # and the oracle on a uniform slice (the adversarial set's near-ties are
+    # test_pip_join_adversarial_points' subject)
+    x, y = nyc_points(300_000, 35)
+    b = M.pip_join(T(x, gpu), T(y, gpu), nyc_chips_r9.upload(), 9).numpy()
+    op, oq = oracle_join(nyc_chips_r9, x, y)
+    assert np.array_equal(b[0], op) and np.array_equal(b[1], oq)
+
+
+def test_comm_single_rank(gpu, nyc_chips_r9):
+    """The C ABI's RCCL path on a one-rank communicator: broadcast from the root keeps the
+    table, the all-gathered offsets are (0, total)."""
+    import ctypes
+    from mosaic_amd import _native as N
+    from mosaic_amd import dist as D
+    ctx = M.GpuContext(gpu)
+    uid = (ctypes.c_uint8 * N.MGPU_COMM_ID_BYTES)()
+    N.check(N.lib().mgpu_comm_unique_id(uid))
+    N.check(N.lib().mgpu_comm_init(ctx.handle, uid, 0, 1))
+    assert D.comm_info(ctx) == (0, 1)
+    d = nyc_chips_r9.upload(ctx)
+    d2 = D.broadcast_chips(d, ctx)
+    assert d2 is d
+    off, tot, counts = D.global_offsets(12345, ctx)
+    assert (off, tot, list(counts)) == (0, 12345, [12345])
+    # a host blob shipped by the host and uploaded joins like the table itself
+    b = D.upload_host_blob(D.host_blob(nyc_chips_r9), ctx)
+    x, y = nyc_points(100_000, 36)
+    r1 = M.pip_join(T(x, gpu), T(y, gpu), d, 9).numpy()
+    r2 = M.pip_join(T(x, gpu), T(y, gpu), b, 9).numpy()
+    assert np.array_equal(r1[0], r2[0]) and np.array_equal(r1[1], r2[1])
+    ctx.close()
