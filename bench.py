@@ -223,10 +223,13 @@ def main():
     kms, sms = [], []
     pairs = 0
     ties = 0
+    mms, ems = [], []
     for _ in range(a.steps):
         r = step()
         kms.append(r.stats["kernel_ms"])
         sms.append(r.stats["stream_kernel_ms"])
+        mms.append(r.stats["mixed_kernel_ms"])
+        ems.append(r.stats["emit_kernel_ms"])
         pairs = len(r)
         ties = r.stats["n_near_ties"]
     torch.cuda.synchronize(dev)
@@ -248,9 +251,17 @@ def main():
     ms_step = elapsed / a.steps * 1e3
     pipeline_ms = float(np.mean(kms))
     stream_ms = float(np.mean(sms))
-    tp = M._native.lib().mgpu_join_tile_points()
-    tiles = (n + tp - 1) // tp
-    alg_bytes = 16.0 * n + 8.0 * pairs + 12.0 * tiles
+    split = r.stats["pipeline"] == M._native.MGPU_PIPELINE_SPLIT
+    if split:
+        # the split pipeline: the dominant kernel is classify_kernel, the one
+        # pass over every point: 16 B read + its code (2 B H3 / 4 B BNG) written per point
+        kernel = "classify_kernel<%s>" % isys.name
+        alg_bytes = (16.0 + (2.0 if isys.code == M._native.MGPU_H3 else 4.0)) * n
+    else:
+        kernel = "pip_join_kernel<%s>" % isys.name
+        tp = M._native.lib().mgpu_join_tile_points()
+        tiles = (n + tp - 1) // tp
+        alg_bytes = 16.0 * n + 8.0 * pairs + 12.0 * tiles
     achieved = alg_bytes / (stream_ms * 1e-3) / 1e9
     out = {
         "metric": METRIC,
@@ -271,9 +282,14 @@ def main():
                    "parallelism": "points sharded x%d, chip table replicated (RCCL broadcast)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "pip_join_kernel<%s>" % isys.name, "kernel_ms": stream_ms,
+                     "kernel": kernel, "kernel_ms": stream_ms,
                      "alg_bytes_per_launch": alg_bytes, "pipeline_ms": pipeline_ms,
-                     "pipeline_GBps": (alg_bytes + 20.0 * pairs) / (pipeline_ms * 1e-3) / 1e9},
+                     # the whole call: 16 B per point in, 12 B per (point_id, polygon_id) pair out
+                     "pipeline_GBps": (16.0 * n + 12.0 * pairs) / (pipeline_ms * 1e-3) / 1e9,
+                     "pipeline_frac": (16.0 * n + 12.0 * pairs) / (pipeline_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+        "pipeline": "split" if split else "fused",
+        "kernels_ms": ({"classify": stream_ms, "mixed": float(np.mean(mms)), "emit": float(np.mean(ems))} if split
+                       else {"pip_join": stream_ms, "rest": pipeline_ms - stream_ms}),
         "pairs_per_gpu": pairs,
         "pairs_total": total_pairs,
         "near_ties": ties,

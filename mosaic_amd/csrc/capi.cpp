@@ -56,8 +56,8 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // offsets, so a byte copy of the blob on another GPU (RCCL broadcast) is a
 // complete chip table there.
 constexpr uint64_t kBlobMagic = 0x4d4f534149434850ULL;  // "MOSAICHP"
-constexpr int kBlobArrays = 20;
-constexpr uint32_t kBlobVersion = 5;
+constexpr int kBlobArrays = 22;
+constexpr uint32_t kBlobVersion = 6;
 struct BlobHeader {
   uint64_t magic;
   uint32_t version, hash_mask, max_probe, n_chips, n_cells;
@@ -78,6 +78,7 @@ struct BlobHeader {
   uint64_t blob_bytes;  // the whole blob (header included)
   uint32_t max_cell_chips, pad4;
   uint32_t raster_pc[4];
+  uint32_t raster_sub_n, raster_sub_w;
 };
 constexpr size_t kBlobHeaderBytes = 1024;
 static_assert(sizeof(BlobHeader) <= kBlobHeaderBytes, "header too large");
@@ -128,6 +129,10 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   for (int k = 0; k < 4; k++) v.raster_pc[k] = h.raster_pc[k];
   v.raster = (const uint16_t*)(base + h.off[18]);
   v.raster_cls = (const uint64_t*)(base + h.off[19]);
+  v.raster_sub_n = h.raster_sub_n;
+  v.raster_sub_w = h.raster_sub_w;
+  v.raster_ref = h.raster_sub_n ? (const uint32_t*)(base + h.off[20]) : nullptr;
+  v.raster_sub = (const uint16_t*)(base + h.off[21]);
   return v;
 }
 
@@ -505,6 +510,11 @@ struct Raster {
   std::vector<uint16_t> cells;
   std::vector<uint64_t> cls;
   uint32_t pc[4] = {0, 0, 0, 0};
+  // second level: ref[pixel] = 1 + block of a refined mixed pixel (0: none); block b's
+  // sub_n x sub_n sub-pixel classes at sub[b * sub_n^2 ..] (BNG: sub-pixel edge sub_w metres)
+  uint32_t sub_n = 0, sub_w = 0;
+  std::vector<uint32_t> ref;
+  std::vector<uint16_t> sub;
   int64_t n_pure = 0;
 };
 
@@ -617,7 +627,8 @@ bool hex_meets_quad(int64_t a, int64_t b, const double q[4][2], double d) {
 }
 
 // pixel budget and size: MGPU_RASTER=0 disables the index; MGPU_RASTER_F = pixel edge
-// as a fraction of the cell edge (default 1/4)
+// as a fraction of the cell edge (default 1/4); MGPU_RASTER_SUB = sub-pixels per mixed
+// pixel edge (default 8; 0: no second level)
 double raster_fraction() {
   const char* s = getenv("MGPU_RASTER_F");
   const double f = s ? atof(s) : 0.25;
@@ -627,25 +638,34 @@ bool raster_enabled() {
   const char* s = getenv("MGPU_RASTER");
   return !(s && atoi(s) == 0);
 }
+int raster_sub_wanted() {
+  const char* s = getenv("MGPU_RASTER_SUB");
+  const int v = s ? atoi(s) : 8;
+  return v >= 2 && v <= 16 ? v : 0;
+}
 constexpr int64_t kRasterMaxPixels = 1LL << 24;
+constexpr int64_t kRasterMaxSub = 1LL << 26;
 
-// classes: per-pixel answers (first | mask << 32, 0 = empty, ~0 = mixed) -> u16 classes
-bool raster_classes(const std::vector<uint64_t>& ans, Raster& R) {
-  R.cells.assign(ans.size(), mgpu::kPixMixed);
-  R.cls.assign(1, 0);  // class 0 = empty
+constexpr uint64_t kAnsMixed = ~0ULL;
+
+// classes over the answers of both levels (first | mask << 32; 0 = empty; kAnsMixed):
+// class 0 = empty, kPixMixed = mixed, the rest ordered by their number of matches so a
+// class id tells its pair count (pc[k]: the first class with more than k + 1 matches)
+void raster_classes(const std::vector<uint64_t>& a1, const std::vector<uint64_t>& a2, Raster& R) {
+  R.cells.assign(a1.size(), mgpu::kPixMixed);
+  R.sub.assign(a2.size(), mgpu::kPixMixed);
+  R.cls.assign(1, 0);
+  auto slot = [&](size_t i) -> uint16_t& { return i < a1.size() ? R.cells[i] : R.sub[i - a1.size()]; };
   std::vector<std::pair<uint64_t, uint32_t>> keyed;
-  keyed.reserve(ans.size());
-  for (size_t i = 0; i < ans.size(); i++) {
-    if (ans[i] == ~0ULL) continue;
-    if ((ans[i] >> 32) == 0) {
-      R.cells[i] = mgpu::kPixEmpty;
-      R.n_pure++;
+  for (size_t i = 0; i < a1.size() + a2.size(); i++) {
+    const uint64_t v = i < a1.size() ? a1[i] : a2[i - a1.size()];
+    if (v == kAnsMixed) continue;
+    if ((v >> 32) == 0) {
+      slot(i) = mgpu::kPixEmpty;
       continue;
     }
-    keyed.push_back({ans[i], (uint32_t)i});
+    keyed.push_back({v, (uint32_t)i});
   }
-  // classes ordered by their number of matches, so a class id tells its pair count
-  // (pc[k]: the first class with more than k + 1 matches)
   auto pc = [](uint64_t v) { return __builtin_popcountll(v >> 32); };
   std::sort(keyed.begin(), keyed.end(), [&](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) {
     const int x = pc(a.first), y = pc(b.first);
@@ -656,15 +676,68 @@ bool raster_classes(const std::vector<uint64_t>& ans, Raster& R) {
       if (R.cls.size() >= mgpu::kPixMixed) break;  // out of classes: the rest stay mixed
       R.cls.push_back(keyed[k].first);
     }
-    R.cells[keyed[k].second] = (uint16_t)(R.cls.size() - 1);
-    R.n_pure++;
+    slot(keyed[k].second) = (uint16_t)(R.cls.size() - 1);
   }
   for (int k = 0; k < 4; k++) {
     uint32_t c = 1;
     while (c < R.cls.size() && pc(R.cls[c]) <= k + 1) c++;
     R.pc[k] = c;
   }
-  return true;
+  R.n_pure = 0;
+  for (uint16_t v : R.cells) R.n_pure += v != mgpu::kPixMixed;
+}
+
+// H3: the answer shared by every point of the rectangle [xa, xb] x [ya, yb] (degrees)
+// whose corners c (projected at exactly those points, in the order (xa, ya), (xb, ya),
+// (xb, yb), (xa, yb)) are given; the certificate is checked on the rectangle widened by
+// (mux, muy) -- its corners lie within ~1e-6 of its size of c, a deviation the margins
+// below carry -- or kAnsMixed.
+struct H3RasterCtx {
+  const mgpu::ChipTableView& hv;
+  int res;
+  double k_res;
+  const mgpu::DenseFace* dense;
+  const std::vector<uint64_t>& grid;
+};
+uint64_t h3_rect_answer(const H3RasterCtx& X, double xa, double ya, double xb, double yb, const Corner* c[4],
+                        double mux, double muy, std::vector<int32_t>& polys, std::vector<int32_t>& ref) {
+  double q[4][2], L = 0;
+  for (int p = 0; p < 4; p++) q[p][0] = c[p]->x, q[p][1] = c[p]->y;
+  for (int p = 0; p < 4; p++)
+    for (int r = p + 1; r < 4; r++) L = std::max(L, std::hypot(q[p][0] - q[r][0], q[p][1] - q[r][1]));
+  const double ang = std::hypot(xb - xa + 2 * mux, yb - ya + 2 * muy) * kPi / 180.0;  // angular diagonal bound
+  const double d_face = 1e-12 + 8.0 * ang * ang + 8e-6 * ang;
+  const double d_hex = 1e-9 * (1.0 + std::fabs(q[0][0]) + std::fabs(q[0][1])) + 8.0 * L * L / X.k_res + 8e-6 * L;
+  bool ok = L < 0.5;
+  for (int p = 0; p < 4 && ok; p++) ok = c[p]->ok && c[p]->face == c[0]->face && c[p]->gap > d_face;
+  if (!ok) return kAnsMixed;
+  double mg;
+  const mgpu::h3::IJK h0 = mgpu::h3::hex2d_to_ijk_fast(q[0][0], q[0][1], &mg);
+  const int64_t a0 = h0.i - h0.k, b0 = h0.j - h0.k;
+  // every cell a point of the rectangle can take is h0 or a neighbour (L < 1/2) whose
+  // hexagon meets the quad; all must give the same polygon list
+  static const int da[7] = {0, 1, -1, 0, 0, 1, -1}, db[7] = {0, 0, 0, 1, -1, 1, -1};
+  const mgpu::DenseFace& D = X.dense[c[0]->face];
+  bool first = true;
+  uint64_t cls = 0;
+  for (int k = 0; k < 7; k++) {
+    const int64_t a = a0 + da[k], b = b0 + db[k];
+    if (!hex_meets_quad(a, b, q, d_hex)) continue;
+    const uint64_t ua = (uint64_t)(a - D.a0), ub = (uint64_t)(b - D.b0);
+    const uint64_t e = (ua < D.w && ub < D.h) ? X.grid[D.base + ub * D.w + ua] : 0;
+    const int64_t m = pixel_answer(X.hv, e, xa - mux, ya - muy, xb + mux, yb + muy);
+    if (m == kPixAnswerMixed) return kAnsMixed;
+    polys.clear();
+    for (uint64_t bits = (uint64_t)m; bits; bits &= bits - 1) polys.push_back(X.hv.chip_poly[(uint32_t)e + __builtin_ctzll(bits)]);
+    if (first) {
+      ref = polys;
+      cls = m ? ((uint32_t)e | ((uint64_t)m << 32)) : 0;
+      first = false;
+    } else if (polys != ref) {
+      return kAnsMixed;
+    }
+  }
+  return first ? kAnsMixed : cls;
 }
 
 bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const double bbox[4],
@@ -690,69 +763,74 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
   const double sx = 1.0 / R.inv_dx, sy = 1.0 / R.inv_dy;  // the pixel size the kernel's index implies
   const double mag = std::max(std::max(std::fabs(bbox[0]), std::fabs(bbox[2])), std::max(std::fabs(bbox[1]), std::fabs(bbox[3])));
   const double ulp = std::nextafter(mag, INFINITY) - mag;
-  const double mux = 1e-6 * sx + 64 * ulp, muy = 1e-6 * sy + 64 * ulp;
-  std::vector<uint64_t> ans((size_t)R.nx * R.ny, ~0ULL);
-  mgpu::parallel_for((int64_t)R.ny, 4, [&](int64_t yb, int64_t ye, int) {
-    std::vector<int32_t> polys, ref;
-    for (int64_t iy = yb; iy < ye; iy++)
-      for (uint32_t ix = 0; ix < R.nx; ix++) {
-        double xa = R.x0 + ix * sx - mux, xb = R.x0 + (ix + 1) * sx + mux;
-        double ya = R.y0 + iy * sy - muy, yb2 = R.y0 + (iy + 1) * sy + muy;
-        if (ix == R.nx - 1) xb = std::max(xb, bbox[2] + mux);  // the last pixel takes the clamped points
-        if (iy == (int64_t)R.ny - 1) yb2 = std::max(yb2, bbox[3] + muy);
-        // quad corners in order around the pixel
-        const Corner c[4] = {h3_corner(xa, ya, res, k_res), h3_corner(xb, ya, res, k_res), h3_corner(xb, yb2, res, k_res),
-                             h3_corner(xa, yb2, res, k_res)};
-        double q[4][2], L = 0;
-        for (int p = 0; p < 4; p++) q[p][0] = c[p].x, q[p][1] = c[p].y;
-        for (int p = 0; p < 4; p++)
-          for (int r = p + 1; r < 4; r++) L = std::max(L, std::hypot(q[p][0] - q[r][0], q[p][1] - q[r][1]));
-        const double ang = std::hypot(xb - xa, yb2 - ya) * kPi / 180.0;  // angular diagonal bound (rad)
-        const double d_face = 1e-12 + 8.0 * ang * ang;
-        const double d_hex = 1e-9 * (1.0 + std::fabs(q[0][0]) + std::fabs(q[0][1])) + 8.0 * L * L / k_res;
-        bool ok = L < 0.5;
-        for (int p = 0; p < 4 && ok; p++) ok = c[p].ok && c[p].face == c[0].face && c[p].gap > d_face;
-        if (!ok) continue;
-        double mg;
-        const mgpu::h3::IJK h0 = mgpu::h3::hex2d_to_ijk_fast(q[0][0], q[0][1], &mg);
-        const int64_t a0 = h0.i - h0.k, b0 = h0.j - h0.k;
-        // every cell a point of the pixel can take is h0 or a neighbour (L < 1/2) whose
-        // hexagon meets the quad; all must give the same polygon list
-        static const int da[7] = {0, 1, -1, 0, 0, 1, -1}, db[7] = {0, 0, 0, 1, -1, 1, -1};
-        const mgpu::DenseFace& D = dense[c[0].face];
-        bool first = true, pure = true;
-        uint64_t cls = 0;
-        for (int k = 0; k < 7 && pure; k++) {
-          const int64_t a = a0 + da[k], b = b0 + db[k];
-          if (!hex_meets_quad(a, b, q, d_hex)) continue;
-          const uint64_t ua = (uint64_t)(a - D.a0), ub = (uint64_t)(b - D.b0);
-          const uint64_t e = (ua < D.w && ub < D.h) ? grid[D.base + ub * D.w + ua] : 0;
-          const int64_t m = pixel_answer(hv, e, xa, ya, xb, yb2);
-          if (m == kPixAnswerMixed) {
-            pure = false;
-            break;
-          }
-          polys.clear();
-          for (uint64_t bits = (uint64_t)m; bits; bits &= bits - 1) polys.push_back(hv.chip_poly[(uint32_t)e + __builtin_ctzll(bits)]);
-          if (first) {
-            ref = polys;
-            cls = m ? ((uint32_t)e | ((uint64_t)m << 32)) : 0;
-            first = false;
-          } else if (polys != ref) {
-            pure = false;
-          }
+  // pixel / sub-pixel edge coordinates (the last ones take the clamped points up to bbox)
+  auto xe = [&](uint32_t ix, double f) {
+    return ix + f >= R.nx ? std::max(R.x0 + R.nx * sx, bbox[2]) : R.x0 + (ix + f) * sx;
+  };
+  auto ye = [&](uint32_t iy, double f) {
+    return iy + f >= R.ny ? std::max(R.y0 + R.ny * sy, bbox[3]) : R.y0 + (iy + f) * sy;
+  };
+  const H3RasterCtx X{hv, res, k_res, dense, grid};
+  // level 1: corners on the pixel grid, two rows at a time
+  std::vector<uint64_t> a1((size_t)R.nx * R.ny, kAnsMixed);
+  {
+    const double mux = 1e-6 * sx + 64 * ulp, muy = 1e-6 * sy + 64 * ulp;
+    mgpu::parallel_for((int64_t)R.ny, 8, [&](int64_t yb, int64_t ye_, int) {
+      std::vector<int32_t> polys, ref;
+      std::vector<Corner> lo(R.nx + 1), hi(R.nx + 1);
+      for (uint32_t ix = 0; ix <= R.nx; ix++) lo[ix] = h3_corner(xe(ix, 0), ye((uint32_t)yb, 0), res, k_res);
+      for (int64_t iy = yb; iy < ye_; iy++) {
+        for (uint32_t ix = 0; ix <= R.nx; ix++) hi[ix] = h3_corner(xe(ix, 0), ye((uint32_t)iy, 1), res, k_res);
+        for (uint32_t ix = 0; ix < R.nx; ix++) {
+          const Corner* c[4] = {&lo[ix], &lo[ix + 1], &hi[ix + 1], &hi[ix]};
+          a1[(size_t)iy * R.nx + ix] =
+              h3_rect_answer(X, xe(ix, 0), ye((uint32_t)iy, 0), xe(ix, 1), ye((uint32_t)iy, 1), c, mux, muy, polys, ref);
         }
-        if (pure && !first) ans[(size_t)iy * R.nx + ix] = cls;
+        std::swap(lo, hi);
       }
-  });
-  return raster_classes(ans, R);
+    });
+  }
+  // level 2: the mixed pixels cut into S x S sub-pixels
+  std::vector<uint64_t> a2;
+  const int S = raster_sub_wanted();
+  std::vector<uint32_t> mixed;
+  for (size_t i = 0; i < a1.size(); i++)
+    if (a1[i] == kAnsMixed) mixed.push_back((uint32_t)i);
+  if (S >= 2 && !mixed.empty() && (int64_t)mixed.size() * S * S <= kRasterMaxSub) {
+    R.sub_n = (uint32_t)S;
+    R.ref.assign(a1.size(), 0);
+    for (size_t k = 0; k < mixed.size(); k++) R.ref[mixed[k]] = (uint32_t)(k + 1);
+    a2.assign(mixed.size() * S * S, kAnsMixed);
+    const double mux = 1e-6 * sx / S + 64 * ulp, muy = 1e-6 * sy / S + 64 * ulp;
+    mgpu::parallel_for((int64_t)mixed.size(), 64, [&](int64_t kb, int64_t ke, int) {
+      std::vector<int32_t> polys, ref;
+      std::vector<Corner> cg((size_t)(S + 1) * (S + 1));
+      for (int64_t k = kb; k < ke; k++) {
+        const uint32_t ix = mixed[k] % R.nx, iy = mixed[k] / R.nx;
+        for (int v = 0; v <= S; v++)
+          for (int u = 0; u <= S; u++) cg[v * (S + 1) + u] = h3_corner(xe(ix, (double)u / S), ye(iy, (double)v / S), res, k_res);
+        for (int v = 0; v < S; v++)
+          for (int u = 0; u < S; u++) {
+            const Corner* c[4] = {&cg[v * (S + 1) + u], &cg[v * (S + 1) + u + 1], &cg[(v + 1) * (S + 1) + u + 1],
+                                  &cg[(v + 1) * (S + 1) + u]};
+            a2[(size_t)k * S * S + v * S + u] = h3_rect_answer(X, xe(ix, (double)u / S), ye(iy, (double)v / S),
+                                                               xe(ix, (double)(u + 1) / S), ye(iy, (double)(v + 1) / S), c,
+                                                               mux, muy, polys, ref);
+          }
+      }
+    });
+  }
+  raster_classes(a1, a2, R);
+  return true;
 }
 
 bool build_raster_bng(const mgpu::ChipTableView& hv, const mgpu::DenseFace& D, uint32_t edge,
                       const std::vector<uint64_t>& grid, Raster& R) {
   if (!raster_enabled() || edge == 0 || grid.empty()) return false;
   // pixels per cell edge: the largest k <= 1 / fraction dividing the edge, within budget
-  int kpc = (int)std::floor(1.0 / raster_fraction() + 1e-9);
+  // (BNG default: 2 -- a raster of 2 x 2 pixels per cell stays in L2 at C4's size)
+  const char* fs = getenv("MGPU_RASTER_F");
+  int kpc = fs ? (int)std::floor(1.0 / raster_fraction() + 1e-9) : 2;
   for (; kpc > 1; kpc--)
     if (edge % kpc == 0 && (double)D.w * kpc * D.h * kpc <= (double)kRasterMaxPixels) break;
   if (kpc < 2) return false;
@@ -761,26 +839,56 @@ bool build_raster_bng(const mgpu::ChipTableView& hv, const mgpu::DenseFace& D, u
   R.nx = D.w * kpc, R.ny = D.h * kpc;
   R.px0 = D.a0 * kpc, R.py0 = D.b0 * kpc;
   R.inv_dx = R.inv_dy = 1.0 / R.pix;
-  const double mu = 1e-6 * R.pix + 64 * (std::nextafter(1e7, INFINITY) - 1e7);
   // BNG pixels hold the match mask itself (the kernel has the cell's grid entry anyway)
+  auto answer = [&](uint64_t e, double xa, double ya, double xb, double yb, double mu) -> uint16_t {
+    const int64_t m = pixel_answer(hv, e, xa - mu, ya - mu, xb + mu, yb + mu);
+    return (m == kPixAnswerMixed || m >= (int64_t)mgpu::kPixMixed) ? mgpu::kPixMixed : (uint16_t)m;
+  };
+  const double mu0 = 64 * (std::nextafter(1e7, INFINITY) - 1e7);
   R.cells.assign((size_t)R.nx * R.ny, mgpu::kPixMixed);
   R.cls.assign(1, 0);
-  std::atomic<int64_t> pure{0};
   mgpu::parallel_for((int64_t)R.ny, 8, [&](int64_t yb, int64_t ye, int) {
-    int64_t np = 0;
     for (int64_t iy = yb; iy < ye; iy++)
       for (uint32_t ix = 0; ix < R.nx; ix++) {
         const uint64_t e = grid[D.base + (size_t)(iy / kpc) * D.w + ix / kpc];
-        const double xa = (double)(R.px0 + (int64_t)ix) * R.pix - mu, xb = (double)(R.px0 + (int64_t)ix + 1) * R.pix + mu;
-        const double ya = (double)(R.py0 + iy) * R.pix - mu, yb2 = (double)(R.py0 + iy + 1) * R.pix + mu;
-        const int64_t m = pixel_answer(hv, e, xa, ya, xb, yb2);
-        if (m == kPixAnswerMixed || m >= (int64_t)mgpu::kPixMixed) continue;
-        R.cells[(size_t)iy * R.nx + ix] = (uint16_t)m;
-        np++;
+        R.cells[(size_t)iy * R.nx + ix] =
+            answer(e, (double)(R.px0 + (int64_t)ix) * R.pix, (double)(R.py0 + iy) * R.pix,
+                   (double)(R.px0 + (int64_t)ix + 1) * R.pix, (double)(R.py0 + iy + 1) * R.pix, 1e-6 * R.pix + mu0);
       }
-    pure += np;
   });
-  R.n_pure = pure;
+  // level 2: sub-pixels of whole metres, S = the largest divisor of the pixel edge <= 8
+  int S = 0;
+  if (raster_sub_wanted())
+    for (int d = std::min<int>(raster_sub_wanted(), (int)R.pix); d >= 2; d--)
+      if (R.pix % d == 0) {
+        S = d;
+        break;
+      }
+  std::vector<uint32_t> mixed;
+  for (size_t i = 0; i < R.cells.size(); i++)
+    if (R.cells[i] == mgpu::kPixMixed) mixed.push_back((uint32_t)i);
+  if (S >= 2 && !mixed.empty() && (int64_t)mixed.size() * S * S <= kRasterMaxSub) {
+    R.sub_n = (uint32_t)S;
+    const uint32_t w = R.pix / S;
+    R.sub_w = w;
+    R.ref.assign(R.cells.size(), 0);
+    for (size_t k = 0; k < mixed.size(); k++) R.ref[mixed[k]] = (uint32_t)(k + 1);
+    R.sub.assign(mixed.size() * S * S, mgpu::kPixMixed);
+    mgpu::parallel_for((int64_t)mixed.size(), 256, [&](int64_t kb, int64_t ke, int) {
+      for (int64_t k = kb; k < ke; k++) {
+        const uint32_t ix = mixed[k] % R.nx, iy = mixed[k] / R.nx;
+        const uint64_t e = grid[D.base + (size_t)(iy / kpc) * D.w + ix / kpc];
+        const double x0 = (double)(R.px0 + (int64_t)ix) * R.pix, y0 = (double)(R.py0 + (int64_t)iy) * R.pix;
+        for (int v = 0; v < S; v++)
+          for (int u = 0; u < S; u++)
+            R.sub[(size_t)k * S * S + v * S + u] =
+                answer(e, x0 + (double)u * w, y0 + (double)v * w, x0 + (double)(u + 1) * w, y0 + (double)(v + 1) * w,
+                       1e-6 * w + mu0);
+      }
+    });
+  }
+  R.n_pure = 0;
+  for (uint16_t v : R.cells) R.n_pure += v != mgpu::kPixMixed;
   return true;
 }
 
@@ -1271,6 +1379,8 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
       {grid.data(), grid.size() * 8, 0},
       {raster.cells.data(), raster.cells.size() * 2, 0},
       {raster.cls.data(), raster.cls.size() * 8, 0},
+      {raster.ref.data(), raster.ref.size() * 4, 0},
+      {raster.sub.data(), raster.sub.size() * 2, 0},
   };
   size_t total = kBlobHeaderBytes;
   BlobHeader hdr{};
@@ -1302,9 +1412,15 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   hdr.raster_inv_dx = raster.inv_dx;
   hdr.raster_inv_dy = raster.inv_dy;
   for (int k = 0; k < 4; k++) hdr.raster_pc[k] = raster.pc[k];
+  hdr.raster_sub_n = raster.sub_n;
+  hdr.raster_sub_w = raster.sub_w;
   if (getenv("MGPU_RASTER_REPORT"))
-    fprintf(stderr, "mgpu raster: mode %d, %u x %u pixels, %zu classes, %.1f%% pure\n", raster.mode, raster.nx, raster.ny,
-            raster.cls.size(), raster.cells.empty() ? 0.0 : 100.0 * raster.n_pure / raster.cells.size());
+    fprintf(stderr, "mgpu raster: mode %d, %u x %u pixels, %zu classes, %.1f%% pure; %u x %u sub-pixels in %zu mixed pixels, "
+            "%.1f%% pure\n", raster.mode, raster.nx, raster.ny, raster.cls.size(),
+            raster.cells.empty() ? 0.0 : 100.0 * raster.n_pure / raster.cells.size(), raster.sub_n, raster.sub_n,
+            raster.sub_n ? raster.sub.size() / (raster.sub_n * raster.sub_n) : (size_t)0,
+            raster.sub.empty() ? 0.0 : 100.0 * std::count_if(raster.sub.begin(), raster.sub.end(), [](uint16_t v) {
+              return v != mgpu::kPixMixed; }) / raster.sub.size());
   for (size_t k = 0; k < parts.size(); k++) {
     parts[k].off = total;
     hdr.off[k] = total;
@@ -1822,9 +1938,9 @@ int32_t mgpu_test_raster_host(int32_t index_system, int32_t res, int64_t n_chips
       continue;
     }
     bool ok = true;
-    uint32_t gi = 0;
-    const uint32_t ri = index_system == MGPU_H3 ? mgpu::raster_index<MGPU_H3>(v, x[i], y[i], &ok, &gi)
-                                                : mgpu::raster_index<MGPU_BNG>(v, x[i], y[i], &ok, &gi);
+    uint32_t gi = 0, sub = 0;
+    const uint32_t ri = index_system == MGPU_H3 ? mgpu::raster_index<MGPU_H3>(v, x[i], y[i], &ok, &gi, &sub)
+                                                : mgpu::raster_index<MGPU_BNG>(v, x[i], y[i], &ok, &gi, &sub);
     if (!ok) {
       out_kind[i] = 3;
       continue;
@@ -1833,7 +1949,7 @@ int32_t mgpu_test_raster_host(int32_t index_system, int32_t res, int64_t n_chips
       out_kind[i] = 2;
       continue;
     }
-    const uint32_t cl = ri == mgpu::kNoPixel ? mgpu::kPixEmpty : v.raster[ri];
+    const uint32_t cl = ri == mgpu::kNoPixel ? mgpu::kPixEmpty : mgpu::raster_class(v, ri, sub);
     if (cl == mgpu::kPixMixed) {
       out_kind[i] = 2;
       continue;

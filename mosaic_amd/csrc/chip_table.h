@@ -167,6 +167,13 @@ struct ChipTableView {
                                // matches for raster_pc[k - 1] <= c < raster_pc[k] (k < 4)
   const uint16_t* raster;      // [ny * nx] classes
   const uint64_t* raster_cls;  // [classes]
+  // second level: a mixed pixel p with raster_ref[p] = 1 + b is cut into sub_n x sub_n
+  // sub-pixels whose classes are raster_sub[b * sub_n^2 + v * sub_n + u] (lonlat: u =
+  // the truncated sub_n * fractional pixel position, clamped; BNG: (metres into the
+  // pixel) / raster_sub_w)
+  uint32_t raster_sub_n, raster_sub_w;
+  const uint32_t* raster_ref;  // [ny * nx], or null: no second level
+  const uint16_t* raster_sub;
 };
 
 enum RasterMode { kRasterNone = 0, kRasterLonLat = 1, kRasterBng = 2 };

@@ -429,14 +429,15 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         by[k] = MGPU_LDPT(&a.y[p]);
       }
     }
-    uint32_t ri[kItems], gix[kItems];
+    uint32_t ri[kItems], gix[kItems], sb[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
       ri[k] = kNoPixel;
       gix[k] = 0;
+      sb[k] = 0;
       if (base + k * kBlock + lane < a.n) {
         bool ok;
-        ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &gix[k]);
+        ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &gix[k], &sb[k]);
         any_bad |= !ok;
       }
     }
@@ -444,7 +445,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     uint64_t ge[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
-      cl[k] = ri[k] < kRasterFull ? (uint32_t)t.raster[ri[k]] : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
+      cl[k] = ri[k] < kRasterFull ? raster_class(t, ri[k], sb[k]) : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
       if (IS == MGPU_BNG) ge[k] = ri[k] < kRasterFull ? t.grid[gix[k]] : 0ull;  // (independent of the pixel load)
     }
     uint64_t ce[kItems];
@@ -963,14 +964,15 @@ __global__ __launch_bounds__(kClsBlock) void classify_kernel(SplitArgs sa) {
         by[k] = __builtin_nontemporal_load(&a.y[p]);
       }
     }
-    uint32_t ri[kClsBatch], gix[kClsBatch];
+    uint32_t ri[kClsBatch], gix[kClsBatch], sb[kClsBatch];
 #pragma unroll
     for (int k = 0; k < kClsBatch; k++) {
       ri[k] = kNoPixel;
       gix[k] = 0;
+      sb[k] = 0;
       if (c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x < a.n) {
         bool ok;
-        ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &gix[k]);
+        ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &gix[k], &sb[k]);
         any_bad |= !ok;
         if (a.ablate == 11) ri[k] = bx[k] == 12345.0 ? 0u : kNoPixel;  // profiling: no pixel loads
       }
@@ -979,7 +981,7 @@ __global__ __launch_bounds__(kClsBlock) void classify_kernel(SplitArgs sa) {
     uint64_t ge[kClsBatch];
 #pragma unroll
     for (int k = 0; k < kClsBatch; k++) {
-      cl[k] = ri[k] < kRasterFull ? (uint32_t)t.raster[ri[k]] : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
+      cl[k] = ri[k] < kRasterFull ? raster_class(t, ri[k], sb[k]) : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
       ge[k] = (IS == MGPU_BNG && ri[k] < kRasterFull) ? t.grid[gix[k]] : 0ull;
     }
 #pragma unroll
@@ -1053,9 +1055,10 @@ __global__ __launch_bounds__(kBlock) void pip_mixed_fix_kernel(JoinArgs a) {
 }
 
 // Ordered output.  Thread i handles the points c0 + 256 k + i (k = 0 .. 15, as
-// classify_kernel): the mixed points' list positions come from the same ballots, and per
-// k one workgroup scan places the pairs of 256 consecutive points -- consecutive lanes
-// write consecutive pairs.
+// classify_kernel: the mixed points' list positions come from the same ballots).  The
+// pair counts go to LDS in point order, one workgroup scan over 16 consecutive counts
+// per thread gives every point's output offset, and consecutive lanes write consecutive
+// pairs.
 template <int IS>
 __global__ __launch_bounds__(kClsBlock) void split_emit_kernel(SplitArgs sa) {
   using Code = typename CodeOf<IS>::T;
@@ -1063,7 +1066,8 @@ __global__ __launch_bounds__(kClsBlock) void split_emit_kernel(SplitArgs sa) {
   const ChipTableView& t = a.chips;
   __shared__ unsigned long long s_bal[64];
   __shared__ uint32_t s_pos[64];
-  __shared__ uint32_t s_w[2][kClsBlock / 64];
+  __shared__ uint32_t s_w[kClsBlock / 64];
+  __shared__ uint32_t s_off[kChunk];  // pair count, then offset, of each point (point order)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t c0 = (int64_t)blockIdx.x * kChunk;
   const Code* codes = (const Code*)sa.codes;
@@ -1085,7 +1089,6 @@ __global__ __launch_bounds__(kClsBlock) void split_emit_kernel(SplitArgs sa) {
     s_pos[lane] = wave_incl_scan(v) - v;
   }
   __syncthreads();
-  uint64_t run = sa.chunk_off[blockIdx.x];
   const unsigned long long lt = (1ull << lane) - 1ull;
   // every answer's load in flight at once (mixed answers, class table)
   uint64_t vv[kClsItems];
@@ -1102,33 +1105,42 @@ __global__ __launch_bounds__(kClsBlock) void split_emit_kernel(SplitArgs sa) {
         v = (uint64_t)((uint32_t)cd[k] >> 8) | ((uint64_t)((uint32_t)cd[k] & 0xFFu) << 32);
     }
     vv[k] = v;
+    s_off[k * kClsBlock + threadIdx.x] = (uint32_t)__popc((uint32_t)(v >> 32));
   }
+  __syncthreads();
+  // thread i scans points 16 i .. 16 i + 15
+  uint32_t c16[kClsItems], sum = 0;
 #pragma unroll
   for (int k = 0; k < kClsItems; k++) {
-    const int64_t p = c0 + (int64_t)k * kClsBlock + threadIdx.x;
-    const uint64_t v = vv[k];
-    const uint32_t first = (uint32_t)v, mask = (uint32_t)(v >> 32), cnt = __popc(mask);
-    const uint32_t incl = wave_incl_scan(cnt);
-    if (lane == 63) s_w[k & 1][wave] = incl;
-    __syncthreads();
-    uint64_t q = run + incl - cnt;
-    uint32_t tot = 0;
+    c16[k] = s_off[threadIdx.x * kClsItems + k];
+    sum += c16[k];
+  }
+  const uint32_t incl = wave_incl_scan(sum);
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  uint32_t run = incl - sum;
+  for (int w = 0; w < wave; w++) run += s_w[w];
 #pragma unroll
-    for (int w = 0; w < kClsBlock / 64; w++) {
-      const uint32_t x = s_w[k & 1][w];
-      if (w < wave) q += x;
-      tot += x;
-    }
-    run += tot;
-    if (mask) {
-      const int64_t pid = sa.point_id ? sa.point_id[p] : sa.id_base + p;
-      for (uint32_t m = mask; m; m &= m - 1) {
-        if ((int64_t)q < sa.capacity) {
-          sa.out_point[q] = pid;
-          sa.out_poly[q] = t.chip_poly[first + __builtin_ctz(m)];
-        }
-        q++;
+  for (int k = 0; k < kClsItems; k++) {
+    s_off[threadIdx.x * kClsItems + k] = run;
+    run += c16[k];
+  }
+  __syncthreads();
+  const uint64_t base = sa.chunk_off[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kClsItems; k++) {
+    const uint64_t v = vv[k];
+    const uint32_t first = (uint32_t)v, mask = (uint32_t)(v >> 32);
+    if (!mask) continue;
+    const int64_t p = c0 + (int64_t)k * kClsBlock + threadIdx.x;
+    uint64_t q = base + s_off[k * kClsBlock + threadIdx.x];
+    const int64_t pid = sa.point_id ? sa.point_id[p] : sa.id_base + p;
+    for (uint32_t m = mask; m; m &= m - 1) {
+      if ((int64_t)q < sa.capacity) {
+        sa.out_point[q] = pid;
+        sa.out_poly[q] = t.chip_poly[first + __builtin_ctz(m)];
       }
+      q++;
     }
   }
 }

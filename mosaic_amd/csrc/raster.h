@@ -23,7 +23,7 @@ MGPU_HDI uint32_t div_fix(uint32_t v, uint32_t d, double inv) {
   return q * d > v ? q - 1 : ((q + 1) * d <= v ? q + 1 : q);
 }
 template <int IS>
-MGPU_HDI uint32_t raster_index(const ChipTableView& t, double px, double py, bool* ok, uint32_t* gi) {
+MGPU_HDI uint32_t raster_index(const ChipTableView& t, double px, double py, bool* ok, uint32_t* gi, uint32_t* sub) {
   if (IS == MGPU_BNG) {
     *ok = px == px && py == py;  // pointToIndex rejects NaN only
     if (!*ok) return kNoPixel;
@@ -33,6 +33,12 @@ MGPU_HDI uint32_t raster_index(const ChipTableView& t, double px, double py, boo
     const uint32_t row = div_fix((uint32_t)nI, t.raster_pix, t.raster_inv_dy);
     const uint32_t ix = col - (uint32_t)t.raster_px0, iy = row - (uint32_t)t.raster_py0;
     if (ix >= t.raster_nx || iy >= t.raster_ny) return kNoPixel;  // outside the dense box: no chip cell
+    if (t.raster_sub_n) {
+      const double inv_w = 1.0 / (double)t.raster_sub_w;
+      const uint32_t u = div_fix((uint32_t)eI - col * t.raster_pix, t.raster_sub_w, inv_w);
+      const uint32_t v = div_fix((uint32_t)nI - row * t.raster_pix, t.raster_sub_w, inv_w);
+      *sub = v * t.raster_sub_n + u;
+    }
     const DenseFace& D = t.dense[0];
     *gi = D.base + (div_fix((uint32_t)nI, t.bng_edge, t.bng_inv_edge) - (uint32_t)D.b0) * D.w +
           (div_fix((uint32_t)eI, t.bng_edge, t.bng_inv_edge) - (uint32_t)D.a0);
@@ -40,10 +46,29 @@ MGPU_HDI uint32_t raster_index(const ChipTableView& t, double px, double py, boo
   }
   *ok = isfinite(px) && isfinite(py);
   if (!*ok || !(px >= t.bbox[0] && px <= t.bbox[2] && py >= t.bbox[1] && py <= t.bbox[3])) return kNoPixel;
-  uint32_t ix = (uint32_t)((px - t.raster_x0) * t.raster_inv_dx), iy = (uint32_t)((py - t.raster_y0) * t.raster_inv_dy);
+  const double tx = (px - t.raster_x0) * t.raster_inv_dx, ty = (py - t.raster_y0) * t.raster_inv_dy;
+  uint32_t ix = (uint32_t)tx, iy = (uint32_t)ty;
   ix = ix < t.raster_nx ? ix : t.raster_nx - 1;
   iy = iy < t.raster_ny ? iy : t.raster_ny - 1;
+  if (t.raster_sub_n) {
+    const double S = (double)t.raster_sub_n;
+    uint32_t u = (uint32_t)((tx - (double)ix) * S), v = (uint32_t)((ty - (double)iy) * S);
+    u = u < t.raster_sub_n ? u : t.raster_sub_n - 1;
+    v = v < t.raster_sub_n ? v : t.raster_sub_n - 1;
+    *sub = v * t.raster_sub_n + u;
+  }
   return iy * t.raster_nx + ix;
+}
+
+// The class of pixel ri (a raster_index result below kRasterFull), refined by its
+// second level when the pixel is mixed.
+MGPU_HDI uint32_t raster_class(const ChipTableView& t, uint32_t ri, uint32_t sub) {
+  uint32_t cl = t.raster[ri];
+  if (cl == kPixMixed && t.raster_ref) {
+    const uint32_t b = t.raster_ref[ri];
+    if (b) cl = t.raster_sub[(size_t)(b - 1) * t.raster_sub_n * t.raster_sub_n + sub];
+  }
+  return cl;
 }
 
 }  // namespace mgpu
