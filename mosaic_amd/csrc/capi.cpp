@@ -824,8 +824,13 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
   return true;
 }
 
+// (BNG: off unless MGPU_RASTER_BNG=1 -- its cell is a few integer operations and one grid
+// load already; on C4 the pixel lookups cost more than the point-in-polygon work they
+// save: split 2.55 ms vs fused 2.25 ms per 1e8 points)
 bool build_raster_bng(const mgpu::ChipTableView& hv, const mgpu::DenseFace& D, uint32_t edge,
                       const std::vector<uint64_t>& grid, Raster& R) {
+  const char* on = getenv("MGPU_RASTER_BNG");
+  if (!(on && atoi(on) == 1)) return false;
   if (!raster_enabled() || edge == 0 || grid.empty()) return false;
   // pixels per cell edge: the largest k <= 1 / fraction dividing the edge, within budget
   // (BNG default: 2 -- a raster of 2 x 2 pixels per cell stays in L2 at C4's size)

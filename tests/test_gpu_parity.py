@@ -580,7 +580,11 @@ def test_pixel_index_on_off_identical(gpu, nyc_chips_r9):
             d0 = c.upload()
         finally:
             del os.environ["MGPU_RASTER"]
-        d1 = c.upload()
+        os.environ["MGPU_RASTER_BNG"] = "1"
+        try:
+            d1 = c.upload()
+        finally:
+            del os.environ["MGPU_RASTER_BNG"]
         a = M.pip_join(T(x, gpu), T(y, gpu), d0, res, index_system=isys).numpy()
         rb = M.pip_join(T(x, gpu), T(y, gpu), d1, res, index_system=isys)
         b = rb.numpy()
