@@ -41,6 +41,7 @@ extern "C" {
 #define MGPU_E_DEVICE -6            /* HIP runtime error */
 #define MGPU_E_INTERNAL -7          /* kernel protocol failure (look-back timeout) */
 #define MGPU_E_UNSUPPORTED -8       /* input outside what the device path builds (H3 kRing near pentagons) */
+#define MGPU_E_EMPTY -9             /* IllegalStateException (JTS: getX / getY of an empty Point) */
 
 #define MGPU_H3 0
 #define MGPU_BNG 1
@@ -92,6 +93,25 @@ int32_t mgpu_check_resolution(int32_t index_system, int32_t res);
 int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t index_system, int32_t res,
                              const double* x, const double* y, int64_t n,
                              int64_t* out_cell, void* stream, mgpu_stats* stats);
+
+/* grid_pointascellid on a geometry column (PointIndexGeom.scala:33-47: GeometryAPI.geometry
+ * (GeometryAPI.scala:81-89) decodes BinaryType as WKB, StringType as WKT, then getCentroid,
+ * then pointToIndex).  Rows are data[offsets[i] .. offsets[i + 1]) (the Arrow binary /
+ * utf8 layout); POINT and MULTIPOINT geometries (WKB big- or little-endian, EWKB / ISO
+ * Z, M; WKT with Java Double.parseDouble rounding) -- other types return
+ * MGPU_E_UNSUPPORTED, malformed rows MGPU_E_WKB (JTS ParseException), empty points
+ * MGPU_E_EMPTY.  `valid` (optional Arrow bitmap, bit offset valid_offset): null rows are
+ * null out -- out_cell 0 and a 0 bit in out_valid ((n + 7) / 8 bytes, optional).
+ * mgpu_points_from_geometry stops at the point (x, y; NaN for null rows).  Device
+ * pointers; synchronises `stream`. */
+#define MGPU_GEOM_WKB 0
+#define MGPU_GEOM_WKT 1
+int32_t mgpu_points_from_geometry(mgpu_ctx* ctx, int32_t format, const uint8_t* data, const int64_t* offsets,
+                                  const uint8_t* valid, int64_t valid_offset, int64_t n, double* out_x, double* out_y,
+                                  void* stream);
+int32_t mgpu_geometry_to_cells(mgpu_ctx* ctx, int32_t index_system, int32_t res, int32_t format, const uint8_t* data,
+                               const int64_t* offsets, const uint8_t* valid, int64_t valid_offset, int64_t n,
+                               int64_t* out_cell, uint8_t* out_valid, void* stream, mgpu_stats* stats);
 
 /* Host-pointer convenience form (copies over PCIe). */
 int32_t mgpu_points_to_cells_host(mgpu_ctx* ctx, int32_t index_system, int32_t res,
@@ -261,6 +281,13 @@ int32_t mgpu_test_chip_contains_host(int32_t index_system, int64_t n_chips, cons
                                      const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
                                      const uint8_t* wkb, int64_t n, const int64_t* chip_row, const double* x,
                                      const double* y, int8_t* out_join_path, int8_t* out_point_locator);
+
+/* TEST ONLY -- the decimal parser of the WKT path (Double.parseDouble semantics) on one
+ * string: characters consumed (0: not a number) and the value.  Host only. */
+int32_t mgpu_test_parse_number(const char* s, int32_t len, double* out);
+/* TEST ONLY -- the WKB / WKT point decoder on one host row: status 0 ok, 1 malformed,
+ * 2 unsupported type, 3 empty. */
+int32_t mgpu_test_decode_point(int32_t format, const uint8_t* data, int64_t len, double* x, double* y);
 
 /* TEST ONLY -- st_contains(chip row, point) evaluated on a HOST blob (the join's
  * classification grid + strip path), to check on the CPU that a shipped blob is a

@@ -20,6 +20,7 @@ MGPU_E_CAPACITY = -5
 MGPU_E_DEVICE = -6
 MGPU_E_INTERNAL = -7
 MGPU_E_UNSUPPORTED = -8
+MGPU_E_EMPTY = -9
 
 MGPU_H3 = 0
 MGPU_BNG = 1
@@ -35,8 +36,11 @@ EXPORTS = (
     "mgpu_tess_destroy", "mgpu_test_chip_contains_host", "mgpu_test_raster_host", "mgpu_pip_join_fetch",
     "mgpu_chips_host_blob", "mgpu_host_free", "mgpu_host_blob_info", "mgpu_chips_upload_blob",
     "mgpu_comm_unique_id", "mgpu_comm_init", "mgpu_comm_info", "mgpu_comm_destroy", "mgpu_chips_broadcast",
-    "mgpu_pair_offsets", "mgpu_test_blob_contains_host",
+    "mgpu_pair_offsets", "mgpu_test_blob_contains_host", "mgpu_points_from_geometry", "mgpu_geometry_to_cells",
+    "mgpu_geometry_to_cells_arrow", "mgpu_pip_join_arrow", "mgpu_test_parse_number", "mgpu_test_decode_point",
 )
+MGPU_GEOM_WKB = 0
+MGPU_GEOM_WKT = 1
 MGPU_COMM_ID_BYTES = 128
 MGPU_PIPELINE_FUSED = 0
 MGPU_PIPELINE_SPLIT = 1
@@ -134,6 +138,13 @@ def lib():
         "mgpu_chips_broadcast": (I32, [P, P, I32, ctypes.POINTER(P), P]),
         "mgpu_pair_offsets": (I32, [P, I64, ctypes.POINTER(I64), ctypes.POINTER(I64), P, P]),
         "mgpu_test_blob_contains_host": (I32, [P, I64, I64, P, P, P, P]),
+        "mgpu_points_from_geometry": (I32, [P, I32, P, P, P, I64, I64, P, P, P]),
+        "mgpu_geometry_to_cells": (I32, [P, I32, I32, I32, P, P, P, I64, I64, P, P, P, ctypes.POINTER(MgpuStats)]),
+        "mgpu_geometry_to_cells_arrow": (I32, [P, I32, I32, P, P, P, P, P]),
+        "mgpu_pip_join_arrow": (I32, [P, P, I32, I32, P, P, P, I64, ctypes.POINTER(I64), P, P, P,
+                                      ctypes.POINTER(MgpuStats)]),
+        "mgpu_test_parse_number": (I32, [ctypes.c_char_p, I32, ctypes.POINTER(ctypes.c_double)]),
+        "mgpu_test_decode_point": (I32, [I32, P, I64, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (rt, args) in sig.items():
         f = getattr(L, name)
@@ -156,7 +167,7 @@ def check(status, what="", required=None):
     msg = last_error() or what
     if status == MGPU_E_CAPACITY:
         raise CapacityError(status, msg, required)
-    if status in (MGPU_E_RESOLUTION, MGPU_E_NAN, MGPU_E_INTERNAL):
+    if status in (MGPU_E_RESOLUTION, MGPU_E_NAN, MGPU_E_INTERNAL, MGPU_E_EMPTY):
         raise IllegalStateException(status, msg)
     if status in (MGPU_E_INVALID_ARG, MGPU_E_WKB):
         raise IllegalArgumentException(status, msg)

@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/mosaic_arrow.h"
 #include "../../include/mosaic_gpu.h"
 #include "bng_core.h"
 #include "chip_table.h"
@@ -29,6 +30,7 @@
 #include "raster.h"
 #include "wkb.h"
 #include "capi_internal.h"
+#include "geom_decode.h"
 
 namespace {
 
@@ -1603,7 +1605,8 @@ int32_t mgpu_st_contains(mgpu_ctx* ctx, const mgpu_chips* chips, const int64_t* 
 
 static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
                          const double* y, const int64_t* point_id, int64_t id_base, int64_t n, int64_t capacity,
-                         int64_t* out_point, int32_t* out_poly, hipStream_t s, bool timed) {
+                         int64_t* out_point, int32_t* out_poly, hipStream_t s, bool timed,
+                         const uint8_t* valid = nullptr, int64_t valid_off = 0) {
   if (!ctx || !chips) return fail(MGPU_E_INVALID_ARG, "ctx/chips is NULL");
   if (int32_t r = check_res(is, res)) return r;
   if (chips->index_system != is)
@@ -1659,6 +1662,11 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   e.out_poly = out_poly;
   a.ties = (unsigned long long*)(base + L.ties);
   a.tie_cap = kTieCap;
+  a.valid = valid;
+  a.valid_off = valid_off;
+  a.mixed_idx = nullptr;
+  a.mixed_res = nullptr;
+  a.chunk_mixed = nullptr;
   HIP_TRY(hipMemsetAsync(base, 0, kWsCounters, s));
   HIP_TRY(hipMemsetAsync(base + L.ties, 0, 8, s));
   // the split pipeline (kernels.h SplitArgs) when the chip table has a pixel index for
@@ -1723,6 +1731,8 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   L2.point_id = point_id;
   L2.id_base = id_base;
   L2.n = n;
+  L2.pts_valid = valid;
+  L2.pts_valid_off = valid_off;
   L2.emit = e;
   L2.n_tiles = tiles;
   L2.pool_ok = false;
@@ -1762,13 +1772,16 @@ int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, 
   return MGPU_OK;
 }
 
-int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
-                      const double* y, const int64_t* point_id, int64_t point_id_base, int64_t n, int64_t capacity,
-                      int64_t* out_n_pairs, int64_t* out_point_id, int32_t* out_polygon_id, void* stream,
-                      mgpu_stats* stats) {
+}  // extern "C"
+
+// mgpu_pip_join with an optional validity bitmap of the points (the Arrow entry's nulls)
+static int32_t pip_join_sync(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
+                             const double* y, const int64_t* point_id, int64_t point_id_base, int64_t n,
+                             int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id, int32_t* out_polygon_id,
+                             void* stream, mgpu_stats* stats, const uint8_t* valid, int64_t valid_off) {
   hipStream_t s = (hipStream_t)stream;
   int32_t st = join_impl(ctx, chips, is, res, x, y, point_id, point_id_base, n, capacity, out_point_id, out_polygon_id,
-                         s, true);
+                         s, true, valid, valid_off);
   if (st) return st;
   unsigned long long h[8] = {0};
   HIP_TRY(hipMemcpyAsync(h, ctx->ws, sizeof h, hipMemcpyDeviceToHost, s));
@@ -1815,6 +1828,16 @@ int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_
   return MGPU_OK;
 }
 
+extern "C" {
+
+int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
+                      const double* y, const int64_t* point_id, int64_t point_id_base, int64_t n, int64_t capacity,
+                      int64_t* out_n_pairs, int64_t* out_point_id, int32_t* out_polygon_id, void* stream,
+                      mgpu_stats* stats) {
+  return pip_join_sync(ctx, chips, is, res, x, y, point_id, point_id_base, n, capacity, out_n_pairs, out_point_id,
+                       out_polygon_id, stream, stats, nullptr, 0);
+}
+
 int32_t mgpu_pip_join_fetch(mgpu_ctx* ctx, int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id,
                             int32_t* out_polygon_id, void* stream) {
   if (!ctx) return fail(MGPU_E_INVALID_ARG, "ctx is NULL");
@@ -1830,8 +1853,9 @@ int32_t mgpu_pip_join_fetch(mgpu_ctx* ctx, int64_t capacity, int64_t* out_n_pair
     // the overflow pool had dropped records: redo the join with a pool that holds them
     const auto c = L;
     int64_t cnt = 0;
-    return mgpu_pip_join(ctx, c.chips, c.is, c.res, c.x, c.y, c.point_id, c.id_base, c.n, capacity, out_n_pairs ? out_n_pairs : &cnt,
-                         out_point_id, out_polygon_id, stream, nullptr);
+    return pip_join_sync(ctx, c.chips, c.is, c.res, c.x, c.y, c.point_id, c.id_base, c.n, capacity,
+                         out_n_pairs ? out_n_pairs : &cnt, out_point_id, out_polygon_id, stream, nullptr, c.pts_valid,
+                         c.pts_valid_off);
   }
   if (L.split) {
     mgpu::SplitArgs sa = L.sargs;
@@ -1982,6 +2006,176 @@ int32_t mgpu_test_blob_contains_host(const void* host_blob, int64_t bytes, int64
     out[i] = (v.chip_flags[c] & mgpu::kChipNoGeom) ? -1 : (mgpu::pip::chip_contains_strips(v, c, x[i], y[i]) ? 1 : 0);
   }
   return MGPU_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ geometry columns, Arrow
+
+static int32_t ensure_scratch(mgpu_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->scratch_bytes) return MGPU_OK;
+  if (ctx->scratch) HIP_TRY(hipFree(ctx->scratch));
+  ctx->scratch = nullptr;
+  ctx->scratch_bytes = 0;
+  HIP_TRY(hipMalloc(&ctx->scratch, bytes));
+  ctx->scratch_bytes = bytes;
+  return MGPU_OK;
+}
+
+// decode into (x, y) and check the decode counters
+static int32_t decode_points(mgpu_ctx* ctx, int32_t format, const uint8_t* data, const void* offsets, int off32,
+                             const uint8_t* valid, int64_t voff, int64_t n, double* x, double* y, hipStream_t s) {
+  if (format != MGPU_GEOM_WKB && format != MGPU_GEOM_WKT) return fail(MGPU_E_INVALID_ARG, "geometry format %d", format);
+  if (n < 0 || (n > 0 && (!data || !offsets || !x || !y))) return fail(MGPU_E_INVALID_ARG, "bad geometry arrays");
+  if (int32_t st = ensure_ws(ctx, 1)) return st;
+  auto* counters = (unsigned long long*)ctx->ws;
+  HIP_TRY(hipMemsetAsync(counters, 0, kWsCounters, s));
+  HIP_TRY(mgpu::launch_decode_points(format, data, offsets, off32, valid, voff, n, x, y, counters, s));
+  unsigned long long h[8] = {0};
+  HIP_TRY(hipMemcpyAsync(h, counters, sizeof h, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (h[4]) return fail(MGPU_E_WKB, "%llu rows are not well-formed %s", h[4], format == MGPU_GEOM_WKB ? "WKB" : "WKT");
+  if (h[5])
+    return fail(MGPU_E_UNSUPPORTED, "%llu rows are neither POINT nor MULTIPOINT (their centroid is not built here)", h[5]);
+  if (h[6]) return fail(MGPU_E_EMPTY, "getX called on empty Point (%llu rows)", h[6]);
+  return MGPU_OK;
+}
+
+extern "C" {
+
+int32_t mgpu_points_from_geometry(mgpu_ctx* ctx, int32_t format, const uint8_t* data, const int64_t* offsets,
+                                  const uint8_t* valid, int64_t valid_offset, int64_t n, double* out_x, double* out_y,
+                                  void* stream) {
+  if (!ctx) return fail(MGPU_E_INVALID_ARG, "ctx is NULL");
+  if (int32_t st = set_device(ctx->device)) return st;
+  return decode_points(ctx, format, data, offsets, 0, valid, valid_offset, n, out_x, out_y, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+static int32_t geometry_cells(mgpu_ctx* ctx, int32_t is, int32_t res, int32_t format, const uint8_t* data,
+                              const void* offsets, int off32, const uint8_t* valid, int64_t voff, int64_t n,
+                              int64_t* out_cell, uint8_t* out_valid, hipStream_t s, mgpu_stats* stats) {
+  if (!ctx) return fail(MGPU_E_INVALID_ARG, "ctx is NULL");
+  if (int32_t r = check_res(is, res)) return r;
+  if (n < 0 || (n > 0 && !out_cell)) return fail(MGPU_E_INVALID_ARG, "bad output array");
+  if (int32_t st = set_device(ctx->device)) return st;
+  if (int32_t st = ensure_scratch(ctx, (size_t)std::max<int64_t>(n, 1) * 16)) return st;
+  double* x = (double*)ctx->scratch;
+  double* y = x + std::max<int64_t>(n, 1);
+  if (int32_t st = decode_points(ctx, format, data, offsets, off32, valid, voff, n, x, y, s)) return st;
+  auto* counters = (unsigned long long*)ctx->ws;
+  auto* ties = (unsigned long long*)((uint8_t*)ctx->ws + ws_layout(1, 0).ties);
+  HIP_TRY(hipMemsetAsync(counters, 0, kWsCounters, s));
+  HIP_TRY(hipMemsetAsync(ties, 0, 8, s));
+  HIP_TRY(hipEventRecord(ctx->ev0, s));
+  HIP_TRY(mgpu::launch_cells(is, res, x, y, n, out_cell, counters, ties, kTieCap, s, valid, voff));
+  HIP_TRY(hipEventRecord(ctx->ev1, s));
+  if (out_valid) HIP_TRY(mgpu::launch_valid_and(valid, voff, nullptr, 0, n, out_valid, s));
+  unsigned long long h[8] = {0};
+  HIP_TRY(hipMemcpyAsync(h, counters, sizeof h, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (stats) {
+    memset(stats, 0, sizeof *stats);
+    stats->n_points = n;
+    stats->n_near_ties = (int64_t)h[1];
+    float ms = 0;
+    hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+    stats->kernel_ms = stats->stream_kernel_ms = ms;
+  }
+  if (h[2]) {
+    if (is == MGPU_BNG) return fail(MGPU_E_NAN, "NaN coordinates are not supported. (%llu points)", h[2]);
+    return fail(MGPU_E_INVALID_ARG, "Latitude or longitude were invalid. (%llu points)", h[2]);
+  }
+  return MGPU_OK;
+}
+
+// an Arrow array on this context's GPU with the given format; *data = its values (offset
+// applied), *valid / *voff = its validity bitmap (null: no nulls)
+static int32_t arrow_column(mgpu_ctx* ctx, const ArrowDeviceArray* a, size_t elem, const void** data,
+                            const uint8_t** valid, int64_t* voff, const char* what) {
+  if (!a) return fail(MGPU_E_INVALID_ARG, "%s: NULL array", what);
+  if (a->device_type != ARROW_DEVICE_ROCM || a->device_id != ctx->device)
+    return fail(MGPU_E_INVALID_ARG, "%s: not on this context's GPU (device type %d, id %lld)", what, a->device_type,
+                (long long)a->device_id);
+  if (a->array.n_buffers < 2 || !a->array.buffers || a->array.length < 0 || a->array.offset < 0)
+    return fail(MGPU_E_INVALID_ARG, "%s: not a primitive Arrow array", what);
+  if (a->sync_event) HIP_TRY(hipEventSynchronize((hipEvent_t)a->sync_event));
+  *data = (const uint8_t*)a->array.buffers[1] + (size_t)a->array.offset * elem;
+  *valid = a->array.null_count != 0 ? (const uint8_t*)a->array.buffers[0] : nullptr;
+  *voff = a->array.offset;
+  return MGPU_OK;
+}
+
+extern "C" {
+
+int32_t mgpu_geometry_to_cells(mgpu_ctx* ctx, int32_t index_system, int32_t res, int32_t format, const uint8_t* data,
+                               const int64_t* offsets, const uint8_t* valid, int64_t valid_offset, int64_t n,
+                               int64_t* out_cell, uint8_t* out_valid, void* stream, mgpu_stats* stats) {
+  return geometry_cells(ctx, index_system, res, format, data, offsets, 0, valid, valid_offset, n, out_cell, out_valid,
+                        (hipStream_t)stream, stats);
+}
+
+int32_t mgpu_geometry_to_cells_arrow(mgpu_ctx* ctx, int32_t index_system, int32_t res,
+                                     const struct ArrowDeviceArray* geom, const struct ArrowSchema* schema,
+                                     int64_t* out_cell, uint8_t* out_valid, void* stream) {
+  if (!ctx || !geom || !schema || !schema->format) return fail(MGPU_E_INVALID_ARG, "NULL argument");
+  const char f = schema->format[0];
+  if (!((f == 'z' || f == 'Z' || f == 'u' || f == 'U') && schema->format[1] == 0))
+    return fail(MGPU_E_INVALID_ARG, "geometry column format '%s': binary (WKB) or utf8 (WKT) expected", schema->format);
+  if (geom->device_type != ARROW_DEVICE_ROCM || geom->device_id != ctx->device)
+    return fail(MGPU_E_INVALID_ARG, "geometry column not on this context's GPU");
+  if (geom->array.n_buffers < 3 || !geom->array.buffers) return fail(MGPU_E_INVALID_ARG, "not a binary Arrow array");
+  if (geom->sync_event) HIP_TRY(hipEventSynchronize((hipEvent_t)geom->sync_event));
+  const bool o32 = f == 'z' || f == 'u';
+  const uint8_t* offs = (const uint8_t*)geom->array.buffers[1] + (size_t)geom->array.offset * (o32 ? 4 : 8);
+  const uint8_t* valid = geom->array.null_count != 0 ? (const uint8_t*)geom->array.buffers[0] : nullptr;
+  return geometry_cells(ctx, index_system, res, (f == 'z' || f == 'Z') ? MGPU_GEOM_WKB : MGPU_GEOM_WKT,
+                        (const uint8_t*)geom->array.buffers[2], offs, o32 ? 1 : 0, valid, geom->array.offset,
+                        geom->array.length, out_cell, out_valid, (hipStream_t)stream, nullptr);
+}
+
+int32_t mgpu_pip_join_arrow(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t index_system, int32_t res,
+                            const struct ArrowDeviceArray* x, const struct ArrowDeviceArray* y,
+                            const struct ArrowDeviceArray* point_id, int64_t capacity, int64_t* out_n_pairs,
+                            int64_t* out_point_id, int32_t* out_polygon_id, void* stream, mgpu_stats* stats) {
+  if (!ctx) return fail(MGPU_E_INVALID_ARG, "ctx is NULL");
+  if (int32_t st = set_device(ctx->device)) return st;
+  hipStream_t s = (hipStream_t)stream;
+  const void *xd, *yd, *pd = nullptr;
+  const uint8_t *xv, *yv, *pv = nullptr;
+  int64_t xo, yo, po = 0;
+  if (int32_t st = arrow_column(ctx, x, 8, &xd, &xv, &xo, "x")) return st;
+  if (int32_t st = arrow_column(ctx, y, 8, &yd, &yv, &yo, "y")) return st;
+  const int64_t n = x->array.length;
+  if (y->array.length != n) return fail(MGPU_E_INVALID_ARG, "x and y differ in length");
+  if (point_id) {
+    if (int32_t st = arrow_column(ctx, point_id, 8, &pd, &pv, &po, "point_id")) return st;
+    if (point_id->array.length != n) return fail(MGPU_E_INVALID_ARG, "point_id and x differ in length");
+    if (pv) return fail(MGPU_E_INVALID_ARG, "point_id has nulls");
+  }
+  const uint8_t* valid = nullptr;
+  int64_t voff = 0;
+  if (xv && yv) {
+    if (int32_t st = ensure_scratch(ctx, (size_t)(n + 7) / 8 + 1)) return st;
+    HIP_TRY(mgpu::launch_valid_and(xv, xo, yv, yo, n, (uint8_t*)ctx->scratch, s));
+    valid = (const uint8_t*)ctx->scratch;
+  } else if (xv || yv) {
+    valid = xv ? xv : yv;
+    voff = xv ? xo : yo;
+  }
+  return pip_join_sync(ctx, chips, index_system, res, (const double*)xd, (const double*)yd, (const int64_t*)pd,
+                       point_id ? 0 : x->array.offset, n, capacity, out_n_pairs, out_point_id, out_polygon_id, stream, stats, valid,
+                       voff);
+}
+
+int32_t mgpu_test_parse_number(const char* s, int32_t len, double* out) {
+  return mgpu::dec::parse_number(s, len, out);
+}
+
+int32_t mgpu_test_decode_point(int32_t format, const uint8_t* data, int64_t len, double* x, double* y) {
+  return format == MGPU_GEOM_WKB ? mgpu::geom::wkb_centroid(data, len, x, y)
+                                 : mgpu::geom::wkt_centroid((const char*)data, len, x, y);
 }
 
 }  // extern "C"

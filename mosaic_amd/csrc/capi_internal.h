@@ -17,6 +17,9 @@ struct mgpu_ctx {
   // the split pipeline's per-point buffers (codes, mixed lists and answers), grown on demand
   void* split_ws = nullptr;
   size_t split_bytes = 0;
+  // scratch of the geometry / Arrow entries (decoded points, validity bitmaps), grown on demand
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
   // the last mgpu_pip_join on this context, whose pair records stay in the workspace
   // until the next call (mgpu_pip_join_fetch)
   struct {
@@ -26,6 +29,8 @@ struct mgpu_ctx {
     const double *x = nullptr, *y = nullptr;
     const int64_t* point_id = nullptr;
     int64_t id_base = 0, n = 0, total = 0;
+    const uint8_t* pts_valid = nullptr;
+    int64_t pts_valid_off = 0;
     mgpu::EmitArgs emit{};
     int64_t n_tiles = 0;
     bool split = false;

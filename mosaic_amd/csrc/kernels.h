@@ -39,6 +39,8 @@ struct JoinArgs {
   const uint16_t* mixed_idx;
   uint64_t* mixed_res;
   const uint32_t* chunk_mixed;
+  const uint8_t* valid;             // null points (Arrow validity bitmap at bit offset valid_off), or null
+  int64_t valid_off;
 };
 
 // The split pipeline (a chip table with a pixel index and at most 32 chips per cell):
@@ -80,9 +82,20 @@ struct EmitArgs {
   int32_t* out_poly;
 };
 
-// ties: [0] count, [1 .. tie_cap] point indices (zero ties[0] before launch)
+// ties: [0] count, [1 .. tie_cap] point indices (zero ties[0] before launch); `valid`
+// (optional Arrow bitmap at bit offset voff): null points get cell 0
 hipError_t launch_cells(int is, int res, const double* x, const double* y, int64_t n, int64_t* out,
-                        unsigned long long* counters, unsigned long long* ties, int64_t tie_cap, hipStream_t s);
+                        unsigned long long* counters, unsigned long long* ties, int64_t tie_cap, hipStream_t s,
+                        const uint8_t* valid = nullptr, int64_t voff = 0);
+// the point (centroid) of each POINT / MULTIPOINT geometry, WKB (format 0) or WKT (1),
+// rows data[offsets[i] .. offsets[i + 1]); null rows (valid bitmap) -> NaN.  counters[4..6]
+// += malformed / unsupported type / empty rows
+hipError_t launch_decode_points(int format, const uint8_t* data, const void* offsets, int off32, const uint8_t* valid,
+                                int64_t voff, int64_t n, double* x, double* y, unsigned long long* counters,
+                                hipStream_t s);
+// AND of two validity bitmaps (either may be null) into out (bit offset 0), n bits
+hipError_t launch_valid_and(const uint8_t* a, int64_t aoff, const uint8_t* b, int64_t boff, int64_t n, uint8_t* out,
+                            hipStream_t s);
 int64_t join_tiles(int64_t n);
 int64_t join_tile_points();
 int64_t join_slot_records();   // records reserved per tile (pairs beyond go to the overflow pool)

@@ -26,6 +26,7 @@
 #include "h3_ring.h"
 #include "kernels.h"
 #include "raster.h"
+#include "geom_decode.h"
 
 namespace mgpu {
 
@@ -63,7 +64,8 @@ template <int IS>
 __global__ __launch_bounds__(kStreamBlock) void cells_kernel(const double* __restrict__ x, const double* __restrict__ y,
                                                        int64_t n, int res, int64_t* __restrict__ out,
                                                        unsigned long long* __restrict__ counters,
-                                                       unsigned long long* __restrict__ ties, int64_t tie_cap) {
+                                                       unsigned long long* __restrict__ ties, int64_t tie_cap,
+                                                       const uint8_t* __restrict__ valid, int64_t voff) {
   const double k_res = h3::k_of_res(res);
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -71,7 +73,9 @@ __global__ __launch_bounds__(kStreamBlock) void cells_kernel(const double* __res
     bool ok;
     int64_t c = 0;
     const double px = x[i], py = y[i];
-    if (IS == MGPU_H3) {
+    if (!pt_valid(valid, voff, i)) {
+      ok = true;  // a null row: null out (cell 0 here, the caller's validity says null)
+    } else if (IS == MGPU_H3) {
       ok = isfinite(px) && isfinite(py);
       if (ok) {
         const h3::FastHex f = h3::fast_hex2d(h3::to_radians_fast(py), h3::to_radians_fast(px), res, k_res, kAllFaces);
@@ -96,7 +100,8 @@ __global__ __launch_bounds__(kStreamBlock) void cells_fix_kernel(const double* _
                                                            int64_t n, int res, int64_t* __restrict__ out,
                                                            unsigned long long* __restrict__ counters,
                                                            const unsigned long long* __restrict__ ties,
-                                                           int64_t tie_cap) {
+                                                           int64_t tie_cap, const uint8_t* __restrict__ valid,
+                                                           int64_t voff) {
   const int64_t nt = (int64_t)ties[0];
   const bool all = nt > tie_cap;
   const int64_t m = all ? n : nt;
@@ -105,7 +110,7 @@ __global__ __launch_bounds__(kStreamBlock) void cells_fix_kernel(const double* _
     const int64_t i = all ? q : (int64_t)ties[1 + q];
     const double px = x[i], py = y[i];
     bool tie = false;
-    if (isfinite(px) && isfinite(py)) {
+    if (isfinite(px) && isfinite(py) && pt_valid(valid, voff, i)) {
       h3::FastHex f = h3::fast_hex2d(h3::to_radians_fast(py), h3::to_radians_fast(px), res, k_res, kAllFaces);
       if (f.tie) h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, &tie);
       out[i] = (int64_t)h3::face_ijk_to_h3_fast(f.face, f.ijk, res);
@@ -435,7 +440,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
       ri[k] = kNoPixel;
       gix[k] = 0;
       sb[k] = 0;
-      if (base + k * kBlock + lane < a.n) {
+      if (base + k * kBlock + lane < a.n && pt_valid(a.valid, a.valid_off, base + k * kBlock + lane)) {
         bool ok;
         ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &gix[k], &sb[k]);
         any_bad |= !ok;
@@ -517,7 +522,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     for (int k = 0; k < kItems; k++) {
       r[k] = Range{0, 0, 0};
       gi[k] = kNoEntry;
-      if (MGPU_VALID(k * kBlock + threadIdx.x)) {
+      if (MGPU_VALID(k * kBlock + threadIdx.x) && pt_valid(a.valid, a.valid_off, MGPU_PT(k * kBlock + threadIdx.x))) {
         bool ok, tie;
         r[k] = chip_probe<IS, SLOW>(t, bx[k], by[k], a.res, res_match, &ok, &tie, a.ablate, &gi[k]);
         any_bad |= !ok;
@@ -549,7 +554,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         nx = MGPU_LDPT(&a.x[MGPU_PT(li + kBlock)]);
         ny = MGPU_LDPT(&a.y[MGPU_PT(li + kBlock)]);
       }
-      if (MGPU_VALID(li)) {
+      if (MGPU_VALID(li) && pt_valid(a.valid, a.valid_off, p)) {
         bool ok, tie;
         if (a.ablate == 3) {  // profiling: no projection, no probe
           ok = true;
@@ -970,7 +975,8 @@ __global__ __launch_bounds__(kClsBlock) void classify_kernel(SplitArgs sa) {
       ri[k] = kNoPixel;
       gix[k] = 0;
       sb[k] = 0;
-      if (c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x < a.n) {
+      const int64_t pk = c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x;
+      if (pk < a.n && pt_valid(a.valid, a.valid_off, pk)) {
         bool ok;
         ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &gix[k], &sb[k]);
         any_bad |= !ok;
@@ -1209,36 +1215,37 @@ __global__ __launch_bounds__(kScanBlock) void tile_scan_kernel(const uint32_t* _
                                                                const uint32_t* __restrict__ gcand, int64_t ng,
                                                                uint64_t* __restrict__ goff,
                                                                unsigned long long* __restrict__ counters) {
+  // thread i owns the contiguous run [i * per, (i + 1) * per): every load is issued
+  // before the one workgroup scan of the run sums (a loop of block scans waits on each)
   __shared__ unsigned long long s_w[kScanBlock / 64];
-  __shared__ unsigned long long s_carry;
-  if (threadIdx.x == 0) s_carry = 0;
-  unsigned long long cand = 0;
-  for (int64_t i = threadIdx.x; i < ng; i += kScanBlock) cand += gcand[i];
-  cand = wave_sum_u64(cand);
-  if ((threadIdx.x & 63) == 0 && cand) atomicAdd(&counters[3], cand);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int64_t b = 0; b < ng; b += kScanBlock) {
-    const int64_t i = b + threadIdx.x;
-    const unsigned long long v = i < ng ? gsum[i] : 0ull;
-    unsigned long long incl = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      unsigned long long u = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += u;
-    }
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    unsigned long long run = s_carry + incl - v, tot = 0;
-    for (int w = 0; w < kScanBlock / 64; w++) {
-      if (w < wave) run += s_w[w];
-      tot += s_w[w];
-    }
-    if (i < ng) goff[i] = run;
-    __syncthreads();
-    if (threadIdx.x == 0) s_carry += tot;
-    __syncthreads();
+  const int64_t per = (ng + kScanBlock - 1) / kScanBlock;
+  const int64_t b = threadIdx.x * per, e = b + per < ng ? b + per : ng;
+  unsigned long long cand = 0, sum = 0;
+  for (int64_t i = b; i < e; i++) {
+    cand += gcand[i];
+    sum += gsum[i];
   }
-  if (threadIdx.x == 0) counters[0] = s_carry;
+  cand = wave_sum_u64(cand);
+  if (lane == 0 && cand) atomicAdd(&counters[3], cand);
+  unsigned long long incl = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long u = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += u;
+  }
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  unsigned long long run = incl - sum, tot = 0;
+  for (int w = 0; w < kScanBlock / 64; w++) {
+    if (w < wave) run += s_w[w];
+    tot += s_w[w];
+  }
+  for (int64_t i = b; i < e; i++) {
+    goff[i] = run;
+    run += gsum[i];
+  }
+  if (threadIdx.x == 0) counters[0] = tot;
 }
 
 // MGPU_NT_OUT=1: nontemporal stores of the output pairs (A/B switch)
@@ -1649,18 +1656,82 @@ hipError_t launch_format_cells(int is, const int64_t* cells, int64_t n, char* ou
 // ---------------------------------------------------------------- launchers
 
 hipError_t launch_cells(int is, int res, const double* x, const double* y, int64_t n, int64_t* out,
-                        unsigned long long* counters, unsigned long long* ties, int64_t tie_cap, hipStream_t s) {
+                        unsigned long long* counters, unsigned long long* ties, int64_t tie_cap, hipStream_t s,
+                        const uint8_t* valid, int64_t voff) {
   if (n <= 0) return hipSuccess;
   int64_t blocks = (n + kStreamBlock - 1) / kStreamBlock;
   if (blocks > 256 * 64) blocks = 256 * 64;
   if (is == MGPU_H3) {
     hipLaunchKernelGGL(cells_kernel<MGPU_H3>, dim3((unsigned)blocks), dim3(kStreamBlock), 0, s, x, y, n, res, out, counters,
-                       ties, tie_cap);
-    hipLaunchKernelGGL(cells_fix_kernel, dim3(256), dim3(kStreamBlock), 0, s, x, y, n, res, out, counters, ties, tie_cap);
+                       ties, tie_cap, valid, voff);
+    hipLaunchKernelGGL(cells_fix_kernel, dim3(256), dim3(kStreamBlock), 0, s, x, y, n, res, out, counters, ties, tie_cap,
+                       valid, voff);
   } else {
     hipLaunchKernelGGL(cells_kernel<MGPU_BNG>, dim3((unsigned)blocks), dim3(kStreamBlock), 0, s, x, y, n, res, out,
-                       counters, ties, tie_cap);
+                       counters, ties, tie_cap, valid, voff);
   }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- geometry columns
+__global__ __launch_bounds__(kStreamBlock) void decode_points_kernel(int format, const uint8_t* __restrict__ data,
+                                                                   const void* __restrict__ off, int off32,
+                                                                   const uint8_t* __restrict__ valid, int64_t voff,
+                                                                   int64_t n, double* __restrict__ ox,
+                                                                   double* __restrict__ oy,
+                                                                   unsigned long long* __restrict__ counters) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int st = geom::kDecOk;
+  if (i < n) {
+    double x = NAN, y = NAN;
+    if (pt_valid(valid, voff, i)) {
+      const int64_t b = off32 ? ((const int32_t*)off)[i] : ((const int64_t*)off)[i];
+      const int64_t e = off32 ? ((const int32_t*)off)[i + 1] : ((const int64_t*)off)[i + 1];
+      if (e < b) {
+        st = geom::kDecMalformed;
+      } else if (format == 0) {
+        st = geom::wkb_centroid(data + b, e - b, &x, &y);
+      } else {
+        st = geom::wkt_centroid((const char*)data + b, e - b, &x, &y);
+      }
+      if (st) x = y = NAN;
+    }
+    ox[i] = x;
+    oy[i] = y;
+  }
+  count_wave(&counters[4], st == geom::kDecMalformed);
+  count_wave(&counters[5], st == geom::kDecUnsupported);
+  count_wave(&counters[6], st == geom::kDecEmpty);
+}
+
+hipError_t launch_decode_points(int format, const uint8_t* data, const void* offsets, int off32, const uint8_t* valid,
+                                int64_t voff, int64_t n, double* x, double* y, unsigned long long* counters,
+                                hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(decode_points_kernel, dim3((unsigned)((n + kStreamBlock - 1) / kStreamBlock)), dim3(kStreamBlock), 0,
+                     s, format, data, offsets, off32, valid, voff, n, x, y, counters);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kStreamBlock) void valid_and_kernel(const uint8_t* __restrict__ a, int64_t aoff,
+                                                               const uint8_t* __restrict__ b, int64_t boff, int64_t n,
+                                                               uint8_t* __restrict__ out) {
+  const int64_t byte = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (byte * 8 >= n) return;
+  uint8_t v = 0;
+  for (int k = 0; k < 8; k++) {
+    const int64_t p = byte * 8 + k;
+    if (p < n && pt_valid(a, aoff, p) && pt_valid(b, boff, p)) v |= (uint8_t)(1u << k);
+  }
+  out[byte] = v;
+}
+
+hipError_t launch_valid_and(const uint8_t* a, int64_t aoff, const uint8_t* b, int64_t boff, int64_t n, uint8_t* out,
+                            hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t bytes = (n + 7) / 8;
+  hipLaunchKernelGGL(valid_and_kernel, dim3((unsigned)((bytes + kStreamBlock - 1) / kStreamBlock)), dim3(kStreamBlock), 0,
+                     s, a, aoff, b, boff, n, out);
   return hipGetLastError();
 }
 

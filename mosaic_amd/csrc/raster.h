@@ -13,6 +13,14 @@ namespace mgpu {
 
 constexpr uint32_t kNoPixel = 0xFFFFFFFFu;
 
+// Arrow-style validity bitmap (bit (off + p), LSB first); null = every row valid.  A null
+// point matches nothing (the reference's expressions are NullIntolerant: null in, null out).
+MGPU_HDI bool pt_valid(const uint8_t* v, int64_t off, int64_t p) {
+  if (!v) return true;
+  const int64_t b = off + p;
+  return (v[b >> 3] >> (b & 7)) & 1;
+}
+
 // Pixel index (chip_table.h) of a point: the pixel, kNoPixel (no chip can match: outside
 // the chip cells' box -- or a non-finite coordinate, *ok = false) or kRasterFull (BNG
 // coordinates outside [0, 1e7): the id + hash path).  BNG: *gi = the cell's dense grid

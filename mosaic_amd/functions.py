@@ -37,14 +37,69 @@ def grid_longlatascellid(lon, lat, resolution, index_system=None, ctx=None, stre
     return (strs, st) if stats else strs
 
 
-def grid_pointascellid(points_xy, resolution, index_system=None, **kw):
-    """grid_pointascellid on POINT geometries given as an (n, 2) float64 tensor or an (x, y) pair.
-    For a point, getCentroid is the point itself (MosaicGeometryJTS.scala:60-64)."""
-    if isinstance(points_xy, (tuple, list)):
-        x, y = points_xy
+class GeometryColumn:
+    """A WKB (BinaryType) or WKT (StringType) geometry column in device memory, laid out
+    as Arrow lays out binary / utf8: one byte buffer, int64 offsets (n + 1), optional
+    validity bitmap (LSB first, 1 = present)."""
+
+    def __init__(self, fmt, data, offsets, valid=None):
+        self.format, self.data, self.offsets, self.valid = fmt, data, offsets, valid
+
+    def __len__(self):
+        return self.offsets.numel() - 1
+
+    @staticmethod
+    def from_rows(rows, device="cuda"):
+        """Python rows (bytes: WKB, str: WKT, None: null) -> device column."""
+        import torch
+        kinds = {type(r) for r in rows if r is not None}
+        if len(kinds) > 1:
+            raise N.IllegalArgumentException(N.MGPU_E_INVALID_ARG, "mixed WKB and WKT rows")
+        fmt = N.MGPU_GEOM_WKT if kinds == {str} else N.MGPU_GEOM_WKB
+        bs = [b"" if r is None else (r.encode() if isinstance(r, str) else bytes(r)) for r in rows]
+        off = np.zeros(len(bs) + 1, np.int64)
+        off[1:] = np.cumsum([len(b) for b in bs])
+        data = np.frombuffer(b"".join(bs) or b"\0", np.uint8)
+        valid = None
+        if any(r is None for r in rows):
+            valid = np.packbits(np.array([r is not None for r in rows], bool), bitorder="little")
+            valid = torch.from_numpy(valid).to(device)
+        return GeometryColumn(fmt, torch.from_numpy(data.copy()).to(device), torch.from_numpy(off).to(device), valid)
+
+
+def grid_pointascellid(points, resolution, index_system=None, ctx=None, stream=None, stats=False):
+    """grid_pointascellid (PointIndexGeom.scala:33-47): the cell of each row's centroid.
+
+    ``points``: a GeometryColumn (WKB / WKT POINT or MULTIPOINT rows decoded on the GPU;
+    null rows give cell 0 -- returned with the validity bitmap as (cells, valid)), an
+    (n, 2) float64 tensor, or an (x, y) pair (a point's centroid is the point itself,
+    MosaicGeometryJTS.scala:60-64).  Other geometry types raise MGPU_E_UNSUPPORTED, an
+    empty point IllegalStateException (JTS getX on an empty point)."""
+    if isinstance(points, GeometryColumn):
+        import ctypes
+        import torch
+        from .context import default_context
+        isys = index_system or _H3
+        res = isys.get_resolution(resolution)
+        dev = points.offsets.device
+        ctx = ctx or default_context(dev)
+        n = len(points)
+        cells = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        valid = torch.empty((n + 7) // 8 + 1, dtype=torch.uint8, device=dev) if points.valid is not None else None
+        st = N.MgpuStats()
+        s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        N.check(N.lib().mgpu_geometry_to_cells(ctx.handle, isys.code, res, points.format, points.data.data_ptr(),
+                                               points.offsets.data_ptr(),
+                                               None if points.valid is None else points.valid.data_ptr(), 0, n,
+                                               cells.data_ptr(), None if valid is None else valid.data_ptr(), s,
+                                               ctypes.byref(st)))
+        out = cells[:n] if valid is None else (cells[:n], valid[:(n + 7) // 8])
+        return (out, st.as_dict()) if stats else out
+    if isinstance(points, (tuple, list)):
+        x, y = points
     else:
-        x, y = points_xy[:, 0].contiguous(), points_xy[:, 1].contiguous()
-    return grid_longlatascellid(x, y, resolution, index_system=index_system, **kw)
+        x, y = points[:, 0].contiguous(), points[:, 1].contiguous()
+    return grid_longlatascellid(x, y, resolution, index_system=index_system, ctx=ctx, stream=stream, stats=stats)
 
 
 def grid_cellkring(cells, k, index_system, loop_only=False, ctx=None, stream=None):

@@ -19,7 +19,7 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def test_library_exports_every_header_symbol():
     from mosaic_amd import _native as N
-    hdr = open(os.path.join(ROOT, "include", "mosaic_gpu.h")).read()
+    hdr = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("mosaic_gpu.h", "mosaic_arrow.h"))
     declared = set(re.findall(r"\b(mgpu_[a-z0-9_]+)\s*\(", hdr))
     assert declared == set(N.EXPORTS)
     L = N.lib()
