@@ -85,8 +85,8 @@ def test_null_rows_and_errors(gpu):
         M.grid_pointascellid(M.GeometryColumn.from_rows(["POINT EMPTY"], gpu), 5)
     with pytest.raises(M.MosaicGpuError):
         M.grid_pointascellid(M.GeometryColumn.from_rows(["POINT (1 2"], gpu), 5)
-    with pytest.raises(M.IllegalArgumentException):  # latitude out of range
-        M.grid_pointascellid(M.GeometryColumn.from_rows(["POINT (10 95)"], gpu), 5)
+    with pytest.raises(M.IllegalArgumentException):  # H3 geoToH3 on a NaN coordinate
+        M.grid_pointascellid(M.GeometryColumn.from_rows(["POINT (NaN 5)"], gpu), 5)
 
 
 def test_pip_join_arrow_nulls_offsets_and_ids(gpu, nyc_chips_r9):
