@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <limits>
 #include <string>
+#include <map>
 #include <vector>
 
 #include "../../include/mosaic_arrow.h"
@@ -58,8 +59,8 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // offsets, so a byte copy of the blob on another GPU (RCCL broadcast) is a
 // complete chip table there.
 constexpr uint64_t kBlobMagic = 0x4d4f534149434850ULL;  // "MOSAICHP"
-constexpr int kBlobArrays = 22;
-constexpr uint32_t kBlobVersion = 6;
+constexpr int kBlobArrays = 23;
+constexpr uint32_t kBlobVersion = 8;
 struct BlobHeader {
   uint64_t magic;
   uint32_t version, hash_mask, max_probe, n_chips, n_cells;
@@ -81,6 +82,7 @@ struct BlobHeader {
   uint32_t max_cell_chips, pad4;
   uint32_t raster_pc[4];
   uint32_t raster_sub_n, raster_sub_w;
+  uint32_t raster_bshift, raster_bnx, raster_bny, pad5;
 };
 constexpr size_t kBlobHeaderBytes = 1024;
 static_assert(sizeof(BlobHeader) <= kBlobHeaderBytes, "header too large");
@@ -133,8 +135,12 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.raster_cls = (const uint64_t*)(base + h.off[19]);
   v.raster_sub_n = h.raster_sub_n;
   v.raster_sub_w = h.raster_sub_w;
-  v.raster_ref = h.raster_sub_n ? (const uint32_t*)(base + h.off[20]) : nullptr;
+  v.raster_rank = h.raster_sub_n ? (const mgpu::RankWord*)(base + h.off[20]) : nullptr;
   v.raster_sub = (const uint16_t*)(base + h.off[21]);
+  v.raster_bshift = h.raster_bshift;
+  v.raster_bnx = h.raster_bnx;
+  v.raster_bny = h.raster_bny;
+  v.raster_blk = h.raster_bshift ? (const uint16_t*)(base + h.off[22]) : nullptr;
   return v;
 }
 
@@ -504,6 +510,17 @@ void build_grid(const mgpu::ChipTableView& hv, uint32_t c, const mgpu::wkb::Flat
 //     component of the plane minus the chip boundary, where JTS's PointLocator returns
 //     the verdict of the pixel centre (interior -> match).
 // Anything else is kPixMixed and takes the full path in the kernel.
+// the second level's rank table over the (ascending) mixed pixels of an n-pixel raster
+static void mixed_rank(const std::vector<uint32_t>& mixed, size_t n, std::vector<mgpu::RankWord>& rank) {
+  rank.assign((n + 63) / 64, mgpu::RankWord{0, 0});
+  for (uint32_t p : mixed) rank[p >> 6].bits |= 1ull << (p & 63);
+  uint64_t c = 0;
+  for (auto& w : rank) {
+    w.base = c;
+    c += (uint64_t)__builtin_popcountll(w.bits);
+  }
+}
+
 struct Raster {
   int32_t mode = mgpu::kRasterNone;
   uint32_t nx = 0, ny = 0, pix = 0;
@@ -515,8 +532,11 @@ struct Raster {
   // second level: ref[pixel] = 1 + block of a refined mixed pixel (0: none); block b's
   // sub_n x sub_n sub-pixel classes at sub[b * sub_n^2 ..] (BNG: sub-pixel edge sub_w metres)
   uint32_t sub_n = 0, sub_w = 0;
-  std::vector<uint32_t> ref;
+  std::vector<mgpu::RankWord> rank;
   std::vector<uint16_t> sub;
+  // blocks of 2^bshift x 2^bshift pixels: the class when all of them share it, else mixed
+  uint32_t bshift = 0, bnx = 0, bny = 0;
+  std::vector<uint16_t> blk;
   int64_t n_pure = 0;
 };
 
@@ -651,14 +671,50 @@ constexpr int64_t kRasterMaxSub = 1LL << 26;
 constexpr uint64_t kAnsMixed = ~0ULL;
 
 // classes over the answers of both levels (first | mask << 32; 0 = empty; kAnsMixed):
-// class 0 = empty, kPixMixed = mixed, the rest ordered by their number of matches so a
-// class id tells its pair count (pc[k]: the first class with more than k + 1 matches)
-void raster_classes(const std::vector<uint64_t>& a1, const std::vector<uint64_t>& a2, Raster& R) {
+// class 0 = empty, kPixMixed = mixed, the rest one per distinct ordered polygon list
+// (chip_poly of the mask's chips -- answers from different cells with the same polygons
+// share a class, represented by the first such answer), ordered by their number of
+// matches so a class id tells its pair count (pc[k]: the first class with more than
+// k + 1 matches)
+void raster_classes(const mgpu::ChipTableView& hv, const std::vector<uint64_t>& a1, const std::vector<uint64_t>& a2,
+                    Raster& R) {
   R.cells.assign(a1.size(), mgpu::kPixMixed);
   R.sub.assign(a2.size(), mgpu::kPixMixed);
   R.cls.assign(1, 0);
   auto slot = [&](size_t i) -> uint16_t& { return i < a1.size() ? R.cells[i] : R.sub[i - a1.size()]; };
-  std::vector<std::pair<uint64_t, uint32_t>> keyed;
+  auto polys_of = [&](uint64_t v) {
+    std::vector<int32_t> ps;
+    for (uint32_t m = (uint32_t)(v >> 32); m; m &= m - 1) ps.push_back(hv.chip_poly[(uint32_t)v + __builtin_ctz(m)]);
+    return ps;
+  };
+  // distinct answers -> their polygon lists -> classes
+  std::map<uint64_t, int32_t> answer_key;
+  std::map<std::vector<int32_t>, int32_t> list_key;
+  std::vector<uint64_t> rep;  // per list: the representative answer
+  std::vector<std::vector<int32_t>> lists;
+  for (size_t i = 0; i < a1.size() + a2.size(); i++) {
+    const uint64_t v = i < a1.size() ? a1[i] : a2[i - a1.size()];
+    if (v == kAnsMixed || (v >> 32) == 0 || answer_key.count(v)) continue;
+    auto ps = polys_of(v);
+    auto it = list_key.find(ps);
+    if (it == list_key.end()) {
+      it = list_key.emplace(ps, (int32_t)lists.size()).first;
+      lists.push_back(ps);
+      rep.push_back(v);
+    }
+    answer_key[v] = it->second;
+  }
+  std::vector<int32_t> order(lists.size());
+  for (size_t k = 0; k < order.size(); k++) order[k] = (int32_t)k;
+  std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+    return lists[a].size() != lists[b].size() ? lists[a].size() < lists[b].size() : lists[a] < lists[b];
+  });
+  std::vector<int32_t> cls_of(lists.size(), -1);
+  for (int32_t k : order) {
+    if (R.cls.size() >= mgpu::kPixMixed) break;  // out of classes: the rest stay mixed
+    cls_of[k] = (int32_t)R.cls.size();
+    R.cls.push_back(rep[k]);
+  }
   for (size_t i = 0; i < a1.size() + a2.size(); i++) {
     const uint64_t v = i < a1.size() ? a1[i] : a2[i - a1.size()];
     if (v == kAnsMixed) continue;
@@ -666,20 +722,10 @@ void raster_classes(const std::vector<uint64_t>& a1, const std::vector<uint64_t>
       slot(i) = mgpu::kPixEmpty;
       continue;
     }
-    keyed.push_back({v, (uint32_t)i});
+    const int32_t c = cls_of[answer_key[v]];
+    if (c >= 0) slot(i) = (uint16_t)c;
   }
   auto pc = [](uint64_t v) { return __builtin_popcountll(v >> 32); };
-  std::sort(keyed.begin(), keyed.end(), [&](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) {
-    const int x = pc(a.first), y = pc(b.first);
-    return x != y ? x < y : a < b;
-  });
-  for (size_t k = 0; k < keyed.size(); k++) {
-    if (k == 0 || keyed[k].first != keyed[k - 1].first) {
-      if (R.cls.size() >= mgpu::kPixMixed) break;  // out of classes: the rest stay mixed
-      R.cls.push_back(keyed[k].first);
-    }
-    slot(keyed[k].second) = (uint16_t)(R.cls.size() - 1);
-  }
   for (int k = 0; k < 4; k++) {
     uint32_t c = 1;
     while (c < R.cls.size() && pc(R.cls[c]) <= k + 1) c++;
@@ -687,6 +733,29 @@ void raster_classes(const std::vector<uint64_t>& a1, const std::vector<uint64_t>
   }
   R.n_pure = 0;
   for (uint16_t v : R.cells) R.n_pure += v != mgpu::kPixMixed;
+}
+
+// the block table over the level-1 classes: the smallest block edge 2^s (s >= 3) whose
+// table fits kRasterBlkBytes (the join kernels hold it in LDS)
+constexpr size_t kRasterBlkBytes = 40 * 1024;
+void raster_blocks(Raster& R) {
+  for (uint32_t sh = 3; sh <= 8; sh++) {
+    const uint32_t bnx = (R.nx + (1u << sh) - 1) >> sh, bny = (R.ny + (1u << sh) - 1) >> sh;
+    if ((size_t)bnx * bny * 2 > kRasterBlkBytes) continue;
+    R.bshift = sh, R.bnx = bnx, R.bny = bny;
+    R.blk.assign((size_t)bnx * bny, mgpu::kPixMixed);
+    for (uint32_t by = 0; by < bny; by++)
+      for (uint32_t bx = 0; bx < bnx; bx++) {
+        const uint32_t x0 = bx << sh, y0 = by << sh;
+        const uint32_t x1 = std::min(R.nx, x0 + (1u << sh)), y1 = std::min(R.ny, y0 + (1u << sh));
+        const uint16_t c = R.cells[(size_t)y0 * R.nx + x0];
+        bool same = c != mgpu::kPixMixed;
+        for (uint32_t y = y0; y < y1 && same; y++)
+          for (uint32_t x = x0; x < x1 && same; x++) same = R.cells[(size_t)y * R.nx + x] == c;
+        if (same) R.blk[(size_t)by * bnx + bx] = c;
+      }
+    return;
+  }
 }
 
 // H3: the answer shared by every point of the rectangle [xa, xb] x [ya, yb] (degrees)
@@ -800,8 +869,7 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
     if (a1[i] == kAnsMixed) mixed.push_back((uint32_t)i);
   if (S >= 2 && !mixed.empty() && (int64_t)mixed.size() * S * S <= kRasterMaxSub) {
     R.sub_n = (uint32_t)S;
-    R.ref.assign(a1.size(), 0);
-    for (size_t k = 0; k < mixed.size(); k++) R.ref[mixed[k]] = (uint32_t)(k + 1);
+    mixed_rank(mixed, a1.size(), R.rank);
     a2.assign(mixed.size() * S * S, kAnsMixed);
     const double mux = 1e-6 * sx / S + 64 * ulp, muy = 1e-6 * sy / S + 64 * ulp;
     mgpu::parallel_for((int64_t)mixed.size(), 64, [&](int64_t kb, int64_t ke, int) {
@@ -822,7 +890,8 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
       }
     });
   }
-  raster_classes(a1, a2, R);
+  raster_classes(hv, a1, a2, R);
+  raster_blocks(R);
   return true;
 }
 
@@ -878,8 +947,7 @@ bool build_raster_bng(const mgpu::ChipTableView& hv, const mgpu::DenseFace& D, u
     R.sub_n = (uint32_t)S;
     const uint32_t w = R.pix / S;
     R.sub_w = w;
-    R.ref.assign(R.cells.size(), 0);
-    for (size_t k = 0; k < mixed.size(); k++) R.ref[mixed[k]] = (uint32_t)(k + 1);
+    mixed_rank(mixed, R.cells.size(), R.rank);
     R.sub.assign(mixed.size() * S * S, mgpu::kPixMixed);
     mgpu::parallel_for((int64_t)mixed.size(), 256, [&](int64_t kb, int64_t ke, int) {
       for (int64_t k = kb; k < ke; k++) {
@@ -1386,8 +1454,9 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
       {grid.data(), grid.size() * 8, 0},
       {raster.cells.data(), raster.cells.size() * 2, 0},
       {raster.cls.data(), raster.cls.size() * 8, 0},
-      {raster.ref.data(), raster.ref.size() * 4, 0},
+      {raster.rank.data(), raster.rank.size() * sizeof(mgpu::RankWord), 0},
       {raster.sub.data(), raster.sub.size() * 2, 0},
+      {raster.blk.data(), raster.blk.size() * 2, 0},
   };
   size_t total = kBlobHeaderBytes;
   BlobHeader hdr{};
@@ -1421,6 +1490,9 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   for (int k = 0; k < 4; k++) hdr.raster_pc[k] = raster.pc[k];
   hdr.raster_sub_n = raster.sub_n;
   hdr.raster_sub_w = raster.sub_w;
+  hdr.raster_bshift = raster.bshift;
+  hdr.raster_bnx = raster.bnx;
+  hdr.raster_bny = raster.bny;
   if (getenv("MGPU_RASTER_REPORT"))
     fprintf(stderr, "mgpu raster: mode %d, %u x %u pixels, %zu classes, %.1f%% pure; %u x %u sub-pixels in %zu mixed pixels, "
             "%.1f%% pure\n", raster.mode, raster.nx, raster.ny, raster.cls.size(),
@@ -1428,6 +1500,11 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
             raster.sub_n ? raster.sub.size() / (raster.sub_n * raster.sub_n) : (size_t)0,
             raster.sub.empty() ? 0.0 : 100.0 * std::count_if(raster.sub.begin(), raster.sub.end(), [](uint16_t v) {
               return v != mgpu::kPixMixed; }) / raster.sub.size());
+  if (getenv("MGPU_RASTER_REPORT") && raster.bshift)
+    fprintf(stderr, "mgpu raster: %u x %u blocks of %u x %u pixels, %.1f%% uniform\n", raster.bnx, raster.bny,
+            1u << raster.bshift, 1u << raster.bshift,
+            100.0 * std::count_if(raster.blk.begin(), raster.blk.end(), [](uint16_t v) { return v != mgpu::kPixMixed; }) /
+                raster.blk.size());
   for (size_t k = 0; k < parts.size(); k++) {
     parts[k].off = total;
     hdr.off[k] = total;
@@ -1967,9 +2044,9 @@ int32_t mgpu_test_raster_host(int32_t index_system, int32_t res, int64_t n_chips
       continue;
     }
     bool ok = true;
-    uint32_t gi = 0, sub = 0;
-    const uint32_t ri = index_system == MGPU_H3 ? mgpu::raster_index<MGPU_H3>(v, x[i], y[i], &ok, &gi, &sub)
-                                                : mgpu::raster_index<MGPU_BNG>(v, x[i], y[i], &ok, &gi, &sub);
+    uint32_t gi = 0, sub = 0, bi = mgpu::kNoPixel;
+    const uint32_t ri = index_system == MGPU_H3 ? mgpu::raster_index<MGPU_H3>(v, x[i], y[i], &ok, &gi, &sub, &bi)
+                                                : mgpu::raster_index<MGPU_BNG>(v, x[i], y[i], &ok, &gi, &sub, &bi);
     if (!ok) {
       out_kind[i] = 3;
       continue;
@@ -1978,7 +2055,7 @@ int32_t mgpu_test_raster_host(int32_t index_system, int32_t res, int64_t n_chips
       out_kind[i] = 2;
       continue;
     }
-    const uint32_t cl = ri == mgpu::kNoPixel ? mgpu::kPixEmpty : mgpu::raster_class(v, ri, sub);
+    const uint32_t cl = ri == mgpu::kNoPixel ? mgpu::kPixEmpty : mgpu::raster_class_blk(v, v.raster_blk, ri, bi, sub);
     if (cl == mgpu::kPixMixed) {
       out_kind[i] = 2;
       continue;

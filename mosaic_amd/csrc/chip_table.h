@@ -108,6 +108,11 @@ struct DenseFace {
   uint32_t base;
 };
 
+struct alignas(16) RankWord {
+  uint64_t bits;  // pixels 64 w .. 64 w + 63 that are mixed
+  uint64_t base;  // mixed pixels before pixel 64 w
+};
+
 struct ChipTableView {
   const HashSlot* slots;
   uint32_t hash_mask;
@@ -167,13 +172,21 @@ struct ChipTableView {
                                // matches for raster_pc[k - 1] <= c < raster_pc[k] (k < 4)
   const uint16_t* raster;      // [ny * nx] classes
   const uint64_t* raster_cls;  // [classes]
-  // second level: a mixed pixel p with raster_ref[p] = 1 + b is cut into sub_n x sub_n
-  // sub-pixels whose classes are raster_sub[b * sub_n^2 + v * sub_n + u] (lonlat: u =
-  // the truncated sub_n * fractional pixel position, clamped; BNG: (metres into the
-  // pixel) / raster_sub_w)
+  // second level: every mixed pixel p is cut into sub_n x sub_n sub-pixels whose classes
+  // are raster_sub[b * sub_n^2 + v * sub_n + u], b = the number of mixed pixels before p
+  // (lonlat: u = the truncated sub_n * fractional pixel position, clamped; BNG: (metres
+  // into the pixel) / raster_sub_w).  b comes from raster_rank (a bitmap of the mixed
+  // pixels with a running count per 64-pixel word: one 16-byte load per mixed point, a
+  // table 1/8 the size of the pixel classes -- it stays in L2 beside them).
   uint32_t raster_sub_n, raster_sub_w;
-  const uint32_t* raster_ref;  // [ny * nx], or null: no second level
+  const RankWord* raster_rank;  // [ceil(ny * nx / 64)], or null: no second level
   const uint16_t* raster_sub;
+  // lonlat: blocks of 2^bshift x 2^bshift pixels, raster_blk[(iy >> bshift) * bnx + (ix >>
+  // bshift)] = the class all of the block's pixels share, else kPixMixed (a table small
+  // enough for LDS: the streaming kernels answer most points without a global load);
+  // bshift = 0: none
+  uint32_t raster_bshift, raster_bnx, raster_bny;
+  const uint16_t* raster_blk;
 };
 
 enum RasterMode { kRasterNone = 0, kRasterLonLat = 1, kRasterBng = 2 };

@@ -945,100 +945,115 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
   return v;
 }
 
+// Persistent: each workgroup copies the pixel block table (chip_table.h raster_blk) into
+// LDS once, then classifies chunks blockIdx.x, blockIdx.x + gridDim.x, ...; a point in a
+// uniform block takes its class from LDS, the rest load their pixel (and sub-pixel) class.
 template <int IS>
-__global__ __launch_bounds__(kClsBlock) void classify_kernel(SplitArgs sa) {
+__global__ __launch_bounds__(kClsBlock) void classify_kernel(SplitArgs sa, int64_t n_chunks) {
   using Code = typename CodeOf<IS>::T;
   const JoinArgs& a = sa.j;
   const ChipTableView& t = a.chips;
+  extern __shared__ uint16_t s_blk[];       // [raster_bny * raster_bnx] (IS == H3)
   __shared__ unsigned long long s_bal[64];  // [item][wave]: the wave's mixed points
   __shared__ uint32_t s_pos[64];
   __shared__ uint32_t s_red[kClsBlock / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  const bool use_blk = IS == MGPU_H3 && t.raster_blk != nullptr && a.ablate != 14;  // (14: profiling, no LDS table)
+  if (use_blk) {
+    const uint32_t nb = t.raster_bnx * t.raster_bny;
+    for (uint32_t i = threadIdx.x; i < nb; i += kClsBlock) s_blk[i] = t.raster_blk[i];
+  }
+  __syncthreads();
   Code* codes = (Code*)sa.codes;
-  uint32_t pairs = 0, mixed_bits = 0;
   bool any_bad = false;
-  for (int b = 0; b < kClsItems; b += kClsBatch) {
-    double bx[kClsBatch], by[kClsBatch];
+  for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {
+    const int64_t c0 = ch * kChunk;
+    uint32_t pairs = 0, mixed_bits = 0;
+    for (int b = 0; b < kClsItems; b += kClsBatch) {
+      double bx[kClsBatch], by[kClsBatch];
 #pragma unroll
-    for (int k = 0; k < kClsBatch; k++) {
-      const int64_t p = c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x;
-      bx[k] = by[k] = 0.0;
-      if (p < a.n) {
-        bx[k] = __builtin_nontemporal_load(&a.x[p]);
-        by[k] = __builtin_nontemporal_load(&a.y[p]);
-      }
-    }
-    uint32_t ri[kClsBatch], gix[kClsBatch], sb[kClsBatch];
-#pragma unroll
-    for (int k = 0; k < kClsBatch; k++) {
-      ri[k] = kNoPixel;
-      gix[k] = 0;
-      sb[k] = 0;
-      const int64_t pk = c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x;
-      if (pk < a.n && pt_valid(a.valid, a.valid_off, pk)) {
-        bool ok;
-        ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &gix[k], &sb[k]);
-        any_bad |= !ok;
-        if (a.ablate == 11) ri[k] = bx[k] == 12345.0 ? 0u : kNoPixel;  // profiling: no pixel loads
-      }
-    }
-    uint32_t cl[kClsBatch];
-    uint64_t ge[kClsBatch];
-#pragma unroll
-    for (int k = 0; k < kClsBatch; k++) {
-      cl[k] = ri[k] < kRasterFull ? raster_class(t, ri[k], sb[k]) : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
-      ge[k] = (IS == MGPU_BNG && ri[k] < kRasterFull) ? t.grid[gix[k]] : 0ull;
-    }
-#pragma unroll
-    for (int k = 0; k < kClsBatch; k++) {
-      const int64_t p = c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x;
-      const bool valid = p < a.n;
-      bool mixed = cl[k] == kPixMixed;
-      Code code;
-      if (IS == MGPU_H3) {
-        code = (Code)cl[k];
-        if (!mixed && cl[k] != kPixEmpty) {
-          const uint32_t c = cl[k];  // the class id gives the match count (raster_pc)
-          pairs += c < t.raster_pc[0] ? 1u : c < t.raster_pc[1] ? 2u : c < t.raster_pc[2] ? 3u : c < t.raster_pc[3] ? 4u
-                   : (uint32_t)__popc((uint32_t)(t.raster_cls[c] >> 32));
+      for (int k = 0; k < kClsBatch; k++) {
+        const int64_t p = c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x;
+        bx[k] = by[k] = 0.0;
+        if (p < a.n) {
+          bx[k] = __builtin_nontemporal_load(&a.x[p]);
+          by[k] = __builtin_nontemporal_load(&a.y[p]);
         }
-      } else {
-        const uint32_t first = (uint32_t)ge[k], m = cl[k];
-        if (!mixed && m && !(m < 256u && first < (1u << 24))) mixed = true;  // no room in the code
-        code = (Code)(mixed ? kCodeMixed32 : (m ? (first << 8) | m : 0u));
-        if (!mixed) pairs += __popc(m);
       }
-      if (valid && a.ablate != 12) codes[p] = code;  // (12: profiling, no code stores)
-      mixed = mixed && valid;
-      const unsigned long long bal = __ballot(mixed);
-      if (lane == 0) s_bal[(b + k) * (kClsBlock / 64) + wave] = bal;
-      if (mixed) mixed_bits |= 1u << (b + k);
+      uint32_t ri[kClsBatch], gix[kClsBatch], sb[kClsBatch], bi[kClsBatch];
+#pragma unroll
+      for (int k = 0; k < kClsBatch; k++) {
+        ri[k] = kNoPixel;
+        gix[k] = 0;
+        sb[k] = 0;
+        bi[k] = kNoPixel;
+        const int64_t pk = c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x;
+        if (pk < a.n && pt_valid(a.valid, a.valid_off, pk)) {
+          bool ok;
+          ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &gix[k], &sb[k], use_blk ? &bi[k] : nullptr);
+          any_bad |= !ok;
+          if (a.ablate == 11) ri[k] = bx[k] == 12345.0 ? 0u : kNoPixel;  // profiling: no pixel loads
+        }
+      }
+      uint32_t cl[kClsBatch];
+      uint64_t ge[kClsBatch];
+#pragma unroll
+      for (int k = 0; k < kClsBatch; k++) {
+        cl[k] = ri[k] < kRasterFull ? raster_class_blk(t, s_blk, ri[k], bi[k], sb[k])
+                                    : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
+        ge[k] = (IS == MGPU_BNG && ri[k] < kRasterFull) ? t.grid[gix[k]] : 0ull;
+      }
+#pragma unroll
+      for (int k = 0; k < kClsBatch; k++) {
+        const int64_t p = c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x;
+        const bool valid = p < a.n;
+        bool mixed = cl[k] == kPixMixed;
+        Code code;
+        if (IS == MGPU_H3) {
+          code = (Code)cl[k];
+          if (!mixed && cl[k] != kPixEmpty) {
+            const uint32_t c = cl[k];  // the class id gives the match count (raster_pc)
+            pairs += c < t.raster_pc[0] ? 1u : c < t.raster_pc[1] ? 2u : c < t.raster_pc[2] ? 3u : c < t.raster_pc[3] ? 4u
+                     : (uint32_t)__popc((uint32_t)(t.raster_cls[c] >> 32));
+          }
+        } else {
+          const uint32_t first = (uint32_t)ge[k], m = cl[k];
+          if (!mixed && m && !(m < 256u && first < (1u << 24))) mixed = true;  // no room in the code
+          code = (Code)(mixed ? kCodeMixed32 : (m ? (first << 8) | m : 0u));
+          if (!mixed) pairs += __popc(m);
+        }
+        if (valid && a.ablate != 12) codes[p] = code;  // (12: profiling, no code stores)
+        mixed = mixed && valid;
+        const unsigned long long bal = __ballot(mixed);
+        if (lane == 0) s_bal[(b + k) * (kClsBlock / 64) + wave] = bal;
+        if (mixed) mixed_bits |= 1u << (b + k);
+      }
     }
+    const uint32_t wp = wave_sum_u32(pairs);
+    if (lane == 0) s_red[wave] = wp;
+    __syncthreads();
+    // mixed points ranked in point order (item-major, then wave, then lane)
+    if (wave == 0) {
+      const uint32_t v = (uint32_t)__popcll(s_bal[lane]);
+      const uint32_t incl = wave_incl_scan(v);
+      s_pos[lane] = incl - v;
+      if (lane == 63) sa.chunk_mixed[ch] = incl;
+      if (lane == 0) {
+        uint32_t tp = 0;
+        for (int w = 0; w < kClsBlock / 64; w++) tp += s_red[w];
+        sa.chunk_pairs[ch] = tp;
+      }
+    }
+    __syncthreads();
+    for (uint32_t m = mixed_bits; m; m &= m - 1) {
+      const int it = __builtin_ctz(m);
+      const int e = it * (kClsBlock / 64) + wave;
+      const uint32_t r = s_pos[e] + (uint32_t)__popcll(s_bal[e] & ((1ull << lane) - 1ull));
+      sa.mixed_idx[c0 + r] = (uint16_t)(it * kClsBlock + threadIdx.x);
+    }
+    __syncthreads();  // (s_bal, s_pos, s_red reused by the next chunk)
   }
   count_wave(&a.counters[2], any_bad);
-  const uint32_t wp = wave_sum_u32(pairs);
-  if (lane == 0) s_red[wave] = wp;
-  __syncthreads();
-  // mixed points ranked in point order (item-major, then wave, then lane)
-  if (wave == 0) {
-    const uint32_t v = (uint32_t)__popcll(s_bal[lane]);
-    const uint32_t incl = wave_incl_scan(v);
-    s_pos[lane] = incl - v;
-    if (lane == 63) sa.chunk_mixed[blockIdx.x] = incl;
-    if (lane == 0) {
-      uint32_t tp = 0;
-      for (int w = 0; w < kClsBlock / 64; w++) tp += s_red[w];
-      sa.chunk_pairs[blockIdx.x] = tp;
-    }
-  }
-  __syncthreads();
-  for (uint32_t m = mixed_bits; m; m &= m - 1) {
-    const int it = __builtin_ctz(m);
-    const int e = it * (kClsBlock / 64) + wave;
-    const uint32_t r = s_pos[e] + (uint32_t)__popcll(s_bal[e] & ((1ull << lane) - 1ull));
-    sa.mixed_idx[c0 + r] = (uint16_t)(it * kClsBlock + threadIdx.x);
-  }
 }
 
 // the mixed points of one chunk per workgroup, a tile of kTile at a time
@@ -1133,20 +1148,57 @@ __global__ __launch_bounds__(kClsBlock) void split_emit_kernel(SplitArgs sa) {
   }
   __syncthreads();
   const uint64_t base = sa.chunk_off[blockIdx.x];
+  if (a.ablate == 13) {  // (profiling: each lane stores its own pairs, no staging)
 #pragma unroll
-  for (int k = 0; k < kClsItems; k++) {
-    const uint64_t v = vv[k];
-    const uint32_t first = (uint32_t)v, mask = (uint32_t)(v >> 32);
-    if (!mask) continue;
-    const int64_t p = c0 + (int64_t)k * kClsBlock + threadIdx.x;
-    uint64_t q = base + s_off[k * kClsBlock + threadIdx.x];
-    const int64_t pid = sa.point_id ? sa.point_id[p] : sa.id_base + p;
-    for (uint32_t m = mask; m; m &= m - 1) {
-      if ((int64_t)q < sa.capacity) {
-        sa.out_point[q] = pid;
-        sa.out_poly[q] = t.chip_poly[first + __builtin_ctz(m)];
+    for (int k = 0; k < kClsItems; k++) {
+      const uint64_t v = vv[k];
+      const uint32_t first = (uint32_t)v, mask = (uint32_t)(v >> 32);
+      if (!mask) continue;
+      const int64_t p = c0 + (int64_t)k * kClsBlock + threadIdx.x;
+      uint64_t q = base + s_off[k * kClsBlock + threadIdx.x];
+      const int64_t pid = sa.point_id ? sa.point_id[p] : sa.id_base + p;
+      for (uint32_t m = mask; m; m &= m - 1) {
+        if ((int64_t)q < sa.capacity) {
+          sa.out_point[q] = pid;
+          sa.out_poly[q] = t.chip_poly[first + __builtin_ctz(m)];
+        }
+        q++;
       }
-      q++;
+    }
+    return;
+  }
+  // The chunk's pairs are one contiguous output range: staged in LDS (polygon id, point)
+  // a window of kChunk pairs at a time, then written by consecutive lanes -- full-line
+  // stores instead of sparse per-point ones.
+  uint32_t mo[kClsItems];
+#pragma unroll
+  for (int k = 0; k < kClsItems; k++) mo[k] = s_off[k * kClsBlock + threadIdx.x];
+  uint32_t total = 0;
+#pragma unroll
+  for (int w = 0; w < kClsBlock / 64; w++) total += s_w[w];
+  __shared__ uint16_t s_pt[kChunk];
+  uint32_t* s_poly = s_off;
+  for (uint32_t w0 = 0; w0 < total; w0 += kChunk) {
+    __syncthreads();  // (s_off read / the previous window written)
+#pragma unroll
+    for (int k = 0; k < kClsItems; k++) {
+      const uint32_t first = (uint32_t)vv[k], mask = (uint32_t)(vv[k] >> 32);
+      uint32_t q = mo[k];
+      if (!mask || q >= w0 + kChunk || q + (uint32_t)__popc(mask) <= w0) continue;
+      for (uint32_t m = mask; m; m &= m - 1, q++)
+        if (q >= w0 && q < w0 + kChunk) {
+          s_poly[q - w0] = t.chip_poly[first + __builtin_ctz(m)];
+          s_pt[q - w0] = (uint16_t)(k * kClsBlock + threadIdx.x);
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = total - w0 < (uint32_t)kChunk ? total - w0 : (uint32_t)kChunk;
+    for (uint32_t i = threadIdx.x; i < cnt; i += kClsBlock) {
+      const uint64_t q = base + w0 + i;
+      if ((int64_t)q >= sa.capacity) break;
+      const int64_t p = c0 + s_pt[i];
+      sa.out_point[q] = sa.point_id ? sa.point_id[p] : sa.id_base + p;
+      sa.out_poly[q] = (int32_t)s_poly[i];
     }
   }
 }
@@ -1768,10 +1820,21 @@ hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t
 int64_t split_chunk() { return kChunk; }
 int64_t split_chunks(int64_t n) { return (n + kChunk - 1) / kChunk; }
 
+// workgroups of `block` threads with `lds` dynamic LDS bytes resident on the whole GPU at once
+static int resident_blocks(const void* kernel, int block, size_t lds) {
+  int dev = 0, cus = 0, per = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, lds) != hipSuccess || per < 1) per = 1;
+  return std::max(cus, 1) * per;
+}
+
 template <int IS>
 static void launch_split_t(const SplitArgs& a, hipStream_t s, hipEvent_t after_classify, hipEvent_t after_mixed) {
   const int64_t nc = split_chunks(a.j.n);
-  hipLaunchKernelGGL(classify_kernel<IS>, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
+  const size_t lds = (IS == MGPU_H3 && a.j.chips.raster_blk) ? (size_t)a.j.chips.raster_bnx * a.j.chips.raster_bny * 2 : 0;
+  const int64_t grid = std::min<int64_t>(nc, (int64_t)resident_blocks((const void*)classify_kernel<IS>, kClsBlock, lds));
+  hipLaunchKernelGGL(classify_kernel<IS>, dim3((unsigned)grid), dim3(kClsBlock), lds, s, a, nc);
   if (after_classify) hipEventRecord(after_classify, s);
   hipLaunchKernelGGL(pip_mixed_kernel<IS>, dim3((unsigned)nc), dim3(kBlock), 0, s, a.j);
   const int64_t fix = nc * kChunkTiles < 512 ? nc * kChunkTiles : 512;

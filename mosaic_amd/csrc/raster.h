@@ -31,7 +31,9 @@ MGPU_HDI uint32_t div_fix(uint32_t v, uint32_t d, double inv) {
   return q * d > v ? q - 1 : ((q + 1) * d <= v ? q + 1 : q);
 }
 template <int IS>
-MGPU_HDI uint32_t raster_index(const ChipTableView& t, double px, double py, bool* ok, uint32_t* gi, uint32_t* sub) {
+MGPU_HDI uint32_t raster_index(const ChipTableView& t, double px, double py, bool* ok, uint32_t* gi, uint32_t* sub,
+                               uint32_t* blk = nullptr) {
+  if (blk) *blk = kNoPixel;
   if (IS == MGPU_BNG) {
     *ok = px == px && py == py;  // pointToIndex rejects NaN only
     if (!*ok) return kNoPixel;
@@ -58,6 +60,7 @@ MGPU_HDI uint32_t raster_index(const ChipTableView& t, double px, double py, boo
   uint32_t ix = (uint32_t)tx, iy = (uint32_t)ty;
   ix = ix < t.raster_nx ? ix : t.raster_nx - 1;
   iy = iy < t.raster_ny ? iy : t.raster_ny - 1;
+  if (blk && t.raster_bshift) *blk = (iy >> t.raster_bshift) * t.raster_bnx + (ix >> t.raster_bshift);
   if (t.raster_sub_n) {
     const double S = (double)t.raster_sub_n;
     uint32_t u = (uint32_t)((tx - (double)ix) * S), v = (uint32_t)((ty - (double)iy) * S);
@@ -72,11 +75,23 @@ MGPU_HDI uint32_t raster_index(const ChipTableView& t, double px, double py, boo
 // second level when the pixel is mixed.
 MGPU_HDI uint32_t raster_class(const ChipTableView& t, uint32_t ri, uint32_t sub) {
   uint32_t cl = t.raster[ri];
-  if (cl == kPixMixed && t.raster_ref) {
-    const uint32_t b = t.raster_ref[ri];
-    if (b) cl = t.raster_sub[(size_t)(b - 1) * t.raster_sub_n * t.raster_sub_n + sub];
+  if (cl == kPixMixed && t.raster_rank) {
+    const RankWord w = t.raster_rank[ri >> 6];
+    const uint64_t bit = 1ull << (ri & 63);
+    if (w.bits & bit) {
+      const uint64_t b = w.base + (uint64_t)__builtin_popcountll(w.bits & (bit - 1));
+      cl = t.raster_sub[b * t.raster_sub_n * t.raster_sub_n + sub];
+    }
   }
   return cl;
+}
+
+// raster_class with the block table first (`blk_table`: raster_blk or its LDS copy; bi
+// from raster_index, kNoPixel: no block)
+MGPU_HDI uint32_t raster_class_blk(const ChipTableView& t, const uint16_t* blk_table, uint32_t ri, uint32_t bi,
+                                   uint32_t sub) {
+  const uint32_t c = bi != kNoPixel ? blk_table[bi] : kPixMixed;
+  return c != kPixMixed ? c : raster_class(t, ri, sub);
 }
 
 }  // namespace mgpu
