@@ -948,20 +948,32 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 // Persistent: each workgroup copies the pixel block table (chip_table.h raster_blk) into
 // LDS once, then classifies chunks blockIdx.x, blockIdx.x + gridDim.x, ...; a point in a
 // uniform block takes its class from LDS, the rest load their pixel (and sub-pixel) class.
+// (512 threads: four workgroups -- 32 waves -- share a CU with their LDS tables; the
+// chunk's mixed points are ranked in point order as in split_emit_kernel)
+constexpr int kCfyBlock = 512;
+constexpr int kCfyItems = kChunk / kCfyBlock;
+#ifndef MGPU_CFY_BATCH
+#define MGPU_CFY_BATCH 4
+#endif
+#ifndef MGPU_CFY_WAVES
+#define MGPU_CFY_WAVES 1  // (8 = at most 64 VGPRs: spills, slower on C2 / C5)
+#endif
+constexpr int kCfyBatch = MGPU_CFY_BATCH;
+static_assert(kCfyItems * (kCfyBlock / 64) == 64, "one wave scans a chunk's ballots");
 template <int IS>
-__global__ __launch_bounds__(kClsBlock) void classify_kernel(SplitArgs sa, int64_t n_chunks) {
+__global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_CFY_WAVES))) void classify_kernel(SplitArgs sa, int64_t n_chunks) {
   using Code = typename CodeOf<IS>::T;
   const JoinArgs& a = sa.j;
   const ChipTableView& t = a.chips;
   extern __shared__ uint16_t s_blk[];       // [raster_bny * raster_bnx] (IS == H3)
   __shared__ unsigned long long s_bal[64];  // [item][wave]: the wave's mixed points
   __shared__ uint32_t s_pos[64];
-  __shared__ uint32_t s_red[kClsBlock / 64];
+  __shared__ uint32_t s_red[kCfyBlock / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool use_blk = IS == MGPU_H3 && t.raster_blk != nullptr && a.ablate != 14;  // (14: profiling, no LDS table)
   if (use_blk) {
     const uint32_t nb = t.raster_bnx * t.raster_bny;
-    for (uint32_t i = threadIdx.x; i < nb; i += kClsBlock) s_blk[i] = t.raster_blk[i];
+    for (uint32_t i = threadIdx.x; i < nb; i += kCfyBlock) s_blk[i] = t.raster_blk[i];
   }
   __syncthreads();
   Code* codes = (Code*)sa.codes;
@@ -969,25 +981,25 @@ __global__ __launch_bounds__(kClsBlock) void classify_kernel(SplitArgs sa, int64
   for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {
     const int64_t c0 = ch * kChunk;
     uint32_t pairs = 0, mixed_bits = 0;
-    for (int b = 0; b < kClsItems; b += kClsBatch) {
-      double bx[kClsBatch], by[kClsBatch];
+    for (int b = 0; b < kCfyItems; b += kCfyBatch) {
+      double bx[kCfyBatch], by[kCfyBatch];
 #pragma unroll
-      for (int k = 0; k < kClsBatch; k++) {
-        const int64_t p = c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x;
+      for (int k = 0; k < kCfyBatch; k++) {
+        const int64_t p = c0 + (int64_t)(b + k) * kCfyBlock + threadIdx.x;
         bx[k] = by[k] = 0.0;
         if (p < a.n) {
           bx[k] = __builtin_nontemporal_load(&a.x[p]);
           by[k] = __builtin_nontemporal_load(&a.y[p]);
         }
       }
-      uint32_t ri[kClsBatch], gix[kClsBatch], sb[kClsBatch], bi[kClsBatch];
+      uint32_t ri[kCfyBatch], gix[kCfyBatch], sb[kCfyBatch], bi[kCfyBatch];
 #pragma unroll
-      for (int k = 0; k < kClsBatch; k++) {
+      for (int k = 0; k < kCfyBatch; k++) {
         ri[k] = kNoPixel;
         gix[k] = 0;
         sb[k] = 0;
         bi[k] = kNoPixel;
-        const int64_t pk = c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x;
+        const int64_t pk = c0 + (int64_t)(b + k) * kCfyBlock + threadIdx.x;
         if (pk < a.n && pt_valid(a.valid, a.valid_off, pk)) {
           bool ok;
           ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &gix[k], &sb[k], use_blk ? &bi[k] : nullptr);
@@ -995,17 +1007,19 @@ __global__ __launch_bounds__(kClsBlock) void classify_kernel(SplitArgs sa, int64
           if (a.ablate == 11) ri[k] = bx[k] == 12345.0 ? 0u : kNoPixel;  // profiling: no pixel loads
         }
       }
-      uint32_t cl[kClsBatch];
-      uint64_t ge[kClsBatch];
+      uint32_t cl[kCfyBatch];
+      uint64_t ge[kCfyBatch];
 #pragma unroll
-      for (int k = 0; k < kClsBatch; k++) {
+      for (int k = 0; k < kCfyBatch; k++) {
         cl[k] = ri[k] < kRasterFull ? raster_class_blk(t, s_blk, ri[k], bi[k], sb[k])
                                     : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
+        if (a.ablate == 15 && ri[k] < kRasterFull)  // (profiling: the LDS table only)
+          cl[k] = bi[k] != kNoPixel ? s_blk[bi[k]] : kPixMixed;
         ge[k] = (IS == MGPU_BNG && ri[k] < kRasterFull) ? t.grid[gix[k]] : 0ull;
       }
 #pragma unroll
-      for (int k = 0; k < kClsBatch; k++) {
-        const int64_t p = c0 + (int64_t)(b + k) * kClsBlock + threadIdx.x;
+      for (int k = 0; k < kCfyBatch; k++) {
+        const int64_t p = c0 + (int64_t)(b + k) * kCfyBlock + threadIdx.x;
         const bool valid = p < a.n;
         bool mixed = cl[k] == kPixMixed;
         Code code;
@@ -1025,7 +1039,7 @@ __global__ __launch_bounds__(kClsBlock) void classify_kernel(SplitArgs sa, int64
         if (valid && a.ablate != 12) codes[p] = code;  // (12: profiling, no code stores)
         mixed = mixed && valid;
         const unsigned long long bal = __ballot(mixed);
-        if (lane == 0) s_bal[(b + k) * (kClsBlock / 64) + wave] = bal;
+        if (lane == 0) s_bal[(b + k) * (kCfyBlock / 64) + wave] = bal;
         if (mixed) mixed_bits |= 1u << (b + k);
       }
     }
@@ -1040,16 +1054,16 @@ __global__ __launch_bounds__(kClsBlock) void classify_kernel(SplitArgs sa, int64
       if (lane == 63) sa.chunk_mixed[ch] = incl;
       if (lane == 0) {
         uint32_t tp = 0;
-        for (int w = 0; w < kClsBlock / 64; w++) tp += s_red[w];
+        for (int w = 0; w < kCfyBlock / 64; w++) tp += s_red[w];
         sa.chunk_pairs[ch] = tp;
       }
     }
     __syncthreads();
     for (uint32_t m = mixed_bits; m; m &= m - 1) {
       const int it = __builtin_ctz(m);
-      const int e = it * (kClsBlock / 64) + wave;
+      const int e = it * (kCfyBlock / 64) + wave;
       const uint32_t r = s_pos[e] + (uint32_t)__popcll(s_bal[e] & ((1ull << lane) - 1ull));
-      sa.mixed_idx[c0 + r] = (uint16_t)(it * kClsBlock + threadIdx.x);
+      sa.mixed_idx[c0 + r] = (uint16_t)(it * kCfyBlock + threadIdx.x);
     }
     __syncthreads();  // (s_bal, s_pos, s_red reused by the next chunk)
   }
@@ -1075,124 +1089,111 @@ __global__ __launch_bounds__(kBlock) void pip_mixed_fix_kernel(JoinArgs a) {
   }
 }
 
-// Ordered output.  Thread i handles the points c0 + 256 k + i (k = 0 .. 15, as
-// classify_kernel: the mixed points' list positions come from the same ballots).  The
-// pair counts go to LDS in point order, one workgroup scan over 16 consecutive counts
-// per thread gives every point's output offset, and consecutive lanes write consecutive
-// pairs.
-template <int IS>
-__global__ __launch_bounds__(kClsBlock) void split_emit_kernel(SplitArgs sa) {
-  using Code = typename CodeOf<IS>::T;
-  const JoinArgs& a = sa.j;
-  const ChipTableView& t = a.chips;
-  __shared__ unsigned long long s_bal[64];
-  __shared__ uint32_t s_pos[64];
-  __shared__ uint32_t s_w[kClsBlock / 64];
-  __shared__ uint32_t s_off[kChunk];  // pair count, then offset, of each point (point order)
+// Ordered output.  Thread i handles the chunk's points 16 i .. 16 i + 15 (their codes:
+// one or two 16-byte loads); a block scan of the threads' mixed counts gives each mixed
+// point its rank in the chunk's mixed list (classify_kernel ranks them in point order
+// too), a second scan of the pair counts each thread's first output slot.  The chunk's
+// pairs are one contiguous output range: staged in LDS (polygon id, point) a window of
+// kEmitWin pairs at a time, then written by consecutive lanes.
+__device__ __forceinline__ uint32_t chunk_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
-  const Code* codes = (const Code*)sa.codes;
-  const Code kMixed = IS == MGPU_H3 ? (Code)kPixMixed : (Code)kCodeMixed32;
-  Code cd[kClsItems];
-#pragma unroll
-  for (int k = 0; k < kClsItems; k++) {
-    const int64_t p = c0 + (int64_t)k * kClsBlock + threadIdx.x;
-    cd[k] = p < a.n ? codes[p] : (Code)0;
-  }
-#pragma unroll
-  for (int k = 0; k < kClsItems; k++) {
-    const unsigned long long bal = __ballot(cd[k] == kMixed);
-    if (lane == 0) s_bal[k * (kClsBlock / 64) + wave] = bal;
-  }
-  __syncthreads();
-  if (wave == 0) {
-    const uint32_t v = (uint32_t)__popcll(s_bal[lane]);
-    s_pos[lane] = wave_incl_scan(v) - v;
-  }
-  __syncthreads();
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  // every answer's load in flight at once (mixed answers, class table)
-  uint64_t vv[kClsItems];
-#pragma unroll
-  for (int k = 0; k < kClsItems; k++) {
-    uint64_t v = 0;
-    if (cd[k] == kMixed) {
-      const int e = k * (kClsBlock / 64) + wave;
-      v = a.mixed_res[c0 + s_pos[e] + (uint32_t)__popcll(s_bal[e] & lt)];
-    } else if (cd[k] != 0) {
-      if (IS == MGPU_H3)
-        v = t.raster_cls[(uint32_t)cd[k]];
-      else
-        v = (uint64_t)((uint32_t)cd[k] >> 8) | ((uint64_t)((uint32_t)cd[k] & 0xFFu) << 32);
-    }
-    vv[k] = v;
-    s_off[k * kClsBlock + threadIdx.x] = (uint32_t)__popc((uint32_t)(v >> 32));
-  }
-  __syncthreads();
-  // thread i scans points 16 i .. 16 i + 15
-  uint32_t c16[kClsItems], sum = 0;
-#pragma unroll
-  for (int k = 0; k < kClsItems; k++) {
-    c16[k] = s_off[threadIdx.x * kClsItems + k];
-    sum += c16[k];
-  }
-  const uint32_t incl = wave_incl_scan(sum);
+  const uint32_t incl = wave_incl_scan(v);
   if (lane == 63) s_w[wave] = incl;
   __syncthreads();
-  uint32_t run = incl - sum;
-  for (int w = 0; w < wave; w++) run += s_w[w];
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < kClsBlock / 64; w++) {
+    before += w < wave ? s_w[w] : 0u;
+    all += s_w[w];
+  }
+  *total = all;
+  return before + incl - v;
+}
+
+constexpr int kEmitWin = 2048;  // pairs staged at a time
+#ifndef MGPU_EMIT_WAVES
+#define MGPU_EMIT_WAVES 5  // (8: 64 VGPRs, spills; 5: none, A/B equal or better)
+#endif
+template <int IS>
+__global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_EMIT_WAVES))) void split_emit_kernel(SplitArgs sa) {
+  using Code = typename CodeOf<IS>::T;
+  constexpr int kWords = kClsItems * (int)sizeof(Code) / 4;  // 32-bit words of a thread's codes
+  const JoinArgs& a = sa.j;
+  const ChipTableView& t = a.chips;
+  __shared__ uint32_t s_w[2][kClsBlock / 64];
+  __shared__ uint32_t s_poly[kEmitWin];  // staging: polygon id
+  __shared__ uint16_t s_pt[kEmitWin];    // staging: point of the chunk
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  const int64_t p0 = c0 + (int64_t)threadIdx.x * kClsItems;
+  const Code kMixed = IS == MGPU_H3 ? (Code)kPixMixed : (Code)kCodeMixed32;
+  uint32_t cw[kWords];
+  if (p0 + kClsItems <= a.n) {
+    const uint4* src = (const uint4*)((const Code*)sa.codes + p0);
+#pragma unroll
+    for (int i = 0; i < kWords / 4; i++) {
+      const uint4 v = src[i];
+      cw[4 * i] = v.x, cw[4 * i + 1] = v.y, cw[4 * i + 2] = v.z, cw[4 * i + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < kWords; i++) cw[i] = 0;
+    const Code* cs = (const Code*)sa.codes;
+    for (int k = 0; k < kClsItems; k++)
+      if (p0 + k < a.n) {
+        const uint32_t c = cs[p0 + k];
+        if (sizeof(Code) == 2)
+          cw[k >> 1] |= c << ((k & 1) * 16);
+        else
+          cw[k] = c;
+      }
+  }
+  auto code = [&](int k) -> Code {
+    return sizeof(Code) == 2 ? (Code)(cw[k >> 1] >> ((k & 1) * 16)) : (Code)cw[k];
+  };
+  // a pure code's answer (first chip | match mask << 32)
+  auto pure = [&](Code c) -> uint64_t {
+    if (IS == MGPU_H3) return t.raster_cls[(uint32_t)c];
+    return (uint64_t)((uint32_t)c >> 8) | ((uint64_t)((uint32_t)c & 0xFFu) << 32);
+  };
+  uint32_t nmix = 0;
+#pragma unroll
+  for (int k = 0; k < kClsItems; k++) nmix += code(k) == kMixed;
+  uint32_t all_mixed;
+  const uint32_t rank0 = chunk_excl_scan(nmix, s_w[0], &all_mixed);
+  uint32_t npair = 0, r = rank0;
 #pragma unroll
   for (int k = 0; k < kClsItems; k++) {
-    s_off[threadIdx.x * kClsItems + k] = run;
-    run += c16[k];
+    const Code c = code(k);
+    if (c == kMixed)
+      npair += __popc((uint32_t)(a.mixed_res[c0 + r++] >> 32));
+    else if (c != 0)
+      npair += IS == MGPU_H3 ? (uint32_t)__popc((uint32_t)(pure(c) >> 32)) : (uint32_t)__popc((uint32_t)c & 0xFFu);
   }
-  __syncthreads();
+  uint32_t total;
+  const uint32_t off0 = chunk_excl_scan(npair, s_w[1], &total);
   const uint64_t base = sa.chunk_off[blockIdx.x];
-  if (a.ablate == 13) {  // (profiling: each lane stores its own pairs, no staging)
+  for (uint32_t w0 = 0; w0 < total; w0 += kEmitWin) {
+    if (off0 < w0 + kEmitWin && off0 + npair > w0) {
+      uint32_t q = off0;
+      r = rank0;
 #pragma unroll
-    for (int k = 0; k < kClsItems; k++) {
-      const uint64_t v = vv[k];
-      const uint32_t first = (uint32_t)v, mask = (uint32_t)(v >> 32);
-      if (!mask) continue;
-      const int64_t p = c0 + (int64_t)k * kClsBlock + threadIdx.x;
-      uint64_t q = base + s_off[k * kClsBlock + threadIdx.x];
-      const int64_t pid = sa.point_id ? sa.point_id[p] : sa.id_base + p;
-      for (uint32_t m = mask; m; m &= m - 1) {
-        if ((int64_t)q < sa.capacity) {
-          sa.out_point[q] = pid;
-          sa.out_poly[q] = t.chip_poly[first + __builtin_ctz(m)];
-        }
-        q++;
+      for (int k = 0; k < kClsItems; k++) {
+        const Code c = code(k);
+        uint64_t v = 0;
+        if (c == kMixed)
+          v = a.mixed_res[c0 + r++];
+        else if (c != 0)
+          v = pure(c);
+        const uint32_t first = (uint32_t)v;
+        for (uint32_t m = (uint32_t)(v >> 32); m; m &= m - 1, q++)
+          if (q >= w0 && q < w0 + kEmitWin) {
+            s_poly[q - w0] = (uint32_t)t.chip_poly[first + __builtin_ctz(m)];
+            s_pt[q - w0] = (uint16_t)(threadIdx.x * kClsItems + k);
+          }
       }
     }
-    return;
-  }
-  // The chunk's pairs are one contiguous output range: staged in LDS (polygon id, point)
-  // a window of kChunk pairs at a time, then written by consecutive lanes -- full-line
-  // stores instead of sparse per-point ones.
-  uint32_t mo[kClsItems];
-#pragma unroll
-  for (int k = 0; k < kClsItems; k++) mo[k] = s_off[k * kClsBlock + threadIdx.x];
-  uint32_t total = 0;
-#pragma unroll
-  for (int w = 0; w < kClsBlock / 64; w++) total += s_w[w];
-  __shared__ uint16_t s_pt[kChunk];
-  uint32_t* s_poly = s_off;
-  for (uint32_t w0 = 0; w0 < total; w0 += kChunk) {
-    __syncthreads();  // (s_off read / the previous window written)
-#pragma unroll
-    for (int k = 0; k < kClsItems; k++) {
-      const uint32_t first = (uint32_t)vv[k], mask = (uint32_t)(vv[k] >> 32);
-      uint32_t q = mo[k];
-      if (!mask || q >= w0 + kChunk || q + (uint32_t)__popc(mask) <= w0) continue;
-      for (uint32_t m = mask; m; m &= m - 1, q++)
-        if (q >= w0 && q < w0 + kChunk) {
-          s_poly[q - w0] = t.chip_poly[first + __builtin_ctz(m)];
-          s_pt[q - w0] = (uint16_t)(k * kClsBlock + threadIdx.x);
-        }
-    }
     __syncthreads();
-    const uint32_t cnt = total - w0 < (uint32_t)kChunk ? total - w0 : (uint32_t)kChunk;
+    const uint32_t cnt = total - w0 < (uint32_t)kEmitWin ? total - w0 : (uint32_t)kEmitWin;
     for (uint32_t i = threadIdx.x; i < cnt; i += kClsBlock) {
       const uint64_t q = base + w0 + i;
       if ((int64_t)q >= sa.capacity) break;
@@ -1200,6 +1201,7 @@ __global__ __launch_bounds__(kClsBlock) void split_emit_kernel(SplitArgs sa) {
       sa.out_point[q] = sa.point_id ? sa.point_id[p] : sa.id_base + p;
       sa.out_poly[q] = (int32_t)s_poly[i];
     }
+    __syncthreads();
   }
 }
 
@@ -1833,8 +1835,8 @@ template <int IS>
 static void launch_split_t(const SplitArgs& a, hipStream_t s, hipEvent_t after_classify, hipEvent_t after_mixed) {
   const int64_t nc = split_chunks(a.j.n);
   const size_t lds = (IS == MGPU_H3 && a.j.chips.raster_blk) ? (size_t)a.j.chips.raster_bnx * a.j.chips.raster_bny * 2 : 0;
-  const int64_t grid = std::min<int64_t>(nc, (int64_t)resident_blocks((const void*)classify_kernel<IS>, kClsBlock, lds));
-  hipLaunchKernelGGL(classify_kernel<IS>, dim3((unsigned)grid), dim3(kClsBlock), lds, s, a, nc);
+  const int64_t grid = std::min<int64_t>(nc, (int64_t)resident_blocks((const void*)classify_kernel<IS>, kCfyBlock, lds));
+  hipLaunchKernelGGL(classify_kernel<IS>, dim3((unsigned)grid), dim3(kCfyBlock), lds, s, a, nc);
   if (after_classify) hipEventRecord(after_classify, s);
   hipLaunchKernelGGL(pip_mixed_kernel<IS>, dim3((unsigned)nc), dim3(kBlock), 0, s, a.j);
   const int64_t fix = nc * kChunkTiles < 512 ? nc * kChunkTiles : 512;
