@@ -287,6 +287,11 @@ int32_t mgpu_test_chip_contains_host(int32_t index_system, int64_t n_chips, cons
 int32_t mgpu_test_parse_number(const char* s, int32_t len, double* out);
 /* TEST ONLY -- the WKB / WKT point decoder on one host row: status 0 ok, 1 malformed,
  * 2 unsupported type, 3 empty. */
+/* Test hooks of the exact H3 route (h3_exact.h), host-side: the route's elementary
+ * operations (fn codes as oracle/oracle.h orc_h3_elementary: correctly rounded libm and
+ * emulated x87 long-double expressions), and point -> cell by the route alone. */
+int32_t mgpu_test_h3_elementary_host(int32_t fn, const double* a, const double* b, int64_t n, double* out);
+int32_t mgpu_test_h3_route_host(const double* lon, const double* lat, int64_t n, int32_t res, int64_t* out_cell);
 int32_t mgpu_test_decode_point(int32_t format, const uint8_t* data, int64_t len, double* x, double* y);
 
 /* TEST ONLY -- st_contains(chip row, point) evaluated on a HOST blob (the join's

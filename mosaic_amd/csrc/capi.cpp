@@ -2250,6 +2250,44 @@ int32_t mgpu_test_parse_number(const char* s, int32_t len, double* out) {
   return mgpu::dec::parse_number(s, len, out);
 }
 
+int32_t mgpu_test_h3_elementary_host(int32_t fn, const double* a, const double* b, int64_t n, double* out) {
+  namespace X = mgpu::exact;
+  for (int64_t i = 0; i < n; ++i) {
+    const double x = a[i], y = b ? b[i] : 0.0;
+    double r = 0.0;
+    switch (fn) {
+      case 0: r = X::cr_sin(x); break;
+      case 1: r = X::cr_cos(x); break;
+      case 2: r = X::cr_tan(x); break;
+      case 3: r = X::cr_acos(x); break;
+      case 4: r = X::cr_atan2(x, y); break;
+      case 5: r = X::ld_add(x, X::kX2Pi); break;
+      case 6: r = X::ld_sub(x, X::kX2Pi); break;
+      case 7: r = X::ld_mul(x, X::kXSqrt7); break;
+      case 8: r = X::ld_div(x, X::kXSin60); break;
+      case 9: r = X::ld_sub(x, X::kXAp7Rot); break;
+      case 10: r = X::ld_div(x, X::kXSqrt7); break;
+      case 11: r = X::ld_add(x, X::kXAp7Rot); break;
+      case 12: r = X::ld_lt(x, X::kXEpsilon) ? 1.0 : 0.0; break;
+      case 13: r = X::ld_ge(x, X::kX2Pi) ? 1.0 : 0.0; break;
+      default: return MGPU_E_INVALID_ARG;
+    }
+    out[i] = r;
+  }
+  return MGPU_OK;
+}
+
+int32_t mgpu_test_h3_route_host(const double* lon, const double* lat, int64_t n, int32_t res, int64_t* out_cell) {
+  if (res < 0 || res > 15) return MGPU_E_RESOLUTION;
+  mgpu::parallel_for(n, 4096, [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; ++i) {
+      bool tie;
+      out_cell[i] = (int64_t)mgpu::h3::point_to_cell(lon[i], lat[i], res, &tie);
+    }
+  });
+  return MGPU_OK;
+}
+
 int32_t mgpu_test_decode_point(int32_t format, const uint8_t* data, int64_t len, double* x, double* y) {
   return format == MGPU_GEOM_WKB ? mgpu::geom::wkb_centroid(data, len, x, y)
                                  : mgpu::geom::wkt_centroid((const char*)data, len, x, y);

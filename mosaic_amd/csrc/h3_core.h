@@ -8,14 +8,14 @@
 // distance -> gnomonic projection into that face's hex2d plane -> hex rounding ->
 // aperture-7 digit extraction from res down to 0 -> base cell lookup + rotations.
 //
-// Numerics.  All arithmetic is IEEE double with FMA contraction disabled (the
-// library is compiled with -ffp-contract=off), so every + - * / rounds exactly as
-// in the JVM path's native H3.  Two things can differ from that path by an ulp:
-// the libm transcendentals (ocml here, glibc there) and the five H3 expressions
-// that use x87 long-double constants.  Both only matter for points whose hex2d
-// coordinates fall within a few ulps of a cell edge; every such point is detected
-// by `margin` below (distance to the nearest decision threshold, in hex units,
-// relative to the coordinate magnitude) and is reported as a near-tie.
+// Numerics.  The H3 route (route_face_ijk, the reference formulation) is exact to the
+// JVM path's native H3 by construction: IEEE double with FMA contraction disabled (the
+// library is compiled with -ffp-contract=off) for every + - * /, H3's five x87
+// long-double expressions emulated bit for bit, and correctly rounded
+// sin/cos/tan/acos/atan2 (h3_exact.h).  The fast path (fast_hex2d) is an
+// approximation trusted only outside a tie band: every point whose hex2d coordinates
+// fall near a decision threshold (`margin` below: distance to the nearest threshold,
+// in hex units, relative to the coordinate magnitude) is a near-tie and takes the route.
 #pragma once
 #include <stdint.h>
 
@@ -31,6 +31,7 @@
 #define H3T_QUAL static const
 #endif
 #include "h3_tables.inc"
+#include "h3_exact.h"
 
 namespace mgpu {
 namespace h3 {
@@ -67,16 +68,18 @@ struct IJK {
 #else
 #define MGPU_COLD_FN static inline
 #endif
-MGPU_LIBM void lm_sincos(double a, double* s, double* c) { sincos(a, s, c); }
-MGPU_LIBM double lm_acos(double a) { return acos(a); }
-MGPU_LIBM double lm_atan2(double y, double x) { return atan2(y, x); }
-MGPU_LIBM double lm_tan(double a) { return tan(a); }
-MGPU_LIBM double lm_sin(double a) { return sin(a); }
-MGPU_LIBM double lm_cos(double a) { return cos(a); }
+// correctly rounded (h3_exact.h), the same on the host and the device
+MGPU_LIBM void lm_sincos(double a, double* s, double* c) { exact::cr_sincos(a, s, c); }
+MGPU_LIBM double lm_acos(double a) { return exact::cr_acos(a); }
+MGPU_LIBM double lm_atan2(double y, double x) { return exact::cr_atan2(y, x); }
+MGPU_LIBM double lm_tan(double a) { return exact::cr_tan(a); }
+MGPU_LIBM double lm_sin(double a) { return exact::cr_sin(a); }
+MGPU_LIBM double lm_cos(double a) { return exact::cr_cos(a); }
 
+// _posAngleRads: `rads + M_2PI` and `tmp -= M_2PI` are x87 long-double expressions
 MGPU_HD double pos_angle(double rads) {
-  double tmp = (rads < 0.0) ? rads + kTwoPi : rads;
-  if (rads >= kTwoPi) tmp -= kTwoPi;
+  double tmp = (rads < 0.0) ? exact::ld_add(rads, exact::kX2Pi) : rads;
+  if (exact::ld_ge(rads, exact::kX2Pi)) tmp = exact::ld_sub(tmp, exact::kX2Pi);
   return tmp;
 }
 
@@ -99,7 +102,7 @@ MGPU_COLD_FN IJK hex2d_to_ijk(double vx, double vy, double* margin) {
   IJK h;
   h.k = 0;
   double a1 = fabs(vx), a2 = fabs(vy);
-  double x2 = a2 / kSin60;
+  double x2 = exact::ld_div(a2, exact::kXSin60);  // a2 / M_SIN60 in long double
   double x1 = a1 + x2 / 2.0;
   int m1 = (int)x1, m2 = (int)x2;
   double r1 = x1 - m1, r2 = x2 - m2;
@@ -178,7 +181,7 @@ MGPU_COLD_FN void geo_to_hex2d(double lat, double lon, int res, int* face, doubl
   *face = f0;
   *face_gap = second - best;
   double r = lm_acos(1 - best / 2);
-  if (r < kEpsilon) {
+  if (exact::ld_lt(r, exact::kXEpsilon)) {
     *vx = *vy = 0.0;
     return;
   }
@@ -188,10 +191,10 @@ MGPU_COLD_FN void geo_to_hex2d(double lat, double lon, int res, int* face, doubl
   lm_sincos(lon - flon, &sdl, &cdl);
   double az = lm_atan2(clat * sdl, lm_cos(flat) * slat - lm_sin(flat) * clat * cdl);
   double theta = pos_angle(H3T_FACE_AXES_AZ_CII[f0][0] - pos_angle(az));
-  if (res % 2) theta = pos_angle(theta - kAp7Rot);
+  if (res % 2) theta = pos_angle(exact::ld_sub(theta, exact::kXAp7Rot));
   r = lm_tan(r);
   r /= kRes0UGnomonic;
-  for (int i = 0; i < res; i++) r *= kSqrt7;
+  for (int i = 0; i < res; i++) r = exact::ld_mul(r, exact::kXSqrt7);
   double st, ct;
   lm_sincos(theta, &st, &ct);
   *vx = r * ct;
@@ -651,10 +654,10 @@ MGPU_HD void hex2d_to_geo(double vx, double vy, int face, int res, double* lat, 
     return;
   }
   double theta = atan2(vy, vx);
-  for (int i = 0; i < res; i++) r /= kSqrt7;
+  for (int i = 0; i < res; i++) r = exact::ld_div(r, exact::kXSqrt7);
   r *= kRes0UGnomonic;
   r = atan(r);
-  if (res % 2) theta = pos_angle(theta + kAp7Rot);
+  if (res % 2) theta = pos_angle(exact::ld_add(theta, exact::kXAp7Rot));
   double az = pos_angle(H3T_FACE_AXES_AZ_CII[face][0] - theta);
   double sinlat = sin(lat0) * cos(r) + cos(lat0) * sin(r) * cos(az);
   if (sinlat > 1.0) sinlat = 1.0;

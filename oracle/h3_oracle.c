@@ -17,6 +17,7 @@
  *  - Degree conversion is JDK Math.toRadians: JDK 8 computes deg / 180.0 * PI.
  */
 #include <math.h>
+#include <quadmath.h>
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
@@ -104,17 +105,31 @@ static void hex2dToCoordIJK(double vx, double vy, CoordIJK* h) {
     ijkNormalize(h);
 }
 
+/* The route's libm: glibc (the reference's, default) or correctly rounded (quadmath's
+ * 113-bit functions rounded once to double) -- the independent restatement the device's
+ * correctly rounded route (mosaic_amd/csrc/h3_exact.h) is checked against bit for bit;
+ * the difference between the two modes is exactly glibc's misrounding. */
+static int g_cr_libm = 0;
+void orc_h3_set_libm(int correctly_rounded) { g_cr_libm = correctly_rounded; }
+static double L_sin(double x) { return g_cr_libm ? (double)sinq((__float128)x) : sin(x); }
+static double L_cos(double x) { return g_cr_libm ? (double)cosq((__float128)x) : cos(x); }
+static double L_tan(double x) { return g_cr_libm ? (double)tanq((__float128)x) : tan(x); }
+static double L_acos(double x) { return g_cr_libm ? (double)acosq((__float128)x) : acos(x); }
+static double L_atan2(double y, double x) {
+    return g_cr_libm ? (double)atan2q((__float128)y, (__float128)x) : atan2(y, x);
+}
+
 static double geoAzimuthRads(double lat1, double lon1, double lat2, double lon2) {
-    return atan2(cos(lat2) * sin(lon2 - lon1),
-                 cos(lat1) * sin(lat2) - sin(lat1) * cos(lat2) * cos(lon2 - lon1));
+    return L_atan2(L_cos(lat2) * L_sin(lon2 - lon1),
+                   L_cos(lat1) * L_sin(lat2) - L_sin(lat1) * L_cos(lat2) * L_cos(lon2 - lon1));
 }
 
 static void geoToHex2d(double lat, double lon, int res, int* face, double* vx, double* vy) {
     /* _geoToVec3d */
-    double r0 = cos(lat);
-    double z = sin(lat);
-    double x = cos(lon) * r0;
-    double y = sin(lon) * r0;
+    double r0 = L_cos(lat);
+    double z = L_sin(lat);
+    double x = L_cos(lon) * r0;
+    double y = L_sin(lon) * r0;
     /* _geoToClosestFace */
     *face = 0;
     double sqd = 5.0;
@@ -123,17 +138,17 @@ static void geoToHex2d(double lat, double lon, int res, int* face, double* vx, d
                       square(H3T_FACE_CENTER_POINT[f][2] - z);
         if (sqdT < sqd) { *face = f; sqd = sqdT; }
     }
-    double r = acos(1 - sqd / 2);
+    double r = L_acos(1 - sqd / 2);
     if (r < EPSILON_L) { *vx = *vy = 0.0L; return; }
     double theta = posAngleRads(H3T_FACE_AXES_AZ_CII[*face][0] -
                                 posAngleRads(geoAzimuthRads(H3T_FACE_CENTER_GEO[*face][0],
                                                             H3T_FACE_CENTER_GEO[*face][1], lat, lon)));
     if (res % 2) theta = posAngleRads(theta - M_AP7_ROT_RADS_L);
-    r = tan(r);
+    r = L_tan(r);
     r /= RES0_U_GNOMONIC;
     for (int i = 0; i < res; i++) r *= M_SQRT7_L;
-    *vx = r * cos(theta);
-    *vy = r * sin(theta);
+    *vx = r * L_cos(theta);
+    *vy = r * L_sin(theta);
 }
 
 /* nearest integer of n / 7 (lround((n) / 7.0) in H3; never a tie) */
@@ -497,4 +512,37 @@ int orc_h3_hex_ring(uint64_t origin, int k, uint64_t* out) {
         }
     }
     return lastIndex != origin;
+}
+
+/* ------------------------------------------------------------------ libm / x87 probe
+ * The reference route's elementary operations as the native H3 library evaluates them
+ * on x86-64 (glibc libm; long-double constants on the x87 unit), for
+ * tests/test_h3_exact_host.py: out[i] = op(a[i], b[i]). */
+void orc_h3_elementary(int fn, const double* a, const double* b, int64_t n, double* out) {
+    for (int64_t i = 0; i < n; i++) {
+        double x = a[i], y = b ? b[i] : 0.0, r;
+        switch (fn) {
+            case 0: r = sin(x); break;
+            case 1: r = cos(x); break;
+            case 2: r = tan(x); break;
+            case 3: r = acos(x); break;
+            case 4: r = atan2(x, y); break;
+            case 5: r = x + M_2PI_L; break;
+            case 6: r = x - M_2PI_L; break;
+            case 7: r = x * M_SQRT7_L; break;
+            case 8: r = x / M_SIN60_L; break;
+            case 9: r = x - M_AP7_ROT_RADS_L; break;
+            case 10: r = x / M_SQRT7_L; break;
+            case 11: r = x + M_AP7_ROT_RADS_L; break;
+            case 12: r = (x < EPSILON_L) ? 1.0 : 0.0; break;
+            case 13: r = (x >= M_2PI_L) ? 1.0 : 0.0; break;
+            case 20: r = (double)sinq((__float128)x); break;
+            case 21: r = (double)cosq((__float128)x); break;
+            case 22: r = (double)tanq((__float128)x); break;
+            case 23: r = (double)acosq((__float128)x); break;
+            case 24: r = (double)atan2q((__float128)x, (__float128)y); break;
+            default: r = 0.0; break;
+        }
+        out[i] = r;
+    }
 }

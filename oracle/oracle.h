@@ -35,6 +35,14 @@
 extern "C" {
 #endif
 
+/* The H3 route's elementary operations as the native library evaluates them (glibc
+ * libm, x87 long-double constants): fn 0 sin, 1 cos, 2 tan, 3 acos, 4 atan2(a, b),
+ * 5 a + M_2PI, 6 a - M_2PI, 7 a * M_SQRT7, 8 a / M_SIN60, 9 a - M_AP7_ROT_RADS,
+ * 10 a / M_SQRT7, 11 a + M_AP7_ROT_RADS, 12 a < EPSILON, 13 a >= M_2PI; 20..24 the
+ * correctly rounded sin, cos, tan, acos, atan2 (libquadmath, rounded once). */
+/* The geoToH3 route's libm: 0 = glibc (the reference's, default), 1 = correctly rounded. */
+void orc_h3_set_libm(int correctly_rounded);
+void orc_h3_elementary(int fn, const double* a, const double* b, int64_t n, double* out);
 /* H3 v3.7 geoToH3 on radians (C-API semantics: 0 on bad input). */
 uint64_t orc_h3_geo_to_h3(double lat_rad, double lon_rad, int res);
 /* H3IndexSystem.pointToIndex(lon, lat, res) in degrees.  jdk = 8 uses JDK 8's

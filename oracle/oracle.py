@@ -34,6 +34,10 @@ def lib():
         L.orc_h3_point_to_index.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int]
         L.orc_h3_points_to_cells.restype = None
         L.orc_h3_points_to_cells.argtypes = [_dp, _dp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _u64p, ctypes.c_int]
+        L.orc_h3_set_libm.restype = None
+        L.orc_h3_set_libm.argtypes = [ctypes.c_int]
+        L.orc_h3_elementary.restype = None
+        L.orc_h3_elementary.argtypes = [ctypes.c_int, _dp, _dp, ctypes.c_int64, _dp]
         L.orc_h3_geo_to_hex2d.restype = None
         L.orc_h3_geo_to_hex2d.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_int), _dp, _dp]
@@ -68,6 +72,31 @@ def h3_points_to_cells(lon, lat, res, jdk=8, threads=None):
     lib().orc_h3_points_to_cells(_ptr(lon, _dp), _ptr(lat, _dp), lon.shape[0], int(res), int(jdk),
                                  _ptr(out, _u64p), int(threads or os.cpu_count() or 1))
     return out.view(np.int64)
+
+
+class h3_libm:
+    """Context manager: the geoToH3 route's libm inside the block -- "glibc" (the
+    reference's, the default) or "cr" (correctly rounded, libquadmath)."""
+
+    def __init__(self, mode):
+        self.cr = {"glibc": 0, "cr": 1}[mode]
+
+    def __enter__(self):
+        lib().orc_h3_set_libm(self.cr)
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_h3_set_libm(0)
+        return False
+
+
+def h3_elementary(fn, a, b=None):
+    """The H3 route's elementary operation `fn` (oracle.h orc_h3_elementary) on arrays."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    bb = None if b is None else np.ascontiguousarray(b, dtype=np.float64)
+    out = np.empty(a.shape[0], dtype=np.float64)
+    lib().orc_h3_elementary(int(fn), _ptr(a, _dp), None if bb is None else _ptr(bb, _dp), a.shape[0], _ptr(out, _dp))
+    return out
 
 
 def h3_geo_to_hex2d(lat_rad, lon_rad, res):

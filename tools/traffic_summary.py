@@ -21,29 +21,37 @@ DESC = {"c2": ("uniform NYC-bbox points, H3 res 9, 263 zones", 9),
         "c5": ("skewed points near 4 fractal polygons, H3 res 9", 9)}[CFG]
 
 
-def per_dispatch(sub, kname):
-    tot = collections.defaultdict(float)
+def per_kernel(sub):
+    """{kernel short name: (mean counter bytes per dispatch, dispatches)} for mgpu kernels."""
+    tot = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(os.path.join(d, sub, "run_counter_collection.csv"))):
-        if kname in r["Kernel_Name"]:
-            tot[r["Dispatch_Id"]] += float(r["Counter_Value"])
-    v = sorted(tot.values())
-    return sum(v) / len(v) * 1024.0, len(v)
+        name = r["Kernel_Name"]
+        if "mgpu::" not in name:
+            continue
+        short = name.split("mgpu::", 1)[1].split("(", 1)[0]
+        tot[short][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {k: (sum(v.values()) / len(v) * 1024.0, len(v)) for k, v in tot.items()}
 
 
-jf, nj = per_dispatch("join_fetch", "pip_join_kernel")
-jw, _ = per_dispatch("join_write", "pip_join_kernel")
-bf, nb = per_dispatch("bng_fetch", "cells_kernel<1>")
-bw, _ = per_dispatch("bng_write", "cells_kernel<1>")
+jf_all, jw_all = per_kernel("join_fetch"), per_kernel("join_write")
+bf, nb = per_kernel("bng_fetch")["cells_kernel<1>"]
+bw, _ = per_kernel("bng_write")["cells_kernel<1>"]
 f_read = bf / (16.0 * N)
 f_write = bw / (8.0 * N)
+# the dominant kernel: classify_kernel in the split pipeline, else the fused pip_join_kernel
+dom = next(k for k in jf_all if k.startswith("classify_kernel") or k.startswith("pip_join_kernel"))
+jf, nj = jf_all[dom]
+jw, _ = jw_all[dom]
 out = {
-    "round": tag, "config": CFG, "points": N, "res": DESC[1],
+    "round": tag, "config": CFG, "points": N, "res": DESC[1], "kernel": dom,
     "join_fetch_bytes_raw": jf, "join_write_bytes_raw": jw, "dispatches": nj,
     "calib_bng_fetch_bytes_raw": bf, "calib_bng_write_bytes_raw": bw,
     "calib_read_factor": f_read, "calib_write_factor": f_write,
     "hbm_read_bytes_per_launch": jf / f_read, "hbm_write_bytes_per_launch": jw / f_write,
     "hbm_bytes_per_launch": jf / f_read + jw / f_write,
-    "note": "pip_join_kernel, 1e8 " + DESC[0] + "; FETCH_SIZE and WRITE_SIZE "
+    "per_kernel": {k: {"hbm_read_bytes": jf_all[k][0] / f_read,
+                       "hbm_write_bytes": jw_all.get(k, (0.0, 0))[0] / f_write} for k in sorted(jf_all)},
+    "note": dom + ", 1e8 " + DESC[0] + "; FETCH_SIZE and WRITE_SIZE "
             "in separate rocprofv3 --pmc passes, each divided by its factor measured on cells_kernel<BNG> "
             "(16 B read + 8 B written per point)",
 }
