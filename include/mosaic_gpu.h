@@ -292,6 +292,10 @@ int32_t mgpu_test_parse_number(const char* s, int32_t len, double* out);
  * emulated x87 long-double expressions), and point -> cell by the route alone. */
 int32_t mgpu_test_h3_elementary_host(int32_t fn, const double* a, const double* b, int64_t n, double* out);
 int32_t mgpu_test_h3_route_host(const double* lon, const double* lat, int64_t n, int32_t res, int64_t* out_cell);
+/* H3 cell geometry as the builder computes it (h3ToGeoBoundary / h3ToGeo, degrees):
+ * out_lonlat[20 n] (up to 10 vertices per cell), out_nverts[n], out_center[2 n]. */
+int32_t mgpu_test_h3_boundary_host(const int64_t* cells, int64_t n, double* out_lonlat, int32_t* out_nverts,
+                                   double* out_center);
 int32_t mgpu_test_decode_point(int32_t format, const uint8_t* data, int64_t len, double* x, double* y);
 
 /* TEST ONLY -- st_contains(chip row, point) evaluated on a HOST blob (the join's

@@ -38,7 +38,7 @@ EXPORTS = (
     "mgpu_comm_unique_id", "mgpu_comm_init", "mgpu_comm_info", "mgpu_comm_destroy", "mgpu_chips_broadcast",
     "mgpu_pair_offsets", "mgpu_test_blob_contains_host", "mgpu_points_from_geometry", "mgpu_geometry_to_cells",
     "mgpu_geometry_to_cells_arrow", "mgpu_pip_join_arrow", "mgpu_test_parse_number", "mgpu_test_decode_point",
-    "mgpu_test_h3_elementary_host", "mgpu_test_h3_route_host",
+    "mgpu_test_h3_elementary_host", "mgpu_test_h3_route_host", "mgpu_test_h3_boundary_host",
 )
 MGPU_GEOM_WKB = 0
 MGPU_GEOM_WKT = 1
@@ -148,6 +148,7 @@ def lib():
         "mgpu_test_decode_point": (I32, [I32, P, I64, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
         "mgpu_test_h3_elementary_host": (I32, [I32, P, P, I64, P]),
         "mgpu_test_h3_route_host": (I32, [P, P, I64, I32, P]),
+        "mgpu_test_h3_boundary_host": (I32, [P, I64, P, P, P]),
     }
     for name, (rt, args) in sig.items():
         f = getattr(L, name)

@@ -160,7 +160,7 @@ def tessellate(polygons, index_system, resolution, keep_core_geometries=True):
     st = L.mgpu_tessellate(index_system.code, res, len(p), p.poly_id.ctypes.data, p.poly_part_off.ctypes.data,
                            p.part_ring_off.ctypes.data, p.ring_off.ctypes.data, p.xy.ctypes.data,
                            1 if keep_core_geometries else 0, ctypes.byref(h))
-    N.check(st, "tessellation failed (H3 polygons must lie on one icosahedron face; BNG res -1 unsupported)")
+    N.check(st, "tessellation failed")
     try:
         n, b = ctypes.c_int64(), ctypes.c_int64()
         N.check(L.mgpu_tess_result_sizes(h, ctypes.byref(n), ctypes.byref(b)))

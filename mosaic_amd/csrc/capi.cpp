@@ -2261,15 +2261,16 @@ int32_t mgpu_test_h3_elementary_host(int32_t fn, const double* a, const double* 
       case 2: r = X::cr_tan(x); break;
       case 3: r = X::cr_acos(x); break;
       case 4: r = X::cr_atan2(x, y); break;
-      case 5: r = X::ld_add(x, X::kX2Pi); break;
-      case 6: r = X::ld_sub(x, X::kX2Pi); break;
-      case 7: r = X::ld_mul(x, X::kXSqrt7); break;
-      case 8: r = X::ld_div(x, X::kXSin60); break;
-      case 9: r = X::ld_sub(x, X::kXAp7Rot); break;
-      case 10: r = X::ld_div(x, X::kXSqrt7); break;
-      case 11: r = X::ld_add(x, X::kXAp7Rot); break;
-      case 12: r = X::ld_lt(x, X::kXEpsilon) ? 1.0 : 0.0; break;
-      case 13: r = X::ld_ge(x, X::kX2Pi) ? 1.0 : 0.0; break;
+      // the integer emulation the device runs (not the host's x87 unit)
+      case 5: r = X::x80_to_double(X::x80_add(X::x80_from_double(x), X::kX2Pi)); break;
+      case 6: r = X::x80_to_double(X::x80_add(X::x80_from_double(x), X::x80_neg(X::kX2Pi))); break;
+      case 7: r = X::x80_to_double(X::x80_mul(X::x80_from_double(x), X::kXSqrt7)); break;
+      case 8: r = X::x80_to_double(X::x80_div(X::x80_from_double(x), X::kXSin60)); break;
+      case 9: r = X::x80_to_double(X::x80_add(X::x80_from_double(x), X::x80_neg(X::kXAp7Rot))); break;
+      case 10: r = X::x80_to_double(X::x80_div(X::x80_from_double(x), X::kXSqrt7)); break;
+      case 11: r = X::x80_to_double(X::x80_add(X::x80_from_double(x), X::kXAp7Rot)); break;
+      case 12: r = X::x80_cmp(X::x80_from_double(x), X::kXEpsilon) < 0 ? 1.0 : 0.0; break;
+      case 13: r = X::x80_cmp(X::x80_from_double(x), X::kX2Pi) >= 0 ? 1.0 : 0.0; break;
       default: return MGPU_E_INVALID_ARG;
     }
     out[i] = r;

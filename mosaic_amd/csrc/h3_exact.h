@@ -188,6 +188,17 @@ MGPU_XD X80 x80_mul(X80 a, X80 b) {
 
 MGPU_XD X80 x80_div(X80 a, X80 b) {
   if (a.m == 0) return X80{0, 0, a.s ^ b.s};
+#if !defined(__HIP_DEVICE_COMPILE__) && defined(__x86_64__)
+  {
+    // host: the same 67 quotient bits by two native 128-bit divisions (the builder
+    // divides by M_SQRT7 once per resolution per cell vertex)
+    const u128 num = (u128)a.m << 63;
+    const u128 q1 = num / b.m, r1 = num % b.m;
+    const u128 n2 = r1 << 3;
+    const u128 q = (q1 << 3) | (n2 / b.m);
+    return x80_round(q, a.e - b.e - 66, (n2 % b.m) != 0, a.s ^ b.s);
+  }
+#endif
   // 67 quotient bits of a.m / b.m (1 integer bit + 66 fraction bits) by long division
   u128 rem = a.m;
   u128 q = 0;
@@ -216,13 +227,29 @@ MGPU_XD int x80_cmp(X80 a, X80 b) {
   return sa > 0 ? mag : -mag;
 }
 
-// (double)((long double)a OP c)
+// (double)((long double)a OP c).  On an x86-64 host `long double` IS the x87 format:
+// there the hardware does it (the chip-table builder runs these per cell vertex); the
+// device -- and the tests, through the x80_* functions -- use the emulation.
+#if !defined(__HIP_DEVICE_COMPILE__) && defined(__x86_64__) && (__LDBL_MANT_DIG__ == 64)
+#define MGPU_NATIVE_X87 1
+inline long double x80_ld(X80 c) {
+  const long double v = __builtin_ldexpl((long double)c.m, c.e);
+  return c.s ? -v : v;
+}
+inline double ld_add(double a, X80 c) { return (double)((long double)a + x80_ld(c)); }
+inline double ld_sub(double a, X80 c) { return (double)((long double)a - x80_ld(c)); }
+inline double ld_mul(double a, X80 c) { return (double)((long double)a * x80_ld(c)); }
+inline double ld_div(double a, X80 c) { return (double)((long double)a / x80_ld(c)); }
+inline bool ld_lt(double a, X80 c) { return (long double)a < x80_ld(c); }
+inline bool ld_ge(double a, X80 c) { return (long double)a >= x80_ld(c); }
+#else
 MGPU_XD double ld_add(double a, X80 c) { return x80_to_double(x80_add(x80_from_double(a), c)); }
 MGPU_XD double ld_sub(double a, X80 c) { return x80_to_double(x80_add(x80_from_double(a), x80_neg(c))); }
 MGPU_XD double ld_mul(double a, X80 c) { return x80_to_double(x80_mul(x80_from_double(a), c)); }
 MGPU_XD double ld_div(double a, X80 c) { return x80_to_double(x80_div(x80_from_double(a), c)); }
 MGPU_XD bool ld_lt(double a, X80 c) { return x80_cmp(x80_from_double(a), c) < 0; }
 MGPU_XD bool ld_ge(double a, X80 c) { return x80_cmp(x80_from_double(a), c) >= 0; }
+#endif
 
 // ------------------------------------------------------------------ double-double
 

@@ -24,7 +24,17 @@
 //     lattice space) and that no edge touches -> core chips,
 //  4. border cells: Sutherland-Hodgman clip of every ring against the convex cell
 //     -> empty (dropped), whole cell (core) or a border chip.
-// Limitation: an H3 polygon must lie on a single icosahedron face.
+// H3 polygons may span several icosahedron faces: steps 1-4 run once per face near
+// the polygon (the faces of its vertices and, close to a face edge, the neighbour
+// across it), each pass keeping the cells whose centre lies on that face (the face
+// _h3ToFaceIjk gives the cell id), so every cell is considered exactly once.  The
+// rings are densified along their lon/lat edges before projection, so the lattice
+// walk follows the true edges (straight in lon/lat, curved in a face's gnomonic
+// plane).  Cell geometry is H3's own h3ToGeoBoundary (h3_boundary.h), with the
+// distortion vertices of Class III cells that cross an icosahedron edge.
+// Limitations (MGPU_E_UNSUPPORTED): a cell crossing the antimeridian or containing a
+// pole (the reference's makeSafeGeometry / makePoleGeometry), a polygon more than
+// ~84 degrees from a face it touches.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -38,6 +48,7 @@
 #include "error.h"
 #include "bng_core.h"
 #include "h3_core.h"
+#include "h3_boundary.h"
 #include "parallel.h"
 #include "wkb.h"
 
@@ -116,11 +127,90 @@ bool in_convex(const std::vector<Pt>& cell, Pt p) {
   return true;
 }
 
+bool is_convex(const std::vector<Pt>& c) {  // closed ccw ring
+  const size_t n = c.size() - 1;
+  for (size_t i = 0; i < n; i++)
+    if (orient(c[(i + n - 1) % n], c[i], c[(i + 1) % n]) < 0) return false;
+  return true;
+}
+
+// A cell ring split into convex pieces (closed ccw rings).  H3 cells are convex in lon/lat
+// except at the distortion vertices Class III cells gain where an edge crosses an
+// icosahedron edge; those are split by ear clipping, then triangles sharing a diagonal
+// are merged while the union stays convex (Hertel-Mehlhorn).
+std::vector<std::vector<Pt>> convex_pieces(const std::vector<Pt>& cell) {
+  if (is_convex(cell)) return {cell};
+  const int n = (int)cell.size() - 1;
+  std::vector<int> idx(n);
+  for (int i = 0; i < n; i++) idx[i] = i;
+  std::vector<std::vector<int>> pieces;
+  while (idx.size() > 3) {
+    const int m = (int)idx.size();
+    bool cut = false;
+    for (int k = 0; k < m && !cut; k++) {
+      const int a = idx[(k + m - 1) % m], b = idx[k], c = idx[(k + 1) % m];
+      if (orient(cell[a], cell[b], cell[c]) <= 0) continue;
+      bool empty = true;
+      for (int q : idx)
+        if (q != a && q != b && q != c && orient(cell[a], cell[b], cell[q]) >= 0 &&
+            orient(cell[b], cell[c], cell[q]) >= 0 && orient(cell[c], cell[a], cell[q]) >= 0)
+          empty = false;
+      if (!empty) continue;
+      pieces.push_back({a, b, c});
+      idx.erase(idx.begin() + k);
+      cut = true;
+    }
+    if (!cut) break;  // degenerate: keep the remainder as one piece
+  }
+  pieces.push_back(idx);
+  auto ring_of = [&](const std::vector<int>& v) {
+    std::vector<Pt> r;
+    for (int q : v) r.push_back(cell[q]);
+    r.push_back(cell[v[0]]);
+    return r;
+  };
+  for (bool merged = true; merged;) {
+    merged = false;
+    for (size_t i = 0; i < pieces.size() && !merged; i++)
+      for (size_t j = i + 1; j < pieces.size() && !merged; j++) {
+        const auto& P = pieces[i];
+        const auto& Q = pieces[j];
+        for (size_t e = 0; e < P.size() && !merged; e++) {
+          const int a = P[e], b = P[(e + 1) % P.size()];
+          for (size_t f = 0; f < Q.size(); f++) {
+            if (Q[f] != b || Q[(f + 1) % Q.size()] != a) continue;
+            // P with its edge a->b replaced by Q's path b -> ... -> a
+            std::vector<int> W;
+            for (size_t t = 0; t < P.size(); t++) W.push_back(P[(e + 1 + t) % P.size()]);  // b .. a
+            for (size_t t = 2; t < Q.size(); t++) W.push_back(Q[(f + t) % Q.size()]);     // after a .. before b
+            if (is_convex(ring_of(W))) {
+              pieces[i] = W;
+              pieces.erase(pieces.begin() + j);
+              merged = true;
+            }
+            break;
+          }
+        }
+      }
+  }
+  std::vector<std::vector<Pt>> out;
+  for (auto& v : pieces) out.push_back(ring_of(v));
+  return out;
+}
+
 
 // ---------------------------------------------------------------- grids
 
 struct Grid {
   virtual ~Grid() {}
+  // a cell whose centre is farther than this (lattice units) from every walked boundary
+  // sample cannot meet the boundary (circumradius + sample spacing + H3's distortion)
+  virtual double far_distance() const { return 1.0; }
+  // whether this pass owns lattice cell (i, j) with id `id` (H3: the cell's centre lies on
+  // this pass's face, and the id is the cell at that lattice position)
+  virtual bool keep(int64_t, long, long) const { return true; }
+  // set when a candidate cell's geometry is outside what the builder supports
+  mutable bool unsupported = false;
   // lattice-space coordinate of an input point
   virtual Pt to_lattice(Pt p) const = 0;
   // lattice cell containing a lattice-space point
@@ -177,6 +267,21 @@ struct H3Grid : Grid {
     mgpu::h3::ijk_normalize(c);
     return (int64_t)mgpu::h3::face_ijk_to_h3(face, c, res);
   }
+  // exact H3 vertices are the lattice corners on this face; beyond a face edge the
+  // neighbour's projection moves them by a second-order amount, a fraction of a
+  // cell only at coarse resolutions
+  double far_distance() const override { return res <= 4 ? 1.25 : 0.75; }
+  bool keep(int64_t id, long i, long j) const override {
+    if (mgpu::h3b::h3_to_face_ijk((uint64_t)id).face != face) return false;
+    // near an icosahedron vertex the lattice positions beyond a pentagon's missing
+    // sector map to ids of cells elsewhere: the id's centre must be this position
+    const Pt g = to_geo(center(i, j));
+    const auto c = mgpu::h3b::cell_center((uint64_t)id);
+    const double dlat = g.y - mgpu::h3b::to_degrees(c.lat), dlon = g.x - mgpu::h3b::to_degrees(c.lon);
+    double spacing = 20.0;  // ~ res-0 centre spacing in degrees
+    for (int r = 0; r < res; r++) spacing /= 2.6457513110645906;
+    return std::fabs(dlat) < 0.01 * spacing && std::fabs(std::remainder(dlon, 360.0)) < 0.01 * spacing / std::max(0.05, std::cos(g.y * M_PI / 180.0));
+  }
   Pt to_geo(Pt v) const {
     // _hex2dToGeo (substrate = 0) then _geoAzDistanceRads
     double r = std::hypot(v.x, v.y);
@@ -205,13 +310,23 @@ struct H3Grid : Grid {
     }
     return {lon * 180.0 / M_PI, lat * 180.0 / M_PI};
   }
+  // H3IndexSystem.indexToGeometry: h3ToGeoBoundary in degrees, closed (ccw)
   std::vector<Pt> boundary(long i, long j) const override {
-    Pt c = center(i, j);
+    const int64_t id = cell_id(i, j);
     std::vector<Pt> b;
-    const double rad = 1.0 / std::sqrt(3.0);
-    for (int k = 0; k < 6; k++) {
-      double a = (30.0 + 60.0 * k) * M_PI / 180.0;
-      b.push_back(to_geo({c.x + rad * cos(a), c.y + rad * sin(a)}));
+    if (!id) return b;
+    for (auto& v : mgpu::h3b::cell_boundary((uint64_t)id))
+      b.push_back({mgpu::h3b::to_degrees(v.lon), mgpu::h3b::to_degrees(v.lat)});
+    double lo = INFINITY, hi = -INFINITY;
+    for (auto& p : b) {
+      lo = std::min(lo, p.x);
+      hi = std::max(hi, p.x);
+    }
+    if (hi - lo > 180.0 || std::fabs(mgpu::h3b::cell_center((uint64_t)id).lat) > 1.5) {
+      // antimeridian or pole cell: the reference re-shapes it (makeSafeGeometry /
+      // makePoleGeometry); not built here
+      unsupported = true;
+      return {};
     }
     b.push_back(b[0]);
     if (ring_area(b) < 0) std::reverse(b.begin(), b.end());
@@ -240,6 +355,7 @@ struct BngGrid : Grid {
     edge = r < 0 ? ten / 2 : ten;
   }
   Pt to_lattice(Pt p) const override { return {p.x / edge, p.y / edge}; }
+  double far_distance() const override { return 0.85; }  // circumradius sqrt(1/2) + 0.1 + slack
   std::pair<long, long> cell_at(Pt q) const override { return {(long)std::floor(q.x), (long)std::floor(q.y)}; }
   Pt center(long i, long j) const override { return {i + 0.5, j + 0.5}; }
   void neighbors(long i, long j, std::vector<std::pair<long, long>>& out) const override {
@@ -279,7 +395,8 @@ struct PairHash {
 // vertex in/on the cell, no ring edge touching a cell edge, the cell centre inside
 // the shell and outside every hole.  Such a cell's chip IS the cell geometry
 // (isCore = coerced.equals(indexGeom), IndexSystem.scala:185).
-bool cell_in_polygon(const std::vector<Pt>& cellb, Pt cc, const Polygon& poly) {
+bool cell_in_polygon(const std::vector<Pt>& cellb, const std::vector<std::vector<Pt>>& pieces, Pt cc,
+                     const Polygon& poly) {
   double cminx = INFINITY, cminy = INFINITY, cmaxx = -INFINITY, cmaxy = -INFINITY;
   for (auto& p : cellb) {
     cminx = std::min(cminx, p.x);
@@ -294,7 +411,8 @@ bool cell_in_polygon(const std::vector<Pt>& cellb, Pt cc, const Polygon& poly) {
         if (std::max(a.x, b.x) < cminx || std::min(a.x, b.x) > cmaxx || std::max(a.y, b.y) < cminy ||
             std::min(a.y, b.y) > cmaxy)
           continue;
-        if (in_convex(cellb, a)) return false;
+        for (auto& pc : pieces)
+          if (in_convex(pc, a)) return false;
         for (size_t k = 0; k + 1 < cellb.size(); k++)
           if (segments_touch(a, b, cellb[k], cellb[k + 1])) return false;
       }
@@ -308,20 +426,20 @@ bool cell_in_polygon(const std::vector<Pt>& cellb, Pt cc, const Polygon& poly) {
   return false;
 }
 
-void tessellate_polygon(const Grid& g, const Polygon& poly, int32_t pid, bool keep_core, std::vector<Chip>& out) {
-  // lattice-space copy of every ring
-  std::vector<std::vector<Pt>> lat_rings;
-  std::vector<const std::vector<Pt>*> geo_rings;
-  for (auto& part : poly.parts)
-    for (auto& ring : part) {
-      std::vector<Pt> lr;
-      for (auto& p : ring) lr.push_back(g.to_lattice(p));
-      lat_rings.push_back(std::move(lr));
-      geo_rings.push_back(&ring);
-    }
-  // 2. border cells: walk every edge in lattice space
-  std::unordered_set<std::pair<long, long>, PairHash> border;
+// `lat_rings`: every ring in the grid's lattice space (densified for H3)
+void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<std::vector<Pt>>& lat_rings, int32_t pid,
+                        bool keep_core, std::vector<Chip>& out) {
+  // 2. border cells: walk every edge in lattice space; per cell the smallest distance
+  // from its centre to a walked sample (samples <= 0.2 apart)
+  std::unordered_map<std::pair<long, long>, float, PairHash> border;
   std::vector<std::pair<long, long>> nb;
+  auto touch = [&](const std::pair<long, long>& c, Pt s) {
+    const Pt cc = g.center(c.first, c.second);
+    const float d = (float)std::hypot(s.x - cc.x, s.y - cc.y);
+    auto it = border.find(c);
+    if (it == border.end()) border.emplace(c, d);
+    else if (d < it->second) it->second = d;
+  };
   for (auto& r : lat_rings)
     for (size_t i = 0; i + 1 < r.size(); i++) {
       Pt a = r[i], b = r[i + 1];
@@ -329,11 +447,12 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, int32_t pid, bool ke
       int steps = std::max(1, (int)std::ceil(len / 0.2));
       for (int s = 0; s <= steps; s++) {
         double t = (double)s / steps;
-        auto c = g.cell_at({a.x + t * (b.x - a.x), a.y + t * (b.y - a.y)});
-        border.insert(c);
+        const Pt q{a.x + t * (b.x - a.x), a.y + t * (b.y - a.y)};
+        auto c = g.cell_at(q);
+        touch(c, q);
         nb.clear();
         g.neighbors(c.first, c.second, nb);
-        for (auto& n : nb) border.insert(n);
+        for (auto& n : nb) touch(n, q);
       }
     }
   // 3. interior cells: even-odd scanline over lattice rows
@@ -361,7 +480,7 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, int32_t pid, bool ke
   }
   for (auto& c : interior) {
     int64_t id = g.cell_id(c.first, c.second);
-    if (!id) continue;
+    if (!id || !g.keep(id, c.first, c.second)) continue;
     Chip ch{id, pid, 1, {}};
     if (keep_core) {
       auto b = g.boundary(c.first, c.second);
@@ -376,11 +495,39 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, int32_t pid, bool ke
     }
     out.push_back(std::move(ch));
   }
-  // 4. border cells: clip
-  std::vector<std::pair<long, long>> bl(border.begin(), border.end());
+  // 4. border cells: clip -- unless the boundary never came near the cell (a ring
+  // neighbour of a walked cell): then it lies wholly inside or outside, decided by its
+  // centre, without its exact geometry
+  std::vector<std::pair<long, long>> bl;
+  bl.reserve(border.size());
+  for (auto& kv : border) bl.push_back(kv.first);
   std::sort(bl.begin(), bl.end());
   for (auto& c : bl) {
+    const int64_t cid = g.cell_id(c.first, c.second);
+    if (!cid || !g.keep(cid, c.first, c.second)) continue;
+    if (border[c] > g.far_distance()) {
+      const Pt cc = g.center(c.first, c.second);
+      bool in = false;
+      for (auto& r : lat_rings)
+        if (point_in_ring(r, cc)) in = !in;
+      if (!in) continue;
+      Chip ch{cid, pid, 1, {}};
+      if (keep_core) {
+        auto b = g.boundary(c.first, c.second);
+        std::vector<mgpu::wkb::Polygon> parts(1);
+        std::vector<double> flat;
+        for (auto& p : b) {
+          flat.push_back(p.x);
+          flat.push_back(p.y);
+        }
+        parts[0].push_back(flat);
+        mgpu::wkb::write_polygons(ch.wkb, parts);
+      }
+      out.push_back(std::move(ch));
+      continue;
+    }
     auto cellb = g.boundary(c.first, c.second);
+    if (cellb.size() < 4) continue;
     double cminx = INFINITY, cminy = INFINITY, cmaxx = -INFINITY, cmaxy = -INFINITY;
     for (auto& p : cellb) {
       cminx = std::min(cminx, p.x);
@@ -396,7 +543,8 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, int32_t pid, bool ke
     }
     cc.x /= (cellb.size() - 1);
     cc.y /= (cellb.size() - 1);
-    if (cell_in_polygon(cellb, cc, poly)) {
+    const auto pieces = convex_pieces(cellb);
+    if (cell_in_polygon(cellb, pieces, cc, poly)) {
       int64_t id = g.cell_id(c.first, c.second);
       if (!id) continue;
       Chip ch{id, pid, 1, {}};
@@ -413,8 +561,12 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, int32_t pid, bool ke
       out.push_back(std::move(ch));
       continue;
     }
+    // (a concave cell is clipped piece by piece: the chip is then a MULTIPOLYGON whose
+    // parts meet along the pieces' diagonals -- the same point set, and PointLocator's
+    // Mod-2 rule puts a point on such a seam in the interior, as for the whole cell)
     std::vector<mgpu::wkb::Polygon> parts;
     double area = 0;
+    for (auto& piece : pieces)
     for (auto& part : poly.parts) {
       mgpu::wkb::Polygon out_part;
       bool shell_ok = false;
@@ -428,7 +580,7 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, int32_t pid, bool ke
           rmaxy = std::max(rmaxy, p.y);
         }
         std::vector<Pt> clipped;
-        if (!(rmaxx < cminx || rminx > cmaxx || rmaxy < cminy || rminy > cmaxy)) clipped = clip_ring(ring, cellb);
+        if (!(rmaxx < cminx || rminx > cmaxx || rmaxy < cminy || rminy > cmaxy)) clipped = clip_ring(ring, piece);
         double a = clipped.empty() ? 0 : std::fabs(ring_area(clipped));
         if (ri == 0) {
           if (a <= 0) break;
@@ -457,21 +609,69 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, int32_t pid, bool ke
   }
 }
 
-int nearest_face(double lon_deg, double lat_deg) {
+// squared chord distances from a point (degrees) to the 20 face centres
+void face_distances(double lon_deg, double lat_deg, double* d) {
   double lat = lat_deg * M_PI / 180.0, lon = lon_deg * M_PI / 180.0;
   double x = cos(lon) * cos(lat), y = sin(lon) * cos(lat), z = sin(lat);
-  int best = 0;
-  double bd = 5;
   for (int f = 0; f < 20; f++) {
     double dx = H3T_FACE_CENTER_POINT[f][0] - x, dy = H3T_FACE_CENTER_POINT[f][1] - y,
            dz = H3T_FACE_CENTER_POINT[f][2] - z;
-    double d = dx * dx + dy * dy + dz * dz;
-    if (d < bd) {
-      bd = d;
-      best = f;
-    }
+    d[f] = dx * dx + dy * dy + dz * dz;
   }
-  return best;
+}
+
+// a ring densified along its lon/lat edges: pieces of at most `step` degrees
+std::vector<Pt> densify(const std::vector<Pt>& r, double step) {
+  std::vector<Pt> o;
+  for (size_t i = 0; i + 1 < r.size(); i++) {
+    const Pt a = r[i], b = r[i + 1];
+    const int n = std::max(1, (int)std::ceil(std::max(std::fabs(b.x - a.x), std::fabs(b.y - a.y)) / step));
+    for (int k = 0; k < n; k++) o.push_back({a.x + (b.x - a.x) * k / n, a.y + (b.y - a.y) * k / n});
+  }
+  if (!r.empty()) o.push_back(r.back());
+  return o;
+}
+
+// H3: every face whose cells can meet the polygon, with the polygon's rings densified
+// (returns false when the polygon is too large for the per-face projection)
+bool h3_faces(const Polygon& poly, int res, std::vector<std::vector<Pt>>& dense, std::vector<int>& faces) {
+  // centre spacing of res-r cells ~ 0.3 / sqrt7^r rad; pieces of a tenth of it
+  double cell = 0.3;
+  for (int i = 0; i < res; i++) cell /= 2.6457513110645906;
+  const double step = std::min(1.0, 0.1 * cell * 180.0 / M_PI);
+  // a cell centred on face g can reach a point p only if g is nearest to some point
+  // within a cell radius (<= 0.25 / sqrt7^r rad) of p; moving p by dt changes a
+  // squared chord distance by <= 2 sin(t) dt, so d_g(p) - d_best(p) < 0.9 / sqrt7^r
+  const double near_edge = 2.5 * cell;
+  int used[20] = {0};  // 2: the nearest face of a vertex, 1: across a nearby face edge
+  double d[20], dmax[20] = {0};
+  for (auto& part : poly.parts)
+    for (auto& ring : part) {
+      dense.push_back(densify(ring, step));
+      for (auto& p : dense.back()) {
+        face_distances(p.x, p.y, d);
+        int best = 0;
+        for (int f = 1; f < 20; f++)
+          if (d[f] < d[best]) best = f;
+        used[best] = 2;
+        for (int f = 0; f < 20; f++) {
+          if (d[f] - d[best] < near_edge && !used[f]) used[f] = 1;
+          dmax[f] = std::max(dmax[f], d[f]);
+        }
+      }
+    }
+  // the gnomonic projection onto a face must stay inside its hemisphere: a face across
+  // an edge that some vertex is > ~84 degrees from is too far to matter; a face that is
+  // some vertex's nearest must project the whole polygon
+  for (int f = 0; f < 20; f++) {
+    if (!used[f]) continue;
+    if (dmax[f] > 1.8) {
+      if (used[f] == 2) return false;
+      continue;
+    }
+    faces.push_back(f);
+  }
+  return true;
 }
 
 }  // namespace
@@ -493,7 +693,7 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
   // polygons are independent: tessellate them in parallel into per-polygon chip lists,
   // then concatenate in input order (the output does not depend on the schedule)
   std::vector<std::vector<Chip>> per(n_polys);
-  std::vector<uint8_t> multi_face(n_polys, 0);
+  std::vector<uint8_t> bad_poly(n_polys, 0);
   mgpu::parallel_for(n_polys, 64, [&](int64_t pb, int64_t pe, int) {
     for (int64_t p = pb; p < pe; p++) {
       Polygon poly;
@@ -511,32 +711,55 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
       }
       if (poly.parts.empty()) continue;
       if (index_system == MGPU_H3) {
-        int face = -1;
-        bool one_face = true;
-        for (auto& part : poly.parts)
-          for (auto& ring : part)
-            for (auto& pt : ring) {
-              int f = nearest_face(pt.x, pt.y);
-              if (face < 0) face = f;
-              else if (f != face) one_face = false;
-            }
-        if (!one_face) {
-          multi_face[p] = 1;
+        std::vector<std::vector<Pt>> dense;
+        std::vector<int> faces;
+        if (!h3_faces(poly, res, dense, faces)) {
+          bad_poly[p] = 1;
           continue;
         }
-        H3Grid g(face, res);
-        tessellate_polygon(g, poly, polygon_id[p], keep_core_geometries != 0, per[p]);
+        for (int face : faces) {
+          H3Grid g(face, res);
+          std::vector<std::vector<Pt>> lat_rings;
+          for (auto& r : dense) {
+            std::vector<Pt> lr;
+            lr.reserve(r.size());
+            for (auto& q : r) lr.push_back(g.to_lattice(q));
+            lat_rings.push_back(std::move(lr));
+          }
+          tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, per[p]);
+          if (g.unsupported) bad_poly[p] = 2;
+        }
+        // a cell reached twice (two lattice positions around a pentagon map to one id):
+        // its chip is computed from the id, so the copies are equal -- keep the first
+        std::unordered_set<int64_t> seen;
+        std::vector<Chip> uniq;
+        uniq.reserve(per[p].size());
+        for (auto& ch : per[p])
+          if (seen.insert(ch.cell).second) uniq.push_back(std::move(ch));
+        per[p].swap(uniq);
       } else {
         BngGrid g(res);
-        tessellate_polygon(g, poly, polygon_id[p], keep_core_geometries != 0, per[p]);
+        std::vector<std::vector<Pt>> lat_rings;
+        for (auto& part : poly.parts)
+          for (auto& ring : part) {
+            std::vector<Pt> lr;
+            for (auto& q : ring) lr.push_back(g.to_lattice(q));
+            lat_rings.push_back(std::move(lr));
+          }
+        tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, per[p]);
       }
     }
   });
-  for (int64_t p = 0; p < n_polys; p++)
-    if (multi_face[p])
-      return mgpu::set_error(MGPU_E_INVALID_ARG,
-                             "tessellate: polygon %d spans several icosahedron faces (not supported by this "
-                             "builder; split it first)", polygon_id[p]);
+  for (int64_t p = 0; p < n_polys; p++) {
+    if (bad_poly[p] == 1)
+      return mgpu::set_error(MGPU_E_UNSUPPORTED,
+                             "tessellate: polygon %d is too large for this builder (more than ~84 degrees from an "
+                             "icosahedron face it touches); split it first", polygon_id[p]);
+    if (bad_poly[p] == 2)
+      return mgpu::set_error(MGPU_E_UNSUPPORTED,
+                             "tessellate: polygon %d meets an H3 cell that crosses the antimeridian or contains a "
+                             "pole (not built here)", polygon_id[p]);
+  }
   mgpu_tess* t = new mgpu_tess();
   size_t total = 0;
   for (auto& v : per) total += v.size();
@@ -577,6 +800,26 @@ int32_t mgpu_tess_result_copy(const mgpu_tess* t, int64_t* cell, int32_t* polygo
 
 int32_t mgpu_tess_destroy(mgpu_tess* t) {
   delete t;
+  return MGPU_OK;
+}
+
+int32_t mgpu_test_h3_boundary_host(const int64_t* cells, int64_t n, double* out_lonlat, int32_t* out_nverts,
+                                   double* out_center) {
+  for (int64_t i = 0; i < n; i++) {
+    const uint64_t h = (uint64_t)cells[i];
+    const int res = (int)((h >> 52) & 15), bc = (int)((h >> 45) & 127);
+    if (((h >> 59) & 15) != 1 || bc >= H3T_NUM_BASE_CELLS || res > 15)
+      return mgpu::set_error(MGPU_E_INVALID_ARG, "h3 boundary: not a cell id");
+    const auto b = mgpu::h3b::cell_boundary(h);
+    out_nverts[i] = (int32_t)b.size();
+    for (size_t v = 0; v < b.size() && v < 10; v++) {
+      out_lonlat[i * 20 + 2 * v] = mgpu::h3b::to_degrees(b[v].lon);
+      out_lonlat[i * 20 + 2 * v + 1] = mgpu::h3b::to_degrees(b[v].lat);
+    }
+    const auto c = mgpu::h3b::cell_center(h);
+    out_center[2 * i] = mgpu::h3b::to_degrees(c.lon);
+    out_center[2 * i + 1] = mgpu::h3b::to_degrees(c.lat);
+  }
   return MGPU_OK;
 }
 

@@ -1,0 +1,170 @@
+"""grid_tessellateexplode across icosahedron faces, and H3 cell geometry (host, no GPU).
+
+Known answers from the reference's own documentation: the MULTIPOLYGON of
+docs/source/api/spatial-indexing.rst:539-552 tessellated at H3 res 0 (8 chips, all
+border, one of them a MULTIPOLYGON) and its grid_polyfill (:216-219, the cells whose
+centre lies in the polygon); the res-9 core chips of NYC taxi zone 1 shown in
+docs/source/usage/kepler.ipynb (cell 23 output).  Invariants on multi-face polygons:
+chips of one cell never repeat, chip areas add up to the polygon's area, and the join
+over the chips equals containment in the original polygons.  The cell geometry
+(h3_boundary.h, h3ToGeoBoundary / h3ToGeo) is checked against geoToH3: every centre
+maps back to its cell, every vertex nudged towards the centre too.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import mosaic_amd as M
+import oracle as O
+from mosaic_amd import _native
+from geom_util import brute_force_pairs, polygons_area, wkb_area, wkt_to_parts
+
+DOC_WKT = "MULTIPOLYGON (((30 20, 45 40, 10 40, 30 20)), ((15 5, 40 10, 10 20, 5 10, 15 5)))"
+DOC_TESSELLATE_RES0 = [577481099093999615, 578044049047420927, 578782920861286399, 577023702256844799,
+                       577938495931154431, 577586652210266111, 577269992861466623, 578360708396220415]
+DOC_MULTIPOLYGON_CHIP = 577586652210266111  # "[01 06 00 ...": the chip meets both parts
+DOC_POLYFILL_RES0 = [577586652210266111, 578360708396220415, 577269992861466623]
+KEPLER_ZONE1_RES9_CORE = [
+    617733150781997055, 617733150856445951, 617733150856970239, 617733150784094207, 617733150843600895,
+    617733150843863039, 617733150844125183, 617733150784880639, 617733150844387327, 617733150844649471,
+    617733150785404927, 617733150844911615, 617733150785667071, 617733150845173759, 617733150785929215,
+    617733150786453503, 617733150846222335, 617733150847270911, 617733150847795199, 617733150848057343]
+
+
+def _P(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def cell_geometry(cells):
+    cells = np.ascontiguousarray(cells, dtype=np.int64)
+    n = len(cells)
+    xy = np.zeros((n, 20))
+    nv = np.zeros(n, np.int32)
+    c = np.zeros((n, 2))
+    _native.check(_native.lib().mgpu_test_h3_boundary_host(_P(cells), n, _P(xy), _P(nv), _P(c)))
+    return xy.reshape(n, 10, 2), nv, c
+
+
+def _wkb(c, i):
+    return bytes(c.wkb[c.wkb_offsets[i]:c.wkb_offsets[i + 1]])
+
+
+def _check_invariants(P, c):
+    for k, pid in enumerate(P.poly_id):
+        rows = np.nonzero(c.polygon_id == pid)[0]
+        assert len(np.unique(c.cell[rows])) == len(rows)
+        area = sum(wkb_area(_wkb(c, i)) for i in rows)
+        assert area == pytest.approx(polygons_area(P, k), rel=1e-9), pid
+
+
+def test_doc_multipolygon_res0():
+    P = M.Polygons.from_lists([(1, wkt_to_parts(DOC_WKT))])
+    c = M.tessellate(P, M.H3IndexSystem(), 0)
+    assert sorted(c.cell.tolist()) == sorted(DOC_TESSELLATE_RES0)
+    assert not c.is_core.any()
+    k = int(np.nonzero(c.cell == DOC_MULTIPOLYGON_CHIP)[0][0])
+    w = _wkb(c, k)
+    assert int.from_bytes(w[1:5], "little" if w[0] == 1 else "big") == 6
+    _check_invariants(P, c)
+    # grid_polyfill: the cells whose centre lies in the polygon
+    _, _, centre = cell_geometry(c.cell)
+    wkb_poly = M.Polygons.from_lists([(1, wkt_to_parts(DOC_WKT))])
+    from geom_util import polygon_set_wkbs
+    (_, w_all), = polygon_set_wkbs(wkb_poly)
+    inside = [int(c.cell[i]) for i in range(len(c)) if O.st_contains(w_all, centre[i, 0], centre[i, 1])]
+    assert sorted(inside) == sorted(DOC_POLYFILL_RES0)
+
+
+@pytest.mark.parametrize("res", [1, 2, 3])
+def test_doc_multipolygon_finer(res):
+    P = M.Polygons.from_lists([(1, wkt_to_parts(DOC_WKT))])
+    c = M.tessellate(P, M.H3IndexSystem(), res)
+    _check_invariants(P, c)
+    # (H3 children are not nested in their parents' boundaries, so no parent invariant)
+    assert len(c) > {1: 20, 2: 100, 3: 500}[res]
+
+
+def test_kepler_zone1_core_chips(nyc_zones):
+    k = int(np.nonzero(nyc_zones.poly_id == 1)[0][0])
+    c = M.tessellate(nyc_zones.select([k]), M.H3IndexSystem(), 9)
+    core = set(c.cell[c.is_core.astype(bool)].tolist())
+    # the reference's core set polyfills the polygon shrunk by a cell radius: a subset of
+    # the cells that lie wholly inside
+    assert set(KEPLER_ZONE1_RES9_CORE) <= core
+
+
+def _star(cx, cy, r0, r1, k, seed):
+    rng = np.random.default_rng(seed)
+    ang = np.sort(rng.uniform(0, 2 * np.pi, k))[::1]
+    rad = rng.uniform(r0, r1, k)
+    shell = [(cx + r * np.cos(a), cy + r * np.sin(a)) for a, r in zip(ang, rad)]
+    shell.append(shell[0])
+    hole = [(cx + 0.1 * r0 * np.cos(a), cy + 0.1 * r0 * np.sin(a)) for a in np.linspace(2 * np.pi, 0, 9)]
+    return [[shell, hole]]
+
+
+def test_multi_face_polygons_join_equals_brute_force():
+    """Polygons across the face 4 / face 9 edge, around an icosahedron vertex (pentagon
+    base cells) and across several faces: invariants at res 2-5, and the join over the
+    chips at res 5 equals containment in the original polygons."""
+    _, _, pent = cell_geometry([(1 << 59) | (bc << 45) | 0x1FFFFFFFFFFF for bc in (14, 24, 38)])
+    P = M.Polygons.from_lists([
+        (1, _star(15.0, 5.0, 2.0, 4.0, 40, 1)),               # across the face 4 / 9 edge
+        (2, _star(pent[0, 0], pent[0, 1], 1.0, 3.0, 30, 2)),  # around a pentagon
+        (3, _star(pent[1, 0], pent[1, 1], 0.5, 2.0, 25, 3)),
+        (4, _star(-40.0, -30.0, 6.0, 12.0, 50, 4)),           # large, several faces
+    ])
+    for res in (2, 3, 4, 5):
+        c = M.tessellate(P, M.H3IndexSystem(), res)
+        _check_invariants(P, c)
+    rng = np.random.default_rng(5)
+    xs, ys = [], []
+    for (cx, cy, r) in [(15.0, 5.0, 4.0), (pent[0, 0], pent[0, 1], 3.0), (pent[1, 0], pent[1, 1], 2.0),
+                        (-40.0, -30.0, 12.0)]:
+        xs.append(rng.uniform(cx - r, cx + r, 4000))
+        ys.append(rng.uniform(cy - r, cy + r, 4000))
+    x, y = np.concatenate(xs), np.concatenate(ys)
+    pts, polys = O.pip_join(0, 5, x, y, c.cell, c.polygon_id, c.is_core, c.wkb_offsets, c.wkb)
+    got = set(zip(pts.tolist(), polys.tolist()))
+    want = brute_force_pairs(P, x, y, O)
+    # chips are cell polygons with straight lon/lat edges; a point between such an edge
+    # and the true (gnomonic) cell border is indexed to the neighbour: vanishingly rare
+    assert len(got ^ want) <= len(want) // 2000, (len(got ^ want), len(want))
+
+
+@pytest.mark.parametrize("res", [0, 1, 2, 3, 5, 8, 11, 15])
+def test_cell_geometry_consistent_with_geo_to_h3(res):
+    rng = np.random.default_rng(40 + res)
+    n = 4000
+    lon = rng.uniform(-180, 180, n)
+    lat = np.degrees(np.arcsin(rng.uniform(-1, 1, n)))
+    cells = np.unique(O.h3_points_to_cells(lon, lat, res))
+    if res <= 1:  # every base cell / all res-1 cells, pentagons included
+        cells = np.unique(np.concatenate([cells, O.h3_points_to_cells(*_sphere_grid(), res)]))
+    xy, nv, centre = cell_geometry(cells)
+    assert np.array_equal(O.h3_points_to_cells(centre[:, 0], centre[:, 1], res), cells)
+    pent = np.array([((int(h) >> 45) & 127) in (4, 14, 24, 38, 49, 58, 63, 72, 83, 97, 107, 117) and
+                     (int(h) & ((1 << (3 * 15)) - 1)) >> (3 * (15 - res)) == 0 for h in cells])
+    if res % 2 == 0:  # Class II: 6 vertices, 5 for pentagons
+        assert np.array_equal(nv, np.where(pent, 5, 6))
+    else:  # Class III: distortion vertices where an edge crosses an icosahedron edge
+        assert (nv[~pent] >= 6).all() and (nv[~pent] <= 8).all() and (nv[pent] == 10).all()
+    bad = tot = 0
+    for k in range(10):
+        m = nv > k
+        v, cc = xy[m, k], centre[m]
+        d = cc - v
+        ok = np.abs(d[:, 0]) < 180  # (antimeridian cells)
+        p = v + 1e-3 * d
+        got = O.h3_points_to_cells(p[:, 0], p[:, 1], res)
+        bad += int(((got != cells[m]) & ok).sum())
+        tot += int(m.sum())
+    # H3's boundary joins its vertices by geodesic-free straight lon/lat edges: near the
+    # poles and for the largest cells a vertex nudged inwards can leave the true region
+    assert bad <= (tot // 200 if res <= 3 else 0), (bad, tot)
+
+
+def _sphere_grid():
+    lon, lat = np.meshgrid(np.linspace(-179.5, 179.5, 360), np.linspace(-89.5, 89.5, 180))
+    return lon.ravel(), lat.ravel()
