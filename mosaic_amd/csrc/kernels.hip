@@ -950,7 +950,10 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 // uniform block takes its class from LDS, the rest load their pixel (and sub-pixel) class.
 // (512 threads: four workgroups -- 32 waves -- share a CU with their LDS tables; the
 // chunk's mixed points are ranked in point order as in split_emit_kernel)
-constexpr int kCfyBlock = 512;
+#ifndef MGPU_CFY_BLOCK
+#define MGPU_CFY_BLOCK 512
+#endif
+constexpr int kCfyBlock = MGPU_CFY_BLOCK;
 constexpr int kCfyItems = kChunk / kCfyBlock;
 #ifndef MGPU_CFY_BATCH
 #define MGPU_CFY_BATCH 4

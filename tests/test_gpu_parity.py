@@ -521,6 +521,25 @@ def test_pip_join_c3_tracts_res10(gpu):
     assert len(np.unique(gp)) == len(gp) and len(gp) > 0.99 * len(x)
 
 
+def test_pip_join_c3_full_table(gpu):
+    """BASELINE config C3 as the bench builds it: all 74,000 tract-like polygons at H3
+    res 10 (9.4M chips, 5.5M of them core, keepCoreGeometries=false -- far beyond the
+    caches), 1.2M points uniform over the whole extent, pair-for-pair against the oracle
+    (exactly one tract per point)."""
+    import bench_workloads as W
+    P = W.tract_polygons()
+    c = M.tessellate(P, M.H3IndexSystem(), 10, keep_core_geometries=False)
+    assert len(c) > 9_000_000 and len(np.unique(c.polygon_id)) == W.N_TRACTS
+    d = c.upload()
+    x, y = W.extent_points(W.TRACT_EXTENT, 1_200_000, 31)
+    r = M.pip_join(T(x, gpu), T(y, gpu), d, 10)
+    gp, gq = r.numpy()
+    with O.h3_libm("cr"):
+        op, oq = O.pip_join(0, 10, x, y, c.cell, c.polygon_id, c.is_core, c.wkb_offsets, c.wkb)
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+    assert len(np.unique(gp)) == len(gp) and len(gp) > 0.99 * len(x)
+
+
 @pytest.mark.parametrize("isys", ["h3", "bng"])
 def test_pip_join_more_than_32_chips_per_cell(gpu, isys):
     """40 nested, overlapping polygons: every cell holds 40 chips, past the 32 the
