@@ -1073,6 +1073,124 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   count_wave(&a.counters[2], any_bad);
 }
 
+// The same classification with one wave per chunk: a lane takes every 64th point of
+// the chunk (item-major, so consecutive lanes read consecutive points), and the chunk's
+// mixed points are ranked in point order by a running wave count plus the item's ballot
+// -- no workgroup barrier per chunk, no LDS scan; the workgroup only shares the LDS copy
+// of the pixel block table.  Waves of a workgroup take chunks blockIdx.x * W + wave,
+// then + gridDim.x * W ...
+#ifndef MGPU_CFY_WAVE
+#define MGPU_CFY_WAVE 1
+#endif
+#ifndef MGPU_CFY_PF
+#define MGPU_CFY_PF 0  // (1: next batch prefetched -- 89 VGPRs, 5 waves/SIMD: C2 +20%)
+#endif
+template <int IS>
+__global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_CFY_WAVES))) void classify_wave_kernel(SplitArgs sa, int64_t n_chunks) {
+  using Code = typename CodeOf<IS>::T;
+  constexpr int kW = kCfyBlock / 64;        // waves per workgroup
+  constexpr int kItems = kChunk / 64;       // points per lane per chunk
+  const JoinArgs& a = sa.j;
+  const ChipTableView& t = a.chips;
+  extern __shared__ uint16_t s_blk[];       // [raster_bny * raster_bnx] (IS == H3)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool use_blk = IS == MGPU_H3 && t.raster_blk != nullptr && a.ablate != 14;
+  if (use_blk) {
+    const uint32_t nb = t.raster_bnx * t.raster_bny;
+    for (uint32_t i = threadIdx.x; i < nb; i += kCfyBlock) s_blk[i] = t.raster_blk[i];
+  }
+  __syncthreads();
+  Code* codes = (Code*)sa.codes;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  bool any_bad = false;
+  const int64_t ch_step = (int64_t)gridDim.x * kW;
+  // batch loads: the next batch's points are requested after this batch's pixel loads,
+  // so the wait for the pixels leaves them in flight (loads retire in order)
+  double bx[kCfyBatch], by[kCfyBatch];
+  auto load_batch = [&](int64_t ch, int b, double* X, double* Y) {
+#pragma unroll
+    for (int k = 0; k < kCfyBatch; k++) {
+      const int64_t p = ch * kChunk + (int64_t)(b + k) * 64 + lane;
+      X[k] = Y[k] = 0.0;
+      if (ch < n_chunks && p < a.n) {
+        X[k] = __builtin_nontemporal_load(&a.x[p]);
+        Y[k] = __builtin_nontemporal_load(&a.y[p]);
+      }
+    }
+  };
+  if (MGPU_CFY_PF) load_batch((int64_t)blockIdx.x * kW + wave, 0, bx, by);
+  for (int64_t ch = (int64_t)blockIdx.x * kW + wave; ch < n_chunks; ch += ch_step) {
+    const int64_t c0 = ch * kChunk;
+    uint32_t pairs = 0, nmixed = 0;  // nmixed: wave-uniform
+    for (int b = 0; b < kItems; b += kCfyBatch) {
+      if (!MGPU_CFY_PF) load_batch(ch, b, bx, by);
+      uint32_t ri[kCfyBatch], gix[kCfyBatch], sb[kCfyBatch], bi[kCfyBatch];
+#pragma unroll
+      for (int k = 0; k < kCfyBatch; k++) {
+        ri[k] = kNoPixel;
+        gix[k] = 0;
+        sb[k] = 0;
+        bi[k] = kNoPixel;
+        const int64_t pk = c0 + (int64_t)(b + k) * 64 + lane;
+        if (pk < a.n && pt_valid(a.valid, a.valid_off, pk)) {
+          bool ok = true;
+          uint32_t g_ = 0, s_ = 0, b_ = kNoPixel;
+          ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &g_, &s_, use_blk ? &b_ : nullptr);
+          gix[k] = g_;
+          sb[k] = s_;
+          bi[k] = b_;
+          any_bad |= !ok;
+        }
+      }
+      uint32_t cl[kCfyBatch];
+      uint64_t ge[kCfyBatch];
+#pragma unroll
+      for (int k = 0; k < kCfyBatch; k++) {
+        cl[k] = ri[k] < kRasterFull ? raster_class_blk(t, s_blk, ri[k], bi[k], sb[k])
+                                    : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
+        ge[k] = (IS == MGPU_BNG && ri[k] < kRasterFull) ? t.grid[gix[k]] : 0ull;
+      }
+      if (MGPU_CFY_PF) {
+        if (b + kCfyBatch < kItems)
+          load_batch(ch, b + kCfyBatch, bx, by);
+        else
+          load_batch(ch + ch_step, 0, bx, by);
+      }
+#pragma unroll
+      for (int k = 0; k < kCfyBatch; k++) {
+        const int64_t p = c0 + (int64_t)(b + k) * 64 + lane;
+        const bool valid = p < a.n;
+        bool mixed = cl[k] == kPixMixed;
+        Code code;
+        if (IS == MGPU_H3) {
+          code = (Code)cl[k];
+          if (!mixed && cl[k] != kPixEmpty) {
+            const uint32_t c = cl[k];
+            pairs += c < t.raster_pc[0] ? 1u : c < t.raster_pc[1] ? 2u : c < t.raster_pc[2] ? 3u : c < t.raster_pc[3] ? 4u
+                     : (uint32_t)__popc((uint32_t)(t.raster_cls[c] >> 32));
+          }
+        } else {
+          const uint32_t first = (uint32_t)ge[k], m = cl[k];
+          if (!mixed && m && !(m < 256u && first < (1u << 24))) mixed = true;
+          code = (Code)(mixed ? kCodeMixed32 : (m ? (first << 8) | m : 0u));
+          if (!mixed) pairs += __popc(m);
+        }
+        if (valid) codes[p] = code;
+        mixed = mixed && valid;
+        const unsigned long long bal = __ballot(mixed);
+        if (mixed) sa.mixed_idx[c0 + nmixed + (uint32_t)__popcll(bal & below)] = (uint16_t)((b + k) * 64 + lane);
+        nmixed += (uint32_t)__popcll(bal);
+      }
+    }
+    pairs = wave_sum_u32(pairs);
+    if (lane == 0) {
+      sa.chunk_pairs[ch] = pairs;
+      sa.chunk_mixed[ch] = nmixed;
+    }
+  }
+  count_wave(&a.counters[2], any_bad);
+}
+
 // the mixed points of one chunk per workgroup, a tile of kTile at a time
 template <int IS>
 __global__ __launch_bounds__(kBlock) MGPU_JOIN_ATTR void pip_mixed_kernel(JoinArgs a) {
@@ -1838,8 +1956,14 @@ template <int IS>
 static void launch_split_t(const SplitArgs& a, hipStream_t s, hipEvent_t after_classify, hipEvent_t after_mixed) {
   const int64_t nc = split_chunks(a.j.n);
   const size_t lds = (IS == MGPU_H3 && a.j.chips.raster_blk) ? (size_t)a.j.chips.raster_bnx * a.j.chips.raster_bny * 2 : 0;
-  const int64_t grid = std::min<int64_t>(nc, (int64_t)resident_blocks((const void*)classify_kernel<IS>, kCfyBlock, lds));
-  hipLaunchKernelGGL(classify_kernel<IS>, dim3((unsigned)grid), dim3(kCfyBlock), lds, s, a, nc);
+  if (MGPU_CFY_WAVE) {
+    const int64_t wg = (nc + kCfyBlock / 64 - 1) / (kCfyBlock / 64);
+    const int64_t grid = std::min<int64_t>(wg, (int64_t)resident_blocks((const void*)classify_wave_kernel<IS>, kCfyBlock, lds));
+    hipLaunchKernelGGL(classify_wave_kernel<IS>, dim3((unsigned)grid), dim3(kCfyBlock), lds, s, a, nc);
+  } else {
+    const int64_t grid = std::min<int64_t>(nc, (int64_t)resident_blocks((const void*)classify_kernel<IS>, kCfyBlock, lds));
+    hipLaunchKernelGGL(classify_kernel<IS>, dim3((unsigned)grid), dim3(kCfyBlock), lds, s, a, nc);
+  }
   if (after_classify) hipEventRecord(after_classify, s);
   hipLaunchKernelGGL(pip_mixed_kernel<IS>, dim3((unsigned)nc), dim3(kBlock), 0, s, a.j);
   const int64_t fix = nc * kChunkTiles < 512 ? nc * kChunkTiles : 512;
