@@ -64,6 +64,7 @@ def parse():
     ap.add_argument("--res", type=int, default=None, help="default: 9 (c2, c5), 10 (c3), 4 (c4)")
     ap.add_argument("--seed", type=int, default=0x20250314)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive measurement")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     return ap.parse_args()
 
@@ -110,6 +111,39 @@ def cpu_baseline(chips, isys, res, wl, seed, target_s):
                       "(C restatement of the reference's cell id + hash join on cell + JTS PointLocator with "
                       "per-candidate WKB re-parse, as its JVM path does), %d threads, %.1f s"
                       % (total_n, isys.name, res, threads, total_t)}
+
+
+def pcie_inclusive(x, y, chips, res, isys, begin, cap, M, reps=3):
+    """The same join with its points starting in (pinned) host memory and its pairs
+    ending there: H2D copy + join + D2H copy of the pairs, on one stream (SURVEY §8d's
+    second number; never `value`)."""
+    dev = x.device
+    hx = torch.empty(x.numel(), dtype=torch.float64, pin_memory=True)
+    hy = torch.empty(y.numel(), dtype=torch.float64, pin_memory=True)
+    hx.copy_(x)
+    hy.copy_(y)
+    hp = torch.empty(cap, dtype=torch.int64, pin_memory=True)
+    hq = torch.empty(cap, dtype=torch.int32, pin_memory=True)
+    dx, dy = torch.empty_like(x), torch.empty_like(y)
+    dp = torch.empty(cap, dtype=torch.int64, device=dev)
+    dq = torch.empty(cap, dtype=torch.int32, device=dev)
+    ts = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        dx.copy_(hx, non_blocking=True)
+        dy.copy_(hy, non_blocking=True)
+        r = M.pip_join(dx, dy, chips, res, index_system=isys, point_id_base=begin, out=(dp, dq), capacity=cap)
+        m = len(r)
+        hp[:m].copy_(dp[:m], non_blocking=True)
+        hq[:m].copy_(dq[:m], non_blocking=True)
+        torch.cuda.synchronize(dev)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts[1:]))
+    n = x.numel()
+    return {"value": n / t, "unit": "points/s", "ms_per_step": t * 1e3,
+            "bytes_over_pcie": 16 * n + 12 * m,
+            "note": "points in pinned host memory, H2D copy + join + D2H copy of the pairs, median of %d" % reps}
 
 
 def workload(a, W, M):
@@ -252,7 +286,13 @@ def main():
     pipeline_ms = float(np.mean(kms))
     stream_ms = float(np.mean(sms))
     split = r.stats["pipeline"] == M._native.MGPU_PIPELINE_SPLIT
-    if split:
+    binned = r.stats["pipeline"] == M._native.MGPU_PIPELINE_BINNED
+    if binned:
+        # the binned pipeline: the dominant kernel is pip_binned_kernel, the
+        # join over the binned points: 16 B read + its 8-byte answer written per point
+        kernel = "pip_binned_kernel<%s>" % isys.name
+        alg_bytes = 24.0 * n
+    elif split:
         # the split pipeline: the dominant kernel is classify_kernel, the one
         # pass over every point: 16 B read + its code (2 B H3 / 4 B BNG) written per point
         kernel = "classify_kernel<%s>" % isys.name
@@ -287,8 +327,9 @@ def main():
                      # the whole call: 16 B per point in, 12 B per (point_id, polygon_id) pair out
                      "pipeline_GBps": (16.0 * n + 12.0 * pairs) / (pipeline_ms * 1e-3) / 1e9,
                      "pipeline_frac": (16.0 * n + 12.0 * pairs) / (pipeline_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
-        "pipeline": "split" if split else "fused",
+        "pipeline": "split" if split else ("binned" if binned else "fused"),
         "kernels_ms": ({"classify": stream_ms, "mixed": float(np.mean(mms)), "emit": float(np.mean(ems))} if split
+                       else {"bin": float(np.mean(mms)), "pip_binned": stream_ms, "emit": float(np.mean(ems))} if binned
                        else {"pip_join": stream_ms, "rest": pipeline_ms - stream_ms}),
         "pairs_per_gpu": pairs,
         "pairs_total": total_pairs,
@@ -302,7 +343,9 @@ def main():
     if os.path.exists(prof):
         try:
             p = json.load(open(prof))
-            if p.get("res") == a.res and p.get("config", "c2") == a.config and p.get("points"):
+            # (only a profile of the kernel this run's pipeline made dominant)
+            same_kernel = p.get("kernel", "pip_join_kernel").split("<")[0] == kernel.split("<")[0]
+            if p.get("res") == a.res and p.get("config", "c2") == a.config and p.get("points") and same_kernel:
                 # measured per launch on p["points"] points of this workload (rocprofv3 PMC
                 # passes, tools/gpu_traffic.sh); scaled to this launch's size if it differs
                 out["roofline"]["traffic"] = p["hbm_bytes_per_launch"] * n / p["points"]
@@ -310,6 +353,8 @@ def main():
                     name, p.get("round", "?"), "" if p["points"] == n else ", measured on %d points, scaled" % p["points"])
         except (ValueError, KeyError):
             pass
+    if rank == 0 and world == 1 and not a.no_pcie:
+        out["pcie_inclusive"] = pcie_inclusive(x, y, chips, a.res, isys, begin, cap, M)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         if table is None:
             table = M.tessellate(zones, isys, a.res, keep_core_geometries=wl.get("keep_core", True))

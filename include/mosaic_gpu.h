@@ -59,16 +59,22 @@ typedef struct mgpu_stats {
     int64_t n_candidates;   /* (point, border chip) PIP evaluations */
     float kernel_ms;        /* device time of the whole call's launches (HIP events) */
     float stream_kernel_ms; /* of which the streaming kernel over all points (pip_join_kernel,
-                               or classify_kernel in the split pipeline) */
-    float mixed_kernel_ms;  /* split pipeline: pip_mixed_kernel + pip_mixed_fix_kernel */
-    float emit_kernel_ms;   /* split pipeline: tile_scan_kernel + split_emit_kernel */
-    int32_t pipeline;       /* MGPU_PIPELINE_FUSED or MGPU_PIPELINE_SPLIT */
+                               classify_kernel in the split pipeline, pip_binned_kernel in
+                               the binned one) */
+    float mixed_kernel_ms;  /* split pipeline: pip_mixed_kernel + pip_mixed_fix_kernel;
+                               binned pipeline: the binning (rank, scan, scatter) */
+    float emit_kernel_ms;   /* split pipeline: tile_scan_kernel + split_emit_kernel;
+                               binned pipeline: fix, count, scan and emit */
+    int32_t pipeline;       /* MGPU_PIPELINE_FUSED, _SPLIT or _BINNED */
     int32_t pad;
 } mgpu_stats;
-/* the join's two pipelines: one fused kernel per tile of points, or -- for a
- * chip table with a pixel index -- classify all points, resolve the mixed ones, emit */
+/* the join's three pipelines: one fused kernel per tile of points; for a chip
+ * table with a pixel index, classify all points, resolve the mixed ones, emit; for a chip
+ * table far larger than the caches, bin the points spatially (counting sort), join the
+ * binned points, gather the answers back in input order */
 #define MGPU_PIPELINE_FUSED 0
 #define MGPU_PIPELINE_SPLIT 1
+#define MGPU_PIPELINE_BINNED 2
 
 const char* mgpu_last_error(void);
 const char* mgpu_version(void);

@@ -45,6 +45,7 @@ MGPU_GEOM_WKT = 1
 MGPU_COMM_ID_BYTES = 128
 MGPU_PIPELINE_FUSED = 0
 MGPU_PIPELINE_SPLIT = 1
+MGPU_PIPELINE_BINNED = 2
 
 
 class MosaicGpuError(RuntimeError):

@@ -1020,6 +1020,7 @@ WsLayout ws_layout(int64_t n_tiles, int64_t pool) {
 
 int32_t ensure_ws(mgpu_ctx* ctx, int64_t n_tiles, int64_t pool = 0) {
   ctx->last.valid = false;  // every call that uses the workspace ends the last join's lifetime
+  ctx->ties_binned = false;
   size_t need = ws_layout(n_tiles, pool).total;
   if (need <= ctx->ws_bytes) return MGPU_OK;
   if (ctx->ws) HIP_TRY(hipFree(ctx->ws));
@@ -1083,6 +1084,7 @@ int32_t mgpu_ctx_destroy(mgpu_ctx* ctx) {
   mgpu_comm_destroy(ctx);
   hipSetDevice(ctx->device);
   if (ctx->split_ws) hipFree(ctx->split_ws);
+  if (ctx->bin_ws) hipFree(ctx->bin_ws);
   if (ctx->ws) hipFree(ctx->ws);
   if (ctx->ev0) hipEventDestroy(ctx->ev0);
   if (ctx->ev1) hipEventDestroy(ctx->ev1);
@@ -1680,6 +1682,52 @@ int32_t mgpu_st_contains(mgpu_ctx* ctx, const mgpu_chips* chips, const int64_t* 
 
 // ------------------------------------------------------------------ join
 
+// The binned pipeline's planner (kernels.h BinArgs): a chip table far larger than the
+// caches and a large batch of points.  MGPU_BIN=0 never, =1 whenever it applies (tests),
+// default: tables of at least MGPU_BIN_MIN_MB (256 MB -- the Infinity Cache) and batches
+// of at least 2^21 points.  The bins tile the chip table's extent (H3: the lon/lat box
+// of the chip cells; BNG: the dense grid's box), about MGPU_BIN_N of them (default 1024),
+// roughly square on the ground.
+static bool plan_bins(const mgpu_chips* chips, int32_t is, int32_t res, int64_t n, const uint8_t* valid,
+                      const mgpu::JoinArgs& a, mgpu::BinArgs& b) {
+  const char* on = getenv("MGPU_BIN");
+  const int mode = on ? atoi(on) : -1;
+  if (mode == 0 || n <= 0 || valid || !a.res_match || a.ablate != 0) return false;
+  if (n >= (int64_t)1 << 32 || chips->view.max_cell_chips > 32) return false;
+  const mgpu::ChipTableView& v = chips->view;
+  double x0, y0, W, H, aspect;
+  if (is == MGPU_H3) {
+    if (v.probe_mode == mgpu::kProbeCellId || !(v.bbox[2] - v.bbox[0] < 360.0) || !(v.bbox[3] - v.bbox[1] < 180.0))
+      return false;
+    x0 = v.bbox[0], y0 = v.bbox[1], W = v.bbox[2] - v.bbox[0], H = v.bbox[3] - v.bbox[1];
+    const double latc = std::min(std::max(std::fabs(v.bbox[1]), std::fabs(v.bbox[3])), 85.0);
+    aspect = W * std::cos(latc * kPi / 180.0) / std::max(H, 1e-12);
+  } else {
+    if (v.probe_mode != mgpu::kProbeDense || res != v.res || v.bng_edge == 0) return false;
+    const mgpu::DenseFace& D = v.dense[0];
+    x0 = (double)D.a0 * v.bng_edge, y0 = (double)D.b0 * v.bng_edge;
+    W = (double)D.w * v.bng_edge, H = (double)D.h * v.bng_edge;
+    aspect = W / std::max(H, 1e-12);
+  }
+  if (!(W > 0) || !(H > 0)) return false;
+  if (mode != 1) {
+    const char* mb = getenv("MGPU_BIN_MIN_MB");
+    const double min_bytes = (mb ? atof(mb) : 256.0) * 1048576.0;
+    if ((double)chips->bytes < min_bytes || n < ((int64_t)1 << 21)) return false;
+  }
+  const char* nbs = getenv("MGPU_BIN_N");
+  const int nb = std::min(std::max(nbs ? atoi(nbs) : 1024, 1), (int)mgpu::bin_max());
+  int nbx = (int)std::lround(std::sqrt(nb * aspect));
+  nbx = std::min(std::max(nbx, 1), nb);
+  const int nby = std::max(nb / nbx, 1);
+  b.x0 = x0, b.y0 = y0;
+  b.nbx = nbx, b.nby = nby;
+  b.inv_bx = nbx / W, b.inv_by = nby / H;
+  const char* xcd = getenv("MGPU_BIN_XCD");
+  b.xcd_runs = xcd ? atoi(xcd) : 1;
+  return true;
+}
+
 static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
                          const double* y, const int64_t* point_id, int64_t id_base, int64_t n, int64_t capacity,
                          int64_t* out_point, int32_t* out_poly, hipStream_t s, bool timed,
@@ -1788,18 +1836,72 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     sa.out_poly = out_poly;
     sa.j = a;
     HIP_TRY(hipMemsetAsync(a.group_cand, 0, nc * 4, s));
-  } else {
+  }
+  mgpu::BinArgs ba{};
+  const bool binned = !split && plan_bins(chips, is, res, n, valid, a, ba);
+  if (binned) {
+    const int64_t nc = mgpu::split_chunks(n), C = mgpu::split_chunk();
+    const int64_t K = mgpu::bin_chunks(n), G = mgpu::bin_groups(n), nb = (int64_t)ba.nbx * ba.nby;
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+      const size_t o = off;
+      off = align_up(off + bytes, 256);
+      return o;
+    };
+    const size_t o_bx = carve((size_t)n * 8), o_by = carve((size_t)n * 8), o_slot = carve((size_t)n * 4),
+                 o_br = carve((size_t)n * 4), o_res = carve((size_t)nc * C * 8), o_cnt = carve((size_t)K * nb * 4),
+                 o_gs = carve((size_t)G * nb * 4), o_pairs = carve(nc * 4), o_off = carve(nc * 8),
+                 o_gperm = carve(nc * 4), o_gcand = carve(nc * 4);
+    if (off > ctx->bin_bytes) {
+      if (ctx->bin_ws) HIP_TRY(hipFree(ctx->bin_ws));
+      ctx->bin_ws = nullptr;
+      ctx->bin_bytes = 0;
+      HIP_TRY(hipMalloc(&ctx->bin_ws, off));
+      ctx->bin_bytes = off;
+    }
+    auto* bb = (uint8_t*)ctx->bin_ws;
+    ba.x = x;
+    ba.y = y;
+    ba.bx = (double*)(bb + o_bx);
+    ba.by = (double*)(bb + o_by);
+    ba.slot = (uint32_t*)(bb + o_slot);
+    ba.binrank = (uint32_t*)(bb + o_br);
+    ba.cnt = (uint32_t*)(bb + o_cnt);
+    ba.gsum = (uint32_t*)(bb + o_gs);
+    mgpu::JoinArgs j = a;
+    j.x = ba.bx;
+    j.y = ba.by;
+    j.mixed_idx = nullptr;
+    j.chunk_mixed = nullptr;
+    j.mixed_res = (uint64_t*)(bb + o_res);
+    j.group_sum = (uint32_t*)(bb + o_gperm);
+    j.group_cand = (uint32_t*)(bb + o_gcand);
+    ba.s.j = j;
+    ba.s.chunk_pairs = (uint32_t*)(bb + o_pairs);
+    ba.s.chunk_off = (uint64_t*)(bb + o_off);
+    ba.s.point_id = point_id;
+    ba.s.id_base = id_base;
+    ba.s.capacity = capacity;
+    ba.s.out_point = out_point;
+    ba.s.out_poly = out_poly;
+    HIP_TRY(hipMemsetAsync(bb + o_gperm, 0, align_up(nc * 4, 256) + nc * 4, s));  // group_sum, group_cand
+    ctx->ties_binned = true;
+  } else if (!split) {
     HIP_TRY(hipMemsetAsync(base + L.gsum, 0, 2 * ((size_t)tiles / 32 + 1) * 4, s));
   }
   if (timed) HIP_TRY(hipEventRecord(ctx->ev0, s));
   if (split)
     HIP_TRY(mgpu::launch_split(is, sa, s, timed ? ctx->ev2 : nullptr, timed ? ctx->ev3 : nullptr));
+  else if (binned)
+    HIP_TRY(mgpu::launch_binned(is, ba, s, timed ? ctx->ev3 : nullptr, timed ? ctx->ev2 : nullptr));
   else
     HIP_TRY(mgpu::launch_join(is, a, e, s, timed ? ctx->ev2 : nullptr));
   if (timed) HIP_TRY(hipEventRecord(ctx->ev1, s));
   auto& L2 = ctx->last;
   L2.split = split;
   L2.sargs = sa;
+  L2.binned = binned;
+  L2.bargs = ba;
   L2.chips = chips;
   L2.is = is;
   L2.res = res;
@@ -1834,6 +1936,30 @@ int32_t mgpu_last_near_ties(mgpu_ctx* ctx, int64_t* out_index, int64_t cap, int6
                                (long long)kTieCap);
   if (n > cap) return fail(MGPU_E_CAPACITY, "%lld near-tie points, capacity %lld", (long long)n, (long long)cap);
   if (n) HIP_TRY(hipMemcpy(out_index, (uint8_t*)ctx->ws + off + 8, (size_t)n * 8, hipMemcpyDeviceToHost));
+  if (n && ctx->ties_binned && ctx->last.binned) {
+    // a binned join queued binned slots: their input positions, by a search over slot[]
+    // (only here, never on the join's path), ascending
+    const mgpu::BinArgs& b = ctx->last.bargs;
+    std::vector<uint32_t> ts(n);
+    for (int64_t k = 0; k < n; k++) ts[k] = (uint32_t)out_index[k];
+    std::sort(ts.begin(), ts.end());
+    ts.erase(std::unique(ts.begin(), ts.end()), ts.end());
+    const int64_t nt = (int64_t)ts.size();
+    uint32_t* dts = nullptr;
+    int64_t* dout = nullptr;
+    HIP_TRY(hipMalloc(&dts, nt * 4));
+    HIP_TRY(hipMalloc(&dout, nt * 8));
+    HIP_TRY(hipMemcpy(dts, ts.data(), nt * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(dout, 0xFF, nt * 8));
+    HIP_TRY(mgpu::launch_bin_unslot(b.slot, b.s.j.n, dts, nt, dout, nullptr));
+    std::vector<int64_t> pos(nt);
+    HIP_TRY(hipMemcpy(pos.data(), dout, nt * 8, hipMemcpyDeviceToHost));
+    hipFree(dts);
+    hipFree(dout);
+    std::sort(pos.begin(), pos.end());
+    for (int64_t k = 0; k < nt; k++) out_index[k] = pos[k];
+    *out_n = nt;
+  }
   return MGPU_OK;
 }
 
@@ -1887,14 +2013,22 @@ static int32_t pip_join_sync(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is,
       hipEventElapsedTime(&m3, ctx->ev0, ctx->ev3);
       stats->mixed_kernel_ms = m3 - ms2;
       stats->emit_kernel_ms = ms - m3;
+    } else if (ctx->last.binned && n > 0) {
+      // ev0 | binning | ev3 | pip_binned_kernel | ev2 | fix, count, scan, emit | ev1
+      float m3 = 0;
+      hipEventElapsedTime(&m3, ctx->ev0, ctx->ev3);
+      stats->mixed_kernel_ms = m3;
+      stats->stream_kernel_ms = ms2 - m3;
+      stats->emit_kernel_ms = ms - ms2;
     }
-    stats->pipeline = ctx->last.split ? MGPU_PIPELINE_SPLIT : MGPU_PIPELINE_FUSED;
+    stats->pipeline = ctx->last.split ? MGPU_PIPELINE_SPLIT
+                      : ctx->last.binned ? MGPU_PIPELINE_BINNED : MGPU_PIPELINE_FUSED;
   }
   // pool records used (counters[5]) within the pool: every record is still in the
   // workspace, so a larger output can be written by mgpu_pip_join_fetch alone (the split
   // pipeline keeps its codes and mixed answers: always)
   ctx->last.total = (int64_t)h[0];
-  ctx->last.pool_ok = ctx->last.split || (int64_t)h[5] <= capacity + ctx->last.n_tiles * mgpu::join_pend_cap();
+  ctx->last.pool_ok = ctx->last.split || ctx->last.binned || (int64_t)h[5] <= capacity + ctx->last.n_tiles * mgpu::join_pend_cap();
   if (h[2]) {
     ctx->last.valid = false;
     if (is == MGPU_BNG) return fail(MGPU_E_NAN, "NaN coordinates are not supported. (%llu points)", h[2]);
@@ -1933,6 +2067,15 @@ int32_t mgpu_pip_join_fetch(mgpu_ctx* ctx, int64_t capacity, int64_t* out_n_pair
     return pip_join_sync(ctx, c.chips, c.is, c.res, c.x, c.y, c.point_id, c.id_base, c.n, capacity,
                          out_n_pairs ? out_n_pairs : &cnt, out_point_id, out_polygon_id, stream, nullptr, c.pts_valid,
                          c.pts_valid_off);
+  }
+  if (L.binned) {
+    mgpu::BinArgs ba = L.bargs;
+    ba.s.capacity = capacity;
+    ba.s.out_point = out_point_id;
+    ba.s.out_poly = out_polygon_id;
+    HIP_TRY(mgpu::launch_bin_emit(ba, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return MGPU_OK;
   }
   if (L.split) {
     mgpu::SplitArgs sa = L.sargs;

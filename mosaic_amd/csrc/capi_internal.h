@@ -17,6 +17,11 @@ struct mgpu_ctx {
   // the split pipeline's per-point buffers (codes, mixed lists and answers), grown on demand
   void* split_ws = nullptr;
   size_t split_bytes = 0;
+  // the binned pipeline's per-point buffers (binned copies, slots, answers), grown on demand
+  void* bin_ws = nullptr;
+  size_t bin_bytes = 0;
+  // the near-tie queue holds binned slots (a binned join was the last workspace user)
+  bool ties_binned = false;
   // scratch of the geometry / Arrow entries (decoded points, validity bitmaps), grown on demand
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -35,6 +40,8 @@ struct mgpu_ctx {
     int64_t n_tiles = 0;
     bool split = false;
     mgpu::SplitArgs sargs{};
+    bool binned = false;
+    mgpu::BinArgs bargs{};
   } last;
 };
 

@@ -68,6 +68,44 @@ int64_t split_chunks(int64_t n);
 hipError_t launch_split(int is, const SplitArgs& a, hipStream_t s, hipEvent_t after_classify, hipEvent_t after_mixed);
 hipError_t launch_split_emit(int is, const SplitArgs& a, hipStream_t s);
 
+// The binned pipeline (a chip table far larger than the caches): the points
+// are counting-sorted by a coarse spatial bin so that the join walks the chip table bin
+// by bin instead of at random, then the answers are gathered back into input order.
+//   bin_rank_kernel     per chunk of bin_chunk() points: bin of each point, its rank among
+//                       the chunk's points of that bin (LDS atomics), the chunk's bin counts
+//   bin_colscan_kernel  + bin_base_kernel: counts -> run offsets (bin-major, chunk-minor)
+//   bin_scatter_kernel  x, y -> their binned slots; slot[i] kept for the gather
+//   pip_binned_kernel   join_tile's phases over the binned points, tiles dealt to the XCDs
+//                       in contiguous runs (one bin's chips stay in one L2); answers
+//                       (first chip | match mask << 32) per slot in j.mixed_res
+//                       (+ pip_mixed_fix_kernel for the tiles holding an H3 near-tie)
+//   bin_count_kernel    pairs per input chunk of split_chunk() points (gathered answers)
+//   tile_scan_kernel    -> output offsets;  bin_emit_kernel: ordered pairs
+struct BinArgs {
+  SplitArgs s;                      // s.j: the BINNED points (x, y = the binned copies),
+                                    // mixed_idx = chunk_mixed = null; s.chunk_pairs / chunk_off:
+                                    // per INPUT chunk; s.j.group_sum / group_cand: per binned chunk
+  const double* x;                  // the input points
+  const double* y;
+  double* bx;                       // [n] binned copies
+  double* by;
+  uint32_t* slot;                   // [n] binned slot of input point i
+  uint32_t* binrank;                // [n] rank << 16 | bin
+  uint32_t* cnt;                    // [bin chunks * nb] counts, then in-group prefixes
+  uint32_t* gsum;                   // [bin groups * nb] group sums, then group bases
+  double x0, y0, inv_bx, inv_by;    // the bin grid over the chip table's extent
+  int32_t nbx, nby;                 // nbx * nby <= bin_max()
+  int32_t xcd_runs;                 // deal each XCD a contiguous run of binned tiles (MGPU_BIN_XCD)
+};
+int64_t bin_chunk();
+int64_t bin_chunks(int64_t n);
+int64_t bin_groups(int64_t n);
+int32_t bin_max();
+hipError_t launch_binned(int is, const BinArgs& a, hipStream_t s, hipEvent_t after_bin, hipEvent_t after_join);
+hipError_t launch_bin_emit(const BinArgs& a, hipStream_t s);
+// input positions of the binned slots ts[0 .. nt) (ascending): out[k] = i with slot[i] == ts[k]
+hipError_t launch_bin_unslot(const uint32_t* slot, int64_t n, const uint32_t* ts, int64_t nt, int64_t* out, hipStream_t s);
+
 // pair_emit_kernel: tile records -> ordered (point_id, polygon_id) output
 struct EmitArgs {
   const uint32_t* tile_count;       // records of each tile

@@ -130,6 +130,12 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -385,11 +391,15 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   const int64_t lbase = gbase + (int64_t)(tile % kChunkTiles) * kGTile;  // first list position
   uint32_t gcount = 0;
   if (G) {
-    const uint32_t nm = a.chunk_mixed[chunk], t0 = (tile % kChunkTiles) * kGTile;
+    // (the binned pipeline: no mixed list -- every point of the chunk, in order)
+    const bool listed = a.mixed_idx != nullptr;
+    const int64_t left = a.n - gbase;
+    const uint32_t nm = listed ? a.chunk_mixed[chunk] : (uint32_t)(left <= 0 ? 0 : (left < kChunk ? left : kChunk));
+    const uint32_t t0 = (tile % kChunkTiles) * kGTile;
     if (nm <= t0) return;
     gcount = nm - t0 < (uint32_t)kGTile ? nm - t0 : (uint32_t)kGTile;
     for (uint32_t li = threadIdx.x; li < (uint32_t)kTile; li += kBlock)
-      s_gidx[li] = li < gcount ? a.mixed_idx[lbase + li] : (uint16_t)0;
+      s_gidx[li] = li < gcount ? (listed ? a.mixed_idx[lbase + li] : (uint16_t)(t0 + li)) : (uint16_t)0;
   }
 #define MGPU_PT(li) (G ? gbase + (int64_t)s_gidx[li] : (int64_t)tile * kTile + (li))
 #define MGPU_VALID(li) (G ? (uint32_t)(li) < gcount : (int64_t)tile * kTile + (li) < a.n)
@@ -410,6 +420,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   MGPU_STAMP(0);
   // ---- phase 1: cells, core matches, candidates
   bool any_tie = false, any_bad = false;
+  uint32_t n_tie_pts = 0;  // (SLOW: the lane's near-tie points, mgpu_stats.n_near_ties)
 #ifndef MGPU_NT_POINTS
 #define MGPU_NT_POINTS 1
 #endif
@@ -563,6 +574,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
           uint32_t gi;
           r = chip_probe<IS, SLOW>(t, px, py, a.res, res_match, &ok, &tie, a.ablate, &gi);
           if (gi != kNoEntry) r = grid_range(t.grid[gi]);
+          n_tie_pts += (SLOW && tie) ? 1u : 0u;
           if (SLOW && tie && a.ties) {  // the audit list of mgpu_last_near_ties
             const unsigned long long q = atomicAdd(&a.ties[0], 1ull);
             if ((int64_t)q < a.tie_cap) a.ties[1 + q] = (unsigned long long)p;
@@ -575,7 +587,10 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     }
   }
   count_wave(&a.counters[2], any_bad);
-  if (SLOW) count_wave(&a.counters[1], any_tie);
+  if (SLOW) {
+    const uint32_t wt = wave_sum_u32(n_tie_pts);
+    if ((threadIdx.x & 63) == 0 && wt) atomicAdd(&a.counters[1], (unsigned long long)wt);
+  }
   if (!SLOW && __syncthreads_or(any_tie)) {
     // a near-tie (or a case only the fix kernel handles): the tile is redone there
     if (threadIdx.x == 0) {
@@ -939,11 +954,6 @@ struct CodeOf<MGPU_BNG> {
   using T = uint32_t;  // BNG: first chip << 8 | match mask (0: none, ~0: mixed)
 };
 
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
-}
 
 // Persistent: each workgroup copies the pixel block table (chip_table.h raster_blk) into
 // LDS once, then classifies chunks blockIdx.x, blockIdx.x + gridDim.x, ...; a point in a
@@ -1828,6 +1838,263 @@ hipError_t launch_format_cells(int is, const int64_t* cells, int64_t n, char* ou
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- binned pipeline
+// (kernels.h BinArgs).  With a chip table far beyond the caches (C3: 9.4M chips, 1.2 GB
+// of border-chip headers, a 60 MB lattice grid) a uniform point stream makes every point
+// fetch its own random grid line and, per candidate, two random header lines -- 8-16x
+// the algorithmic bytes.  A counting sort of the points by a coarse spatial bin (one
+// histogram pass, one scatter pass: no full sort, the order inside a bin is irrelevant)
+// lets the join walk the table bin by bin: the tiles of a bin run on one XCD and share
+// its chips in that XCD's L2.  The answers are per binned slot; the emit gathers them
+// back in input order (a chunk's slots fall in one short run per bin).
+constexpr int kBinBlock = 1024;
+constexpr int kBinChunk = 65536;                  // points per rank / scatter workgroup
+constexpr int kBinItems = kBinChunk / kBinBlock;  // per thread
+constexpr int kBinMax = 4096;                     // bins
+constexpr int kBinGroup = 64;                     // chunk rows per first-level column scan
+constexpr int kBinBatch = 8;                      // point loads in flight per thread
+static_assert(kBinChunk <= 65536 && kBinMax <= 65536, "rank << 16 | bin");
+static_assert(kBinMax % 1024 == 0, "bin_base_kernel: whole bins per thread");
+
+__device__ __forceinline__ uint32_t bin_of(const BinArgs& b, double x, double y) {
+  // NaN and points outside the extent clamp to an edge bin (the bin only orders the work)
+  const double fx = (x - b.x0) * b.inv_bx, fy = (y - b.y0) * b.inv_by;
+  const int ix = fx >= 0.0 ? (fx < (double)b.nbx ? (int)fx : b.nbx - 1) : 0;
+  const int iy = fy >= 0.0 ? (fy < (double)b.nby ? (int)fy : b.nby - 1) : 0;
+  // boustrophedon rows: consecutive bins are neighbours
+  return (uint32_t)(iy * b.nbx + ((iy & 1) ? b.nbx - 1 - ix : ix));
+}
+
+// per chunk: each point's bin and its rank among the chunk's points of that bin (LDS
+// atomics: the order inside a bin is arbitrary, slot[i] records where each point went),
+// and the chunk's row of bin counts
+__global__ __launch_bounds__(kBinBlock) void bin_rank_kernel(BinArgs b) {
+  __shared__ uint32_t s_h[kBinMax];
+  const int nb = b.nbx * b.nby;
+  for (int i = threadIdx.x; i < nb; i += kBinBlock) s_h[i] = 0;
+  __syncthreads();
+  const int64_t n = b.s.j.n, c0 = (int64_t)blockIdx.x * kBinChunk;
+  for (int k0 = 0; k0 < kBinItems; k0 += kBinBatch) {
+    double px[kBinBatch], py[kBinBatch];
+#pragma unroll
+    for (int k = 0; k < kBinBatch; k++) {
+      const int64_t p = c0 + (int64_t)(k0 + k) * kBinBlock + threadIdx.x;
+      px[k] = py[k] = 0.0;
+      if (p < n) {
+        px[k] = __builtin_nontemporal_load(&b.x[p]);
+        py[k] = __builtin_nontemporal_load(&b.y[p]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kBinBatch; k++) {
+      const int64_t p = c0 + (int64_t)(k0 + k) * kBinBlock + threadIdx.x;
+      if (p < n) {
+        const uint32_t bi = bin_of(b, px[k], py[k]);
+        const uint32_t r = atomicAdd(&s_h[bi], 1u);
+        b.binrank[p] = r << 16 | bi;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb; i += kBinBlock) b.cnt[(int64_t)blockIdx.x * nb + i] = s_h[i];
+}
+
+// cnt[chunk][bin] -> its exclusive prefix over the chunks of its group of kBinGroup;
+// gsum[group][bin] = the group's sum
+__global__ __launch_bounds__(256) void bin_colscan_kernel(BinArgs b, int64_t n_chunks) {
+  const int nb = b.nbx * b.nby;
+  const int bin = blockIdx.x * 256 + threadIdx.x;
+  if (bin >= nb) return;
+  const int64_t k0 = (int64_t)blockIdx.y * kBinGroup;
+  uint32_t v[kBinGroup];
+#pragma unroll
+  for (int k = 0; k < kBinGroup; k++) v[k] = k0 + k < n_chunks ? b.cnt[(k0 + k) * nb + bin] : 0u;
+  uint32_t run = 0;
+#pragma unroll
+  for (int k = 0; k < kBinGroup; k++) {
+    if (k0 + k < n_chunks) b.cnt[(k0 + k) * nb + bin] = run;
+    run += v[k];
+  }
+  b.gsum[(int64_t)blockIdx.y * nb + bin] = run;
+}
+
+// one workgroup: each bin's total, the bins' exclusive scan (slots are bin-major), then
+// gsum[group][bin] = the first slot of the bin's points of that group of chunks
+__global__ __launch_bounds__(1024) void bin_base_kernel(BinArgs b, int64_t n_groups) {
+  __shared__ uint32_t s_w[16];
+  constexpr int kPer = kBinMax / 1024;
+  const int nb = b.nbx * b.nby;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t mine = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const int bin = threadIdx.x * kPer + k;
+    if (bin < nb)
+      for (int64_t g = 0; g < n_groups; g++) mine += b.gsum[g * nb + bin];
+  }
+  const uint32_t incl = wave_incl_scan(mine);
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  uint32_t run = incl - mine;
+  for (int w = 0; w < wave; w++) run += s_w[w];
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const int bin = threadIdx.x * kPer + k;
+    if (bin < nb)
+      for (int64_t g = 0; g < n_groups; g++) {
+        const uint32_t v = b.gsum[g * nb + bin];
+        b.gsum[g * nb + bin] = run;
+        run += v;
+      }
+  }
+}
+
+// x, y -> their slots (bin run base + rank); slot[i] kept for the gather
+__global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
+  __shared__ uint32_t s_off[kBinMax];
+  const int nb = b.nbx * b.nby;
+  const int64_t k = blockIdx.x, g = k / kBinGroup;
+  for (int i = threadIdx.x; i < nb; i += kBinBlock) s_off[i] = b.gsum[g * nb + i] + b.cnt[k * nb + i];
+  __syncthreads();
+  const int64_t n = b.s.j.n, c0 = k * kBinChunk;
+  for (int k0 = 0; k0 < kBinItems; k0 += kBinBatch) {
+    double px[kBinBatch], py[kBinBatch];
+    uint32_t br[kBinBatch];
+#pragma unroll
+    for (int q = 0; q < kBinBatch; q++) {
+      const int64_t p = c0 + (int64_t)(k0 + q) * kBinBlock + threadIdx.x;
+      px[q] = py[q] = 0.0;
+      br[q] = 0;
+      if (p < n) {
+        px[q] = __builtin_nontemporal_load(&b.x[p]);
+        py[q] = __builtin_nontemporal_load(&b.y[p]);
+        br[q] = __builtin_nontemporal_load(&b.binrank[p]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kBinBatch; q++) {
+      const int64_t p = c0 + (int64_t)(k0 + q) * kBinBlock + threadIdx.x;
+      if (p < n) {
+        const uint32_t sl = s_off[br[q] & 0xFFFFu] + (br[q] >> 16);
+        b.bx[sl] = px[q];
+        b.by[sl] = py[q];
+        b.slot[p] = sl;
+      }
+    }
+  }
+}
+
+// the join over the binned points: join_tile's phases (G mode, no mixed list: every
+// point of the chunk), the answers per slot in mixed_res.  xcd_runs: block b runs tile
+// (b % 8) * per_xcd + b / 8 -- blocks b and b + 8 share an XCD, so each XCD walks one
+// contiguous run of tiles (= of bins) and a bin's chips are fetched into one L2
+template <int IS>
+__global__ __launch_bounds__(kBlock) MGPU_JOIN_ATTR void pip_binned_kernel(JoinArgs a, uint32_t per_xcd, uint32_t n_tiles) {
+  const uint32_t tile = per_xcd ? (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3) : blockIdx.x;
+  if (tile < n_tiles) join_tile<IS, false, true>(a, tile);
+}
+
+// the answers of input points p0 .. p0 + 15 (their slots in 16-byte loads)
+constexpr int kBinEmitItems = kChunk / kClsBlock;
+static_assert(kBinEmitItems == 16, "four 16-byte slot loads per thread");
+__device__ __forceinline__ void bin_gather(const BinArgs& b, int64_t p0, uint64_t* v) {
+  const int64_t n = b.s.j.n;
+  uint32_t sl[kBinEmitItems];
+  if (p0 + kBinEmitItems <= n) {
+    const uint4* src = (const uint4*)(b.slot + p0);
+#pragma unroll
+    for (int i = 0; i < kBinEmitItems / 4; i++) {
+      const uint4 q = src[i];
+      sl[4 * i] = q.x, sl[4 * i + 1] = q.y, sl[4 * i + 2] = q.z, sl[4 * i + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kBinEmitItems; k++) sl[k] = p0 + k < n ? b.slot[p0 + k] : 0xFFFFFFFFu;
+  }
+#pragma unroll
+  for (int k = 0; k < kBinEmitItems; k++) v[k] = sl[k] != 0xFFFFFFFFu ? b.s.j.mixed_res[sl[k]] : 0ull;
+}
+
+// pairs of each input chunk of kChunk points
+__global__ __launch_bounds__(kClsBlock) void bin_count_kernel(BinArgs b) {
+  __shared__ uint32_t s_w[kClsBlock / 64];
+  uint64_t v[kBinEmitItems];
+  bin_gather(b, (int64_t)blockIdx.x * kChunk + (int64_t)threadIdx.x * kBinEmitItems, v);
+  uint32_t np = 0;
+#pragma unroll
+  for (int k = 0; k < kBinEmitItems; k++) np += __popc((uint32_t)(v[k] >> 32));
+  np = wave_sum_u32(np);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = np;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int w = 0; w < kClsBlock / 64; w++) tot += s_w[w];
+    b.s.chunk_pairs[blockIdx.x] = tot;
+  }
+}
+
+// ordered output of one input chunk (as split_emit_kernel: the chunk's pairs are one
+// contiguous range, staged in LDS a window at a time, written by consecutive lanes)
+__global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_EMIT_WAVES))) void bin_emit_kernel(BinArgs b) {
+  const SplitArgs& sa = b.s;
+  const ChipTableView& t = sa.j.chips;
+  __shared__ uint32_t s_w[kClsBlock / 64];
+  __shared__ uint32_t s_poly[kEmitWin];
+  __shared__ uint16_t s_pt[kEmitWin];
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  const int l0 = threadIdx.x * kBinEmitItems;
+  uint64_t v[kBinEmitItems];
+  bin_gather(b, c0 + l0, v);
+  uint32_t npair = 0;
+#pragma unroll
+  for (int k = 0; k < kBinEmitItems; k++) npair += __popc((uint32_t)(v[k] >> 32));
+  uint32_t total;
+  const uint32_t off0 = chunk_excl_scan(npair, s_w, &total);
+  const uint64_t base = sa.chunk_off[blockIdx.x];
+  for (uint32_t w0 = 0; w0 < total; w0 += kEmitWin) {
+    if (off0 < w0 + kEmitWin && off0 + npair > w0) {
+      uint32_t q = off0;
+#pragma unroll
+      for (int k = 0; k < kBinEmitItems; k++) {
+        const uint32_t first = (uint32_t)v[k];
+        for (uint32_t m = (uint32_t)(v[k] >> 32); m; m &= m - 1, q++)
+          if (q >= w0 && q < w0 + kEmitWin) {
+            s_poly[q - w0] = (uint32_t)t.chip_poly[first + __builtin_ctz(m)];
+            s_pt[q - w0] = (uint16_t)(l0 + k);
+          }
+      }
+    }
+    __syncthreads();
+    const uint32_t cnt = total - w0 < (uint32_t)kEmitWin ? total - w0 : (uint32_t)kEmitWin;
+    for (uint32_t i = threadIdx.x; i < cnt; i += kClsBlock) {
+      const uint64_t q = base + w0 + i;
+      if ((int64_t)q >= sa.capacity) break;
+      const int64_t p = c0 + s_pt[i];
+      sa.out_point[q] = sa.point_id ? sa.point_id[p] : sa.id_base + p;
+      sa.out_poly[q] = (int32_t)s_poly[i];
+    }
+    __syncthreads();
+  }
+}
+
+// input positions of a few binned slots (the near-tie audit list of a binned join)
+__global__ __launch_bounds__(256) void bin_unslot_kernel(const uint32_t* __restrict__ slot, int64_t n,
+                                                         const uint32_t* __restrict__ ts, int64_t nt,
+                                                         int64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint32_t s = slot[i];
+    int64_t lo = 0, hi = nt;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (ts[mid] < s)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    if (lo < nt && ts[lo] == s) out[lo] = i;
+  }
+}
+
 // ---------------------------------------------------------------- launchers
 
 hipError_t launch_cells(int is, int res, const double* x, const double* y, int64_t n, int64_t* out,
@@ -1991,6 +2258,56 @@ hipError_t launch_split_emit(int is, const SplitArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(split_emit_kernel<MGPU_H3>, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
   else
     hipLaunchKernelGGL(split_emit_kernel<MGPU_BNG>, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+int64_t bin_chunk() { return kBinChunk; }
+int64_t bin_chunks(int64_t n) { return (n + kBinChunk - 1) / kBinChunk; }
+int64_t bin_groups(int64_t n) { return (bin_chunks(n) + kBinGroup - 1) / kBinGroup; }
+int32_t bin_max() { return kBinMax; }
+
+template <int IS>
+static void launch_binned_t(const BinArgs& a, hipStream_t s, hipEvent_t after_bin, hipEvent_t after_join) {
+  const int64_t n = a.s.j.n, K = bin_chunks(n), G = bin_groups(n), nb = (int64_t)a.nbx * a.nby;
+  hipLaunchKernelGGL(bin_rank_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
+  hipLaunchKernelGGL(bin_colscan_kernel, dim3((unsigned)((nb + 255) / 256), (unsigned)G), dim3(256), 0, s, a, K);
+  hipLaunchKernelGGL(bin_base_kernel, dim3(1), dim3(1024), 0, s, a, G);
+  hipLaunchKernelGGL(bin_scatter_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
+  if (after_bin) hipEventRecord(after_bin, s);
+  const int64_t nc = split_chunks(n), tiles = nc * kChunkTiles;
+  const uint32_t per = a.xcd_runs ? (uint32_t)((tiles + 7) / 8) : 0u;
+  const int64_t grid = per ? 8 * (int64_t)per : tiles;
+  hipLaunchKernelGGL(pip_binned_kernel<IS>, dim3((unsigned)grid), dim3(kBlock), 0, s, a.s.j, per, (uint32_t)tiles);
+  if (after_join) hipEventRecord(after_join, s);
+  const int64_t fix = tiles < 512 ? tiles : 512;
+  hipLaunchKernelGGL(pip_mixed_fix_kernel<IS>, dim3((unsigned)fix), dim3(kBlock), 0, s, a.s.j);
+  hipLaunchKernelGGL(bin_count_kernel, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.s.chunk_pairs, a.s.j.group_cand, nc,
+                     a.s.chunk_off, a.s.j.counters);
+  hipLaunchKernelGGL(bin_emit_kernel, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
+}
+
+hipError_t launch_binned(int is, const BinArgs& a, hipStream_t s, hipEvent_t after_bin, hipEvent_t after_join) {
+  if (a.s.j.n <= 0) return hipSuccess;
+  if (a.nbx < 1 || a.nby < 1 || (int64_t)a.nbx * a.nby > kBinMax) return hipErrorInvalidValue;
+  if (is == MGPU_H3)
+    launch_binned_t<MGPU_H3>(a, s, after_bin, after_join);
+  else
+    launch_binned_t<MGPU_BNG>(a, s, after_bin, after_join);
+  return hipGetLastError();
+}
+
+// only the ordered output of a binned join already computed (mgpu_pip_join_fetch)
+hipError_t launch_bin_emit(const BinArgs& a, hipStream_t s) {
+  if (a.s.j.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bin_emit_kernel, dim3((unsigned)split_chunks(a.s.j.n)), dim3(kClsBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_bin_unslot(const uint32_t* slot, int64_t n, const uint32_t* ts, int64_t nt, int64_t* out, hipStream_t s) {
+  if (n <= 0 || nt <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(bin_unslot_kernel, dim3((unsigned)blocks), dim3(256), 0, s, slot, n, ts, nt, out);
   return hipGetLastError();
 }
 

@@ -1,0 +1,167 @@
+"""The binned join pipeline (spatial counting sort of the points, join over
+the binned points, answers gathered back into input order) against the oracle, through
+the C ABI.  MGPU_BIN=1 forces it on tables of any size (the planner's default takes it
+only for tables beyond the Infinity Cache, e.g. C3); MGPU_SPLIT=0 keeps the split
+pipeline of pixel-indexed tables out of the way.  Bit-exact is the bar, as everywhere."""
+import contextlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import mosaic_amd as M
+import oracle as O
+from geom_util import nyc_points
+from test_gpu_parity import T, adversarial_points, oracle_join, oracle_join_cr
+
+pytestmark = pytest.mark.gpu
+BINNED = 2  # MGPU_PIPELINE_BINNED
+
+
+@contextlib.contextmanager
+def env(**kw):
+    old = {k: os.environ.get(k) for k in kw}
+    os.environ.update({k: str(v) for k, v in kw.items()})
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def binned_join(x, y, chips, res, gpu, nb=1024, xcd=1, **kw):
+    with env(MGPU_BIN=1, MGPU_SPLIT=0, MGPU_BIN_N=nb, MGPU_BIN_XCD=xcd):
+        r = M.pip_join(T(x, gpu), T(y, gpu), chips, res, **kw)
+    assert r.stats["pipeline"] == BINNED
+    return r
+
+
+@pytest.mark.parametrize("nb,xcd", [(1, 1), (64, 0), (1024, 1), (4096, 1)])
+def test_binned_nyc_equals_oracle(gpu, nyc_chips_r9, nb, xcd):
+    """NYC zones, H3 res 9, ragged sizes (not a multiple of any chunk or tile)."""
+    d = nyc_chips_r9.upload()
+    x, y = nyc_points(1_234_567, 41)
+    r = binned_join(x, y, d, 9, gpu, nb=nb, xcd=xcd)
+    gp, gq = r.numpy()
+    op, oq = oracle_join(nyc_chips_r9, x, y)
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+    assert r.stats["n_pairs"] == len(op) and r.stats["n_candidates"] > 0
+
+
+@pytest.mark.parametrize("n", [1, 7, 4095, 4097, 65537])
+def test_binned_small_batches(gpu, nyc_chips_r9, n):
+    d = nyc_chips_r9.upload()
+    x, y = nyc_points(n, 42 + n)
+    gp, gq = binned_join(x, y, d, 9, gpu).numpy()
+    op, oq = oracle_join(nyc_chips_r9, x, y)
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+
+
+def test_binned_point_ids_capacity_and_fetch(gpu, nyc_chips_r9):
+    """Explicit point ids, an id base, and a capacity overflow answered by
+    mgpu_pip_join_fetch from the kept answers (no second join)."""
+    d = nyc_chips_r9.upload()
+    x, y = nyc_points(300_000, 43)
+    op, oq = oracle_join(nyc_chips_r9, x, y)
+    ids = np.arange(300_000, dtype=np.int64) * 5 + 3
+    gp, gq = binned_join(x, y, d, 9, gpu, point_id=torch.from_numpy(ids).to(gpu)).numpy()
+    assert np.array_equal(gp, ids[op]) and np.array_equal(gq, oq)
+    gp, gq = binned_join(x, y, d, 9, gpu, point_id_base=10 ** 11).numpy()
+    assert np.array_equal(gp, op + 10 ** 11) and np.array_equal(gq, oq)
+    r = binned_join(x, y, d, 9, gpu, capacity=None)  # default capacity n + n/8 suffices here
+    assert np.array_equal(r.numpy()[0], op)
+    with pytest.raises(M.CapacityError) as ei:
+        binned_join(x, y, d, 9, gpu, capacity=100)
+    assert ei.value.required == len(op)
+
+
+def test_binned_overlapping_polygons(gpu):
+    """Five overlapping squares: 5 pairs per point (more than the default capacity), the
+    per-point answer masks carry every match in polygon order."""
+    sq = [(0.0, 0.0), (1.0, 0.0), (1.0, 1.0), (0.0, 1.0), (0.0, 0.0)]
+    bx, by, sc = -74.0, 40.7, 0.05
+    polys = [(pid, [[[(bx + sc * u * (1 + 0.01 * pid), by + sc * v * (1 + 0.01 * pid)) for u, v in sq]]])
+             for pid in (5, 3, 9, 1, 7)]
+    c = M.tessellate(M.Polygons.from_lists(polys), M.H3IndexSystem(), 8)
+    rng = np.random.default_rng(44)
+    x = bx + sc * rng.uniform(-0.05, 1.1, 200_000)
+    y = by + sc * rng.uniform(-0.05, 1.1, 200_000)
+    gp, gq = binned_join(x, y, c.upload(), 8, gpu).numpy()
+    op, oq = oracle_join(c, x, y, res=8)
+    assert len(op) > 3 * len(x)
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+
+
+def test_binned_adversarial_points_and_near_tie_positions(gpu, nyc_chips_r9):
+    """Points on H3 cell corners (the near-tie route runs in pip_mixed_fix_kernel over the
+    binned tiles): pairs equal the correctly rounded oracle, and mgpu_last_near_ties
+    reports INPUT positions -- the same list the fused pipeline reports."""
+    d = nyc_chips_r9.upload()
+    x, y = adversarial_points(nyc_chips_r9)
+    r = binned_join(x, y, d, 9, gpu)
+    ties_b = np.sort(d.ctx.last_near_ties())
+    gp, gq = r.numpy()
+    op, oq = oracle_join_cr(nyc_chips_r9, x, y)
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+    with env(MGPU_BIN=0, MGPU_SPLIT=0):
+        rf = M.pip_join(T(x, gpu), T(y, gpu), d, 9)
+    ties_f = np.sort(d.ctx.last_near_ties())
+    assert rf.stats["pipeline"] == 0
+    assert len(ties_b) > 0 and np.array_equal(ties_b, ties_f)
+    assert r.stats["n_near_ties"] == rf.stats["n_near_ties"]
+
+
+def test_binned_bng_london(gpu):
+    """BNG (C4's districts, res 3 and 4): bins over the dense grid's box."""
+    import bench_workloads as W
+    P = W.london_districts()
+    for res in (3, 4):
+        c = M.tessellate(P, M.BNGIndexSystem(), res)
+        x, y = W.london_points(1_000_000, 45 + res)
+        r = binned_join(x, y, c.upload(), res, gpu, index_system=M.BNGIndexSystem())
+        op, oq = oracle_join(c, x, y, res=res, isys=1)
+        gp, gq = r.numpy()
+        assert np.array_equal(gp, op) and np.array_equal(gq, oq), res
+
+
+def test_binned_points_outside_and_nan(gpu, nyc_chips_r9):
+    """Points far outside the chip table's extent (clamped to edge bins, matching
+    nothing) mixed with inside points; a NaN coordinate still raises as in the reference."""
+    d = nyc_chips_r9.upload()
+    x, y = nyc_points(200_000, 46)
+    x[::7] += 3.0
+    y[::11] -= 2.0
+    gp, gq = binned_join(x, y, d, 9, gpu).numpy()
+    op, oq = oracle_join(nyc_chips_r9, x, y)
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+    x[5] = np.nan
+    with env(MGPU_BIN=1, MGPU_SPLIT=0):
+        with pytest.raises(M.IllegalArgumentException):
+            M.pip_join(T(x, gpu), T(y, gpu), d, 9)
+
+
+def test_binned_c3_full_table(gpu):
+    """BASELINE config C3's whole table (74,000 tract-like polygons, 9.4M chips at res
+    10) -- the case the binned pipeline is for -- with 2.5M points: the planner picks it
+    by itself (table beyond the Infinity Cache, batch >= 2^21 points), pairs equal the
+    oracle and the fused pipeline."""
+    import bench_workloads as W
+    P = W.tract_polygons()
+    c = M.tessellate(P, M.H3IndexSystem(), 10, keep_core_geometries=False)
+    d = c.upload()
+    x, y = W.extent_points(W.TRACT_EXTENT, 2_500_000, 47)
+    r = M.pip_join(T(x, gpu), T(y, gpu), d, 10)
+    assert r.stats["pipeline"] == BINNED
+    gp, gq = r.numpy()
+    with O.h3_libm("cr"):
+        op, oq = O.pip_join(0, 10, x, y, c.cell, c.polygon_id, c.is_core, c.wkb_offsets, c.wkb)
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+    with env(MGPU_BIN=0):
+        rf = M.pip_join(T(x, gpu), T(y, gpu), d, 10)
+    assert rf.stats["pipeline"] == 0
+    fp, fq = rf.numpy()
+    assert np.array_equal(fp, gp) and np.array_equal(fq, gq)
