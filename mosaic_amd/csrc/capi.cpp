@@ -1686,7 +1686,7 @@ int32_t mgpu_st_contains(mgpu_ctx* ctx, const mgpu_chips* chips, const int64_t* 
 // caches and a large batch of points.  MGPU_BIN=0 never, =1 whenever it applies (tests),
 // default: tables of at least MGPU_BIN_MIN_MB (256 MB -- the Infinity Cache) and batches
 // of at least 2^21 points.  The bins tile the chip table's extent (H3: the lon/lat box
-// of the chip cells; BNG: the dense grid's box), about MGPU_BIN_N of them (default 1024),
+// of the chip cells; BNG: the dense grid's box), about MGPU_BIN_N of them (default 64),
 // roughly square on the ground.
 static bool plan_bins(const mgpu_chips* chips, int32_t is, int32_t res, int64_t n, const uint8_t* valid,
                       const mgpu::JoinArgs& a, mgpu::BinArgs& b) {
@@ -1716,7 +1716,7 @@ static bool plan_bins(const mgpu_chips* chips, int32_t is, int32_t res, int64_t 
     if ((double)chips->bytes < min_bytes || n < ((int64_t)1 << 21)) return false;
   }
   const char* nbs = getenv("MGPU_BIN_N");
-  const int nb = std::min(std::max(nbs ? atoi(nbs) : 1024, 1), (int)mgpu::bin_max());
+  const int nb = std::min(std::max(nbs ? atoi(nbs) : 64, 1), (int)mgpu::bin_max());
   int nbx = (int)std::lround(std::sqrt(nb * aspect));
   nbx = std::min(std::max(nbx, 1), nb);
   const int nby = std::max(nb / nbx, 1);
@@ -1792,6 +1792,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   a.mixed_idx = nullptr;
   a.mixed_res = nullptr;
   a.chunk_mixed = nullptr;
+  a.poly_answers = 0;
   HIP_TRY(hipMemsetAsync(base, 0, kWsCounters, s));
   HIP_TRY(hipMemsetAsync(base + L.ties, 0, 8, s));
   // the split pipeline (kernels.h SplitArgs) when the chip table has a pixel index for
@@ -1848,8 +1849,9 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
       off = align_up(off + bytes, 256);
       return o;
     };
+    const size_t o_perm = carve((size_t)n * 4), o_rorig = carve((size_t)n * 8);
     const size_t o_bx = carve((size_t)n * 8), o_by = carve((size_t)n * 8), o_slot = carve((size_t)n * 4),
-                 o_br = carve((size_t)n * 4), o_res = carve((size_t)nc * C * 8), o_cnt = carve((size_t)K * nb * 4),
+                 o_pre = carve((size_t)K * nb * 4), o_res = carve((size_t)nc * C * 8), o_cnt = carve((size_t)K * nb * 4),
                  o_gs = carve((size_t)G * nb * 4), o_pairs = carve(nc * 4), o_off = carve(nc * 8),
                  o_gperm = carve(nc * 4), o_gcand = carve(nc * 4);
     if (off > ctx->bin_bytes) {
@@ -1865,7 +1867,9 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     ba.bx = (double*)(bb + o_bx);
     ba.by = (double*)(bb + o_by);
     ba.slot = (uint32_t*)(bb + o_slot);
-    ba.binrank = (uint32_t*)(bb + o_br);
+    ba.pre = (uint32_t*)(bb + o_pre);
+    ba.perm = (uint32_t*)(bb + o_perm);
+    ba.res = (uint64_t*)(bb + o_rorig);
     ba.cnt = (uint32_t*)(bb + o_cnt);
     ba.gsum = (uint32_t*)(bb + o_gs);
     mgpu::JoinArgs j = a;
@@ -1873,6 +1877,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     j.y = ba.by;
     j.mixed_idx = nullptr;
     j.chunk_mixed = nullptr;
+    j.poly_answers = 1;
     j.mixed_res = (uint64_t*)(bb + o_res);
     j.group_sum = (uint32_t*)(bb + o_gperm);
     j.group_cand = (uint32_t*)(bb + o_gcand);

@@ -41,6 +41,7 @@ struct JoinArgs {
   const uint32_t* chunk_mixed;
   const uint8_t* valid;             // null points (Arrow validity bitmap at bit offset valid_off), or null
   int64_t valid_off;
+  int poly_answers;                 // binned pipeline: a one-match answer is (polygon id | 1 << 32)
 };
 
 // The split pipeline (a chip table with a pixel index and at most 32 chips per cell):
@@ -71,15 +72,16 @@ hipError_t launch_split_emit(int is, const SplitArgs& a, hipStream_t s);
 // The binned pipeline (a chip table far larger than the caches): the points
 // are counting-sorted by a coarse spatial bin so that the join walks the chip table bin
 // by bin instead of at random, then the answers are gathered back into input order.
-//   bin_rank_kernel     per chunk of bin_chunk() points: bin of each point, its rank among
-//                       the chunk's points of that bin (LDS atomics), the chunk's bin counts
+//   bin_hist_kernel     per chunk of bin_chunk() points: the chunk's bin counts
 //   bin_colscan_kernel  + bin_base_kernel: counts -> run offsets (bin-major, chunk-minor)
-//   bin_scatter_kernel  x, y -> their binned slots; slot[i] kept for the gather
+//   bin_scatter_kernel  x, y -> their binned slots (sorted by bin in LDS, written as runs);
+//                       slot[i] kept for the gather
 //   pip_binned_kernel   join_tile's phases over the binned points, tiles dealt to the XCDs
 //                       in contiguous runs (one bin's chips stay in one L2); answers
 //                       (first chip | match mask << 32) per slot in j.mixed_res
 //                       (+ pip_mixed_fix_kernel for the tiles holding an H3 near-tie)
-//   bin_count_kernel    pairs per input chunk of split_chunk() points (gathered answers)
+//   bin_gather_kernel   the answers back in input order (bin runs read whole, placed via
+//                       perm[] in LDS); pairs per input chunk of split_chunk() points
 //   tile_scan_kernel    -> output offsets;  bin_emit_kernel: ordered pairs
 struct BinArgs {
   SplitArgs s;                      // s.j: the BINNED points (x, y = the binned copies),
@@ -90,8 +92,10 @@ struct BinArgs {
   double* bx;                       // [n] binned copies
   double* by;
   uint32_t* slot;                   // [n] binned slot of input point i
-  uint32_t* binrank;                // [n] rank << 16 | bin
-  uint32_t* cnt;                    // [bin chunks * nb] counts, then in-group prefixes
+  uint32_t* perm;                   // [n] input point of binned slot s
+  uint64_t* res;                    // [n] the answers (first chip | match mask << 32) in input order
+  uint32_t* cnt;                    // [bin chunks * nb] bin counts per chunk of bin_chunk() points
+  uint32_t* pre;                    // [bin chunks * nb] their prefixes within the chunk's group
   uint32_t* gsum;                   // [bin groups * nb] group sums, then group bases
   double x0, y0, inv_bx, inv_by;    // the bin grid over the chip table's extent
   int32_t nbx, nby;                 // nbx * nby <= bin_max()

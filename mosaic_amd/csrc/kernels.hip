@@ -720,10 +720,26 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   if (G) {
     // the split pipeline: each listed point's answer, and the chunk's pair count
     uint32_t mine = 0;
-    for (uint32_t li = threadIdx.x; li < gcount; li += kBlock) {
-      const uint32_t m = s_mask[li];
-      a.mixed_res[lbase + li] = (uint64_t)s_first[li] | ((uint64_t)m << 32);
-      mine += __popc(m);
+    // the binned pipeline: one match is answered by its polygon id (the chip is local
+    // here; in input order, where the emit runs, every lookup would be a random line);
+    // the lane's lookups are issued together, then its answers stored
+    uint64_t v[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      const uint32_t li = threadIdx.x + k * kBlock;
+      v[k] = 0;
+      if (li < gcount) {
+        const uint32_t m = s_mask[li];
+        v[k] = (uint64_t)s_first[li] | ((uint64_t)m << 32);
+        if (a.poly_answers && m && !(m & (m - 1)))
+          v[k] = (uint64_t)(uint32_t)t.chip_poly[s_first[li] + __builtin_ctz(m)] | (1ull << 32);
+        mine += __popc(m);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      const uint32_t li = threadIdx.x + k * kBlock;
+      if (li < gcount) a.mixed_res[lbase + li] = v[k];
     }
     const unsigned long long tot = wave_sum_u64(mine);
     if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&a.group_sum[chunk], (uint32_t)tot);
@@ -1847,14 +1863,12 @@ hipError_t launch_format_cells(int is, const int64_t* cells, int64_t n, char* ou
 // lets the join walk the table bin by bin: the tiles of a bin run on one XCD and share
 // its chips in that XCD's L2.  The answers are per binned slot; the emit gathers them
 // back in input order (a chunk's slots fall in one short run per bin).
-constexpr int kBinBlock = 1024;
-constexpr int kBinChunk = 65536;                  // points per rank / scatter workgroup
-constexpr int kBinItems = kBinChunk / kBinBlock;  // per thread
-constexpr int kBinMax = 4096;                     // bins
+constexpr int kBinBlock = 512;
+constexpr int kBinChunk = 4096;                   // points per histogram / scatter workgroup
+constexpr int kBinItems = kBinChunk / kBinBlock;  // per thread, all in flight
+constexpr int kBinMax = 512;                      // bins
 constexpr int kBinGroup = 64;                     // chunk rows per first-level column scan
-constexpr int kBinBatch = 8;                      // point loads in flight per thread
-static_assert(kBinChunk <= 65536 && kBinMax <= 65536, "rank << 16 | bin");
-static_assert(kBinMax % 1024 == 0, "bin_base_kernel: whole bins per thread");
+static_assert(kBinMax == kBinBlock, "one bin per thread in the workgroup scans");
 
 __device__ __forceinline__ uint32_t bin_of(const BinArgs& b, double x, double y) {
   // NaN and points outside the extent clamp to an edge bin (the bin only orders the work)
@@ -1865,42 +1879,32 @@ __device__ __forceinline__ uint32_t bin_of(const BinArgs& b, double x, double y)
   return (uint32_t)(iy * b.nbx + ((iy & 1) ? b.nbx - 1 - ix : ix));
 }
 
-// per chunk: each point's bin and its rank among the chunk's points of that bin (LDS
-// atomics: the order inside a bin is arbitrary, slot[i] records where each point went),
-// and the chunk's row of bin counts
-__global__ __launch_bounds__(kBinBlock) void bin_rank_kernel(BinArgs b) {
+// per chunk of kBinChunk points: its row of bin counts
+__global__ __launch_bounds__(kBinBlock) void bin_hist_kernel(BinArgs b) {
   __shared__ uint32_t s_h[kBinMax];
   const int nb = b.nbx * b.nby;
-  for (int i = threadIdx.x; i < nb; i += kBinBlock) s_h[i] = 0;
+  if ((int)threadIdx.x < nb) s_h[threadIdx.x] = 0;
   __syncthreads();
   const int64_t n = b.s.j.n, c0 = (int64_t)blockIdx.x * kBinChunk;
-  for (int k0 = 0; k0 < kBinItems; k0 += kBinBatch) {
-    double px[kBinBatch], py[kBinBatch];
+  double px[kBinItems], py[kBinItems];
 #pragma unroll
-    for (int k = 0; k < kBinBatch; k++) {
-      const int64_t p = c0 + (int64_t)(k0 + k) * kBinBlock + threadIdx.x;
-      px[k] = py[k] = 0.0;
-      if (p < n) {
-        px[k] = __builtin_nontemporal_load(&b.x[p]);
-        py[k] = __builtin_nontemporal_load(&b.y[p]);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kBinBatch; k++) {
-      const int64_t p = c0 + (int64_t)(k0 + k) * kBinBlock + threadIdx.x;
-      if (p < n) {
-        const uint32_t bi = bin_of(b, px[k], py[k]);
-        const uint32_t r = atomicAdd(&s_h[bi], 1u);
-        b.binrank[p] = r << 16 | bi;
-      }
+  for (int k = 0; k < kBinItems; k++) {
+    const int64_t p = c0 + (int64_t)k * kBinBlock + threadIdx.x;
+    px[k] = py[k] = 0.0;
+    if (p < n) {
+      px[k] = __builtin_nontemporal_load(&b.x[p]);
+      py[k] = __builtin_nontemporal_load(&b.y[p]);
     }
   }
+#pragma unroll
+  for (int k = 0; k < kBinItems; k++)
+    if (c0 + (int64_t)k * kBinBlock + threadIdx.x < n) atomicAdd(&s_h[bin_of(b, px[k], py[k])], 1u);
   __syncthreads();
-  for (int i = threadIdx.x; i < nb; i += kBinBlock) b.cnt[(int64_t)blockIdx.x * nb + i] = s_h[i];
+  if ((int)threadIdx.x < nb) b.cnt[(int64_t)blockIdx.x * nb + threadIdx.x] = s_h[threadIdx.x];
 }
 
-// cnt[chunk][bin] -> its exclusive prefix over the chunks of its group of kBinGroup;
-// gsum[group][bin] = the group's sum
+// pre[chunk][bin] = the exclusive prefix of cnt over the chunks of its group of
+// kBinGroup; gsum[group][bin] = the group's sum
 __global__ __launch_bounds__(256) void bin_colscan_kernel(BinArgs b, int64_t n_chunks) {
   const int nb = b.nbx * b.nby;
   const int bin = blockIdx.x * 256 + threadIdx.x;
@@ -1912,7 +1916,7 @@ __global__ __launch_bounds__(256) void bin_colscan_kernel(BinArgs b, int64_t n_c
   uint32_t run = 0;
 #pragma unroll
   for (int k = 0; k < kBinGroup; k++) {
-    if (k0 + k < n_chunks) b.cnt[(k0 + k) * nb + bin] = run;
+    if (k0 + k < n_chunks) b.pre[(k0 + k) * nb + bin] = run;
     run += v[k];
   }
   b.gsum[(int64_t)blockIdx.y * nb + bin] = run;
@@ -1920,68 +1924,128 @@ __global__ __launch_bounds__(256) void bin_colscan_kernel(BinArgs b, int64_t n_c
 
 // one workgroup: each bin's total, the bins' exclusive scan (slots are bin-major), then
 // gsum[group][bin] = the first slot of the bin's points of that group of chunks
-__global__ __launch_bounds__(1024) void bin_base_kernel(BinArgs b, int64_t n_groups) {
-  __shared__ uint32_t s_w[16];
-  constexpr int kPer = kBinMax / 1024;
+__global__ __launch_bounds__(kBinBlock) void bin_base_kernel(BinArgs b, int64_t n_groups) {
+  __shared__ uint32_t s_w[kBinBlock / 64];
   const int nb = b.nbx * b.nby;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bin = threadIdx.x;
   uint32_t mine = 0;
-#pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const int bin = threadIdx.x * kPer + k;
-    if (bin < nb)
-      for (int64_t g = 0; g < n_groups; g++) mine += b.gsum[g * nb + bin];
-  }
+  if (bin < nb)
+    for (int64_t g = 0; g < n_groups; g++) mine += b.gsum[g * nb + bin];
   const uint32_t incl = wave_incl_scan(mine);
   if (lane == 63) s_w[wave] = incl;
   __syncthreads();
   uint32_t run = incl - mine;
   for (int w = 0; w < wave; w++) run += s_w[w];
-#pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const int bin = threadIdx.x * kPer + k;
-    if (bin < nb)
-      for (int64_t g = 0; g < n_groups; g++) {
-        const uint32_t v = b.gsum[g * nb + bin];
-        b.gsum[g * nb + bin] = run;
-        run += v;
-      }
-  }
+  if (bin < nb)
+    for (int64_t g = 0; g < n_groups; g++) {
+      const uint32_t v = b.gsum[g * nb + bin];
+      b.gsum[g * nb + bin] = run;
+      run += v;
+    }
 }
 
-// x, y -> their slots (bin run base + rank); slot[i] kept for the gather
-__global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
-  __shared__ uint32_t s_off[kBinMax];
+// The chunk's bin runs: s_off[bin] = its first binned slot, s_loc[bin] = its first
+// position in the chunk's bin-sorted order (the scan of the chunk's counts); every lane
+// of the workgroup ends holding nothing, the tables are in LDS after the barrier.
+__device__ __forceinline__ void bin_runs(const BinArgs& b, int64_t k, uint32_t* s_off, uint32_t* s_loc,
+                                         uint32_t* s_w) {
   const int nb = b.nbx * b.nby;
-  const int64_t k = blockIdx.x, g = k / kBinGroup;
-  for (int i = threadIdx.x; i < nb; i += kBinBlock) s_off[i] = b.gsum[g * nb + i] + b.cnt[k * nb + i];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t g = k / kBinGroup;
+  const int bin = threadIdx.x;
+  uint32_t c = 0;
+  if (bin < nb) {
+    c = b.cnt[k * nb + bin];
+    s_off[bin] = b.gsum[g * nb + bin] + b.pre[k * nb + bin];
+  }
+  const uint32_t incl = wave_incl_scan(c);
+  if (lane == 63) s_w[wave] = incl;
   __syncthreads();
+  uint32_t before = incl - c;
+  for (int w = 0; w < wave; w++) before += s_w[w];
+  if (bin < nb) s_loc[bin] = before;
+  __syncthreads();
+}
+
+// the bin of position lp of the chunk's bin-sorted order (the last bin starting at or
+// before it; empty bins start where the next one does)
+__device__ __forceinline__ uint32_t bin_at(const uint32_t* s_loc, int nb, uint32_t lp) {
+  uint32_t lo = 0, hi = (uint32_t)nb;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (s_loc[mid] <= lp)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// Per chunk: each point's rank among the chunk's points of its bin (LDS atomics -- any
+// order inside a bin will do: perm[slot] and slot[i] record where each point went), the
+// chunk's points sorted by bin in LDS, then written as contiguous runs (one per bin) by
+// consecutive lanes: whole cache lines, not one scattered 8-byte store per point.
+__global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
+  __shared__ double s_val[kBinChunk];   // x, then y, in the chunk's bin-sorted order
+  __shared__ uint16_t s_li[kBinChunk];  // the point's index in the chunk
+  __shared__ uint32_t s_off[kBinMax];
+  __shared__ uint32_t s_loc[kBinMax];
+  __shared__ uint32_t s_rank[kBinMax];
+  __shared__ uint32_t s_w[kBinBlock / 64];
+  const int nb = b.nbx * b.nby;
+  const int64_t k = blockIdx.x;
   const int64_t n = b.s.j.n, c0 = k * kBinChunk;
-  for (int k0 = 0; k0 < kBinItems; k0 += kBinBatch) {
-    double px[kBinBatch], py[kBinBatch];
-    uint32_t br[kBinBatch];
+  // the chunk's points load while the run tables are built
+  double px[kBinItems], py[kBinItems];
 #pragma unroll
-    for (int q = 0; q < kBinBatch; q++) {
-      const int64_t p = c0 + (int64_t)(k0 + q) * kBinBlock + threadIdx.x;
-      px[q] = py[q] = 0.0;
-      br[q] = 0;
-      if (p < n) {
-        px[q] = __builtin_nontemporal_load(&b.x[p]);
-        py[q] = __builtin_nontemporal_load(&b.y[p]);
-        br[q] = __builtin_nontemporal_load(&b.binrank[p]);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < kBinBatch; q++) {
-      const int64_t p = c0 + (int64_t)(k0 + q) * kBinBlock + threadIdx.x;
-      if (p < n) {
-        const uint32_t sl = s_off[br[q] & 0xFFFFu] + (br[q] >> 16);
-        b.bx[sl] = px[q];
-        b.by[sl] = py[q];
-        b.slot[p] = sl;
-      }
+  for (int q = 0; q < kBinItems; q++) {
+    const int64_t p = c0 + (int64_t)q * kBinBlock + threadIdx.x;
+    px[q] = py[q] = 0.0;
+    if (p < n) {
+      px[q] = __builtin_nontemporal_load(&b.x[p]);
+      py[q] = __builtin_nontemporal_load(&b.y[p]);
     }
   }
+  if ((int)threadIdx.x < nb) s_rank[threadIdx.x] = 0;
+  bin_runs(b, k, s_off, s_loc, s_w);
+  uint32_t lps[kBinItems];
+#pragma unroll
+  for (int q = 0; q < kBinItems; q++) {
+    const int64_t p = c0 + (int64_t)q * kBinBlock + threadIdx.x;
+    lps[q] = 0xFFFFFFFFu;
+    if (p < n) {
+      const uint32_t bi = bin_of(b, px[q], py[q]);
+      const uint32_t r = atomicAdd(&s_rank[bi], 1u);
+      lps[q] = s_loc[bi] + r;
+      s_val[lps[q]] = px[q];
+      s_li[lps[q]] = (uint16_t)(q * kBinBlock + threadIdx.x);
+      b.slot[p] = s_off[bi] + r;
+    }
+  }
+  __syncthreads();
+  const int64_t left = n - c0;
+  const uint32_t m = left < kBinChunk ? (uint32_t)left : (uint32_t)kBinChunk;
+  uint32_t sls[kBinItems];
+#pragma unroll
+  for (int q = 0; q < kBinItems; q++) {
+    const uint32_t lp = q * kBinBlock + threadIdx.x;
+    sls[q] = 0xFFFFFFFFu;
+    if (lp < m) {
+      const uint32_t bi = bin_at(s_loc, nb, lp);
+      sls[q] = s_off[bi] + (lp - s_loc[bi]);
+      b.bx[sls[q]] = s_val[lp];
+      b.perm[sls[q]] = (uint32_t)(c0 + s_li[lp]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kBinItems; q++)
+    if (lps[q] != 0xFFFFFFFFu) s_val[lps[q]] = py[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kBinItems; q++)
+    if (sls[q] != 0xFFFFFFFFu) b.by[sls[q]] = s_val[q * kBinBlock + threadIdx.x];
 }
 
 // the join over the binned points: join_tile's phases (G mode, no mixed list: every
@@ -1994,42 +2058,68 @@ __global__ __launch_bounds__(kBlock) MGPU_JOIN_ATTR void pip_binned_kernel(JoinA
   if (tile < n_tiles) join_tile<IS, false, true>(a, tile);
 }
 
-// the answers of input points p0 .. p0 + 15 (their slots in 16-byte loads)
+// The answers back in input order, per chunk of kBinChunk input points: the chunk's bin
+// runs are read run by run (consecutive lanes, consecutive slots: coalesced, one page
+// per run) and placed by perm[] into LDS, then written out in input order; the pairs of
+// each split_chunk() of input points are counted on the way (the emit's offsets).
 constexpr int kBinEmitItems = kChunk / kClsBlock;
-static_assert(kBinEmitItems == 16, "four 16-byte slot loads per thread");
-__device__ __forceinline__ void bin_gather(const BinArgs& b, int64_t p0, uint64_t* v) {
+static_assert(kBinEmitItems == 16, "four 16-byte answer loads per thread");
+static_assert(kBinChunk % kChunk == 0 && kBinChunk / kChunk <= kBinBlock / 64, "emit chunks inside a bin chunk");
+__global__ __launch_bounds__(kBinBlock) void bin_gather_kernel(BinArgs b) {
+  __shared__ uint64_t s_v[kBinChunk];
+  __shared__ uint32_t s_off[kBinMax];
+  __shared__ uint32_t s_loc[kBinMax];
+  __shared__ uint32_t s_w[kBinBlock / 64];
+  const int nb = b.nbx * b.nby;
+  const int64_t k = blockIdx.x;
+  const int64_t n = b.s.j.n, c0 = k * kBinChunk;
+  bin_runs(b, k, s_off, s_loc, s_w);
+  const int64_t left = n - c0;
+  const uint32_t m = left < kBinChunk ? (uint32_t)left : (uint32_t)kBinChunk;
+  for (uint32_t lp = threadIdx.x; lp < m; lp += kBinBlock) {
+    const uint32_t bi = bin_at(s_loc, nb, lp);
+    const uint32_t sl = s_off[bi] + (lp - s_loc[bi]);
+    s_v[b.perm[sl] - (uint32_t)c0] = b.s.j.mixed_res[sl];
+  }
+  __syncthreads();
+  constexpr int kPerWave = kChunk / (kBinBlock / 64) * (kBinChunk / kChunk);  // points per wave
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t np = 0;
+  for (int i = wave * kPerWave + lane; i < (wave + 1) * kPerWave; i += 64)
+    if ((uint32_t)i < m) {
+      const uint64_t v = s_v[i];
+      b.res[c0 + i] = v;
+      np += __popc((uint32_t)(v >> 32));
+    }
+  np = wave_sum_u32(np);
+  // waves w .. w + W/E - 1 cover emit chunk (w * E / W): their sums meet in s_w
+  __syncthreads();
+  if (lane == 0) s_w[wave] = np;
+  __syncthreads();
+  constexpr int kE = kBinChunk / kChunk, kWpe = (kBinBlock / 64) / kE;  // emit chunks, waves per emit chunk
+  if ((int)threadIdx.x < kE) {
+    const int64_t e = k * kE + threadIdx.x;
+    if (e * kChunk < n) {
+      uint32_t t = 0;
+      for (int w = 0; w < kWpe; w++) t += s_w[threadIdx.x * kWpe + w];
+      b.s.chunk_pairs[e] = t;
+    }
+  }
+}
+
+// the answers of input points p0 .. p0 + 15, in input order
+__device__ __forceinline__ void bin_answers(const BinArgs& b, int64_t p0, uint64_t* v) {
   const int64_t n = b.s.j.n;
-  uint32_t sl[kBinEmitItems];
   if (p0 + kBinEmitItems <= n) {
-    const uint4* src = (const uint4*)(b.slot + p0);
+    const ulonglong2* src = (const ulonglong2*)(b.res + p0);
 #pragma unroll
-    for (int i = 0; i < kBinEmitItems / 4; i++) {
-      const uint4 q = src[i];
-      sl[4 * i] = q.x, sl[4 * i + 1] = q.y, sl[4 * i + 2] = q.z, sl[4 * i + 3] = q.w;
+    for (int i = 0; i < kBinEmitItems / 2; i++) {
+      const ulonglong2 q = src[i];
+      v[2 * i] = q.x, v[2 * i + 1] = q.y;
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < kBinEmitItems; k++) sl[k] = p0 + k < n ? b.slot[p0 + k] : 0xFFFFFFFFu;
-  }
-#pragma unroll
-  for (int k = 0; k < kBinEmitItems; k++) v[k] = sl[k] != 0xFFFFFFFFu ? b.s.j.mixed_res[sl[k]] : 0ull;
-}
-
-// pairs of each input chunk of kChunk points
-__global__ __launch_bounds__(kClsBlock) void bin_count_kernel(BinArgs b) {
-  __shared__ uint32_t s_w[kClsBlock / 64];
-  uint64_t v[kBinEmitItems];
-  bin_gather(b, (int64_t)blockIdx.x * kChunk + (int64_t)threadIdx.x * kBinEmitItems, v);
-  uint32_t np = 0;
-#pragma unroll
-  for (int k = 0; k < kBinEmitItems; k++) np += __popc((uint32_t)(v[k] >> 32));
-  np = wave_sum_u32(np);
-  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = np;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t tot = 0;
-    for (int w = 0; w < kClsBlock / 64; w++) tot += s_w[w];
-    b.s.chunk_pairs[blockIdx.x] = tot;
+    for (int k = 0; k < kBinEmitItems; k++) v[k] = p0 + k < n ? b.res[p0 + k] : 0ull;
   }
 }
 
@@ -2044,7 +2134,7 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   const int64_t c0 = (int64_t)blockIdx.x * kChunk;
   const int l0 = threadIdx.x * kBinEmitItems;
   uint64_t v[kBinEmitItems];
-  bin_gather(b, c0 + l0, v);
+  bin_answers(b, c0 + l0, v);
   uint32_t npair = 0;
 #pragma unroll
   for (int k = 0; k < kBinEmitItems; k++) npair += __popc((uint32_t)(v[k] >> 32));
@@ -2056,8 +2146,16 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
       uint32_t q = off0;
 #pragma unroll
       for (int k = 0; k < kBinEmitItems; k++) {
-        const uint32_t first = (uint32_t)v[k];
-        for (uint32_t m = (uint32_t)(v[k] >> 32); m; m &= m - 1, q++)
+        const uint32_t first = (uint32_t)v[k], msk = (uint32_t)(v[k] >> 32);
+        if (msk == 1u) {  // one match: first is the polygon id (JoinArgs.poly_answers)
+          if (q >= w0 && q < w0 + kEmitWin) {
+            s_poly[q - w0] = first;
+            s_pt[q - w0] = (uint16_t)(l0 + k);
+          }
+          q++;
+          continue;
+        }
+        for (uint32_t m = msk; m; m &= m - 1, q++)
           if (q >= w0 && q < w0 + kEmitWin) {
             s_poly[q - w0] = (uint32_t)t.chip_poly[first + __builtin_ctz(m)];
             s_pt[q - w0] = (uint16_t)(l0 + k);
@@ -2269,9 +2367,9 @@ int32_t bin_max() { return kBinMax; }
 template <int IS>
 static void launch_binned_t(const BinArgs& a, hipStream_t s, hipEvent_t after_bin, hipEvent_t after_join) {
   const int64_t n = a.s.j.n, K = bin_chunks(n), G = bin_groups(n), nb = (int64_t)a.nbx * a.nby;
-  hipLaunchKernelGGL(bin_rank_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
+  hipLaunchKernelGGL(bin_hist_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
   hipLaunchKernelGGL(bin_colscan_kernel, dim3((unsigned)((nb + 255) / 256), (unsigned)G), dim3(256), 0, s, a, K);
-  hipLaunchKernelGGL(bin_base_kernel, dim3(1), dim3(1024), 0, s, a, G);
+  hipLaunchKernelGGL(bin_base_kernel, dim3(1), dim3(kBinBlock), 0, s, a, G);
   hipLaunchKernelGGL(bin_scatter_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
   if (after_bin) hipEventRecord(after_bin, s);
   const int64_t nc = split_chunks(n), tiles = nc * kChunkTiles;
@@ -2281,7 +2379,7 @@ static void launch_binned_t(const BinArgs& a, hipStream_t s, hipEvent_t after_bi
   if (after_join) hipEventRecord(after_join, s);
   const int64_t fix = tiles < 512 ? tiles : 512;
   hipLaunchKernelGGL(pip_mixed_fix_kernel<IS>, dim3((unsigned)fix), dim3(kBlock), 0, s, a.s.j);
-  hipLaunchKernelGGL(bin_count_kernel, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
+  hipLaunchKernelGGL(bin_gather_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.s.chunk_pairs, a.s.j.group_cand, nc,
                      a.s.chunk_off, a.s.j.counters);
   hipLaunchKernelGGL(bin_emit_kernel, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);

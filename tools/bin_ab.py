@@ -17,10 +17,13 @@ sys.path.insert(0, ROOT)
 VARIANTS = {
     "auto": {},
     "fused": {"MGPU_BIN": "0", "MGPU_SPLIT": "0"},
+    "bin16": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "16"},
+    "bin32": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "32"},
+    "bin64": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "64"},
+    "bin128": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "128"},
     "bin256": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "256"},
     "bin1024": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "1024"},
-    "bin4096": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "4096"},
-    "bin1024_noxcd": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "1024", "MGPU_BIN_XCD": "0"},
+    "bin256_noxcd": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "256", "MGPU_BIN_XCD": "0"},
 }
 
 
@@ -29,7 +32,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--points", type=int, default=None)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="fused,bin256,bin1024,bin4096,bin1024_noxcd,auto")
+    ap.add_argument("--variants", default="fused,bin16,bin32,bin64,bin128,bin256,auto")
     a = ap.parse_args()
     import mosaic_amd as M
     import bench as B
