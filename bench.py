@@ -293,9 +293,9 @@ def main():
         kernel = "pip_binned_kernel<%s>" % isys.name
         alg_bytes = 24.0 * n
     elif split:
-        # the split pipeline: the dominant kernel is classify_kernel, the one
+        # the split pipeline: the dominant kernel is classify_wave_kernel, the one
         # pass over every point: 16 B read + its code (2 B H3 / 4 B BNG) written per point
-        kernel = "classify_kernel<%s>" % isys.name
+        kernel = "classify_wave_kernel<%s>" % isys.name
         alg_bytes = (16.0 + (2.0 if isys.code == M._native.MGPU_H3 else 4.0)) * n
     else:
         kernel = "pip_join_kernel<%s>" % isys.name
