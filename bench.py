@@ -4,8 +4,8 @@
 Workload (BASELINE.json configs[1], "C2"): 100M synthetic points per GPU, uniform in
 the NYC taxi-zone bounding box, joined against the 263 NYC taxi zones
 (python/test/data/NYC_Taxi_Zones.geojson, committed as tests/golden/nyc_taxi_zones.npz)
-tessellated at H3 resolution 9.  One step = one fused pass (cell id -> chip probe ->
-is_core OR st_contains -> ordered pair output) over the GPU's resident points.
+tessellated at H3 resolution 9.  One step = one join (cell id -> chip probe -> is_core OR
+st_contains -> ordered pair output) over the GPU's resident points.
 
 Multi-GPU (torchrun, one process per GPU): points are sharded by contiguous id range
 (weak scaling: the per-GPU point count is fixed), the chip table is built on rank 0
@@ -15,16 +15,20 @@ mgpu_chips_broadcast, mgpu_pair_offsets; mosaic_amd/csrc/comm.cpp).  torch.distr
 (gloo) is only the control plane: the RCCL unique id, the barriers and the max over
 ranks of the barrier-bracketed K steps.
 
-A step is one mgpu_pip_join call: pip_join_kernel (cell id -> chip probe -> is_core
-OR st_contains -> per-tile pair records), pip_fix_kernel (tiles holding an H3 near-tie),
-tile_scan_kernel and pair_emit_kernel (ordered (point_id, polygon_id) output).
+A step is one mgpu_pip_join call, whichever of the library's three pipelines its planner
+picks for the chip table: split (C2, C5: classify_wave_kernel over every
+point by its pixel, pip_mixed_kernel for the mixed ones, split_emit_kernel), binned (C3:
+bin_hist / bin_scatter, pip_binned_kernel over the binned points, bin_gather /
+bin_emit) or fused (C4: pip_join_kernel, pip_fix_kernel, tile_scan_kernel,
+pair_emit_kernel).  Every step ends with the ordered (point_id, polygon_id) pairs.
 
-Also reported: the dominant kernel's (pip_join_kernel) achieved bandwidth against the
-HBM roofline -- algorithmic bytes per launch = 16 B per point read + 8 B per pair
-record written + 12 B per tile (256 points), over its average duration
-measured with HIP events on the launch stream -- the HBM bytes the PMC counters saw
-(profiles/pmc_join_traffic.json, when it was measured on this workload), and a CPU
-baseline: the oracle's multithreaded C restatement of the reference path on a
+Also reported: the dominant kernel's achieved bandwidth against the HBM roofline --
+algorithmic bytes per launch (DESIGN.md §3: classify 18 B/point; binned join 24 B/point;
+fused join 16 B/point + 8 B/pair + 12 B/tile) over its average duration measured with HIP
+events on the launch stream -- the HBM bytes the PMC counters saw for that kernel
+(profiles/pmc_join_traffic*.json, when measured on this workload and kernel), the
+PCIe-inclusive rate (points in pinned host memory, pairs back to it; never `value`), and
+a CPU baseline: the oracle's multithreaded C restatement of the reference path on a
 bounded sample (rank 0, N=1 only).
 """
 import argparse

@@ -158,10 +158,13 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 // candidates are abandoned by the streaming kernel after phase 1 and redone by
 // pip_fix_kernel, which evaluates list overflows on the spot and chips past the
 // 32nd of a cell in phase 3.
-constexpr int kCandCap = kTile;
+#ifndef MGPU_CANDCAP
+#define MGPU_CANDCAP 512  // (256: BNG res 3's 1.25 candidates per point sent most tiles to the fix kernel)
+#endif
+constexpr int kCandCap = MGPU_CANDCAP;
 constexpr int kMixCap = kTile / 2;  // mixed-cell candidates (phase 2b), after the list in s_buf
 #ifndef MGPU_OUTCAP
-#define MGPU_OUTCAP 352
+#define MGPU_OUTCAP 448
 #endif
 constexpr int kOutCap = MGPU_OUTCAP;  // pairs a tile stages in LDS
 #ifndef MGPU_STASH
@@ -2281,11 +2284,14 @@ int64_t join_slot_records() { return kSlot; }
 int64_t join_pend_cap() { return kMixCap; }
 int64_t join_pend_words() { return kPendWords; }
 
+constexpr int64_t kFixGrid = 8192;   // fix-kernel workgroups (one wave each; idle ones exit at once)
 hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s, hipEvent_t after_stream) {
   if (a.n_tiles <= 0) return hipSuccess;
   // BNG has no near-ties, but its tiles still go dirty on a cell of more than 32
   // chips, a candidate-list overflow or a chip without a strip index
-  const unsigned fix_blocks = (unsigned)(a.n_tiles < 512 ? a.n_tiles : 512);
+  // (the fix kernel walks the dirty list grid-stride; a grid that fills the GPU, since a
+  // workload with many border-chip candidates per point -- BNG res 3 -- dirties most tiles)
+  const unsigned fix_blocks = (unsigned)(a.n_tiles < kFixGrid ? a.n_tiles : kFixGrid);
   if (is == MGPU_H3) {
     hipLaunchKernelGGL(pip_join_kernel<MGPU_H3>, dim3(join_grid<MGPU_H3>(a.n_tiles)), dim3(kBlock), 0, s, a);
     if (after_stream) hipEventRecord(after_stream, s);
@@ -2331,7 +2337,7 @@ static void launch_split_t(const SplitArgs& a, hipStream_t s, hipEvent_t after_c
   }
   if (after_classify) hipEventRecord(after_classify, s);
   hipLaunchKernelGGL(pip_mixed_kernel<IS>, dim3((unsigned)nc), dim3(kBlock), 0, s, a.j);
-  const int64_t fix = nc * kChunkTiles < 512 ? nc * kChunkTiles : 512;
+  const int64_t fix = nc * kChunkTiles < kFixGrid ? nc * kChunkTiles : kFixGrid;
   hipLaunchKernelGGL(pip_mixed_fix_kernel<IS>, dim3((unsigned)fix), dim3(kBlock), 0, s, a.j);
   if (after_mixed) hipEventRecord(after_mixed, s);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.chunk_pairs, a.j.group_cand, nc,
@@ -2377,7 +2383,7 @@ static void launch_binned_t(const BinArgs& a, hipStream_t s, hipEvent_t after_bi
   const int64_t grid = per ? 8 * (int64_t)per : tiles;
   hipLaunchKernelGGL(pip_binned_kernel<IS>, dim3((unsigned)grid), dim3(kBlock), 0, s, a.s.j, per, (uint32_t)tiles);
   if (after_join) hipEventRecord(after_join, s);
-  const int64_t fix = tiles < 512 ? tiles : 512;
+  const int64_t fix = tiles < kFixGrid ? tiles : kFixGrid;
   hipLaunchKernelGGL(pip_mixed_fix_kernel<IS>, dim3((unsigned)fix), dim3(kBlock), 0, s, a.s.j);
   hipLaunchKernelGGL(bin_gather_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.s.chunk_pairs, a.s.j.group_cand, nc,
