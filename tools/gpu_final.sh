@@ -1,17 +1,9 @@
 #!/bin/bash
-# Round-end measurements: 2-rank C3 protocol rehearsal, the default bench line (C2, CPU
-# baseline), its rocprofv3 kernel-trace stats, and the other configs' bench lines.
+# Full GPU suite + the C4 res-3 500M bench line (with CPU baseline and PCIe rate)
 set -o pipefail
-TAG=${1:-fin}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-bash tools/gpu_dist_rehearsal.sh c3 &&
-timeout -k 10 400 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 -u bench.py --no-cpu-baseline > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/bench_prof_$TAG.err &&
-for c in c3 c4 c5; do
-  timeout -k 10 400 python -u bench.py --config $c > gpurun_out/bench_${c}_$TAG.json 2> gpurun_out/bench_${c}_$TAG.err || exit 1
-done
-rc=$?
-cat gpurun_out/bench_$TAG.json
-echo "exit $rc"
-exit $rc
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_final.log 2>&1 || { echo "gpu suite failed"; tail -40 gpurun_out/pytest_gpu_final.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu_final.log
+timeout -k 10 500 python3 -u bench.py --config c4 --points 500000000 --res 3 --steps 5 --warmup 2 > gpurun_out/final_c4_500m_r3.json 2> gpurun_out/final_c4_500m_r3.err || exit 1
+cut -c1-300 gpurun_out/final_c4_500m_r3.json
