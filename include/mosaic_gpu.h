@@ -215,8 +215,10 @@ int32_t mgpu_pair_offsets(mgpu_ctx* ctx, int64_t local_pairs, int64_t* out_offse
 int32_t mgpu_st_contains(mgpu_ctx* ctx, const mgpu_chips* chips, const int64_t* chip_row,
                          const double* x, const double* y, int64_t n, int8_t* out, void* stream);
 
-/* The fused hot path: cell id per point, equi-join against the chip table's
- * cell ids, `is_core OR st_contains` filter; emits (point_id, polygon_id) pairs
+/* The hot path: cell id per point, equi-join against the chip table's
+ * cell ids, `is_core OR st_contains` filter (one of three pipelines, chosen per call:
+ * split for pixel-indexed tables, binned for tables beyond the caches, else fused --
+ * mgpu_stats.pipeline); emits (point_id, polygon_id) pairs
  * ordered by input position then polygon id (sorted by point_id when point ids
  * ascend, e.g. contiguous id shards).  point_id may be NULL: ids are
  * point_id_base + index.  Device pointers.  Synchronises `stream` to return the
@@ -238,7 +240,8 @@ int32_t mgpu_pip_join_fetch(mgpu_ctx* ctx, int64_t capacity, int64_t* out_n_pair
 
 /* Asynchronous form: the pair count is left in device memory (*d_n_pairs, one
  * int64) and nothing synchronises -- graph-capturable once mgpu_ctx_reserve has
- * sized the workspace. */
+ * sized the workspace and one call of the same size has grown the split / binned
+ * pipeline's buffers. */
 int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t index_system, int32_t res,
                             const double* x, const double* y, const int64_t* point_id, int64_t point_id_base,
                             int64_t n, int64_t capacity, int64_t* d_n_pairs, int64_t* out_point_id,
@@ -251,7 +254,8 @@ int32_t mgpu_ctx_reserve(mgpu_ctx* ctx, int64_t max_points);
  * After mgpu_pip_join: the points the H3 route resolved inside its tie band
  * (mgpu_stats.n_near_ties).  After mgpu_points_to_cells: every point the fast
  * projection handed to the route (a superset).  Tests recompute exactly these points
- * with the CPU oracle at full bench sizes.  Unordered; at most 65536 are kept.
+ * with the CPU oracle at full bench sizes.  Unordered (ascending after a binned join,
+ * whose queue holds binned slots mapped back here); at most 65536 are kept.
  * Synchronises the device.  MGPU_E_CAPACITY (with *out_n set) if cap is too small
  * or more than 65536 were found. */
 int32_t mgpu_last_near_ties(mgpu_ctx* ctx, int64_t* out_index, int64_t cap, int64_t* out_n);
