@@ -145,8 +145,9 @@ int32_t mgpu_bng_format_device(mgpu_ctx* ctx, const int64_t* cells, int64_t n, c
  * BNGIndexSystem.kRing / kLoop, BNGIndexSystem.scala:221-252 (the cell, then loops
  * 1..k; a loop = pointToIndex of the 8k corners around the cell, kept when isValid),
  * in the reference's order.  H3: H3IndexSystem.kRing / kLoop, H3IndexSystem.scala:
- * 182-205 (H3 v3.7 kRing spiral / hexRing order); a cell whose walk reaches one of the
- * 12 pentagon base cells returns MGPU_E_UNSUPPORTED (not built on the device).  Cell i's list
+ * 182-205 (H3 v3.7 kRing spiral / hexRing order; a walk that meets a pentagon takes H3's
+ * _kRingInternal hash-set order, and kLoop Mosaic's kRing(k) diff kRing(k - 1) in Scala
+ * HashSet order -- built for k <= 64, MGPU_E_UNSUPPORTED beyond).  Cell i's list
  * is out_cells[out_offsets[i] .. out_offsets[i + 1]); device pointers; *out_total =
  * entries needed (MGPU_E_CAPACITY when above `capacity`).  0 <= k <= 1024. */
 int32_t mgpu_grid_kring(mgpu_ctx* ctx, int32_t index_system, const int64_t* cells, int64_t n, int32_t k,

@@ -1176,25 +1176,54 @@ int32_t mgpu_grid_kring(mgpu_ctx* ctx, int32_t index_system, const int64_t* cell
   if (int32_t st = set_device(ctx->device)) return st;
   hipStream_t s = (hipStream_t)stream;
   if (int32_t st = ensure_ws(ctx, mgpu::join_tiles(n))) return st;
-  auto* counters = (unsigned long long*)ctx->ws;
-  auto* chunk = (int64_t*)((uint8_t*)ctx->ws + ws_layout(mgpu::join_tiles(n), 0).where);
+  // workspace: counters, the chunk sums (tile_where region), per-cell counts mc[n] (the
+  // records region, >= 16 n bytes) and the fallback list fb_idx[n] (the pending region)
+  const WsLayout L = ws_layout(mgpu::join_tiles(n), 0);
+  auto* base = (uint8_t*)ctx->ws;
+  auto* counters = (unsigned long long*)base;
+  auto* chunk = (int64_t*)(base + L.where);
+  auto* mc = (int64_t*)(base + L.recs);
+  auto* fb_idx = (uint32_t*)(base + L.pend);
   HIP_TRY(hipMemsetAsync(counters, 0, kWsCounters, s));
-  HIP_TRY(mgpu::launch_cell_kring(index_system, cells, n, k, loop_only, out_cells, capacity, out_offsets, chunk,
-                                   counters, s));
-  unsigned long long h[4] = {0};
-  int64_t total = 0;
+  HIP_TRY(mgpu::launch_kring_count(index_system, cells, n, k, loop_only, mc, chunk, fb_idx, counters, s));
+  unsigned long long h[6] = {0};
   HIP_TRY(hipMemcpyAsync(h, counters, sizeof h, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(&total, out_offsets + n, sizeof total, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  if (out_total) *out_total = total;
   if (h[2] && index_system == MGPU_H3)
     return fail(MGPU_E_INVALID_ARG, "%llu cells are not H3 cell ids", h[2]);
   if (h[2])
     return fail(MGPU_E_INVALID_ARG, "%llu cells are not BNG cells or reach ids BNGIndexSystem.isValid cannot parse "
                 "(NumberFormatException in the reference)", h[2]);
-  if (h[3])
-    return fail(MGPU_E_UNSUPPORTED, "grid_kring: %llu H3 cells reach a pentagon base cell within k = %d "
-                "(pentagon neighbourhoods are not built on the device)", h[3], k);
+  // H3 walks that met a pentagon: H3's _kRingInternal / Mosaic's kLoop fallback, in
+  // batches of cells whose scratch fits 256 MB, once for the lengths, once (after the
+  // offsets) for the lists
+  const int64_t n_fb = (int64_t)h[3];
+  uint64_t* scratch = nullptr;
+  int64_t batch = 0;
+  if (n_fb) {
+    if (k > mgpu::kring_fallback_max_k())
+      return fail(MGPU_E_UNSUPPORTED, "grid_kring: %lld H3 cells reach a pentagon within k = %d; pentagon "
+                  "neighbourhoods are built for k <= %d", (long long)n_fb, k, mgpu::kring_fallback_max_k());
+    const int64_t words = mgpu::kring_fallback_words(k);
+    batch = std::max<int64_t>(1, std::min<int64_t>(n_fb, ((int64_t)256 << 20) / 8 / words));
+    HIP_TRY(hipMalloc(&scratch, (size_t)batch * words * 8));
+    for (int64_t j0 = 0; j0 < n_fb; j0 += batch)
+      HIP_TRY(mgpu::launch_kring_fallback(cells, fb_idx, j0, std::min(n_fb, j0 + batch), k, loop_only, mc, chunk,
+                                          out_offsets, out_cells, capacity, scratch, 0, counters, s));
+  }
+  HIP_TRY(mgpu::launch_kring_write(index_system, cells, n, k, loop_only, mc, chunk, out_offsets, out_cells, capacity,
+                                   s));
+  for (int64_t j0 = 0; j0 < n_fb; j0 += batch)
+    HIP_TRY(mgpu::launch_kring_fallback(cells, fb_idx, j0, std::min(n_fb, j0 + batch), k, loop_only, mc, chunk,
+                                        out_offsets, out_cells, capacity, scratch, 1, counters, s));
+  int64_t total = 0;
+  HIP_TRY(hipMemcpyAsync(h, counters, sizeof h, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&total, out_offsets + n, sizeof total, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (scratch) hipFree(scratch);
+  if (out_total) *out_total = total;
+  if (h[4])
+    return fail(MGPU_E_INTERNAL, "grid_kring: %llu pentagon walks overflowed their hash set (inconsistent tables)", h[4]);
   if (total > capacity)
     return fail(MGPU_E_CAPACITY, "grid_kring: %lld ids, capacity %lld", (long long)total, (long long)capacity);
   return MGPU_OK;

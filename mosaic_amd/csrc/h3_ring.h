@@ -6,12 +6,13 @@
 // hexRangeDistances, hexRing).  One thread walks one cell's spiral (kRing) or ring
 // (hexRing) in the reference's output order.
 //
-// Scope of this version: walks that stay among hexagon base cells.  A walk that
-// reaches a cell of one of the 12 pentagon base cells returns kUnsupported and the
-// C-ABI call fails loudly (MGPU_E_UNSUPPORTED); the reference's pentagon handling
-// (the K-subsequence rotations, the _kRingInternal hash-set fallback, Mosaic's
-// kLoop set-difference fallback) is restated in the oracle only
-// (oracle/h3_oracle.c); walks next to the south polar pentagon are not yet consistent there.
+// Pentagons as in H3 v3.7: h3NeighborRotations' K-subsequence rotations; a spiral or
+// ring that meets a pentagon fails (as hexRangeDistances / hexRing do), and the caller
+// then takes the reference's fallbacks -- kring_hash (H3 C's _kRingInternal: a DFS
+// into an open-addressing hash set keyed by h % maxKringSize, whose nonzero entries in
+// array order are what H3-Java's kRing returns) and kloop_diff (Mosaic's kLoop on
+// PentagonEncounteredException: kRing(k).toSet diff kRing(k - 1).toSet, iterated in
+// Scala 2.12 HashSet order).  Restated beside the oracle's oracle/h3_oracle.c.
 #pragma once
 #include <stdint.h>
 
@@ -35,23 +36,33 @@ MGPU_HD uint64_t rotate_digits(uint64_t h, int n) {
   return (h & ~kDigitsMask) | d;
 }
 
-// h3NeighborRotations restricted to hexagon base cells (kUnsupported otherwise).
-// The digit walk: from the finest digit up, NEW_DIGIT / NEW_ADJUSTMENT (_II for a
-// Class III child resolution, _III for Class II) until no step is carried; a step
-// carried past resolution 1 crosses into the neighbouring base cell, whose frame is
-// reached by baseCellNeighbor60CCWRots ccw rotations of every digit.
+MGPU_HD uint64_t with_base(uint64_t h, int b) { return (h & ~(127ULL << 45)) | ((uint64_t)b << 45); }
+MGPU_HD bool polar_pentagon(int b) { return b == 4 || b == 117; }
+MGPU_HD bool is_pentagon(uint64_t h) { return pentagon_base(base_of(h)) && h3::leading_nonzero(h, res_of(h)) == 0; }
+
+// H3 v3.7 h3NeighborRotations: the neighbour of h in direction dir (after *rotations
+// ccw rotations of dir), *rotations updated; 0 where H3 leaves it undefined (the
+// deleted K direction of a pentagon).  The digit walk: from the finest digit up,
+// NEW_DIGIT / NEW_ADJUSTMENT (_II for a Class III child resolution, _III for Class II)
+// until no step is carried; a step carried past resolution 1 crosses into the
+// neighbouring base cell, whose frame is reached by baseCellNeighbor60CCWRots rotations.
 MGPU_HD uint64_t neighbor(uint64_t h, int dir, int* rotations) {
   const int res = res_of(h);
   const int old_base = base_of(h);
-  if (pentagon_base(old_base)) return kUnsupported;
+  const int old_lead = h3::leading_nonzero(h, res);
   for (int i = 0; i < *rotations; i++) dir = h3::rot60ccw(dir);
   int new_rot = 0;
   for (int r = res - 1;; r--) {
     if (r == -1) {
-      const int nb = H3T_BASE_CELL_NEIGHBORS[old_base][dir];
-      if (nb == H3T_INVALID_BASE_CELL || pentagon_base(nb)) return kUnsupported;
-      h = (h & ~(127ULL << 45)) | ((uint64_t)nb << 45);
+      h = with_base(h, H3T_BASE_CELL_NEIGHBORS[old_base][dir]);
       new_rot = H3T_BASE_CELL_NEIGHBOR_ROTS[old_base][dir];
+      if (base_of(h) == H3T_INVALID_BASE_CELL) {
+        // the deleted K vertex at the base-cell level: the edge borders the IK neighbour
+        h = with_base(h, H3T_BASE_CELL_NEIGHBORS[old_base][5]);
+        new_rot = H3T_BASE_CELL_NEIGHBOR_ROTS[old_base][5];
+        h = h3::rotate_ccw(h, res);
+        *rotations += 1;
+      }
       break;
     }
     const int sh = (h3::kMaxRes - (r + 1)) * 3;
@@ -68,7 +79,37 @@ MGPU_HD uint64_t neighbor(uint64_t h, int dir, int* rotations) {
     if (next == 0) break;
     dir = next;
   }
-  h = rotate_digits(h, new_rot);
+  const int new_base = base_of(h);
+  if (pentagon_base(new_base)) {
+    bool adjusted = false;
+    if (h3::leading_nonzero(h, res) == 1) {
+      if (old_base != new_base) {
+        // into the deleted K subsequence of a pentagon base cell from a neighbour
+        const int f = H3T_BASE_CELL_DATA[old_base][0];
+        const bool cw = H3T_BASE_CELL_DATA[new_base][5] == f || H3T_BASE_CELL_DATA[new_base][6] == f;
+        h = cw ? h3::rotate_cw(h, res) : h3::rotate_ccw(h, res);
+        adjusted = true;
+      } else if (old_lead == 3) {  // from within the same pentagon
+        h = h3::rotate_ccw(h, res);
+        *rotations += 1;
+      } else if (old_lead == 5) {
+        h = h3::rotate_cw(h, res);
+        *rotations += 5;
+      } else {
+        return 0;  // the K direction is deleted from here
+      }
+    }
+    for (int i = 0; i < new_rot; i++) h = h3::rotate_pent_ccw(h, res);
+    if (old_base != new_base) {
+      if (polar_pentagon(new_base)) {
+        if (old_base != 118 && old_base != 8 && h3::leading_nonzero(h, res) != 3) *rotations += 1;
+      } else if (h3::leading_nonzero(h, res) == 5 && !adjusted) {
+        *rotations += 1;
+      }
+    }
+  } else {
+    h = rotate_digits(h, new_rot);
+  }
   *rotations = (*rotations + new_rot) % 6;
   return h;
 }
@@ -76,41 +117,46 @@ MGPU_HD uint64_t neighbor(uint64_t h, int dir, int* rotations) {
 // J, JK, K, IK, I, IJ; rings start one step in I
 __host__ __device__ constexpr int direction(int i) { return (int)((0x231546u >> (4 * (5 - i))) & 0xF); }
 constexpr int kNextRing = 4;
+constexpr int64_t kFallback = -2;  // the walk met a pentagon: take the reference's fallback
+
+MGPU_HD int64_t max_kring(int k) { return 3 * (int64_t)k * (k + 1) + 1; }
 
 // kRing(h, k) in hexRangeDistances' spiral order: number of ids (written to out when
-// out != nullptr), or -1 when the walk is outside this version's scope
+// out != nullptr), or kFallback where hexRangeDistances fails (a pentagon)
 MGPU_HD int64_t kring(uint64_t h, int k, int64_t* out) {
   int64_t idx = 0;
   if (out) out[idx] = (int64_t)h;
   idx++;
-  if (pentagon_base(base_of(h))) return -1;
+  if (is_pentagon(h)) return kFallback;
   int rot = 0;
   for (int ring = 1; ring <= k; ring++) {
     h = neighbor(h, kNextRing, &rot);
-    if (h == kUnsupported) return -1;
+    if (h == 0 || is_pentagon(h)) return kFallback;
     for (int d = 0; d < 6; d++) {
       for (int s = 0; s < ring; s++) {
         h = neighbor(h, direction(d), &rot);
-        if (h == kUnsupported) return -1;
+        if (h == 0) return kFallback;
         if (out) out[idx] = (int64_t)h;
         idx++;
+        if (is_pentagon(h)) return kFallback;
       }
     }
   }
   return idx;
 }
 
-// hexRing(h, k): 6k ids (1 for k = 0) in hexRing's order, or -1 (out of scope)
+// hexRing(h, k): 6k ids (1 for k = 0) in hexRing's order, or kFallback where H3-Java
+// throws PentagonEncounteredException
 MGPU_HD int64_t hex_ring(uint64_t h, int k, int64_t* out) {
   if (k == 0) {
     if (out) out[0] = (int64_t)h;
     return 1;
   }
-  if (pentagon_base(base_of(h))) return -1;
+  if (is_pentagon(h)) return kFallback;
   int rot = 0;
   for (int ring = 0; ring < k; ring++) {
     h = neighbor(h, kNextRing, &rot);
-    if (h == kUnsupported) return -1;
+    if (h == 0 || is_pentagon(h)) return kFallback;
   }
   const uint64_t first = h;
   int64_t idx = 0;
@@ -119,14 +165,113 @@ MGPU_HD int64_t hex_ring(uint64_t h, int k, int64_t* out) {
   for (int d = 0; d < 6; d++) {
     for (int s = 0; s < k; s++) {
       h = neighbor(h, direction(d), &rot);
-      if (h == kUnsupported) return -1;
+      if (h == 0) return kFallback;
       if (s != k - 1 || d != 5) {
         if (out) out[idx] = (int64_t)h;
         idx++;
+        if (is_pentagon(h)) return kFallback;
       }
     }
   }
-  return h == first ? idx : -1;
+  return h == first ? idx : kFallback;
+}
+
+// H3 C _kRingInternal from h with k rings into the hash set tab[max_kring(k)] (zeroed
+// here) with dist[] -- the same depth-first order as the recursion (an explicit stack of
+// depth k + 1: stk[], nxt[] of kMaxFallbackK + 2 entries).  Returns false if the set
+// overflowed (only possible with inconsistent tables; H3 would not terminate).
+constexpr int kMaxFallbackK = 64;
+MGPU_HD bool kring_hash(uint64_t h, int k, uint64_t* tab, int32_t* dist) {
+  const int64_t m = max_kring(k);
+  for (int64_t i = 0; i < m; i++) tab[i] = 0, dist[i] = 0;
+  uint64_t stk[kMaxFallbackK + 2];
+  int nxt[kMaxFallbackK + 2];
+  int depth = 0;
+  stk[0] = h;
+  nxt[0] = -1;
+  while (depth >= 0) {
+    if (nxt[depth] < 0) {  // visit stk[depth] at distance depth
+      const uint64_t c = stk[depth];
+      bool expand = false;
+      if (c != 0) {
+        int64_t off = (int64_t)(c % (uint64_t)m), probes = 0;
+        while (tab[off] != 0 && tab[off] != c) {
+          off = off + 1 == m ? 0 : off + 1;
+          if (++probes >= m) return false;
+        }
+        if (!(tab[off] == c && dist[off] <= depth)) {
+          tab[off] = c;
+          dist[off] = depth;
+          expand = depth < k;
+        }
+      }
+      if (!expand) {
+        depth--;
+        continue;
+      }
+      nxt[depth] = 0;
+    }
+    if (nxt[depth] < 6) {
+      int rot = 0;
+      const uint64_t child = neighbor(stk[depth], direction(nxt[depth]++), &rot);
+      depth++;
+      stk[depth] = child;
+      nxt[depth] = -1;
+    } else {
+      depth--;
+    }
+  }
+  return true;
+}
+
+// c into the open-addressing set tab[m] (keyed by c % m, as kring_hash)
+MGPU_HD void hash_insert(uint64_t* tab, int64_t m, uint64_t c) {
+  int64_t off = (int64_t)(c % (uint64_t)m);
+  for (int64_t probes = 0; probes < m && tab[off] != 0 && tab[off] != c; probes++) off = off + 1 == m ? 0 : off + 1;
+  if (tab[off] == 0) tab[off] = c;
+}
+
+// the rank of a cell id in a Scala 2.12 immutable.HashSet's iteration (the trie indexed
+// by 5-bit chunks of improve(##), lowest chunk first; ## of an H3 id = Long.hashCode)
+MGPU_HD uint64_t scala_set_rank(uint64_t v) {
+  uint32_t h = (uint32_t)(v ^ (v >> 32));
+  h = h + ~(h << 9);
+  h ^= h >> 14;
+  h += h << 4;
+  h ^= h >> 10;
+  uint64_t key = 0;  // 7 chunks of 5 bits, the lowest chunk most significant
+  for (int j = 0; j < 7; j++) key = (key << 5) | ((h >> (5 * j)) & 31u);
+  return key;
+}
+
+// kRing(h, k) entries of tab that kRing(h, k - 1) (tab2) lacks, in Scala HashSet order
+// (out, returns the count)
+MGPU_HD int64_t kloop_diff(const uint64_t* tab, int64_t m, const uint64_t* tab2, int64_t m2, int64_t* out) {
+  int64_t n = 0;
+  for (int64_t i = 0; i < m; i++) {
+    const uint64_t c = tab[i];
+    if (c == 0) continue;
+    int64_t off = (int64_t)(c % (uint64_t)m2), probes = 0;
+    bool inner = false;
+    while (tab2[off] != 0 && probes < m2) {
+      if (tab2[off] == c) {
+        inner = true;
+        break;
+      }
+      off = off + 1 == m2 ? 0 : off + 1;
+      probes++;
+    }
+    if (inner) continue;
+    // insertion by rank (the lists are ~6k long)
+    const uint64_t r = scala_set_rank(c);
+    int64_t j = n++;
+    while (j > 0 && scala_set_rank((uint64_t)out[j - 1]) > r) {
+      out[j] = out[j - 1];
+      j--;
+    }
+    out[j] = (int64_t)c;
+  }
+  return n;
 }
 
 // structural check of an H3 cell id (mode 1, res, base cell, digits 0..6 then 7s)

@@ -152,9 +152,27 @@ hipError_t launch_emit(const EmitArgs& e, int64_t n_tiles, hipStream_t s);
 int64_t format_chunks(int64_t n);
 hipError_t launch_format_cells(int is, const int64_t* cells, int64_t n, char* out, int64_t out_bytes,
                                int64_t* offsets, int64_t* chunk, unsigned long long* counters, hipStream_t s);
-// BNG kRing / kLoop lists: out[offsets[i] .. offsets[i + 1]) (written when within capacity)
-hipError_t launch_cell_kring(int is, const int64_t* cells, int64_t n, int k, int loop_only, int64_t* out, int64_t capacity,
-                            int64_t* offsets, int64_t* chunk, unsigned long long* counters, hipStream_t s);
+// kRing / kLoop lists (BNG; H3 with the pentagon fallbacks), in three steps:
+//   launch_kring_count     mc[i] = list length, -1 (invalid cell) or -2 (an H3 walk met a
+//                          pentagon; fb_idx lists those, counters[3] = their number),
+//                          chunk[] = the direct lists' sums per chunk
+//   launch_kring_fallback  those cells fb_idx[j0 .. j1) with H3's _kRingInternal / Mosaic's
+//                          kLoop set difference, kring_fallback_words(k) u64 of scratch per
+//                          cell (k <= kring_fallback_max_k()); write = 0: their lengths into
+//                          mc and chunk; write = 1 (after launch_kring_write): their lists
+//   launch_kring_write     chunk scan, offsets[n + 1], the direct lists at out[offsets[i]]
+//                          (written when within capacity)
+int64_t format_chunks(int64_t n);
+hipError_t launch_kring_count(int is, const int64_t* cells, int64_t n, int k, int loop_only, int64_t* mc,
+                              int64_t* chunk, uint32_t* fb_idx, unsigned long long* counters, hipStream_t s);
+int64_t kring_fallback_words(int k);
+int32_t kring_fallback_max_k();
+hipError_t launch_kring_fallback(const int64_t* cells, const uint32_t* fb_idx, int64_t j0, int64_t j1, int k,
+                                 int loop_only, int64_t* mc, int64_t* chunk, const int64_t* offsets, int64_t* out,
+                                 int64_t capacity, uint64_t* scratch, int write, unsigned long long* counters,
+                                 hipStream_t s);
+hipError_t launch_kring_write(int is, const int64_t* cells, int64_t n, int k, int loop_only, const int64_t* mc,
+                              int64_t* chunk, int64_t* offsets, int64_t* out, int64_t capacity, hipStream_t s);
 // counters[2] += chip rows outside [0, n_chips) (their out is -2)
 hipError_t launch_st_contains(const ChipTableView& t, const int64_t* row, const double* x, const double* y, int64_t n,
                               int8_t* out, unsigned long long* counters, hipStream_t s);

@@ -1764,29 +1764,43 @@ __device__ __forceinline__ int64_t cell_kring(int is, int64_t id, int k, bool lo
   if (is == MGPU_BNG) return bng_kring(id, k, loop_only, out);
   if (!h3ring::valid_cell((uint64_t)id)) return -1;
   const int64_t m = loop_only ? h3ring::hex_ring((uint64_t)id, k, out) : h3ring::kring((uint64_t)id, k, out);
-  return m < 0 ? -2 : m;
+  return m < 0 ? h3ring::kFallback : m;
 }
 
+// per cell: mc[i] = its list length, -1 (not a cell of the index system) or kFallback
+// (an H3 walk that met a pentagon: kring_fallback_kernel decides it); the fallback cells
+// are listed in fb_idx (counters[3] = their number); chunk_tot = the direct lists' sums
 __global__ __launch_bounds__(kFmtBlock) void kring_count_kernel(int is, const int64_t* __restrict__ cells, int64_t n, int k,
-                                                              int loop_only, int64_t* __restrict__ chunk_tot,
+                                                              int loop_only, int64_t* __restrict__ mc,
+                                                              int64_t* __restrict__ chunk_tot, uint32_t* __restrict__ fb_idx,
                                                               unsigned long long* __restrict__ counters) {
   __shared__ unsigned long long s_w[kFmtBlock / 64];
   const int64_t c0 = (int64_t)blockIdx.x * kFmtChunk;
+  const int lane = threadIdx.x & 63;
   unsigned long long sum = 0;
-  bool bad = false, unsup = false;
+  bool bad = false;
   for (int sl = 0; sl < kFmtSlices; sl++) {
     const int64_t i = c0 + sl * kFmtBlock + threadIdx.x;
+    bool fb = false;
     if (i < n) {
       const int64_t m = cell_kring(is, cells[i], k, loop_only != 0, nullptr);
+      mc[i] = m;
       sum += m < 0 ? 0ull : (unsigned long long)m;
       bad |= m == -1;
-      unsup |= m == -2;
+      fb = m == h3ring::kFallback;
+    }
+    const unsigned long long bal = __ballot(fb);
+    if (bal) {
+      const int leader = __ffsll((long long)bal) - 1;
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(&counters[3], (unsigned long long)__popcll(bal));
+      base = __shfl(base, leader, 64);
+      if (fb) fb_idx[base + __popcll(bal & ((1ull << lane) - 1ull))] = (uint32_t)i;
     }
   }
   count_wave(&counters[2], bad);
-  count_wave(&counters[3], unsup);
   sum = wave_sum_u64(sum);
-  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = sum;
+  if (lane == 0) s_w[threadIdx.x >> 6] = sum;
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long t = 0;
@@ -1795,8 +1809,73 @@ __global__ __launch_bounds__(kFmtBlock) void kring_count_kernel(int is, const in
   }
 }
 
+// The H3 cells whose walk met a pentagon, fb_idx[j0 .. j1), one thread each, with the
+// reference's fallbacks (h3_ring.h kring_hash / kloop_diff) in kring_fallback_words(k)
+// words of scratch per cell.  Count mode: mc[i] = -(length + 3), chunk_tot += length;
+// write mode: the list at out[offsets[i]] (when it fits the capacity).  counters[4] +=
+// walks whose hash set overflowed (inconsistent tables; never expected).
+__host__ __device__ constexpr int64_t kring_fb_words(int k) {
+  return 2 * (3 * (int64_t)k * (k + 1) + 1) + (3 * (int64_t)k * (k + 1) + 2) / 2 +
+         (k > 0 ? (3 * (int64_t)(k - 1) * k + 1) + (3 * (int64_t)(k - 1) * k + 2) / 2 : 0) + 2;
+}
+__global__ __launch_bounds__(64) void kring_fallback_kernel(const int64_t* __restrict__ cells, const uint32_t* __restrict__ fb_idx,
+                                                            int64_t j0, int64_t j1, int k, int loop_only,
+                                                            int64_t* __restrict__ mc, int64_t* __restrict__ chunk_tot,
+                                                            const int64_t* __restrict__ offsets, int64_t* __restrict__ out,
+                                                            int64_t capacity, uint64_t* __restrict__ scratch, int write,
+                                                            unsigned long long* __restrict__ counters) {
+  const int64_t j = j0 + (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (j >= j1) return;
+  const int64_t i = fb_idx[j];
+  const uint64_t h = (uint64_t)cells[i];
+  const int64_t m = h3ring::max_kring(k), m2 = k > 0 ? h3ring::max_kring(k - 1) : 1;
+  uint64_t* tab = scratch + (j - j0) * kring_fb_words(k);
+  int32_t* dist = (int32_t*)(tab + m);
+  uint64_t* tab2 = tab + m + (m + 1) / 2;
+  int32_t* dist2 = (int32_t*)(tab2 + m2);
+  int64_t* list = (int64_t*)(tab2 + m2 + (m2 + 1) / 2);
+  bool ok = true;
+  int64_t cnt = 0;
+  if (!loop_only) {  // (here the spiral failed: H3's _kRingInternal)
+    ok = h3ring::kring_hash(h, k, tab, dist);
+    for (int64_t q = 0; q < m; q++)
+      if (tab[q]) list[cnt++] = (int64_t)tab[q];
+  } else {
+    // kRing(h, k) and kRing(h, k - 1) as H3-Java gives them -- the spiral where it
+    // succeeds (its cells put into a hash set: toSet), else the hash-set walk
+    const int64_t ma = h3ring::kring(h, k, list);
+    if (ma >= 0) {
+      for (int64_t q = 0; q < m; q++) tab[q] = 0;
+      for (int64_t q = 0; q < ma; q++) h3ring::hash_insert(tab, m, (uint64_t)list[q]);
+    } else {
+      ok = h3ring::kring_hash(h, k, tab, dist);
+    }
+    const int64_t ms = h3ring::kring(h, k - 1, list);
+    if (ms >= 0) {
+      for (int64_t q = 0; q < m2; q++) tab2[q] = 0;
+      for (int64_t q = 0; q < ms; q++) h3ring::hash_insert(tab2, m2, (uint64_t)list[q]);
+    } else {
+      ok = ok && h3ring::kring_hash(h, k - 1, tab2, dist2);
+    }
+    cnt = ok ? h3ring::kloop_diff(tab, m, tab2, m2, list) : 0;
+  }
+  if (!ok) {
+    atomicAdd(&counters[4], 1ull);
+    cnt = 0;
+  }
+  if (!write) {
+    mc[i] = -(cnt + 3);
+    atomicAdd((unsigned long long*)&chunk_tot[i / kFmtChunk], (unsigned long long)cnt);
+    return;
+  }
+  const int64_t o = offsets[i];
+  if (o + cnt <= capacity)
+    for (int64_t q = 0; q < cnt; q++) out[o + q] = list[q];
+}
+
 __global__ __launch_bounds__(kFmtBlock) void kring_write_kernel(int is, const int64_t* __restrict__ cells, int64_t n, int k,
-                                                              int loop_only, const int64_t* __restrict__ chunk_off,
+                                                              int loop_only, const int64_t* __restrict__ mc,
+                                                              const int64_t* __restrict__ chunk_off,
                                                               int64_t* __restrict__ offsets, int64_t* __restrict__ out,
                                                               int64_t capacity) {
   __shared__ uint32_t s_w[kFmtBlock / 64];
@@ -1806,10 +1885,10 @@ __global__ __launch_bounds__(kFmtBlock) void kring_write_kernel(int is, const in
     const int64_t s0 = c0 + sl * kFmtBlock;
     if (s0 >= n) break;
     const int64_t i = s0 + threadIdx.x;
-    int64_t m = 0;
+    int64_t m = 0, v = 0;
     if (i < n) {
-      m = cell_kring(is, cells[i], k, loop_only != 0, nullptr);
-      if (m < 0) m = 0;
+      v = mc[i];
+      m = v >= 0 ? v : (v <= -3 ? -(v + 3) : 0);
     }
     uint32_t tot;
     const uint32_t ex = block_excl_scan((uint32_t)m, s_w, &tot);
@@ -1817,7 +1896,8 @@ __global__ __launch_bounds__(kFmtBlock) void kring_write_kernel(int is, const in
       const int64_t o = carry + ex;
       offsets[i] = o;
       if (i == n - 1) offsets[n] = o + m;
-      if (m && o + m <= capacity) cell_kring(is, cells[i], k, loop_only != 0, out + o);
+      // (fallback cells are written by kring_fallback_kernel in write mode)
+      if (v > 0 && o + m <= capacity) cell_kring(is, cells[i], k, loop_only != 0, out + o);
     }
     carry += tot;
   }
@@ -1825,15 +1905,35 @@ __global__ __launch_bounds__(kFmtBlock) void kring_write_kernel(int is, const in
 
 int64_t format_chunks(int64_t n) { return (n + kFmtChunk - 1) / kFmtChunk; }
 
-hipError_t launch_cell_kring(int is, const int64_t* cells, int64_t n, int k, int loop_only, int64_t* out, int64_t capacity,
-                            int64_t* offsets, int64_t* chunk, unsigned long long* counters, hipStream_t s) {
+hipError_t launch_kring_count(int is, const int64_t* cells, int64_t n, int k, int loop_only, int64_t* mc,
+                              int64_t* chunk, uint32_t* fb_idx, unsigned long long* counters, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kring_count_kernel, dim3((unsigned)format_chunks(n)), dim3(kFmtBlock), 0, s, is, cells, n, k,
+                     loop_only, mc, chunk, fb_idx, counters);
+  return hipGetLastError();
+}
+
+int64_t kring_fallback_words(int k) { return kring_fb_words(k); }
+int32_t kring_fallback_max_k() { return h3ring::kMaxFallbackK; }
+
+hipError_t launch_kring_fallback(const int64_t* cells, const uint32_t* fb_idx, int64_t j0, int64_t j1, int k,
+                                 int loop_only, int64_t* mc, int64_t* chunk, const int64_t* offsets, int64_t* out,
+                                 int64_t capacity, uint64_t* scratch, int write, unsigned long long* counters,
+                                 hipStream_t s) {
+  if (j1 <= j0) return hipSuccess;
+  if (k > h3ring::kMaxFallbackK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kring_fallback_kernel, dim3((unsigned)((j1 - j0 + 63) / 64)), dim3(64), 0, s, cells, fb_idx, j0, j1,
+                     k, loop_only, mc, chunk, offsets, out, capacity, scratch, write, counters);
+  return hipGetLastError();
+}
+
+hipError_t launch_kring_write(int is, const int64_t* cells, int64_t n, int k, int loop_only, const int64_t* mc,
+                              int64_t* chunk, int64_t* offsets, int64_t* out, int64_t capacity, hipStream_t s) {
   hipError_t e = hipMemsetAsync(offsets, 0, sizeof(int64_t), s);
   if (e != hipSuccess || n <= 0) return e;
   const int64_t nc = format_chunks(n);
-  hipLaunchKernelGGL(kring_count_kernel, dim3((unsigned)nc), dim3(kFmtBlock), 0, s, is, cells, n, k, loop_only, chunk,
-                     counters);
   hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScan), 0, s, chunk, nc);
-  hipLaunchKernelGGL(kring_write_kernel, dim3((unsigned)nc), dim3(kFmtBlock), 0, s, is, cells, n, k, loop_only, chunk,
+  hipLaunchKernelGGL(kring_write_kernel, dim3((unsigned)nc), dim3(kFmtBlock), 0, s, is, cells, n, k, loop_only, mc, chunk,
                      offsets, out, capacity);
   return hipGetLastError();
 }

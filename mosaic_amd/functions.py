@@ -104,8 +104,9 @@ def grid_pointascellid(points, resolution, index_system=None, ctx=None, stream=N
 
 def grid_cellkring(cells, k, index_system, loop_only=False, ctx=None, stream=None):
     """grid_cellkring / grid_cellkloop (CellKRing.scala:68, CellKLoop.scala:63 ->
-    IndexSystem.kRing / kLoop) over a device int64 column, on the GPU (BNG; H3 away
-    from the 12 pentagon base cells, else MosaicGpuError MGPU_E_UNSUPPORTED).  Returns
+    IndexSystem.kRing / kLoop) over a device int64 column, on the GPU (BNG and H3; H3
+    pentagon neighbourhoods in the reference's fallback order, for k <= 64, else
+    MosaicGpuError MGPU_E_UNSUPPORTED).  Returns
     (ids int64 tensor, offsets int64 tensor of n + 1): cell i's list is
     ids[offsets[i]:offsets[i + 1]], in the reference's order."""
     import ctypes

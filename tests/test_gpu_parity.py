@@ -188,37 +188,48 @@ def test_bng_kring_kloop_equal_oracle(gpu, res):
 H3_PENTAGON_BASE_CELLS = {4, 14, 24, 38, 49, 58, 63, 72, 83, 97, 107, 117}
 
 
+def h3_pentagon_cells(res):
+    """The 12 pentagons of a resolution: a pentagon base cell with every digit 0."""
+    unused = sum(7 << (3 * (15 - r)) for r in range(res + 1, 16))
+    return [(1 << 59) | (res << 52) | (b << 45) | unused for b in sorted(H3_PENTAGON_BASE_CELLS)]
+
+
+def assert_h3_rings_equal_oracle(gpu, cells, ks=(0, 1, 2, 4), tag=""):
+    I = M.H3IndexSystem()
+    cells = np.asarray(cells, dtype=np.int64)
+    for k in ks:
+        for loop in (False, True):
+            refs = [O.h3_k_loop(int(c), k) if loop else O.h3_k_ring(int(c), k) for c in cells]
+            ids, off = M.grid_cellkring(torch.from_numpy(cells).to(gpu), k, I, loop_only=loop)
+            ids, off = ids.cpu().numpy(), off.cpu().numpy()
+            for i, c in enumerate(cells):
+                assert [int(v) for v in ids[off[i]:off[i + 1]]] == refs[i], (tag, k, loop, hex(int(c)))
+
+
 @pytest.mark.parametrize("res", [1, 2, 3, 5, 7, 9, 11, 13, 15])
 def test_h3_kring_kloop_equal_oracle(gpu, res):
     """grid_cellkring / grid_cellkloop for H3 on the GPU == the oracle's restatement of
     H3IndexSystem.kRing / kLoop (H3IndexSystem.scala:182-205 -> H3 v3.7 kRing spiral /
-    hexRing), lists in order, on global cells whose k-neighbourhood stays among
-    hexagon base cells (the device's scope; base-cell crossings included).  Cells
-    reaching a pentagon base cell raise MosaicGpuError (MGPU_E_UNSUPPORTED); ids that
-    are no H3 cell raise IllegalArgumentException."""
+    hexRing), lists in order, on global cells -- base-cell crossings and pentagon
+    neighbourhoods included (the walks that meet a pentagon take H3's _kRingInternal
+    hash-set order, and kLoop Mosaic's kRing(k) diff kRing(k - 1) in Scala HashSet
+    order); ids that are no H3 cell raise IllegalArgumentException."""
     rng = np.random.default_rng(900 + res)
     lon = rng.uniform(-180, 180, 600)
     lat = np.degrees(np.arcsin(rng.uniform(-1, 1, 600)))
     cells = O.h3_points_to_cells(lon, lat, res).astype(np.int64)
-    I = M.H3IndexSystem()
-    for k in (0, 1, 2, 4):
-        inside = np.array([all(((x >> 45) & 127) not in H3_PENTAGON_BASE_CELLS for x in O.h3_k_ring(int(c), k + 1))
-                           for c in cells])
-        good = cells[inside]
-        if len(good) == 0:  # res 1, k = 4: every neighbourhood reaches a pentagon base cell
-            continue
-        for loop in (False, True):
-            refs = [O.h3_k_loop(int(c), k) if loop else O.h3_k_ring(int(c), k) for c in good]
-            ids, off = M.grid_cellkring(torch.from_numpy(good).to(gpu), k, I, loop_only=loop)
-            ids, off = ids.cpu().numpy(), off.cpu().numpy()
-            for i, c in enumerate(good):
-                assert [int(v) for v in ids[off[i]:off[i + 1]]] == refs[i], (res, k, loop, hex(int(c)))
-    pent = np.array([((int(c) >> 45) & 127) in H3_PENTAGON_BASE_CELLS for c in cells])
-    if pent.any():  # a cell of a pentagon base cell: outside the device path's scope
-        with pytest.raises(M.MosaicGpuError):
-            M.grid_cellkring(torch.from_numpy(cells[pent][:1]).to(gpu), 1, I)
+    assert_h3_rings_equal_oracle(gpu, cells, tag="global r%d" % res)
     with pytest.raises(M.IllegalArgumentException):
-        M.grid_cellkring(torch.tensor([1051200030000], dtype=torch.int64, device=gpu), 1, I)
+        M.grid_cellkring(torch.tensor([1051200030000], dtype=torch.int64, device=gpu), 1, M.H3IndexSystem())
+
+
+@pytest.mark.parametrize("res", [0, 1, 2, 4, 6, 9, 12, 15])
+def test_h3_kring_kloop_pentagons_equal_oracle(gpu, res):
+    """The 12 pentagons of a resolution and the cells of their 2-rings (polar pentagons
+    4 and 117 included): device == oracle for k = 0..4, ring and loop."""
+    pents = h3_pentagon_cells(res)
+    near = sorted({c for p in pents for c in O.h3_k_ring(p, 2)})
+    assert_h3_rings_equal_oracle(gpu, pents + near, ks=(0, 1, 2, 3, 4), tag="pentagons r%d" % res)
 
 
 def test_index_system_scalar_k_ring_k_loop(gpu):
