@@ -245,12 +245,15 @@ MGPU_HD uint64_t with_digit(uint64_t h, int r, int d) {
   int s = (kMaxRes - r) * 3;
   return (h & ~(7ULL << s)) | ((uint64_t)d << s);
 }
+// (no exit inside the loop: an early return here gave wrong per-lane results in waves
+// whose lanes took different paths, h3_ring.h)
 MGPU_HD int leading_nonzero(uint64_t h, int res) {
-  for (int r = 1; r <= res; r++) {
-    int d = digit_at(h, r);
-    if (d) return d;
+  int lead = 0;
+  for (int r = kMaxRes; r >= 1; r--) {
+    const int d = digit_at(h, r);
+    lead = (r <= res && d != 0) ? d : lead;
   }
-  return 0;
+  return lead;
 }
 MGPU_HD uint64_t rotate_ccw(uint64_t h, int res) {
   for (int r = 1; r <= res; r++) h = with_digit(h, r, rot60ccw(digit_at(h, r)));

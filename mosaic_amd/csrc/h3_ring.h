@@ -38,7 +38,26 @@ MGPU_HD uint64_t rotate_digits(uint64_t h, int n) {
 
 MGPU_HD uint64_t with_base(uint64_t h, int b) { return (h & ~(127ULL << 45)) | ((uint64_t)b << 45); }
 MGPU_HD bool polar_pentagon(int b) { return b == 4 || b == 117; }
-MGPU_HD bool is_pentagon(uint64_t h) { return pentagon_base(base_of(h)) && h3::leading_nonzero(h, res_of(h)) == 0; }
+// the first nonzero digit of resolutions 1..res (0: none), without an exit inside the
+// loop (lanes of a wave take different paths through these walks; early returns inside
+// loops gave wrong per-lane results in mixed waves on gfx950)
+MGPU_HD int lead_digit(uint64_t h, int res) {
+  int lead = 0;
+  for (int r = h3::kMaxRes; r >= 1; r--) {
+    const int d = (int)((h >> ((h3::kMaxRes - r) * 3)) & 7);
+    lead = (r <= res && d != 0) ? d : lead;
+  }
+  return lead;
+}
+// all digits rotated 60 degrees ccw / cw (unused digits 7 stay 7)
+MGPU_HD uint64_t rot_ccw(uint64_t h) { return rotate_digits(h, 1); }
+MGPU_HD uint64_t rot_cw(uint64_t h) { return rotate_digits(h, 5); }
+// H3 _h3RotatePent60ccw: ccw, and once more when the leading digit lands on K
+MGPU_HD uint64_t rot_pent_ccw(uint64_t h, int res) {
+  h = rot_ccw(h);
+  return lead_digit(h, res) == 1 ? rot_ccw(h) : h;
+}
+MGPU_HD bool is_pentagon(uint64_t h) { return pentagon_base(base_of(h)) && lead_digit(h, res_of(h)) == 0; }
 
 // H3 v3.7 h3NeighborRotations: the neighbour of h in direction dir (after *rotations
 // ccw rotations of dir), *rotations updated; 0 where H3 leaves it undefined (the
@@ -46,10 +65,15 @@ MGPU_HD bool is_pentagon(uint64_t h) { return pentagon_base(base_of(h)) && h3::l
 // NEW_DIGIT / NEW_ADJUSTMENT (_II for a Class III child resolution, _III for Class II)
 // until no step is carried; a step carried past resolution 1 crosses into the
 // neighbouring base cell, whose frame is reached by baseCellNeighbor60CCWRots rotations.
-MGPU_HD uint64_t neighbor(uint64_t h, int dir, int* rotations) {
+#if defined(MGPU_RING_NOINLINE) && defined(__HIP_DEVICE_COMPILE__)
+#define MGPU_RING_FN __host__ __device__ __attribute__((noinline))
+#else
+#define MGPU_RING_FN MGPU_HD
+#endif
+MGPU_RING_FN uint64_t neighbor(uint64_t h, int dir, int* rotations) {
   const int res = res_of(h);
   const int old_base = base_of(h);
-  const int old_lead = h3::leading_nonzero(h, res);
+  const int old_lead = lead_digit(h, res);
   for (int i = 0; i < *rotations; i++) dir = h3::rot60ccw(dir);
   int new_rot = 0;
   for (int r = res - 1;; r--) {
@@ -60,7 +84,7 @@ MGPU_HD uint64_t neighbor(uint64_t h, int dir, int* rotations) {
         // the deleted K vertex at the base-cell level: the edge borders the IK neighbour
         h = with_base(h, H3T_BASE_CELL_NEIGHBORS[old_base][5]);
         new_rot = H3T_BASE_CELL_NEIGHBOR_ROTS[old_base][5];
-        h = h3::rotate_ccw(h, res);
+        h = rot_ccw(h);
         *rotations += 1;
       }
       break;
@@ -80,30 +104,31 @@ MGPU_HD uint64_t neighbor(uint64_t h, int dir, int* rotations) {
     dir = next;
   }
   const int new_base = base_of(h);
+  bool undefined = false;
   if (pentagon_base(new_base)) {
     bool adjusted = false;
-    if (h3::leading_nonzero(h, res) == 1) {
+    if (lead_digit(h, res) == 1) {
       if (old_base != new_base) {
         // into the deleted K subsequence of a pentagon base cell from a neighbour
         const int f = H3T_BASE_CELL_DATA[old_base][0];
         const bool cw = H3T_BASE_CELL_DATA[new_base][5] == f || H3T_BASE_CELL_DATA[new_base][6] == f;
-        h = cw ? h3::rotate_cw(h, res) : h3::rotate_ccw(h, res);
+        h = cw ? rot_cw(h) : rot_ccw(h);
         adjusted = true;
       } else if (old_lead == 3) {  // from within the same pentagon
-        h = h3::rotate_ccw(h, res);
+        h = rot_ccw(h);
         *rotations += 1;
       } else if (old_lead == 5) {
-        h = h3::rotate_cw(h, res);
+        h = rot_cw(h);
         *rotations += 5;
       } else {
-        return 0;  // the K direction is deleted from here
+        undefined = true;  // the K direction is deleted from here
       }
     }
-    for (int i = 0; i < new_rot; i++) h = h3::rotate_pent_ccw(h, res);
-    if (old_base != new_base) {
+    for (int i = 0; i < new_rot && !undefined; i++) h = rot_pent_ccw(h, res);
+    if (old_base != new_base && !undefined) {
       if (polar_pentagon(new_base)) {
-        if (old_base != 118 && old_base != 8 && h3::leading_nonzero(h, res) != 3) *rotations += 1;
-      } else if (h3::leading_nonzero(h, res) == 5 && !adjusted) {
+        if (old_base != 118 && old_base != 8 && lead_digit(h, res) != 3) *rotations += 1;
+      } else if (lead_digit(h, res) == 5 && !adjusted) {
         *rotations += 1;
       }
     }
@@ -111,7 +136,7 @@ MGPU_HD uint64_t neighbor(uint64_t h, int dir, int* rotations) {
     h = rotate_digits(h, new_rot);
   }
   *rotations = (*rotations + new_rot) % 6;
-  return h;
+  return undefined ? 0 : h;
 }
 
 // J, JK, K, IK, I, IJ; rings start one step in I
@@ -122,27 +147,31 @@ constexpr int64_t kFallback = -2;  // the walk met a pentagon: take the referenc
 MGPU_HD int64_t max_kring(int k) { return 3 * (int64_t)k * (k + 1) + 1; }
 
 // kRing(h, k) in hexRangeDistances' spiral order: number of ids (written to out when
-// out != nullptr), or kFallback where hexRangeDistances fails (a pentagon)
+// out != nullptr), or kFallback where hexRangeDistances fails (a pentagon).  (Single
+// exit, no return inside the loops: lanes of a wave leave the walk at different steps.)
 MGPU_HD int64_t kring(uint64_t h, int k, int64_t* out) {
   int64_t idx = 0;
   if (out) out[idx] = (int64_t)h;
   idx++;
-  if (is_pentagon(h)) return kFallback;
+  bool fail = is_pentagon(h);
   int rot = 0;
-  for (int ring = 1; ring <= k; ring++) {
+  for (int ring = 1; ring <= k && !fail; ring++) {
     h = neighbor(h, kNextRing, &rot);
-    if (h == 0 || is_pentagon(h)) return kFallback;
-    for (int d = 0; d < 6; d++) {
-      for (int s = 0; s < ring; s++) {
+    fail = h == 0 || is_pentagon(h);
+    for (int d = 0; d < 6 && !fail; d++) {
+      for (int s = 0; s < ring && !fail; s++) {
         h = neighbor(h, direction(d), &rot);
-        if (h == 0) return kFallback;
-        if (out) out[idx] = (int64_t)h;
-        idx++;
-        if (is_pentagon(h)) return kFallback;
+        if (h == 0) {
+          fail = true;
+        } else {
+          if (out) out[idx] = (int64_t)h;
+          idx++;
+          fail = is_pentagon(h);
+        }
       }
     }
   }
-  return idx;
+  return fail ? kFallback : idx;
 }
 
 // hexRing(h, k): 6k ids (1 for k = 0) in hexRing's order, or kFallback where H3-Java
@@ -152,28 +181,31 @@ MGPU_HD int64_t hex_ring(uint64_t h, int k, int64_t* out) {
     if (out) out[0] = (int64_t)h;
     return 1;
   }
-  if (is_pentagon(h)) return kFallback;
+  bool fail = is_pentagon(h);
   int rot = 0;
-  for (int ring = 0; ring < k; ring++) {
+  for (int ring = 0; ring < k && !fail; ring++) {
     h = neighbor(h, kNextRing, &rot);
-    if (h == 0 || is_pentagon(h)) return kFallback;
+    fail = h == 0 || is_pentagon(h);
   }
   const uint64_t first = h;
   int64_t idx = 0;
-  if (out) out[idx] = (int64_t)h;
-  idx++;
-  for (int d = 0; d < 6; d++) {
-    for (int s = 0; s < k; s++) {
+  if (!fail) {
+    if (out) out[idx] = (int64_t)h;
+    idx++;
+  }
+  for (int d = 0; d < 6 && !fail; d++) {
+    for (int s = 0; s < k && !fail; s++) {
       h = neighbor(h, direction(d), &rot);
-      if (h == 0) return kFallback;
-      if (s != k - 1 || d != 5) {
+      if (h == 0) {
+        fail = true;
+      } else if (s != k - 1 || d != 5) {
         if (out) out[idx] = (int64_t)h;
         idx++;
-        if (is_pentagon(h)) return kFallback;
+        fail = is_pentagon(h);
       }
     }
   }
-  return h == first ? idx : kFallback;
+  return (fail || h != first) ? kFallback : idx;
 }
 
 // H3 C _kRingInternal from h with k rings into the hash set tab[max_kring(k)] (zeroed
