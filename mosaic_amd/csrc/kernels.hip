@@ -1415,6 +1415,7 @@ __global__ __launch_bounds__(kResolveBlock) void pip_resolve_kernel(JoinArgs a) 
 // (~3e3 per 1e8 points, coalesced chunks of 1024) and pair_emit_kernel adds the counts
 // of the tile's predecessors inside its group.  counters[0] = total pairs.
 constexpr int kScanBlock = 1024;
+constexpr int kScanLds = 24576;  // counts staged in LDS (96 KB): 1e8 points in 4096-point chunks
 __global__ __launch_bounds__(kScanBlock) void tile_scan_kernel(const uint32_t* __restrict__ gsum,
                                                                const uint32_t* __restrict__ gcand, int64_t ng,
                                                                uint64_t* __restrict__ goff,
@@ -1422,13 +1423,27 @@ __global__ __launch_bounds__(kScanBlock) void tile_scan_kernel(const uint32_t* _
   // thread i owns the contiguous run [i * per, (i + 1) * per): every load is issued
   // before the one workgroup scan of the run sums (a loop of block scans waits on each)
   __shared__ unsigned long long s_w[kScanBlock / 64];
+  __shared__ uint32_t s_v[kScanLds];          // the counts, loaded coalesced (ng <= kScanLds)
+  __shared__ unsigned long long s_base[kScanBlock];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t per = (ng + kScanBlock - 1) / kScanBlock;
   const int64_t b = threadIdx.x * per, e = b + per < ng ? b + per : ng;
   unsigned long long cand = 0, sum = 0;
-  for (int64_t i = b; i < e; i++) {
-    cand += gcand[i];
-    sum += gsum[i];
+  const bool lds = ng <= kScanLds;
+  if (lds) {
+    // coalesced loads (every count in flight at once), then each thread's contiguous run
+    // from LDS; offsets written back coalesced
+    for (int64_t i = threadIdx.x; i < ng; i += kScanBlock) {
+      cand += gcand[i];
+      s_v[i] = gsum[i];
+    }
+    __syncthreads();
+    for (int64_t i = b; i < e; i++) sum += s_v[i];
+  } else {
+    for (int64_t i = b; i < e; i++) {
+      cand += gcand[i];
+      sum += gsum[i];
+    }
   }
   cand = wave_sum_u64(cand);
   if (lane == 0 && cand) atomicAdd(&counters[3], cand);
@@ -1445,9 +1460,22 @@ __global__ __launch_bounds__(kScanBlock) void tile_scan_kernel(const uint32_t* _
     if (w < wave) run += s_w[w];
     tot += s_w[w];
   }
-  for (int64_t i = b; i < e; i++) {
-    goff[i] = run;
-    run += gsum[i];
+  if (lds) {
+    // s_v[i] = the offset of i within its thread's run (< 2^32), s_base = the run's base
+    s_base[threadIdx.x] = run;
+    uint32_t rel = 0;
+    for (int64_t i = b; i < e; i++) {
+      const uint32_t v = s_v[i];
+      s_v[i] = rel;
+      rel += v;
+    }
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < ng; i += kScanBlock) goff[i] = s_base[i / per] + s_v[i];
+  } else {
+    for (int64_t i = b; i < e; i++) {
+      goff[i] = run;
+      run += gsum[i];
+    }
   }
   if (threadIdx.x == 0) counters[0] = tot;
 }
