@@ -2011,6 +2011,17 @@ int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, 
 
 }  // extern "C"
 
+// The join's one host wait: the blocking hipStreamSynchronize, or (MGPU_SPIN=1) a spin on
+// the stream's completion (A/B switch: the blocking wake-up may cost the short C2 step tens of us)
+static hipError_t stream_wait(hipStream_t s) {
+  static const bool spin = getenv("MGPU_SPIN") && atoi(getenv("MGPU_SPIN")) == 1;
+  if (!spin) return hipStreamSynchronize(s);
+  hipError_t q;
+  while ((q = hipStreamQuery(s)) == hipErrorNotReady) {
+  }
+  return q;
+}
+
 // mgpu_pip_join with an optional validity bitmap of the points (the Arrow entry's nulls)
 static int32_t pip_join_sync(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
                              const double* y, const int64_t* point_id, int64_t point_id_base, int64_t n,
@@ -2022,7 +2033,7 @@ static int32_t pip_join_sync(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is,
   if (st) return st;
   unsigned long long h[8] = {0};
   HIP_TRY(hipMemcpyAsync(h, ctx->ws, sizeof h, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   if (out_n_pairs) *out_n_pairs = (int64_t)h[0];
   if (getenv("MGPU_DEBUG_COUNTERS")) {  // profiling builds (-DMGPU_STATS)
     unsigned long long d[16] = {0};
