@@ -2011,10 +2011,10 @@ int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, 
 
 }  // extern "C"
 
-// The join's one host wait: the blocking hipStreamSynchronize, or (MGPU_SPIN=1) a spin on
-// the stream's completion (A/B switch: the blocking wake-up may cost the short C2 step tens of us)
+// The join's one host wait: a spin on the stream's completion (MGPU_SPIN=0: the blocking
+// hipStreamSynchronize; its wake-up cost C2's 1.5 ms step 1.3-1.9%, profiles/r2_spin_ab.txt)
 static hipError_t stream_wait(hipStream_t s) {
-  static const bool spin = getenv("MGPU_SPIN") && atoi(getenv("MGPU_SPIN")) == 1;
+  static const bool spin = !(getenv("MGPU_SPIN") && atoi(getenv("MGPU_SPIN")) == 0);
   if (!spin) return hipStreamSynchronize(s);
   hipError_t q;
   while ((q = hipStreamQuery(s)) == hipErrorNotReady) {

@@ -122,10 +122,19 @@ def broadcast_host_blob(blob, src=0, group=None):
     rank = dist.get_rank(group)
     size = torch.tensor([len(blob) if rank == src else 0], dtype=torch.int64)
     dist.broadcast(size, src, group=group)
-    buf = torch.frombuffer(bytearray(blob), dtype=torch.uint8) if rank == src else \
-        torch.empty(int(size.item()), dtype=torch.uint8)
-    dist.broadcast(buf, src, group=group)
-    return bytes(buf.numpy().tobytes())
+    n = int(size.item())
+    # in pieces of at most 1 GiB: a single gloo broadcast of C3's 4.7 GB blob arrived
+    # truncated to its size modulo 2^32
+    out = np.empty(n, dtype=np.uint8) if rank != src else None
+    piece = 1 << 30
+    for off in range(0, n, piece):
+        m = min(piece, n - off)
+        if rank == src:
+            t = torch.from_numpy(np.frombuffer(blob, dtype=np.uint8, count=m, offset=off).copy())
+        else:
+            t = torch.from_numpy(out[off:off + m])
+        dist.broadcast(t, src, group=group)
+    return blob if rank == src else out.tobytes()
 
 
 def gather_offsets_host(local_count, group=None):
