@@ -95,7 +95,9 @@ def host_blob(table):
                                          table.wkb_offsets.ctypes.data, wkb.ctypes.data, ctypes.byref(p),
                                          ctypes.byref(nb)))
     try:
-        return ctypes.string_at(p.value, nb.value)
+        # (not ctypes.string_at: its size is a C int -- C3's 4.7 GB blob came back mod 2^32)
+        arr = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(int(nb.value),))
+        return arr.tobytes()
     finally:
         N.lib().mgpu_host_free(p)
 
@@ -123,8 +125,7 @@ def broadcast_host_blob(blob, src=0, group=None):
     size = torch.tensor([len(blob) if rank == src else 0], dtype=torch.int64)
     dist.broadcast(size, src, group=group)
     n = int(size.item())
-    # in pieces of at most 1 GiB: a single gloo broadcast of C3's 4.7 GB blob arrived
-    # truncated to its size modulo 2^32
+    # in pieces of at most 1 GiB (keeps every gloo message well inside 32-bit sizes)
     out = np.empty(n, dtype=np.uint8) if rank != src else None
     piece = 1 << 30
     for off in range(0, n, piece):
