@@ -7,10 +7,13 @@ the NYC taxi-zone bounding box, joined against the 263 NYC taxi zones
 tessellated at H3 resolution 9.  One step = one join (cell id -> chip probe -> is_core OR
 st_contains -> ordered pair output) over the GPU's resident points.
 
-Multi-GPU (torchrun, one process per GPU): points are sharded by contiguous id range
-(weak scaling: the per-GPU point count is fixed), the chip table is built on rank 0
-and replicated with one RCCL broadcast, per-rank pair counts are all-gathered (RCCL)
-for the global output offsets -- both through the C ABI (mgpu_comm_init,
+Multi-GPU (one process per GPU): `--gpus N` under torchrun (WORLD_SIZE set) runs as that
+rank; without WORLD_SIZE and N > 1 it starts the N ranks itself (child processes, before
+anything touches a GPU) and exits with their status -- never a 1-GPU line for N GPUs.
+Points are sharded by contiguous id range (weak scaling: the per-GPU point count is
+fixed), the chip table is built on rank 0 and replicated with one RCCL broadcast; every
+timed step ends with the RCCL all-gather of the per-rank pair counts (this rank's slice of
+the globally ordered output) -- both through the C ABI (mgpu_comm_init,
 mgpu_chips_broadcast, mgpu_pair_offsets; mosaic_amd/csrc/comm.cpp).  torch.distributed
 (gloo) is only the control plane: the RCCL unique id, the barriers and the max over
 ranks of the barrier-bracketed K steps.
@@ -196,16 +199,52 @@ def workload(a, W, M):
             "data": "synthetic (uniform points in the NYC zone bbox; real NYC taxi-zone polygons from the reference)"}
 
 
+def spawn_ranks(a):
+    """`--gpus N` without a launcher: start N ranks of this script (one per GPU, the
+    torchrun environment variables set, rendezvous on 127.0.0.1) and return the first
+    failing rank's status (the others are then stopped).  Nothing here touches a GPU:
+    counting devices does not initialise one on this stack."""
+    import socket
+    import subprocess
+    have = torch.cuda.device_count()
+    if have < a.gpus and os.environ.get("MGPU_DIST_BACKEND", "rccl") != "gloo":
+        print("--gpus %d: only %d GPUs visible" % (a.gpus, have), file=sys.stderr)
+        return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            st = p.poll()
+            if st is None:
+                continue
+            procs.remove(p)
+            if st != 0 and rc == 0:
+                rc = st
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     a = parse()
-    import mosaic_amd as M
-    from mosaic_amd import dist as D
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0 and a.gpus > 1:
+        sys.exit(spawn_ranks(a))
+    world = max(world, 1)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
+    if a.gpus != world:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (a.gpus, world))
+    import mosaic_amd as M
+    from mosaic_amd import dist as D
     # MGPU_DIST_BACKEND=gloo and more ranks than GPUs: a protocol rehearsal on a
     # 1-GPU box (never a measurement: the chip blob and the counts travel over gloo);
     # the real run is RCCL through the C ABI, one rank per GPU
@@ -247,8 +286,13 @@ def main():
     ctx.reserve(n)
 
     def step():
-        return M.pip_join(x, y, chips, a.res, index_system=isys, point_id_base=begin, out=(out_p, out_q),
-                          capacity=cap)
+        r = M.pip_join(x, y, chips, a.res, index_system=isys, point_id_base=begin, out=(out_p, out_q),
+                       capacity=cap)
+        # N > 1: this rank's slice of the globally ordered output (RCCL all-gather of the
+        # per-rank pair counts, mgpu_pair_offsets), part of every step
+        if world > 1:
+            r.offsets = D.gather_offsets_host(len(r)) if rehearsal else D.global_offsets(len(r), ctx)
+        return r
 
     log("points generated; warmup")
     for _ in range(a.warmup):
@@ -279,10 +323,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        if rehearsal:
-            off, total_pairs, _ = D.gather_offsets_host(pairs)
-        else:
-            off, total_pairs, _ = D.global_offsets(pairs, ctx)
+        off, total_pairs, _ = r.offsets
     else:
         total_pairs = pairs
 
@@ -323,7 +364,9 @@ def main():
         "config": {"workload": wl["workload"] % (n, a.res),
                    "points_per_gpu": n, "polygons": len(zones.poly_part_off) - 1, "chips": info["chips"],
                    "chip_cells": info["cells"], "index_system": isys.name, "resolution": a.res,
-                   "parallelism": "points sharded x%d, chip table replicated (RCCL broadcast)" % world},
+                   "parallelism": ("points sharded x%d, chip table replicated (%s)"
+                                   % (world, "gloo host blob: a protocol rehearsal, not a measurement" if rehearsal
+                                      else "RCCL broadcast") if world > 1 else "one GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": kernel, "kernel_ms": stream_ms,
@@ -338,10 +381,9 @@ def main():
         "pairs_per_gpu": pairs,
         "pairs_total": total_pairs,
         "near_ties": ties,
+        "libm_overrides": r.stats["libm_overrides"],
         "candidates_per_point": float(r.stats["n_candidates"]) / n,
     }
-    if os.environ.get("MGPU_ABLATE"):
-        out["ablate"] = os.environ["MGPU_ABLATE"]
     name = "pmc_join_traffic.json" if a.config == "c2" else "pmc_join_traffic_%s.json" % a.config
     prof = os.path.join(ROOT, "profiles", name)
     if os.path.exists(prof):

@@ -66,15 +66,24 @@ typedef struct mgpu_stats {
     float emit_kernel_ms;   /* split pipeline: tile_scan_kernel + split_emit_kernel;
                                binned pipeline: fix, count, scan and emit */
     int32_t pipeline;       /* MGPU_PIPELINE_FUSED, _SPLIT or _BINNED */
-    int32_t pad;
+    int32_t libm_overrides; /* near-tie cells the reference's libm placed differently from the
+                               device's correctly rounded route (the call was then completed
+                               with the reference's cells; h3_libm option) */
 } mgpu_stats;
 /* the join's three pipelines: one fused kernel per tile of points; for a chip
  * table with a pixel index, classify all points, resolve the mixed ones, emit; for a chip
  * table far larger than the caches, bin the points spatially (counting sort), join the
  * binned points, gather the answers back in input order */
+#define MGPU_PIPELINE_AUTO (-1)
 #define MGPU_PIPELINE_FUSED 0
 #define MGPU_PIPELINE_SPLIT 1
 #define MGPU_PIPELINE_BINNED 2
+
+/* H3 near-tie points (the few whose cell an ulp of libm can move): the reference's
+ * arithmetic -- H3-Java's JNI library on the host: platform glibc sin/cos/tan/acos/atan2,
+ * x87 long double -- or the device's correctly rounded route. */
+#define MGPU_LIBM_REFERENCE 0
+#define MGPU_LIBM_CORRECTLY_ROUNDED 1
 
 const char* mgpu_last_error(void);
 const char* mgpu_version(void);
@@ -86,6 +95,35 @@ int32_t mgpu_join_tile_points(void);
  * mgpu_comm_init, the RCCL communicator; destroyed with the context). */
 int32_t mgpu_ctx_create(int32_t device_id, mgpu_ctx** out);
 int32_t mgpu_ctx_destroy(mgpu_ctx* ctx);
+
+/* Per-context options (no reference counterpart: the reference's planner is Spark's).
+ * Nothing is read from the process environment; a JVM host sets these per context.
+ *   "h3_libm"         MGPU_LIBM_REFERENCE (default) / MGPU_LIBM_CORRECTLY_ROUNDED
+ *   "pipeline"        MGPU_PIPELINE_AUTO (default), or force _FUSED, _SPLIT (tables with a
+ *                     pixel index), _BINNED (whenever it applies, at any size)
+ *   "bin_count"       bins of the binned pipeline, 1..512 (default 64)
+ *   "bin_min_mb"      the planner bins for chip tables of at least this size (256)
+ *   "bin_min_points"  ... and batches of at least this many points (2^21)
+ *   "bin_xcd"         1 (default): binned tiles dealt to the 8 XCDs in contiguous runs
+ *   "spin_us"         synchronous calls poll their stream (yielding the core between polls)
+ *                     at most this long, then block in hipStreamSynchronize (default 2000;
+ *                     0 = block at once)
+ *   "raster", "raster_bng", "raster_sub", "raster_milli"
+ *                     the chip-table builder of mgpu_chips_upload on this context
+ *                     (mgpu_build_opts below)
+ * MGPU_E_INVALID_ARG for an unknown key or a value out of range. */
+int32_t mgpu_ctx_set_option(mgpu_ctx* ctx, const char* key, int64_t value);
+int32_t mgpu_ctx_get_option(const mgpu_ctx* ctx, const char* key, int64_t* value);
+
+/* Chip-table builder options (mgpu_chips_host_blob_ex; mgpu_chips_upload takes its
+ * context's).  raster: 1 = build the pixel index where it pays (H3 res >= 5), 0 = never;
+ * raster_bng: 1 = build it for BNG tables too (default 0: measured slower on C4);
+ * raster_sub: sub-pixels per mixed pixel edge (2..16, 0 = no second level; default 8);
+ * raster_milli: pixel edge / mean cell edge x 1000 (10..1000, default 250). */
+typedef struct mgpu_build_opts {
+    int32_t raster, raster_bng, raster_sub, raster_milli;
+} mgpu_build_opts;
+void mgpu_build_opts_default(mgpu_build_opts* opts);
 
 /* IndexSystem.getResolution for an integer resolution (H3IndexSystem.scala:45-60,
  * BNGIndexSystem.scala:349-360).  Returns MGPU_OK or MGPU_E_RESOLUTION. */
@@ -178,6 +216,9 @@ int32_t mgpu_chips_info(const mgpu_chips* chips, int64_t* n_chips, int64_t* n_ce
 int32_t mgpu_chips_host_blob(int32_t index_system, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
                              const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb, uint8_t** out,
                              int64_t* bytes);
+int32_t mgpu_chips_host_blob_ex(int32_t index_system, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
+                                const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb,
+                                const mgpu_build_opts* opts, uint8_t** out, int64_t* bytes);
 int32_t mgpu_host_free(void* p);
 int32_t mgpu_host_blob_info(const void* host_blob, int64_t bytes, int32_t* index_system, int64_t* n_chips,
                             int64_t* n_cells, int64_t* n_vertices);
@@ -224,7 +265,11 @@ int32_t mgpu_st_contains(mgpu_ctx* ctx, const mgpu_chips* chips, const int64_t* 
  * ascend, e.g. contiguous id shards).  point_id may be NULL: ids are
  * point_id_base + index.  Device pointers.  Synchronises `stream` to return the
  * pair count in *out_n_pairs; if it exceeds `capacity` only the first `capacity`
- * pairs are written and MGPU_E_CAPACITY is returned. */
+ * pairs are written and MGPU_E_CAPACITY is returned.
+ * H3 cells are the reference's bit for bit: the device decides every point outside a
+ * 2^-40 tie band around the cell boundaries; the few inside it (mgpu_stats.n_near_ties)
+ * are recomputed on the host with the reference's libm (option h3_libm), and when that
+ * moves a cell the join is rerun with the corrected cells (mgpu_stats.libm_overrides). */
 int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t index_system, int32_t res,
                       const double* x, const double* y, const int64_t* point_id, int64_t point_id_base,
                       int64_t n, int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id,
@@ -242,7 +287,8 @@ int32_t mgpu_pip_join_fetch(mgpu_ctx* ctx, int64_t capacity, int64_t* out_n_pair
 /* Asynchronous form: the pair count is left in device memory (*d_n_pairs, one
  * int64) and nothing synchronises -- graph-capturable once mgpu_ctx_reserve has
  * sized the workspace and one call of the same size has grown the split / binned
- * pipeline's buffers. */
+ * pipeline's buffers.  Without a host step, H3 near-ties keep the device's correctly
+ * rounded cells: mgpu_last_near_ties lists them for the caller to audit. */
 int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t index_system, int32_t res,
                             const double* x, const double* y, const int64_t* point_id, int64_t point_id_base,
                             int64_t n, int64_t capacity, int64_t* d_n_pairs, int64_t* out_point_id,
@@ -250,15 +296,12 @@ int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t inde
 int32_t mgpu_ctx_reserve(mgpu_ctx* ctx, int64_t max_points);
 
 /* Parity audit (no reference counterpart): the input positions of the H3 near-tie
- * points of the last call on `ctx` -- the only points where the device libm could
- * place a point in a different cell than the reference's H3-Java (glibc) path.
- * After mgpu_pip_join: the points the H3 route resolved inside its tie band
- * (mgpu_stats.n_near_ties).  After mgpu_points_to_cells: every point the fast
- * projection handed to the route (a superset).  Tests recompute exactly these points
- * with the CPU oracle at full bench sizes.  Unordered (ascending after a binned join,
- * whose queue holds binned slots mapped back here); at most 65536 are kept.
- * Synchronises the device.  MGPU_E_CAPACITY (with *out_n set) if cap is too small
- * or more than 65536 were found. */
+ * points of the last call on `ctx` (mgpu_pip_join, mgpu_points_to_cells, the geometry
+ * entries) -- the points the device's route resolved inside its tie band
+ * (mgpu_stats.n_near_ties), the only ones whose cell an ulp of libm can move; the
+ * synchronous calls gave each of them the reference's cell.  Ascending.  Synchronises
+ * the device.  MGPU_E_CAPACITY (with *out_n set) if cap is too small; MGPU_E_INTERNAL
+ * if an asynchronous join found more than the queue holds. */
 int32_t mgpu_last_near_ties(mgpu_ctx* ctx, int64_t* out_index, int64_t cap, int64_t* out_n);
 
 /* Host-pointer convenience form of mgpu_pip_join (copies points in, pairs out). */
@@ -303,6 +346,9 @@ int32_t mgpu_test_parse_number(const char* s, int32_t len, double* out);
  * emulated x87 long-double expressions), and point -> cell by the route alone. */
 int32_t mgpu_test_h3_elementary_host(int32_t fn, const double* a, const double* b, int64_t n, double* out);
 int32_t mgpu_test_h3_route_host(const double* lon, const double* lat, int64_t n, int32_t res, int64_t* out_cell);
+/* The near-tie resolver of the synchronous calls (h3_glibc.cpp: the reference's libm and
+ * x87 arithmetic) on n host points. */
+int32_t mgpu_test_h3_glibc_host(const double* lon, const double* lat, int64_t n, int32_t res, int64_t* out_cell);
 /* H3 cell geometry as the builder computes it (h3ToGeoBoundary / h3ToGeo, degrees):
  * out_lonlat[20 n] (up to 10 vertices per cell), out_nverts[n], out_center[2 n]. */
 int32_t mgpu_test_h3_boundary_host(const int64_t* cells, int64_t n, double* out_lonlat, int32_t* out_nverts,

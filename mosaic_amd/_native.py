@@ -39,13 +39,18 @@ EXPORTS = (
     "mgpu_pair_offsets", "mgpu_test_blob_contains_host", "mgpu_points_from_geometry", "mgpu_geometry_to_cells",
     "mgpu_geometry_to_cells_arrow", "mgpu_pip_join_arrow", "mgpu_test_parse_number", "mgpu_test_decode_point",
     "mgpu_test_h3_elementary_host", "mgpu_test_h3_route_host", "mgpu_test_h3_boundary_host",
+    "mgpu_ctx_set_option", "mgpu_ctx_get_option", "mgpu_build_opts_default", "mgpu_chips_host_blob_ex",
+    "mgpu_test_h3_glibc_host",
 )
 MGPU_GEOM_WKB = 0
 MGPU_GEOM_WKT = 1
 MGPU_COMM_ID_BYTES = 128
+MGPU_PIPELINE_AUTO = -1
 MGPU_PIPELINE_FUSED = 0
 MGPU_PIPELINE_SPLIT = 1
 MGPU_PIPELINE_BINNED = 2
+MGPU_LIBM_REFERENCE = 0
+MGPU_LIBM_CORRECTLY_ROUNDED = 1
 
 
 class MosaicGpuError(RuntimeError):
@@ -74,10 +79,16 @@ class MgpuStats(ctypes.Structure):
     _fields_ = [("n_points", ctypes.c_int64), ("n_pairs", ctypes.c_int64), ("n_near_ties", ctypes.c_int64),
                 ("n_candidates", ctypes.c_int64), ("kernel_ms", ctypes.c_float),
                 ("stream_kernel_ms", ctypes.c_float), ("mixed_kernel_ms", ctypes.c_float),
-                ("emit_kernel_ms", ctypes.c_float), ("pipeline", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("emit_kernel_ms", ctypes.c_float), ("pipeline", ctypes.c_int32), ("libm_overrides", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class BuildOpts(ctypes.Structure):
+    """mgpu_build_opts: the chip-table builder's pixel-index options."""
+    _fields_ = [("raster", ctypes.c_int32), ("raster_bng", ctypes.c_int32), ("raster_sub", ctypes.c_int32),
+                ("raster_milli", ctypes.c_int32)]
 
 
 _lib = None
@@ -150,6 +161,12 @@ def lib():
         "mgpu_test_h3_elementary_host": (I32, [I32, P, P, I64, P]),
         "mgpu_test_h3_route_host": (I32, [P, P, I64, I32, P]),
         "mgpu_test_h3_boundary_host": (I32, [P, I64, P, P, P]),
+        "mgpu_ctx_set_option": (I32, [P, ctypes.c_char_p, I64]),
+        "mgpu_ctx_get_option": (I32, [P, ctypes.c_char_p, ctypes.POINTER(I64)]),
+        "mgpu_build_opts_default": (None, [ctypes.POINTER(BuildOpts)]),
+        "mgpu_chips_host_blob_ex": (I32, [I32, I64, P, P, P, P, P, ctypes.POINTER(BuildOpts), ctypes.POINTER(P),
+                                          ctypes.POINTER(I64)]),
+        "mgpu_test_h3_glibc_host": (I32, [P, P, I64, I32, P]),
     }
     for name, (rt, args) in sig.items():
         f = getattr(L, name)

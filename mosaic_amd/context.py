@@ -6,6 +6,7 @@ and the config keys of package.scala:18-19 (index system, geometry API).  The
 geometry API is fixed to JTS semantics (GeometryAPI("JTS"), api/GeometryAPI.scala:125-131):
 that is what the chip predicates reproduce.
 """
+import contextlib
 import ctypes
 import threading
 
@@ -34,15 +35,43 @@ class GpuContext:
     def reserve(self, max_points):
         N.check(N.lib().mgpu_ctx_reserve(self.handle, int(max_points)))
 
+    def set_option(self, key, value):
+        """mgpu_ctx_set_option: the planner and tuning options of this context (keys in
+        include/mosaic_gpu.h: h3_libm, pipeline, bin_count, bin_min_mb, bin_min_points,
+        bin_xcd, spin_us, raster, raster_bng, raster_sub, raster_milli)."""
+        N.check(N.lib().mgpu_ctx_set_option(self.handle, key.encode(), int(value)))
+
+    def get_option(self, key):
+        v = ctypes.c_int64()
+        N.check(N.lib().mgpu_ctx_get_option(self.handle, key.encode(), ctypes.byref(v)))
+        return v.value
+
+    @contextlib.contextmanager
+    def options(self, **kw):
+        """Set options for the duration of a block, then restore them."""
+        old = {k: self.get_option(k) for k in kw}
+        try:
+            for k, v in kw.items():
+                self.set_option(k, v)
+            yield self
+        finally:
+            for k, v in old.items():
+                self.set_option(k, v)
+
     def last_near_ties(self):
         """Sorted input positions of the near-tie points of the last join / cell-id call
         on this context (mgpu_last_near_ties): the parity audit list."""
         import numpy as np
         n = ctypes.c_int64()
-        cap = 1 << 16
-        buf = np.zeros(cap, np.int64)
-        N.check(N.lib().mgpu_last_near_ties(self.handle, buf.ctypes.data, cap, ctypes.byref(n)))
-        return np.sort(buf[:n.value])
+        cap = 1 << 12
+        while True:
+            buf = np.zeros(cap, np.int64)
+            st = N.lib().mgpu_last_near_ties(self.handle, buf.ctypes.data, cap, ctypes.byref(n))
+            if st == N.MGPU_E_CAPACITY and n.value > cap:
+                cap = int(n.value)
+                continue
+            N.check(st)
+            return buf[:n.value]
 
     def close(self):
         if self.handle:

@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <sched.h>
 #include <array>
 #include <atomic>
 #include <cmath>
@@ -32,6 +34,7 @@
 #include "wkb.h"
 #include "capi_internal.h"
 #include "geom_decode.h"
+#include "h3_glibc.h"
 
 namespace {
 
@@ -648,23 +651,11 @@ bool hex_meets_quad(int64_t a, int64_t b, const double q[4][2], double d) {
   return true;
 }
 
-// pixel budget and size: MGPU_RASTER=0 disables the index; MGPU_RASTER_F = pixel edge
-// as a fraction of the cell edge (default 1/4); MGPU_RASTER_SUB = sub-pixels per mixed
-// pixel edge (default 8; 0: no second level)
-double raster_fraction() {
-  const char* s = getenv("MGPU_RASTER_F");
-  const double f = s ? atof(s) : 0.25;
-  return f > 0.01 && f <= 1.0 ? f : 0.25;
-}
-bool raster_enabled() {
-  const char* s = getenv("MGPU_RASTER");
-  return !(s && atoi(s) == 0);
-}
-int raster_sub_wanted() {
-  const char* s = getenv("MGPU_RASTER_SUB");
-  const int v = s ? atoi(s) : 8;
-  return v >= 2 && v <= 16 ? v : 0;
-}
+// pixel budget and size (mgpu_build_opts): raster = 0 disables the index; raster_milli =
+// pixel edge as a fraction of the cell edge (default 1/4); raster_sub = sub-pixels per
+// mixed pixel edge (default 8; 0: no second level)
+double raster_fraction(const mgpu_build_opts& o) { return o.raster_milli / 1000.0; }
+int raster_sub_wanted(const mgpu_build_opts& o) { return o.raster_sub >= 2 && o.raster_sub <= 16 ? o.raster_sub : 0; }
 constexpr int64_t kRasterMaxPixels = 1LL << 24;
 constexpr int64_t kRasterMaxSub = 1LL << 26;
 
@@ -812,14 +803,15 @@ uint64_t h3_rect_answer(const H3RasterCtx& X, double xa, double ya, double xb, d
 }
 
 bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const double bbox[4],
-                     const mgpu::DenseFace* dense, const std::vector<uint64_t>& grid, Raster& R) {
-  if (!raster_enabled() || res < 5 || !(bbox[2] - bbox[0] < 360.0) || grid.empty()) return false;
+                     const mgpu::DenseFace* dense, const std::vector<uint64_t>& grid, Raster& R,
+                     const mgpu_build_opts& bo) {
+  if (!bo.raster || res < 5 || !(bbox[2] - bbox[0] < 360.0) || grid.empty()) return false;
   const double W = bbox[2] - bbox[0], Hh = bbox[3] - bbox[1];
   if (!(W > 0) || !(Hh > 0)) return false;
   const double edge_deg = 1107.712591 / std::pow(mgpu::h3::kSqrt7, res) / 111.195;  // mean cell edge
   const double latc = std::max(std::fabs(bbox[1]), std::fabs(bbox[3]));
   if (latc > 80.0) return false;
-  double dyp = raster_fraction() * edge_deg, dxp = dyp / std::cos(latc * kPi / 180.0);
+  double dyp = raster_fraction(bo) * edge_deg, dxp = dyp / std::cos(latc * kPi / 180.0);
   double nxd = std::ceil(W / dxp), nyd = std::ceil(Hh / dyp);
   if (nxd * nyd > (double)kRasterMaxPixels) {
     const double s = std::sqrt(nxd * nyd / (double)kRasterMaxPixels) * 1.01;
@@ -863,7 +855,7 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
   }
   // level 2: the mixed pixels cut into S x S sub-pixels
   std::vector<uint64_t> a2;
-  const int S = raster_sub_wanted();
+  const int S = raster_sub_wanted(bo);
   std::vector<uint32_t> mixed;
   for (size_t i = 0; i < a1.size(); i++)
     if (a1[i] == kAnsMixed) mixed.push_back((uint32_t)i);
@@ -895,18 +887,15 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
   return true;
 }
 
-// (BNG: off unless MGPU_RASTER_BNG=1 -- its cell is a few integer operations and one grid
+// (BNG: off unless raster_bng = 1 -- its cell is a few integer operations and one grid
 // load already; on C4 the pixel lookups cost more than the point-in-polygon work they
 // save: split 2.55 ms vs fused 2.25 ms per 1e8 points)
 bool build_raster_bng(const mgpu::ChipTableView& hv, const mgpu::DenseFace& D, uint32_t edge,
-                      const std::vector<uint64_t>& grid, Raster& R) {
-  const char* on = getenv("MGPU_RASTER_BNG");
-  if (!(on && atoi(on) == 1)) return false;
-  if (!raster_enabled() || edge == 0 || grid.empty()) return false;
+                      const std::vector<uint64_t>& grid, Raster& R, const mgpu_build_opts& bo) {
+  if (!bo.raster_bng || !bo.raster || edge == 0 || grid.empty()) return false;
   // pixels per cell edge: the largest k <= 1 / fraction dividing the edge, within budget
-  // (BNG default: 2 -- a raster of 2 x 2 pixels per cell stays in L2 at C4's size)
-  const char* fs = getenv("MGPU_RASTER_F");
-  int kpc = fs ? (int)std::floor(1.0 / raster_fraction() + 1e-9) : 2;
+  // (default fraction 1/4 -> 2: a raster of 2 x 2 pixels per cell stays in L2 at C4's size)
+  int kpc = bo.raster_milli == 250 ? 2 : (int)std::floor(1.0 / raster_fraction(bo) + 1e-9);
   for (; kpc > 1; kpc--)
     if (edge % kpc == 0 && (double)D.w * kpc * D.h * kpc <= (double)kRasterMaxPixels) break;
   if (kpc < 2) return false;
@@ -934,8 +923,8 @@ bool build_raster_bng(const mgpu::ChipTableView& hv, const mgpu::DenseFace& D, u
   });
   // level 2: sub-pixels of whole metres, S = the largest divisor of the pixel edge <= 8
   int S = 0;
-  if (raster_sub_wanted())
-    for (int d = std::min<int>(raster_sub_wanted(), (int)R.pix); d >= 2; d--)
+  if (raster_sub_wanted(bo))
+    for (int d = std::min<int>(raster_sub_wanted(bo), (int)R.pix); d >= 2; d--)
       if (R.pix % d == 0) {
         S = d;
         break;
@@ -984,9 +973,8 @@ int32_t set_error(int32_t code, const char* fmt, ...) {
 namespace {
 
 // Workspace layout (each region 256-byte aligned):
-//   [counters 16 x u64] [near-tie queue u64 x (1 + kTieCap)] [tile_count u32 x T]
+//   [counters 16 x u64] [fast-path tie queue u64 x (1 + kTieCap)] [tile_count u32 x T]
 //   [tile_where u64 x T] [group_off u64 x T/32 (T)] [group_sum u32 x T/32] [dirty tiles u32 x T]
-//   [tile_pend u32 x T] [pending mixed-cell candidates u64 x T * pend cap]
 //   [records u64 x (T * slot records + pool)]
 // counters: [0] pairs [1] route near-ties [2] invalid points [3] candidates (tile_scan_kernel)
 //           [5] pool records used [6] dirty tiles (u32) [8..] MGPU_STATS
@@ -995,32 +983,28 @@ namespace {
 constexpr size_t kWsCounters = 128;  // 16 x u64
 
 struct WsLayout {
-  size_t count, where, off, gsum, dirty, ties, tpend, pend, recs, total;
+  size_t count, where, off, gsum, dirty, ties, recs, total;
 };
-// near-tie queue: mgpu_points_to_cells (overflow: the fix kernel redoes every point) and the
-// join's audit list (mgpu_last_near_ties)
+// mgpu_points_to_cells' queue of the points its fast projection hands to the H3 route
+// (overflow: the route pass redoes every point)
 constexpr int64_t kTieCap = 1 << 16;
 
 WsLayout ws_layout(int64_t n_tiles, int64_t pool) {
   WsLayout L;
   size_t T = (size_t)std::max<int64_t>(n_tiles, 1);
-  // the near-tie queue sits at a fixed offset (mgpu_last_near_ties reads it for any size)
   L.ties = align_up(kWsCounters, 256);
   L.count = align_up(L.ties + (size_t)(kTieCap + 1) * 8, 256);
   L.where = align_up(L.count + T * 4, 256);
   L.off = align_up(L.where + T * 8, 256);
   L.gsum = align_up(L.off + T * 8, 256);
   L.dirty = align_up(L.gsum + 2 * (T / 32 + 1) * 4, 256);  // group pair sums, group candidate sums
-  L.tpend = align_up(L.dirty + T * 4 * 4, 256);  // (the split pipeline's mixed tiles: 64 points)
-  L.pend = align_up(L.tpend + T * 4, 256);
-  L.recs = align_up(L.pend + T * (size_t)(mgpu::join_pend_cap() * mgpu::join_pend_words()) * 8, 256);
+  L.recs = align_up(L.dirty + T * 4 * 4, 256);  // (the split pipeline's mixed tiles: 64 points)
   L.total = align_up(L.recs + (T * (size_t)mgpu::join_slot_records() + (size_t)std::max<int64_t>(pool, 0)) * 8, 256);
   return L;
 }
 
 int32_t ensure_ws(mgpu_ctx* ctx, int64_t n_tiles, int64_t pool = 0) {
   ctx->last.valid = false;  // every call that uses the workspace ends the last join's lifetime
-  ctx->ties_binned = false;
   size_t need = ws_layout(n_tiles, pool).total;
   if (need <= ctx->ws_bytes) return MGPU_OK;
   if (ctx->ws) HIP_TRY(hipFree(ctx->ws));
@@ -1029,6 +1013,85 @@ int32_t ensure_ws(mgpu_ctx* ctx, int64_t n_tiles, int64_t pool = 0) {
   HIP_TRY(hipMalloc(&ctx->ws, need));
   ctx->ws_bytes = need;
   return MGPU_OK;
+}
+
+// The H3 route's near-tie queue (kernels.h JoinArgs.tie_queue): 2 header words, then
+// 4 words per record.  The head the synchronous calls copy back with the counters.
+constexpr int64_t kTqInit = 1 << 12;
+constexpr int64_t kTqHead = 64;
+constexpr size_t kPinWords = 16 + 2 + 4 * kTqHead;
+
+int32_t ensure_tq(mgpu_ctx* ctx, int64_t cap) {
+  if (cap <= ctx->tq_cap) return MGPU_OK;
+  if (ctx->tq) HIP_TRY(hipFree(ctx->tq));
+  ctx->tq = nullptr;
+  ctx->tq_cap = 0;
+  HIP_TRY(hipMalloc(&ctx->tq, (size_t)(2 + 4 * cap) * 8));
+  ctx->tq_cap = cap;
+  return MGPU_OK;
+}
+
+int32_t ensure_ovr(mgpu_ctx* ctx, int64_t words) {
+  if (words <= ctx->ovr_cap) return MGPU_OK;
+  if (ctx->ovr) HIP_TRY(hipFree(ctx->ovr));
+  ctx->ovr = nullptr;
+  ctx->ovr_cap = 0;
+  HIP_TRY(hipMalloc(&ctx->ovr, (size_t)words * 8));
+  ctx->ovr_cap = words;
+  return MGPU_OK;
+}
+
+// The synchronous calls' host wait (option spin_us): poll the stream, yielding the core
+// between polls, for at most spin_us, then block.  The poll saves the blocking wake-up
+// (1.3-1.9% of C2's 1.5 ms step, profiles/r2_spin_ab.txt); the bound keeps a long join
+// (or a stuck one) from holding a host core.
+hipError_t stream_wait(const mgpu_ctx* ctx, hipStream_t s) {
+  const int64_t us = ctx->opt.spin_us;
+  if (us > 0) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto lim = std::chrono::microseconds(us);
+    for (;;) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q != hipErrorNotReady) return q;
+      if (std::chrono::steady_clock::now() - t0 > lim) break;
+      sched_yield();
+    }
+  }
+  return hipStreamSynchronize(s);
+}
+
+// A near-tie record of the queue (kernels.h JoinArgs.tie_queue)
+struct TieRec {
+  int64_t pos;
+  double x, y;
+  uint64_t key;
+};
+
+// Records of the queue: the head from the pinned copy, the rest read back.
+int32_t read_ties(mgpu_ctx* ctx, int64_t n, std::vector<TieRec>& out) {
+  out.resize((size_t)n);
+  const uint64_t* head = ctx->pin + 16;
+  const int64_t nh = std::min(n, kTqHead);
+  if (nh) memcpy(out.data(), head + 2, (size_t)nh * 32);
+  if (n > nh) HIP_TRY(hipMemcpy(out.data() + nh, ctx->tq + 2 + 4 * nh, (size_t)(n - nh) * 32, hipMemcpyDeviceToHost));
+  return MGPU_OK;
+}
+
+// The reference's libm for the near-ties (h3_glibc.cpp); cells = true: keys are cell
+// ids, else lattice keys.  Returns the records whose answer differs as (pos, key),
+// sorted by position.
+std::vector<std::pair<int64_t, uint64_t>> libm_second_opinion(const std::vector<TieRec>& ties, int res, bool cells) {
+  std::vector<uint64_t> ref(ties.size());
+  mgpu::parallel_for((int64_t)ties.size(), 256, [&](int64_t b, int64_t e, int) {
+    for (int64_t k = b; k < e; k++)
+      ref[k] = cells ? mgpu::h3glibc::point_to_cell(ties[k].x, ties[k].y, res)
+                     : mgpu::h3glibc::lattice_key(ties[k].x, ties[k].y, res);
+  });
+  std::vector<std::pair<int64_t, uint64_t>> diff;
+  for (size_t k = 0; k < ties.size(); k++)
+    if (ref[k] != ties[k].key) diff.push_back({ties[k].pos, ref[k]});
+  std::sort(diff.begin(), diff.end());
+  return diff;
 }
 
 int32_t check_res(int32_t is, int32_t res) {
@@ -1066,13 +1129,15 @@ int32_t mgpu_ctx_create(int32_t device_id, mgpu_ctx** out) {
   HIP_TRY(hipSetDevice(device_id));
   mgpu_ctx* c = new mgpu_ctx();
   c->device = device_id;
-  HIP_TRY(hipEventCreate(&c->ev0));
-  HIP_TRY(hipEventCreate(&c->ev1));
-  HIP_TRY(hipEventCreate(&c->ev2));
-  HIP_TRY(hipEventCreate(&c->ev3));
-  int32_t st = ensure_ws(c, 1);
+  int32_t st = MGPU_OK;
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess ||
+      hipHostMalloc((void**)&c->pin, kPinWords * 8, hipHostMallocDefault) != hipSuccess)
+    st = fail(MGPU_E_DEVICE, "mgpu_ctx_create: events / pinned page");
+  if (!st) st = ensure_ws(c, 1);
+  if (!st) st = ensure_tq(c, kTqInit);
   if (st) {
-    delete c;
+    mgpu_ctx_destroy(c);
     return st;
   }
   *out = c;
@@ -1085,7 +1150,11 @@ int32_t mgpu_ctx_destroy(mgpu_ctx* ctx) {
   hipSetDevice(ctx->device);
   if (ctx->split_ws) hipFree(ctx->split_ws);
   if (ctx->bin_ws) hipFree(ctx->bin_ws);
+  if (ctx->scratch) hipFree(ctx->scratch);
+  if (ctx->tq) hipFree(ctx->tq);
+  if (ctx->ovr) hipFree(ctx->ovr);
   if (ctx->ws) hipFree(ctx->ws);
+  if (ctx->pin) hipHostFree(ctx->pin);
   if (ctx->ev0) hipEventDestroy(ctx->ev0);
   if (ctx->ev1) hipEventDestroy(ctx->ev1);
   if (ctx->ev2) hipEventDestroy(ctx->ev2);
@@ -1094,12 +1163,132 @@ int32_t mgpu_ctx_destroy(mgpu_ctx* ctx) {
   return MGPU_OK;
 }
 
+int32_t mgpu_ctx_set_option(mgpu_ctx* ctx, const char* key, int64_t v) {
+  if (!ctx || !key) return fail(MGPU_E_INVALID_ARG, "ctx/key is NULL");
+  mgpu_options& o = ctx->opt;
+  const std::string k = key;
+  auto bad = [&]() { return fail(MGPU_E_INVALID_ARG, "option %s: value %lld out of range", key, (long long)v); };
+  if (k == "h3_libm") {
+    if (v != MGPU_LIBM_REFERENCE && v != MGPU_LIBM_CORRECTLY_ROUNDED) return bad();
+    o.h3_libm = v;
+  } else if (k == "pipeline") {
+    if (v < MGPU_PIPELINE_AUTO || v > MGPU_PIPELINE_BINNED) return bad();
+    o.pipeline = v;
+  } else if (k == "bin_count") {
+    if (v < 1 || v > mgpu::bin_max()) return bad();
+    o.bin_count = v;
+  } else if (k == "bin_min_mb") {
+    if (v < 0) return bad();
+    o.bin_min_mb = v;
+  } else if (k == "bin_min_points") {
+    if (v < 0) return bad();
+    o.bin_min_points = v;
+  } else if (k == "bin_xcd") {
+    if (v != 0 && v != 1) return bad();
+    o.bin_xcd = v;
+  } else if (k == "spin_us") {
+    if (v < 0 || v > 10000000) return bad();
+    o.spin_us = v;
+  } else if (k == "raster" || k == "raster_bng") {
+    if (v != 0 && v != 1) return bad();
+    (k == "raster" ? o.raster : o.raster_bng) = v;
+  } else if (k == "raster_sub") {
+    if (!(v == 0 || (v >= 2 && v <= 16))) return bad();
+    o.raster_sub = v;
+  } else if (k == "raster_milli") {
+    if (v < 10 || v > 1000) return bad();
+    o.raster_milli = v;
+  } else {
+    return fail(MGPU_E_INVALID_ARG, "unknown option %s", key);
+  }
+  return MGPU_OK;
+}
+
+int32_t mgpu_ctx_get_option(const mgpu_ctx* ctx, const char* key, int64_t* v) {
+  if (!ctx || !key || !v) return fail(MGPU_E_INVALID_ARG, "NULL argument");
+  const mgpu_options& o = ctx->opt;
+  const std::pair<const char*, int64_t> all[] = {
+      {"h3_libm", o.h3_libm},       {"pipeline", o.pipeline}, {"bin_count", o.bin_count},
+      {"bin_min_mb", o.bin_min_mb}, {"bin_min_points", o.bin_min_points}, {"bin_xcd", o.bin_xcd},
+      {"spin_us", o.spin_us},       {"raster", o.raster},     {"raster_bng", o.raster_bng},
+      {"raster_sub", o.raster_sub}, {"raster_milli", o.raster_milli}};
+  for (const auto& kv : all)
+    if (strcmp(kv.first, key) == 0) {
+      *v = kv.second;
+      return MGPU_OK;
+    }
+  return fail(MGPU_E_INVALID_ARG, "unknown option %s", key);
+}
+
 int32_t mgpu_ctx_reserve(mgpu_ctx* ctx, int64_t max_points) {
   if (!ctx) return fail(MGPU_E_INVALID_ARG, "ctx is NULL");
   if (int32_t st = set_device(ctx->device)) return st;
   const int64_t tiles = mgpu::join_tiles(max_points);
-  return ensure_ws(ctx, tiles, max_points + tiles * mgpu::join_pend_cap());
+  return ensure_ws(ctx, tiles, max_points);
 }
+
+}  // extern "C"
+
+// IndexSystem.pointToIndex over a batch: the kernels (fast path + the H3 route for the
+// points it cannot decide), then -- H3 with the reference's libm -- the route's near-ties
+// recomputed on the host (h3_glibc.cpp) and the cells that moves written back.  A
+// near-tie queue that overflowed is grown and the call redone.
+static int32_t cells_impl(mgpu_ctx* ctx, int32_t is, int32_t res, const double* x, const double* y, int64_t n,
+                          int64_t* out_cell, hipStream_t s, const uint8_t* valid, int64_t voff, mgpu_stats* stats) {
+  auto* counters = (unsigned long long*)ctx->ws;
+  auto* ties = (unsigned long long*)((uint8_t*)ctx->ws + ws_layout(1, 0).ties);
+  int64_t n_ties = 0, n_fixed = 0;
+  for (int attempt = 0;; attempt++) {
+    HIP_TRY(hipMemsetAsync(counters, 0, kWsCounters, s));
+    HIP_TRY(hipMemsetAsync(ties, 0, 8, s));
+    HIP_TRY(hipMemsetAsync(ctx->tq, 0, 16, s));
+    HIP_TRY(hipEventRecord(ctx->ev0, s));
+    HIP_TRY(mgpu::launch_cells(is, res, x, y, n, out_cell, counters, ties, kTieCap, ctx->tq, ctx->tq_cap, s, valid, voff));
+    HIP_TRY(hipEventRecord(ctx->ev1, s));
+    // invalid coordinates must reach the caller as IllegalArgument / IllegalState, so the
+    // status is read back (the cell column itself stays on the device)
+    HIP_TRY(hipMemcpyAsync(ctx->pin, counters, 16 * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(ctx->pin + 16, ctx->tq, (2 + 4 * kTqHead) * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(stream_wait(ctx, s));
+    if (ctx->pin[2]) {
+      if (is == MGPU_BNG) return fail(MGPU_E_NAN, "NaN coordinates are not supported. (%llu points)", (unsigned long long)ctx->pin[2]);
+      return fail(MGPU_E_INVALID_ARG, "Latitude or longitude were invalid. (%llu points)", (unsigned long long)ctx->pin[2]);
+    }
+    n_ties = (int64_t)ctx->pin[16];
+    if (n_ties > ctx->tq_cap) {
+      if (attempt >= 2) return fail(MGPU_E_INTERNAL, "near-tie queue overflowed twice");
+      if (int32_t st = ensure_tq(ctx, n_ties + n_ties / 4 + 1024)) return st;
+      continue;
+    }
+    break;
+  }
+  if (stats) {
+    memset(stats, 0, sizeof *stats);
+    stats->n_points = n;
+    stats->n_near_ties = n_ties;
+    float ms = 0;
+    hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+    stats->kernel_ms = stats->stream_kernel_ms = ms;
+  }
+  if (is == MGPU_H3 && n_ties > 0 && ctx->opt.h3_libm == MGPU_LIBM_REFERENCE) {
+    std::vector<TieRec> tr;
+    if (int32_t st = read_ties(ctx, n_ties, tr)) return st;
+    const auto diff = libm_second_opinion(tr, res, true);
+    n_fixed = (int64_t)diff.size();
+    if (n_fixed) {
+      std::vector<int64_t> hv(2 * diff.size());
+      for (size_t k = 0; k < diff.size(); k++) hv[k] = diff[k].first, hv[diff.size() + k] = (int64_t)diff[k].second;
+      if (int32_t st = ensure_ovr(ctx, (int64_t)hv.size())) return st;
+      HIP_TRY(hipMemcpyAsync(ctx->ovr, hv.data(), hv.size() * 8, hipMemcpyHostToDevice, s));
+      HIP_TRY(mgpu::launch_scatter_i64((const int64_t*)ctx->ovr, (const int64_t*)ctx->ovr + n_fixed, n_fixed, out_cell, s));
+      HIP_TRY(stream_wait(ctx, s));
+    }
+  }
+  if (stats) stats->libm_overrides = (int32_t)n_fixed;
+  return MGPU_OK;
+}
+
+extern "C" {
 
 int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t is, int32_t res, const double* x, const double* y, int64_t n,
                              int64_t* out_cell, void* stream, mgpu_stats* stats) {
@@ -1107,35 +1296,8 @@ int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t is, int32_t res, const doubl
   if (int32_t r = check_res(is, res)) return r;
   if (n < 0 || (n > 0 && (!x || !y || !out_cell))) return fail(MGPU_E_INVALID_ARG, "bad point arrays");
   if (int32_t st = set_device(ctx->device)) return st;
-  hipStream_t s = (hipStream_t)stream;
   if (int32_t st = ensure_ws(ctx, 1)) return st;
-  auto* counters = (unsigned long long*)ctx->ws;
-  auto* ties = (unsigned long long*)((uint8_t*)ctx->ws + ws_layout(1, 0).ties);
-  HIP_TRY(hipMemsetAsync(counters, 0, kWsCounters, s));
-  HIP_TRY(hipMemsetAsync(ties, 0, 8, s));
-  HIP_TRY(hipEventRecord(ctx->ev0, s));
-  HIP_TRY(mgpu::launch_cells(is, res, x, y, n, out_cell, counters, ties, kTieCap, s));
-  HIP_TRY(hipEventRecord(ctx->ev1, s));
-  unsigned long long h[8] = {0};
-  // invalid coordinates must reach the caller as IllegalArgument / IllegalState,
-  // so the status is read back (the cell column itself stays on the device)
-  HIP_TRY(hipMemcpyAsync(h, counters, sizeof h, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  if (stats) {
-    stats->n_points = n;
-    stats->n_pairs = 0;
-    stats->n_near_ties = (int64_t)h[1];
-    stats->n_candidates = 0;
-    float ms = 0;
-    hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
-    stats->kernel_ms = ms;
-    stats->stream_kernel_ms = ms;
-  }
-  if (h[2]) {
-    if (is == MGPU_BNG) return fail(MGPU_E_NAN, "NaN coordinates are not supported. (%llu points)", h[2]);
-    return fail(MGPU_E_INVALID_ARG, "Latitude or longitude were invalid. (%llu points)", h[2]);
-  }
-  return MGPU_OK;
+  return cells_impl(ctx, is, res, x, y, n, out_cell, (hipStream_t)stream, nullptr, 0, stats);
 }
 
 int32_t mgpu_format_cells_device(mgpu_ctx* ctx, int32_t index_system, const int64_t* cells, int64_t n, char* out,
@@ -1176,14 +1338,14 @@ int32_t mgpu_grid_kring(mgpu_ctx* ctx, int32_t index_system, const int64_t* cell
   if (int32_t st = set_device(ctx->device)) return st;
   hipStream_t s = (hipStream_t)stream;
   if (int32_t st = ensure_ws(ctx, mgpu::join_tiles(n))) return st;
-  // workspace: counters, the chunk sums (tile_where region), per-cell counts mc[n] (the
-  // records region, >= 16 n bytes) and the fallback list fb_idx[n] (the pending region)
+  // workspace: counters, the chunk sums (tile_where region), per-cell counts mc[n] and the
+  // fallback list fb_idx[n] (the records region, >= 16 n bytes)
   const WsLayout L = ws_layout(mgpu::join_tiles(n), 0);
   auto* base = (uint8_t*)ctx->ws;
   auto* counters = (unsigned long long*)base;
   auto* chunk = (int64_t*)(base + L.where);
   auto* mc = (int64_t*)(base + L.recs);
-  auto* fb_idx = (uint32_t*)(base + L.pend);
+  auto* fb_idx = (uint32_t*)(base + L.recs + (size_t)std::max<int64_t>(n, 1) * 8);
   HIP_TRY(hipMemsetAsync(counters, 0, kWsCounters, s));
   HIP_TRY(mgpu::launch_kring_count(index_system, cells, n, k, loop_only, mc, chunk, fb_idx, counters, s));
   unsigned long long h[6] = {0};
@@ -1199,6 +1361,12 @@ int32_t mgpu_grid_kring(mgpu_ctx* ctx, int32_t index_system, const int64_t* cell
   // offsets) for the lists
   const int64_t n_fb = (int64_t)h[3];
   uint64_t* scratch = nullptr;
+  struct Free {  // the fallback scratch is freed on every return path
+    uint64_t*& p;
+    ~Free() {
+      if (p) hipFree(p);
+    }
+  } free_scratch{scratch};
   int64_t batch = 0;
   if (n_fb) {
     if (k > mgpu::kring_fallback_max_k())
@@ -1220,7 +1388,6 @@ int32_t mgpu_grid_kring(mgpu_ctx* ctx, int32_t index_system, const int64_t* cell
   HIP_TRY(hipMemcpyAsync(h, counters, sizeof h, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(&total, out_offsets + n, sizeof total, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  if (scratch) hipFree(scratch);
   if (out_total) *out_total = total;
   if (h[4])
     return fail(MGPU_E_INTERNAL, "grid_kring: %llu pentagon walks overflowed their hash set (inconsistent tables)", h[4]);
@@ -1262,7 +1429,7 @@ int32_t mgpu_points_to_cells_host(mgpu_ctx* ctx, int32_t is, int32_t res, const 
 // is by mgpu_chips_upload, evaluated in place by mgpu_test_chip_contains_host.
 static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
                           const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb,
-                          std::vector<uint8_t>& host, BlobHeader& hdr_out) {
+                          std::vector<uint8_t>& host, BlobHeader& hdr_out, const mgpu_build_opts& bo) {
   if (index_system != MGPU_H3 && index_system != MGPU_BNG)
     return fail(MGPU_E_INVALID_ARG, "unknown index system %d (0 = H3, 1 = BNG)", index_system);
   if (n_chips < 0 || n_chips > (int64_t)std::numeric_limits<int32_t>::max())
@@ -1440,8 +1607,8 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     hv.ring_env = geo.ring_env.data();
     hv.vtx = geo.vtx.data();
     bool ok = index_system == MGPU_H3
-                  ? build_raster_h3(hv, lres, mgpu::h3::k_of_res(lres), bbox, dense, grid, raster)
-                  : build_raster_bng(hv, dense[0], bng_edge, grid, raster);
+                  ? build_raster_h3(hv, lres, mgpu::h3::k_of_res(lres), bbox, dense, grid, raster, bo)
+                  : build_raster_bng(hv, dense[0], bng_edge, grid, raster, bo);
     if (!ok) raster = Raster{};
   }
   uint32_t cap = 16;
@@ -1524,18 +1691,6 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   hdr.raster_bshift = raster.bshift;
   hdr.raster_bnx = raster.bnx;
   hdr.raster_bny = raster.bny;
-  if (getenv("MGPU_RASTER_REPORT"))
-    fprintf(stderr, "mgpu raster: mode %d, %u x %u pixels, %zu classes, %.1f%% pure; %u x %u sub-pixels in %zu mixed pixels, "
-            "%.1f%% pure\n", raster.mode, raster.nx, raster.ny, raster.cls.size(),
-            raster.cells.empty() ? 0.0 : 100.0 * raster.n_pure / raster.cells.size(), raster.sub_n, raster.sub_n,
-            raster.sub_n ? raster.sub.size() / (raster.sub_n * raster.sub_n) : (size_t)0,
-            raster.sub.empty() ? 0.0 : 100.0 * std::count_if(raster.sub.begin(), raster.sub.end(), [](uint16_t v) {
-              return v != mgpu::kPixMixed; }) / raster.sub.size());
-  if (getenv("MGPU_RASTER_REPORT") && raster.bshift)
-    fprintf(stderr, "mgpu raster: %u x %u blocks of %u x %u pixels, %.1f%% uniform\n", raster.bnx, raster.bny,
-            1u << raster.bshift, 1u << raster.bshift,
-            100.0 * std::count_if(raster.blk.begin(), raster.blk.end(), [](uint16_t v) { return v != mgpu::kPixMixed; }) /
-                raster.blk.size());
   for (size_t k = 0; k < parts.size(); k++) {
     parts[k].off = total;
     hdr.off[k] = total;
@@ -1548,6 +1703,23 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     if (p.bytes) memcpy(host.data() + p.off, p.src, p.bytes);
   hdr_out = hdr;
   return MGPU_OK;
+}
+
+static int32_t check_build_opts(const mgpu_build_opts& o) {
+  if ((o.raster != 0 && o.raster != 1) || (o.raster_bng != 0 && o.raster_bng != 1) ||
+      !(o.raster_sub == 0 || (o.raster_sub >= 2 && o.raster_sub <= 16)) || o.raster_milli < 10 || o.raster_milli > 1000)
+    return fail(MGPU_E_INVALID_ARG, "build options out of range (raster %d, raster_bng %d, raster_sub %d, raster_milli %d)",
+                o.raster, o.raster_bng, o.raster_sub, o.raster_milli);
+  return MGPU_OK;
+}
+
+static mgpu_build_opts build_opts_of(const mgpu_ctx* ctx) {
+  mgpu_build_opts o;
+  o.raster = (int32_t)ctx->opt.raster;
+  o.raster_bng = (int32_t)ctx->opt.raster_bng;
+  o.raster_sub = (int32_t)ctx->opt.raster_sub;
+  o.raster_milli = (int32_t)ctx->opt.raster_milli;
+  return o;
 }
 
 // A blob header read back from memory: magic, version, sizes and array offsets checked.
@@ -1587,13 +1759,34 @@ int32_t adopt_device_blob(mgpu_ctx* ctx, void* dev_blob, int64_t bytes, mgpu_chi
 
 extern "C" {
 
+void mgpu_build_opts_default(mgpu_build_opts* o) {
+  if (!o) return;
+  o->raster = 1;
+  o->raster_bng = 0;
+  o->raster_sub = 8;
+  o->raster_milli = 250;
+}
+
 int32_t mgpu_chips_host_blob(int32_t index_system, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
                              const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb, uint8_t** out,
                              int64_t* bytes) {
+  return mgpu_chips_host_blob_ex(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, nullptr, out, bytes);
+}
+
+int32_t mgpu_chips_host_blob_ex(int32_t index_system, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
+                                const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb,
+                                const mgpu_build_opts* opts, uint8_t** out, int64_t* bytes) {
   if (!out || !bytes) return fail(MGPU_E_INVALID_ARG, "out/bytes is NULL");
+  mgpu_build_opts bo;
+  mgpu_build_opts_default(&bo);
+  if (opts) {
+    if (int32_t st = check_build_opts(*opts)) return st;
+    bo = *opts;
+  }
   std::vector<uint8_t> host;
   BlobHeader hdr;
-  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr)) return st;
+  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr, bo))
+    return st;
   uint8_t* p = (uint8_t*)malloc(host.size());
   if (!p) return fail(MGPU_E_INTERNAL, "out of host memory (%zu bytes)", host.size());
   memcpy(p, host.data(), host.size());
@@ -1642,7 +1835,8 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
   if (!ctx || !out) return fail(MGPU_E_INVALID_ARG, "ctx/out is NULL");
   std::vector<uint8_t> host;
   BlobHeader hdr;
-  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr))
+  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr,
+                              build_opts_of(ctx)))
     return st;
   return mgpu_chips_upload_blob(ctx, host.data(), (int64_t)host.size(), out);
 }
@@ -1712,16 +1906,15 @@ int32_t mgpu_st_contains(mgpu_ctx* ctx, const mgpu_chips* chips, const int64_t* 
 // ------------------------------------------------------------------ join
 
 // The binned pipeline's planner (kernels.h BinArgs): a chip table far larger than the
-// caches and a large batch of points.  MGPU_BIN=0 never, =1 whenever it applies (tests),
-// default: tables of at least MGPU_BIN_MIN_MB (256 MB -- the Infinity Cache) and batches
-// of at least 2^21 points.  The bins tile the chip table's extent (H3: the lon/lat box
-// of the chip cells; BNG: the dense grid's box), about MGPU_BIN_N of them (default 64),
-// roughly square on the ground.
-static bool plan_bins(const mgpu_chips* chips, int32_t is, int32_t res, int64_t n, const uint8_t* valid,
-                      const mgpu::JoinArgs& a, mgpu::BinArgs& b) {
-  const char* on = getenv("MGPU_BIN");
-  const int mode = on ? atoi(on) : -1;
-  if (mode == 0 || n <= 0 || valid || !a.res_match || a.ablate != 0) return false;
+// caches and a large batch of points.  Option pipeline = MGPU_PIPELINE_BINNED forces it
+// whenever it applies; auto takes it for tables of at least bin_min_mb (256 MB -- the
+// Infinity Cache) and batches of at least bin_min_points (2^21).  The bins tile the chip
+// table's extent (H3: the lon/lat box of the chip cells; BNG: the dense grid's box),
+// about bin_count of them (default 64), roughly square on the ground.
+static bool plan_bins(const mgpu_options& o, const mgpu_chips* chips, int32_t is, int32_t res, int64_t n,
+                      const uint8_t* valid, const mgpu::JoinArgs& a, mgpu::BinArgs& b) {
+  const bool forced = o.pipeline == MGPU_PIPELINE_BINNED;
+  if (!(forced || o.pipeline == MGPU_PIPELINE_AUTO) || n <= 0 || valid || !a.res_match) return false;
   if (n >= (int64_t)1 << 32 || chips->view.max_cell_chips > 32) return false;
   const mgpu::ChipTableView& v = chips->view;
   double x0, y0, W, H, aspect;
@@ -1739,28 +1932,24 @@ static bool plan_bins(const mgpu_chips* chips, int32_t is, int32_t res, int64_t 
     aspect = W / std::max(H, 1e-12);
   }
   if (!(W > 0) || !(H > 0)) return false;
-  if (mode != 1) {
-    const char* mb = getenv("MGPU_BIN_MIN_MB");
-    const double min_bytes = (mb ? atof(mb) : 256.0) * 1048576.0;
-    if ((double)chips->bytes < min_bytes || n < ((int64_t)1 << 21)) return false;
-  }
-  const char* nbs = getenv("MGPU_BIN_N");
-  const int nb = std::min(std::max(nbs ? atoi(nbs) : 64, 1), (int)mgpu::bin_max());
+  if (!forced && ((double)chips->bytes < (double)o.bin_min_mb * 1048576.0 || n < o.bin_min_points)) return false;
+  const int nb = (int)std::min<int64_t>(std::max<int64_t>(o.bin_count, 1), mgpu::bin_max());
   int nbx = (int)std::lround(std::sqrt(nb * aspect));
   nbx = std::min(std::max(nbx, 1), nb);
   const int nby = std::max(nb / nbx, 1);
   b.x0 = x0, b.y0 = y0;
   b.nbx = nbx, b.nby = nby;
   b.inv_bx = nbx / W, b.inv_by = nby / H;
-  const char* xcd = getenv("MGPU_BIN_XCD");
-  b.xcd_runs = xcd ? atoi(xcd) : 1;
+  b.xcd_runs = (int32_t)o.bin_xcd;
   return true;
 }
 
+// Launch one join on `s` (nothing waits here).  n_ovr > 0: the route's near-ties take
+// the first n_ovr libm overrides of ctx->ovr (ascending input positions, lattice keys).
 static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
                          const double* y, const int64_t* point_id, int64_t id_base, int64_t n, int64_t capacity,
                          int64_t* out_point, int32_t* out_poly, hipStream_t s, bool timed,
-                         const uint8_t* valid = nullptr, int64_t valid_off = 0) {
+                         const uint8_t* valid = nullptr, int64_t valid_off = 0, int64_t n_ovr = 0) {
   if (!ctx || !chips) return fail(MGPU_E_INVALID_ARG, "ctx/chips is NULL");
   if (int32_t r = check_res(is, res)) return r;
   if (chips->index_system != is)
@@ -1771,14 +1960,13 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   if (capacity < 0 || (capacity > 0 && (!out_point || !out_poly))) return fail(MGPU_E_INVALID_ARG, "bad output arrays");
   if (int32_t st = set_device(ctx->device)) return st;
   int64_t tiles = mgpu::join_tiles(n);
-  // pool: the records of tiles with more pairs than points (bounded by the capacity;
-  // a total beyond it is reported as MGPU_E_CAPACITY either way)
-  // (+ room for the tentative records of deferred mixed-cell candidates, so exhausting
-  // the pool still implies a total beyond the capacity)
-  const int64_t pool = capacity + tiles * mgpu::join_pend_cap();
+  // pool: the records of tiles with more pairs than points (bounded by the capacity; a
+  // total beyond it is reported as MGPU_E_CAPACITY either way)
+  const int64_t pool = capacity;
   if (int32_t st = ensure_ws(ctx, tiles, pool)) return st;
   auto* base = (uint8_t*)ctx->ws;
   const WsLayout L = ws_layout(tiles, pool);
+  const mgpu_options& o = ctx->opt;
   mgpu::JoinArgs a;
   a.x = x;
   a.y = y;
@@ -1795,15 +1983,13 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   a.tile_count = (uint32_t*)(base + L.count);
   a.tile_where = (uint64_t*)(base + L.where);
   a.recs = (uint64_t*)(base + L.recs);
-  a.tile_pend = (uint32_t*)(base + L.tpend);
-  a.pend = (uint64_t*)(base + L.pend);
-  {
-    const char* ab = getenv("MGPU_ABLATE");  // profiling switch, never set in production runs
-    a.ablate = ab ? atoi(ab) : 0;
-  }
+  a.tie_queue = ctx->tq;
+  a.tie_cap = ctx->tq_cap;
+  a.ovr = ctx->ovr;
+  a.n_ovr = n_ovr;
+  a.pos_of = nullptr;
   mgpu::EmitArgs e;
   e.tile_count = a.tile_count;
-  e.tile_dead = a.tile_pend;
   e.group_off = (uint64_t*)(base + L.off);
   a.group_sum = (uint32_t*)(base + L.gsum);
   a.group_cand = a.group_sum + (tiles / 32 + 1);
@@ -1814,8 +2000,6 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   e.capacity = capacity;
   e.out_point = out_point;
   e.out_poly = out_poly;
-  a.ties = (unsigned long long*)(base + L.ties);
-  a.tie_cap = kTieCap;
   a.valid = valid;
   a.valid_off = valid_off;
   a.mixed_idx = nullptr;
@@ -1823,21 +2007,20 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   a.chunk_mixed = nullptr;
   a.poly_answers = 0;
   HIP_TRY(hipMemsetAsync(base, 0, kWsCounters, s));
-  HIP_TRY(hipMemsetAsync(base + L.ties, 0, 8, s));
+  HIP_TRY(hipMemsetAsync(ctx->tq, 0, 16, s));
   // the split pipeline (kernels.h SplitArgs) when the chip table has a pixel index for
-  // this resolution and no cell holds more than 32 chips (MGPU_SPLIT=0: always fused)
-  const char* sp = getenv("MGPU_SPLIT");
-  const bool split = !(sp && atoi(sp) == 0) && n > 0 && chips->view.raster_mode != mgpu::kRasterNone && a.res_match &&
-                     (is == MGPU_H3 || res == chips->view.res) && chips->view.max_cell_chips <= 32 &&
-                     (a.ablate == 0 || a.ablate >= 10);  // (>= 10: split-pipeline profiling switches)
+  // this resolution and no cell holds more than 32 chips
+  const bool split = (o.pipeline == MGPU_PIPELINE_AUTO || o.pipeline == MGPU_PIPELINE_SPLIT) && n > 0 &&
+                     chips->view.raster_mode != mgpu::kRasterNone && a.res_match &&
+                     (is == MGPU_H3 || res == chips->view.res) && chips->view.max_cell_chips <= 32;
   mgpu::SplitArgs sa{};
   if (split) {
     const int64_t nc = mgpu::split_chunks(n), C = mgpu::split_chunk();
     size_t off = 0;
     auto carve = [&](size_t bytes) {
-      const size_t o = off;
+      const size_t o_ = off;
       off = align_up(off + bytes, 256);
-      return o;
+      return o_;
     };
     const size_t o_codes = carve((size_t)nc * C * 4), o_idx = carve((size_t)nc * C * 2), o_res = carve((size_t)nc * C * 8);
     const size_t o_pairs = carve(nc * 4), o_mixed = carve(nc * 4), o_cand = carve(nc * 4), o_off = carve(nc * 8);
@@ -1868,15 +2051,15 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     HIP_TRY(hipMemsetAsync(a.group_cand, 0, nc * 4, s));
   }
   mgpu::BinArgs ba{};
-  const bool binned = !split && plan_bins(chips, is, res, n, valid, a, ba);
+  const bool binned = !split && plan_bins(o, chips, is, res, n, valid, a, ba);
   if (binned) {
     const int64_t nc = mgpu::split_chunks(n), C = mgpu::split_chunk();
     const int64_t K = mgpu::bin_chunks(n), G = mgpu::bin_groups(n), nb = (int64_t)ba.nbx * ba.nby;
     size_t off = 0;
     auto carve = [&](size_t bytes) {
-      const size_t o = off;
+      const size_t o_ = off;
       off = align_up(off + bytes, 256);
-      return o;
+      return o_;
     };
     const size_t o_perm = carve((size_t)n * 4), o_rorig = carve((size_t)n * 8);
     const size_t o_bx = carve((size_t)n * 8), o_by = carve((size_t)n * 8), o_slot = carve((size_t)n * 4),
@@ -1907,6 +2090,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     j.mixed_idx = nullptr;
     j.chunk_mixed = nullptr;
     j.poly_answers = 1;
+    j.pos_of = ba.perm;
     j.mixed_res = (uint64_t*)(bb + o_res);
     j.group_sum = (uint32_t*)(bb + o_gperm);
     j.group_cand = (uint32_t*)(bb + o_gcand);
@@ -1919,7 +2103,6 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     ba.s.out_point = out_point;
     ba.s.out_poly = out_poly;
     HIP_TRY(hipMemsetAsync(bb + o_gperm, 0, align_up(nc * 4, 256) + nc * 4, s));  // group_sum, group_cand
-    ctx->ties_binned = true;
   } else if (!split) {
     HIP_TRY(hipMemsetAsync(base + L.gsum, 0, 2 * ((size_t)tiles / 32 + 1) * 4, s));
   }
@@ -1948,6 +2131,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   L2.pts_valid_off = valid_off;
   L2.emit = e;
   L2.n_tiles = tiles;
+  L2.n_ovr = n_ovr;
   L2.pool_ok = false;
   L2.total = -1;
   L2.valid = true;
@@ -1957,43 +2141,21 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
 int32_t mgpu_last_near_ties(mgpu_ctx* ctx, int64_t* out_index, int64_t cap, int64_t* out_n) {
   if (!ctx || !out_n || cap < 0 || (cap > 0 && !out_index)) return fail(MGPU_E_INVALID_ARG, "bad arguments");
   *out_n = 0;
-  if (!ctx->ws) return MGPU_OK;
+  if (!ctx->tq) return MGPU_OK;
   if (int32_t st = set_device(ctx->device)) return st;
-  // the queue sits at the same offset for every workspace size (ws_layout)
-  const size_t off = ws_layout(1, 0).ties;
-  unsigned long long cnt = 0;
+  uint64_t cnt = 0;
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(&cnt, (uint8_t*)ctx->ws + off, 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&cnt, ctx->tq, 8, hipMemcpyDeviceToHost));
   const int64_t n = (int64_t)cnt;
   *out_n = n;
-  if (n > kTieCap) return fail(MGPU_E_CAPACITY, "%lld near-tie points: more than the %lld kept", (long long)n,
-                               (long long)kTieCap);
+  if (n > ctx->tq_cap)
+    return fail(MGPU_E_INTERNAL, "%lld near-tie points: more than the queue of an asynchronous join holds (%lld)",
+                (long long)n, (long long)ctx->tq_cap);
   if (n > cap) return fail(MGPU_E_CAPACITY, "%lld near-tie points, capacity %lld", (long long)n, (long long)cap);
-  if (n) HIP_TRY(hipMemcpy(out_index, (uint8_t*)ctx->ws + off + 8, (size_t)n * 8, hipMemcpyDeviceToHost));
-  if (n && ctx->ties_binned && ctx->last.binned) {
-    // a binned join queued binned slots: their input positions, by a search over slot[]
-    // (only here, never on the join's path), ascending
-    const mgpu::BinArgs& b = ctx->last.bargs;
-    std::vector<uint32_t> ts(n);
-    for (int64_t k = 0; k < n; k++) ts[k] = (uint32_t)out_index[k];
-    std::sort(ts.begin(), ts.end());
-    ts.erase(std::unique(ts.begin(), ts.end()), ts.end());
-    const int64_t nt = (int64_t)ts.size();
-    uint32_t* dts = nullptr;
-    int64_t* dout = nullptr;
-    HIP_TRY(hipMalloc(&dts, nt * 4));
-    HIP_TRY(hipMalloc(&dout, nt * 8));
-    HIP_TRY(hipMemcpy(dts, ts.data(), nt * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(dout, 0xFF, nt * 8));
-    HIP_TRY(mgpu::launch_bin_unslot(b.slot, b.s.j.n, dts, nt, dout, nullptr));
-    std::vector<int64_t> pos(nt);
-    HIP_TRY(hipMemcpy(pos.data(), dout, nt * 8, hipMemcpyDeviceToHost));
-    hipFree(dts);
-    hipFree(dout);
-    std::sort(pos.begin(), pos.end());
-    for (int64_t k = 0; k < nt; k++) out_index[k] = pos[k];
-    *out_n = nt;
-  }
+  std::vector<uint64_t> rec((size_t)n * 4);
+  if (n) HIP_TRY(hipMemcpy(rec.data(), ctx->tq + 2, (size_t)n * 32, hipMemcpyDeviceToHost));
+  for (int64_t k = 0; k < n; k++) out_index[k] = (int64_t)rec[4 * k];
+  std::sort(out_index, out_index + n);
   return MGPU_OK;
 }
 
@@ -2011,42 +2173,54 @@ int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, 
 
 }  // extern "C"
 
-// The join's one host wait: a spin on the stream's completion (MGPU_SPIN=0: the blocking
-// hipStreamSynchronize; its wake-up cost C2's 1.5 ms step 1.3-1.9%, profiles/r2_spin_ab.txt)
-static hipError_t stream_wait(hipStream_t s) {
-  static const bool spin = !(getenv("MGPU_SPIN") && atoi(getenv("MGPU_SPIN")) == 0);
-  if (!spin) return hipStreamSynchronize(s);
-  hipError_t q;
-  while ((q = hipStreamQuery(s)) == hipErrorNotReady) {
-  }
-  return q;
-}
-
-// mgpu_pip_join with an optional validity bitmap of the points (the Arrow entry's nulls)
+// mgpu_pip_join with an optional validity bitmap of the points (the Arrow entry's nulls).
+// One join; then, for H3 with the reference's libm, the route's near-ties (counted in the
+// same copy as the pair count, their first kTqHead records with it) recomputed on the
+// host with the reference's arithmetic (h3_glibc.cpp).  Where that moves a point's cell
+// -- glibc misrounding an argument that decides it -- the join is run again with those
+// cells as overrides, so the output is the reference's.  A near-tie queue that overflowed
+// is grown and the join redone.
 static int32_t pip_join_sync(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
                              const double* y, const int64_t* point_id, int64_t point_id_base, int64_t n,
                              int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id, int32_t* out_polygon_id,
                              void* stream, mgpu_stats* stats, const uint8_t* valid, int64_t valid_off) {
   hipStream_t s = (hipStream_t)stream;
-  int32_t st = join_impl(ctx, chips, is, res, x, y, point_id, point_id_base, n, capacity, out_point_id, out_polygon_id,
-                         s, true, valid, valid_off);
-  if (st) return st;
-  unsigned long long h[8] = {0};
-  HIP_TRY(hipMemcpyAsync(h, ctx->ws, sizeof h, hipMemcpyDeviceToHost, s));
-  HIP_TRY(stream_wait(s));
-  if (out_n_pairs) *out_n_pairs = (int64_t)h[0];
-  if (getenv("MGPU_DEBUG_COUNTERS")) {  // profiling builds (-DMGPU_STATS)
-    unsigned long long d[16] = {0};
-    HIP_TRY(hipMemcpy(d, ctx->ws, sizeof d, hipMemcpyDeviceToHost));
-    fprintf(stderr, "mgpu counters:");
-    for (int k = 0; k < 16; k++) fprintf(stderr, " %llu", d[k]);
-    fprintf(stderr, "\n");
+  const bool reference_libm = is == MGPU_H3 && ctx && ctx->opt.h3_libm == MGPU_LIBM_REFERENCE;
+  int64_t n_ovr = 0, n_ties = 0;
+  uint64_t h[8] = {0};
+  for (int attempt = 0;; attempt++) {
+    int32_t st = join_impl(ctx, chips, is, res, x, y, point_id, point_id_base, n, capacity, out_point_id,
+                           out_polygon_id, s, true, valid, valid_off, n_ovr);
+    if (st) return st;
+    HIP_TRY(hipMemcpyAsync(ctx->pin, ctx->ws, 16 * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(ctx->pin + 16, ctx->tq, (2 + 4 * kTqHead) * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(stream_wait(ctx, s));
+    memcpy(h, ctx->pin, sizeof h);
+    n_ties = (int64_t)ctx->pin[16];
+    if (h[2]) break;  // invalid coordinates: reported below
+    if (attempt >= 3) return fail(MGPU_E_INTERNAL, "pip_join: near-tie resolution did not settle");
+    if (n_ties > ctx->tq_cap) {
+      if (int32_t e = ensure_tq(ctx, n_ties + n_ties / 4 + 1024)) return e;
+      continue;
+    }
+    if (!reference_libm || n_ties == 0 || n_ovr > 0) break;
+    std::vector<TieRec> tr;
+    if (int32_t e = read_ties(ctx, n_ties, tr)) return e;
+    const auto diff = libm_second_opinion(tr, res, false);
+    if (diff.empty()) break;
+    std::vector<uint64_t> hv(2 * diff.size());
+    for (size_t k = 0; k < diff.size(); k++) hv[2 * k] = (uint64_t)diff[k].first, hv[2 * k + 1] = diff[k].second;
+    if (int32_t e = ensure_ovr(ctx, (int64_t)hv.size())) return e;
+    HIP_TRY(hipMemcpy(ctx->ovr, hv.data(), hv.size() * 8, hipMemcpyHostToDevice));
+    n_ovr = (int64_t)diff.size();
   }
+  if (out_n_pairs) *out_n_pairs = (int64_t)h[0];
   if (stats) {
     stats->n_points = n;
     stats->n_pairs = (int64_t)h[0];
-    stats->n_near_ties = (int64_t)h[1];
+    stats->n_near_ties = n_ties;
     stats->n_candidates = (int64_t)h[3];
+    stats->libm_overrides = (int32_t)n_ovr;
     float ms = 0, ms2 = 0;
     hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
     if (n > 0) hipEventElapsedTime(&ms2, ctx->ev0, ctx->ev2);
@@ -2071,13 +2245,13 @@ static int32_t pip_join_sync(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is,
   }
   // pool records used (counters[5]) within the pool: every record is still in the
   // workspace, so a larger output can be written by mgpu_pip_join_fetch alone (the split
-  // pipeline keeps its codes and mixed answers: always)
+  // and binned pipelines keep their answers: always)
   ctx->last.total = (int64_t)h[0];
-  ctx->last.pool_ok = ctx->last.split || ctx->last.binned || (int64_t)h[5] <= capacity + ctx->last.n_tiles * mgpu::join_pend_cap();
+  ctx->last.pool_ok = ctx->last.split || ctx->last.binned || (int64_t)h[5] <= capacity;
   if (h[2]) {
     ctx->last.valid = false;
-    if (is == MGPU_BNG) return fail(MGPU_E_NAN, "NaN coordinates are not supported. (%llu points)", h[2]);
-    return fail(MGPU_E_INVALID_ARG, "Latitude or longitude were invalid. (%llu points)", h[2]);
+    if (is == MGPU_BNG) return fail(MGPU_E_NAN, "NaN coordinates are not supported. (%llu points)", (unsigned long long)h[2]);
+    return fail(MGPU_E_INVALID_ARG, "Latitude or longitude were invalid. (%llu points)", (unsigned long long)h[2]);
   }
   if ((int64_t)h[0] > capacity)
     return fail(MGPU_E_CAPACITY, "%lld pairs do not fit capacity %lld", (long long)h[0], (long long)capacity);
@@ -2190,7 +2364,9 @@ int32_t mgpu_test_chip_contains_host(int32_t index_system, int64_t n_chips, cons
                                      const double* y, int8_t* out_join_path, int8_t* out_point_locator) {
   std::vector<uint8_t> host;
   BlobHeader hdr;
-  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr))
+  mgpu_build_opts bo;
+  mgpu_build_opts_default(&bo);
+  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr, bo))
     return st;
   const mgpu::ChipTableView v = view_from_header(hdr, host.data());
   for (int64_t i = 0; i < n; i++) {
@@ -2220,7 +2396,10 @@ int32_t mgpu_test_raster_host(int32_t index_system, int32_t res, int64_t n_chips
                               uint32_t* out_first, uint32_t* out_mask, int32_t* out_chip_poly) {
   std::vector<uint8_t> host;
   BlobHeader hdr;
-  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr))
+  mgpu_build_opts bo;  // (the BNG pixel index too: this hook tests the index itself)
+  mgpu_build_opts_default(&bo);
+  bo.raster_bng = 1;
+  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr, bo))
     return st;
   const mgpu::ChipTableView v = view_from_header(hdr, host.data());
   for (int64_t c = 0; c < n_chips; c++) out_chip_poly[c] = v.chip_poly[c];
@@ -2329,28 +2508,10 @@ static int32_t geometry_cells(mgpu_ctx* ctx, int32_t is, int32_t res, int32_t fo
   double* x = (double*)ctx->scratch;
   double* y = x + std::max<int64_t>(n, 1);
   if (int32_t st = decode_points(ctx, format, data, offsets, off32, valid, voff, n, x, y, s)) return st;
-  auto* counters = (unsigned long long*)ctx->ws;
-  auto* ties = (unsigned long long*)((uint8_t*)ctx->ws + ws_layout(1, 0).ties);
-  HIP_TRY(hipMemsetAsync(counters, 0, kWsCounters, s));
-  HIP_TRY(hipMemsetAsync(ties, 0, 8, s));
-  HIP_TRY(hipEventRecord(ctx->ev0, s));
-  HIP_TRY(mgpu::launch_cells(is, res, x, y, n, out_cell, counters, ties, kTieCap, s, valid, voff));
-  HIP_TRY(hipEventRecord(ctx->ev1, s));
-  if (out_valid) HIP_TRY(mgpu::launch_valid_and(valid, voff, nullptr, 0, n, out_valid, s));
-  unsigned long long h[8] = {0};
-  HIP_TRY(hipMemcpyAsync(h, counters, sizeof h, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  if (stats) {
-    memset(stats, 0, sizeof *stats);
-    stats->n_points = n;
-    stats->n_near_ties = (int64_t)h[1];
-    float ms = 0;
-    hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
-    stats->kernel_ms = stats->stream_kernel_ms = ms;
-  }
-  if (h[2]) {
-    if (is == MGPU_BNG) return fail(MGPU_E_NAN, "NaN coordinates are not supported. (%llu points)", h[2]);
-    return fail(MGPU_E_INVALID_ARG, "Latitude or longitude were invalid. (%llu points)", h[2]);
+  if (int32_t st = cells_impl(ctx, is, res, x, y, n, out_cell, s, valid, voff, stats)) return st;
+  if (out_valid) {
+    HIP_TRY(mgpu::launch_valid_and(valid, voff, nullptr, 0, n, out_valid, s));
+    HIP_TRY(stream_wait(ctx, s));
   }
   return MGPU_OK;
 }
@@ -2473,6 +2634,14 @@ int32_t mgpu_test_h3_route_host(const double* lon, const double* lat, int64_t n,
       bool tie;
       out_cell[i] = (int64_t)mgpu::h3::point_to_cell(lon[i], lat[i], res, &tie);
     }
+  });
+  return MGPU_OK;
+}
+
+int32_t mgpu_test_h3_glibc_host(const double* lon, const double* lat, int64_t n, int32_t res, int64_t* out_cell) {
+  if (res < 0 || res > 15) return MGPU_E_RESOLUTION;
+  mgpu::parallel_for(n, 4096, [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; ++i) out_cell[i] = (int64_t)mgpu::h3glibc::point_to_cell(lon[i], lat[i], res);
   });
   return MGPU_OK;
 }

@@ -7,8 +7,23 @@
 #include "chip_table.h"
 #include "kernels.h"
 
+// Per-context options (mgpu_ctx_set_option; include/mosaic_gpu.h lists the keys).  They
+// replace process environment variables: a JVM host sets them per context.
+struct mgpu_options {
+  int64_t h3_libm = MGPU_LIBM_REFERENCE;  // near-tie cells: the reference's libm or correctly rounded
+  int64_t pipeline = MGPU_PIPELINE_AUTO;  // the join's planner (or a forced pipeline)
+  int64_t bin_count = 64;                 // binned pipeline: bins over the chip table's extent
+  int64_t bin_min_mb = 256;               // ... for chip tables of at least this size
+  int64_t bin_min_points = 1 << 21;       // ... and batches of at least this many points
+  int64_t bin_xcd = 1;                    // ... tiles dealt to the XCDs in contiguous runs
+  int64_t spin_us = 2000;                 // synchronous calls: poll (yielding) this long, then block
+  // the chip-table builder of mgpu_chips_upload on this context (mgpu_build_opts)
+  int64_t raster = 1, raster_bng = 0, raster_sub = 8, raster_milli = 250;
+};
+
 struct mgpu_ctx {
   int device = 0;
+  mgpu_options opt;
   // workspace: tile status words + ticket + counters
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -20,8 +35,14 @@ struct mgpu_ctx {
   // the binned pipeline's per-point buffers (binned copies, slots, answers), grown on demand
   void* bin_ws = nullptr;
   size_t bin_bytes = 0;
-  // the near-tie queue holds binned slots (a binned join was the last workspace user)
-  bool ties_binned = false;
+  // the H3 route's near-tie queue (kernels.h JoinArgs.tie_queue; grown when a call
+  // overflows it, then the call is redone), the libm overrides of the join being run,
+  // and a pinned host page for the counters and the queue's head
+  uint64_t* tq = nullptr;
+  int64_t tq_cap = 0;
+  uint64_t* ovr = nullptr;
+  int64_t ovr_cap = 0;
+  uint64_t* pin = nullptr;
   // scratch of the geometry / Arrow entries (decoded points, validity bitmaps), grown on demand
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -38,6 +59,7 @@ struct mgpu_ctx {
     int64_t pts_valid_off = 0;
     mgpu::EmitArgs emit{};
     int64_t n_tiles = 0;
+    int64_t n_ovr = 0;  // libm overrides the join ran with
     bool split = false;
     mgpu::SplitArgs sargs{};
     bool binned = false;

@@ -24,14 +24,19 @@ struct JoinArgs {
   int64_t pool_cap;
   unsigned long long* pool_used;    // zeroed before launch
   uint32_t* dirty;                  // [n_tiles] tiles with a near-tie point (for pip_fix_kernel)
-  uint64_t* pend;                   // [n_tiles * join_pend_cap()] mixed-cell candidates {li << 32 | chip}
-  uint32_t* tile_pend;              // [n_tiles] pending candidates of each tile (pip_resolve_kernel)
   uint32_t* n_dirty;                // zeroed before launch
   unsigned long long* counters;     // [0] pairs [1] near-ties [2] invalid [3] candidates
-  unsigned long long* ties;         // pip_fix_kernel: [0] count, [1 .. tie_cap] input positions of the
-  int64_t tie_cap;                  // near-tie points the H3 route resolved (zero ties[0] before launch)
-  int ablate;                       // profiling only (MGPU_ABLATE): 1 = no PIP (border = miss), 2 = no probe,
-                                    // 3 = no projection either
+  // The H3 route's near-ties (the points it resolved inside its tie band): tie_queue[0] =
+  // count (zeroed before launch), record q = tie_queue[2 + 4q ..] {input position, x bits,
+  // y bits, lattice key of the route's (face, ijk)} while q < tie_cap.  The host resolves
+  // them with the reference's libm (h3_glibc.h) and, where that moves a cell, reruns the
+  // join with the overrides: ovr[2k] = input position (ascending), ovr[2k + 1] = the
+  // lattice key to use instead of the route's.
+  uint64_t* tie_queue;
+  int64_t tie_cap;
+  const uint64_t* ovr;
+  int64_t n_ovr;
+  const uint32_t* pos_of;           // binned pipeline: input position of binned slot s (else null)
   // split pipeline (launch_split): the mixed points of chunk c are the chunk's listed
   // points c * split_chunk() + mixed_idx[c * split_chunk() + m], m < chunk_mixed[c]; their
   // answers (first chip | match mask << 32) go to mixed_res at the same list position;
@@ -99,7 +104,7 @@ struct BinArgs {
   uint32_t* gsum;                   // [bin groups * nb] group sums, then group bases
   double x0, y0, inv_bx, inv_by;    // the bin grid over the chip table's extent
   int32_t nbx, nby;                 // nbx * nby <= bin_max()
-  int32_t xcd_runs;                 // deal each XCD a contiguous run of binned tiles (MGPU_BIN_XCD)
+  int32_t xcd_runs;                 // deal each XCD a contiguous run of binned tiles (option bin_xcd)
 };
 int64_t bin_chunk();
 int64_t bin_chunks(int64_t n);
@@ -107,13 +112,10 @@ int64_t bin_groups(int64_t n);
 int32_t bin_max();
 hipError_t launch_binned(int is, const BinArgs& a, hipStream_t s, hipEvent_t after_bin, hipEvent_t after_join);
 hipError_t launch_bin_emit(const BinArgs& a, hipStream_t s);
-// input positions of the binned slots ts[0 .. nt) (ascending): out[k] = i with slot[i] == ts[k]
-hipError_t launch_bin_unslot(const uint32_t* slot, int64_t n, const uint32_t* ts, int64_t nt, int64_t* out, hipStream_t s);
 
 // pair_emit_kernel: tile records -> ordered (point_id, polygon_id) output
 struct EmitArgs {
   const uint32_t* tile_count;       // records of each tile
-  const uint32_t* tile_dead;        // of which dead (pip_resolve_kernel)
   uint64_t* group_off;              // [n_tiles / 32] written by the tile scan
   const uint64_t* tile_where;
   const uint64_t* recs;
@@ -124,11 +126,20 @@ struct EmitArgs {
   int32_t* out_poly;
 };
 
-// ties: [0] count, [1 .. tie_cap] point indices (zero ties[0] before launch); `valid`
-// (optional Arrow bitmap at bit offset voff): null points get cell 0
+// ties: [0] count, [1 .. tie_cap] positions of the points the fast projection hands to the
+// H3 route (zero ties[0] before launch; on overflow the route pass redoes every point);
+// tie_queue / tq_cap: the route's own near-ties as JoinArgs.tie_queue, the key being the
+// route's cell id (zero tie_queue[0] before launch).  `valid` (optional Arrow bitmap at bit
+// offset voff): null points get cell 0
 hipError_t launch_cells(int is, int res, const double* x, const double* y, int64_t n, int64_t* out,
-                        unsigned long long* counters, unsigned long long* ties, int64_t tie_cap, hipStream_t s,
-                        const uint8_t* valid = nullptr, int64_t voff = 0);
+                        unsigned long long* counters, unsigned long long* ties, int64_t tie_cap,
+                        uint64_t* tie_queue, int64_t tq_cap, hipStream_t s, const uint8_t* valid = nullptr,
+                        int64_t voff = 0);
+// out[pos[k]] = val[k], k < n (the host's libm corrections of near-tie cells)
+hipError_t launch_scatter_i64(const int64_t* pos, const int64_t* val, int64_t n, int64_t* out, hipStream_t s);
+// x[pos[k]], y[pos[k]] -> xy[2k], xy[2k + 1] (coordinates of a few points, for the host)
+hipError_t launch_gather_xy(const double* x, const double* y, const int64_t* pos, int64_t n, double* xy,
+                            hipStream_t s);
 // the point (centroid) of each POINT / MULTIPOINT geometry, WKB (format 0) or WKT (1),
 // rows data[offsets[i] .. offsets[i + 1]); null rows (valid bitmap) -> NaN.  counters[4..6]
 // += malformed / unsupported type / empty rows
@@ -141,8 +152,6 @@ hipError_t launch_valid_and(const uint8_t* a, int64_t aoff, const uint8_t* b, in
 int64_t join_tiles(int64_t n);
 int64_t join_tile_points();
 int64_t join_slot_records();   // records reserved per tile (pairs beyond go to the overflow pool)
-int64_t join_pend_cap();       // pending mixed-cell candidates kept per tile
-int64_t join_pend_words();     // u64 words per pending candidate
 // `after_stream` (optional) is recorded right after pip_join_kernel
 hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s, hipEvent_t after_stream);
 // pair_emit_kernel alone, over the records a join left in the workspace

@@ -94,14 +94,27 @@ __global__ __launch_bounds__(kStreamBlock) void cells_kernel(const double* __res
   }
 }
 
+// A near-tie of the H3 route, queued for the host's libm pass (JoinArgs.tie_queue)
+__device__ __forceinline__ void tie_record(uint64_t* tq, int64_t cap, int64_t pos, double x, double y, uint64_t key) {
+  const unsigned long long q = atomicAdd((unsigned long long*)tq, 1ull);
+  if ((int64_t)q < cap) {
+    uint64_t* r = tq + 2 + 4 * q;
+    r[0] = (uint64_t)pos;
+    r[1] = (uint64_t)__double_as_longlong(x);
+    r[2] = (uint64_t)__double_as_longlong(y);
+    r[3] = key;
+  }
+}
+
 // The queued near-ties by the H3 route; if the queue overflowed, every point again
-// (fast path + route where needed).
+// (fast path + route where needed).  The route's own near-ties go to tie_queue with
+// their (correctly rounded) cell.
 __global__ __launch_bounds__(kStreamBlock) void cells_fix_kernel(const double* __restrict__ x, const double* __restrict__ y,
                                                            int64_t n, int res, int64_t* __restrict__ out,
                                                            unsigned long long* __restrict__ counters,
                                                            const unsigned long long* __restrict__ ties,
-                                                           int64_t tie_cap, const uint8_t* __restrict__ valid,
-                                                           int64_t voff) {
+                                                           int64_t tie_cap, uint64_t* __restrict__ tq, int64_t tq_cap,
+                                                           const uint8_t* __restrict__ valid, int64_t voff) {
   const int64_t nt = (int64_t)ties[0];
   const bool all = nt > tie_cap;
   const int64_t m = all ? n : nt;
@@ -113,7 +126,9 @@ __global__ __launch_bounds__(kStreamBlock) void cells_fix_kernel(const double* _
     if (isfinite(px) && isfinite(py) && pt_valid(valid, voff, i)) {
       h3::FastHex f = h3::fast_hex2d(h3::to_radians_fast(py), h3::to_radians_fast(px), res, k_res, kAllFaces);
       if (f.tie) h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, &tie);
-      out[i] = (int64_t)h3::face_ijk_to_h3_fast(f.face, f.ijk, res);
+      const int64_t c = (int64_t)h3::face_ijk_to_h3_fast(f.face, f.ijk, res);
+      out[i] = c;
+      if (tie) tie_record(tq, tq_cap, i, px, py, (uint64_t)c);
     }
     count_wave(&counters[1], tie);
   }
@@ -173,19 +188,8 @@ constexpr int kOutCap = MGPU_OUTCAP;  // pairs a tile stages in LDS
 constexpr int kStash = MGPU_STASH;  // candidates whose coordinates phase 1 leaves in LDS
 static_assert(kCandCap * 2 + kMixCap * 2 + kStash * 16 <= kOutCap * 6, "phase 1-2 lists fit the staging buffer");
 constexpr int kMaskBits = 32;
-// MGPU_DEFER=1: the streaming kernel does not walk mixed-cell candidates itself.  It
-// writes them as tentative pair records (in their sorted place) and lists them, with
-// their record index, in the tile's pending list; pip_resolve_kernel walks every
-// pending candidate of a group of tiles with all lanes busy and marks the misses'
-// records dead; pair_emit_kernel drops dead records.  A tile reserves kSlot records in
-// its slot; more go to the overflow pool.
-#ifndef MGPU_DEFER
-#define MGPU_DEFER 0
-#endif
+// A tile reserves kSlot records in its slot; more go to the overflow pool.
 constexpr int kSlot = 2 * kTile;
-constexpr uint64_t kDeadRec = ~0ULL;
-// pending entry: x, y (f64 bits), chip | record index << 32, walk info (chip_quick)
-constexpr int kPendWords = 4;
 
 // chips of a cell: first, count, core mask (bits < 16)
 struct Range {
@@ -216,14 +220,47 @@ __device__ __forceinline__ Range grid_range(uint64_t e) {
   return Range{(uint32_t)e, (uint32_t)(e >> 32) & 0xFFFF, (uint32_t)(e >> 48)};
 }
 
+// The H3 route for a point the fast projection could not decide (fix kernels only).  A
+// near-tie of the route itself is queued for the host's libm pass; a host override (the
+// reference's libm moved the cell) replaces the route's (face, ijk).  `p` = the kernel's
+// point index (the binned slot in the binned pipeline: a.pos_of maps it to the input
+// position, which keys the queue and the overrides).
+__device__ __forceinline__ void route_point(const JoinArgs& a, int64_t p, double px, double py, h3::FastHex* f,
+                                                      bool* tie) {
+  h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), a.res, &f->face, &f->ijk, tie);
+  if (!*tie) return;
+  const int64_t pos = a.pos_of ? (int64_t)a.pos_of[p] : p;
+  uint64_t key = h3::lattice_key(f->face, f->ijk);
+  if (a.n_ovr) {
+    int64_t lo = 0, hi = a.n_ovr;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (a.ovr[2 * mid] < (uint64_t)pos)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    if (lo < a.n_ovr && a.ovr[2 * lo] == (uint64_t)pos) {
+      key = a.ovr[2 * lo + 1];
+      f->face = (int)(key >> 56);
+      h3::IJK c{(int)((key >> 28) & 0xFFFFFFFULL) - (1 << 27), (int)(key & 0xFFFFFFFULL) - (1 << 27), 0};
+      h3::ijk_normalize(c);
+      f->ijk = c;
+    }
+  }
+  if (a.tie_queue) tie_record(a.tie_queue, a.tie_cap, pos, px, py, key);
+}
+
 template <int IS, bool SLOW>
-__device__ __forceinline__ Range chip_probe(const ChipTableView& t, double px, double py, int res, bool res_match,
-                                            bool* ok, bool* tie, int ablate, uint32_t* gi) {
+__device__ __forceinline__ Range chip_probe(const JoinArgs& a, int64_t p, double px, double py, bool* ok, bool* tie,
+                                            uint32_t* gi) {
+  const ChipTableView& t = a.chips;
+  const int res = a.res;
   *tie = false;
   *gi = kNoEntry;
   if (IS == MGPU_BNG) {
     *ok = px == px && py == py;  // pointToIndex rejects NaN only
-    if (!*ok || !res_match) return Range{0, 0, 0};
+    if (!*ok || !a.res_match) return Range{0, 0, 0};
     const int32_t eI = bng::d2i(px), nI = bng::d2i(py);
     // whole-metre coordinates in [0, 1e7): the cell id is a bijection of (eI / edge,
     // nI / edge) (capi.cpp build_bng_dense), so the dense grid replaces id + hash probe
@@ -235,9 +272,7 @@ __device__ __forceinline__ Range chip_probe(const ChipTableView& t, double px, d
       row = row * ed > (uint32_t)nI ? row - 1 : ((row + 1) * ed <= (uint32_t)nI ? row + 1 : row);
       const DenseFace& D = t.dense[0];
       const uint32_t da = col - (uint32_t)D.a0, db = row - (uint32_t)D.b0;
-      if (ablate == 2) return Range{0, (da ^ db) == 0x12345 ? 1u : 0u, 0};  // profiling: no probe
       if (da >= D.w || db >= D.h) return Range{0, 0, 0};
-      if (ablate == 6) return Range{(da * 7u + db) % t.n_chips, 1, 1};  // profiling: no grid load, one core chip
       *gi = D.base + db * D.w + da;
       return Range{0, 0, 0};
     }
@@ -246,7 +281,7 @@ __device__ __forceinline__ Range chip_probe(const ChipTableView& t, double px, d
     return probe_range(t, (uint64_t)c);
   }
   *ok = isfinite(px) && isfinite(py);
-  if (!*ok || !res_match) return Range{0, 0, 0};
+  if (!*ok || !a.res_match) return Range{0, 0, 0};
   const double lat = h3::to_radians_fast(py), lon = h3::to_radians_fast(px);
   if (t.probe_mode != kProbeCellId) {
     // outside the chip cells' bounding box no cell can match
@@ -257,11 +292,10 @@ __device__ __forceinline__ Range chip_probe(const ChipTableView& t, double px, d
         *tie = true;
         return Range{0, 0, 0};
       }
-      h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, tie);
+      route_point(a, p, px, py, &f, tie);
     }
     if (t.probe_mode == kProbeDense) {
       const int32_t ga = f.ijk.i - f.ijk.k, gb = f.ijk.j - f.ijk.k;
-      if (ablate == 2) return Range{0, (ga ^ gb) == 0x12345 ? 1u : 0u, 0};  // profiling: projection, no probe
       DenseFace D;
       const int fu = __builtin_amdgcn_readfirstlane(f.face);
       if (__all(f.face == fu)) {
@@ -271,13 +305,10 @@ __device__ __forceinline__ Range chip_probe(const ChipTableView& t, double px, d
       }
       const uint32_t da = (uint32_t)(ga - D.a0), db = (uint32_t)(gb - D.b0);
       if (da >= D.w || db >= D.h) return Range{0, 0, 0};
-      if (ablate == 6) return Range{(da * 7u + db) % t.n_chips, 1, 1};  // profiling: no grid load, one core chip
       *gi = D.base + db * D.w + da;
       return Range{0, 0, 0};
     }
-    const uint64_t key = h3::lattice_key(f.face, f.ijk);
-    if (ablate == 2) return Range{0, key == 0x123456789ULL ? 1u : 0u, 0};  // profiling: projection, no probe
-    return probe_range(t, key);
+    return probe_range(t, h3::lattice_key(f.face, f.ijk));
   }
   h3::FastHex f = h3::fast_hex2d(lat, lon, res, t.k_res > 0 ? t.k_res : h3::k_of_res(res), kAllFaces);
   if (f.tie) {
@@ -285,7 +316,7 @@ __device__ __forceinline__ Range chip_probe(const ChipTableView& t, double px, d
       *tie = true;
       return Range{0, 0, 0};
     }
-    h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), res, &f.face, &f.ijk, tie);
+    route_point(a, p, px, py, &f, tie);
   }
   return probe_range(t, h3::face_ijk_to_h3_fast(f.face, f.ijk, res));
 }
@@ -299,7 +330,7 @@ __device__ __forceinline__ bool chip_is_core(const ChipTableView& t, const Range
 // abandons the tile, the fix kernel evaluates the candidate on the spot).
 template <bool SLOW, int CAND_CAP = kCandCap>
 __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, const Range& r, double px, double py,
-                                            bool do_pip, bool& any_tie, uint32_t* s_ncand, uint16_t* s_cand_pj,
+                                            bool& any_tie, uint32_t* s_ncand, uint16_t* s_cand_pj,
                                             double2* s_cand_xy, uint32_t* s_first, uint16_t* s_cnt,
                                             uint32_t* s_mask) {
   // the streaming kernel keeps no sequential PIP path (its registers would cap
@@ -311,7 +342,7 @@ __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, cons
   for (uint32_t j = 16; j < nj; j++)
     if (t.chip_flags[r.first + j] & kChipCore) border &= ~(1u << j);
   uint32_t mask = lowm & ~border;
-  if (border && do_pip) {
+  if (border) {
     const uint32_t nb = __popc(border);
     uint32_t j0 = atomicAdd(s_ncand, nb);
     for (uint32_t b = border; b; b &= b - 1) {
@@ -329,7 +360,7 @@ __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, cons
   }
   s_first[li] = r.first;
   // (the streaming kernel reads no counts: its s_cnt doubles as the raster's list)
-  if (SLOW || MGPU_DEFER) s_cnt[li] = (uint16_t)(r.count > 0xFFFF ? 0xFFFF : r.count);
+  if (SLOW) s_cnt[li] = (uint16_t)(r.count > 0xFFFF ? 0xFFFF : r.count);
   s_mask[li] = mask;
 }
 
@@ -418,7 +449,6 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   const ChipTableView& t = a.chips;
   const int64_t base = (int64_t)tile * kTile;
   const bool res_match = a.res_match;
-  const bool do_pip = a.ablate != 1;
 
   MGPU_STAMP(0);
   // ---- phase 1: cells, core matches, candidates
@@ -432,8 +462,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #else
 #define MGPU_LDPT(ptr) (*(ptr))
 #endif
-  if (!G && !SLOW && kBlock == 64 && t.raster_mode != kRasterNone && a.ablate == 0 && res_match &&
-      (IS == MGPU_H3 || a.res == t.res)) {
+  if (!G && !SLOW && kBlock == 64 && t.raster_mode != kRasterNone && res_match && (IS == MGPU_H3 || a.res == t.res)) {
     // pass A: the lane's four points load together, then their pixels' classes: a
     // pure pixel's matches are final (no projection, no candidates); the rest are
     // listed (s_cnt is free in the streaming kernel) for pass B
@@ -509,10 +538,10 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
       if (q < nlist) {
         bool ok, tie;
         uint32_t gi;
-        Range r = chip_probe<IS, SLOW>(t, px, py, a.res, res_match, &ok, &tie, a.ablate, &gi);
+        Range r = chip_probe<IS, SLOW>(a, base + li, px, py, &ok, &tie, &gi);
         if (gi != kNoEntry) r = grid_range(t.grid[gi]);
         any_tie |= tie;
-        phase1_item<SLOW, kCap>(t, li, r, px, py, do_pip, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
+        phase1_item<SLOW, kCap>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
       }
     }
   } else if (IS == MGPU_BNG) {
@@ -538,7 +567,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
       gi[k] = kNoEntry;
       if (MGPU_VALID(k * kBlock + threadIdx.x) && pt_valid(a.valid, a.valid_off, MGPU_PT(k * kBlock + threadIdx.x))) {
         bool ok, tie;
-        r[k] = chip_probe<IS, SLOW>(t, bx[k], by[k], a.res, res_match, &ok, &tie, a.ablate, &gi[k]);
+        r[k] = chip_probe<IS, SLOW>(a, MGPU_PT(k * kBlock + threadIdx.x), bx[k], by[k], &ok, &tie, &gi[k]);
         any_bad |= !ok;
       }
     }
@@ -548,7 +577,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
       if (gi[k] != kNoEntry) r[k] = grid_range(ge[k]);
-      phase1_item<SLOW, kCap>(t, k * kBlock + threadIdx.x, r[k], bx[k], by[k], do_pip, any_tie, &s_ncand, s_cand_pj,
+      phase1_item<SLOW, kCap>(t, k * kBlock + threadIdx.x, r[k], bx[k], by[k], any_tie, &s_ncand, s_cand_pj,
                         s_cand_xy, s_first, s_cnt, s_mask);
     }
   } else {
@@ -570,23 +599,14 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
       }
       if (MGPU_VALID(li) && pt_valid(a.valid, a.valid_off, p)) {
         bool ok, tie;
-        if (a.ablate == 3) {  // profiling: no projection, no probe
-          ok = true;
-          tie = false;
-        } else {
-          uint32_t gi;
-          r = chip_probe<IS, SLOW>(t, px, py, a.res, res_match, &ok, &tie, a.ablate, &gi);
-          if (gi != kNoEntry) r = grid_range(t.grid[gi]);
-          n_tie_pts += (SLOW && tie) ? 1u : 0u;
-          if (SLOW && tie && a.ties) {  // the audit list of mgpu_last_near_ties
-            const unsigned long long q = atomicAdd(&a.ties[0], 1ull);
-            if ((int64_t)q < a.tie_cap) a.ties[1 + q] = (unsigned long long)p;
-          }
-        }
+        uint32_t gi;
+        r = chip_probe<IS, SLOW>(a, p, px, py, &ok, &tie, &gi);
+        if (gi != kNoEntry) r = grid_range(t.grid[gi]);
+        n_tie_pts += (SLOW && tie) ? 1u : 0u;
         any_bad |= !ok;
         any_tie |= tie;
       }
-      phase1_item<SLOW, kCap>(t, li, r, px, py, do_pip, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
+      phase1_item<SLOW, kCap>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
     }
   }
   count_wave(&a.counters[2], any_bad);
@@ -602,7 +622,6 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
       if (!G) {
         a.tile_count[tile] = 0;
         a.tile_where[tile] = kNoDst;
-        a.tile_pend[tile] = 0;
       }
     }
     return;
@@ -622,41 +641,26 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     const int li = pj & 1023;
     const uint32_t ch = s_first[li] + (pj >> 10);
     const int64_t p = MGPU_PT(li);
-    bool hit;
-    if (a.ablate == 4) {  // profiling: candidate list only
-      hit = (ch ^ pj) == 0x7FFFFFFF;
+    double px, py;
+    if (c < (uint32_t)kStash) {
+      const double2 q = s_cand_xy[c];
+      px = q.x;
+      py = q.y;
     } else {
-      double px, py;
-      if (c < (uint32_t)kStash) {
-        const double2 q = s_cand_xy[c];
-        px = q.x;
-        py = q.y;
+      px = a.x[p];
+      py = a.y[p];
+    }
+    const int q = pip::chip_quick(t, ch, px, py, nullptr);
+    bool hit = q == pip::kQuickYes;
+    if (q >= pip::kQuickStrips) {
+      const uint32_t m = atomicAdd(&s_nmix, 1u);
+      if (m < (uint32_t)kMix && (SLOW || q == pip::kQuickStrips)) {
+        s_mix[m] = (uint16_t)c;
+      } else if (!SLOW) {
+        redo = true;  // list full / chip without strip index: pip_fix_kernel
       } else {
-        px = a.x[p];
-        py = a.y[p];
-      }
-      uint64_t walk = 0;
-      const int q = pip::chip_quick(t, ch, px, py, (MGPU_DEFER && !SLOW) ? &walk : nullptr);
-      hit = q == pip::kQuickYes;
-      if (q >= pip::kQuickStrips && a.ablate != 5) {
-        const uint32_t m = atomicAdd(&s_nmix, 1u);
-        if (m < (uint32_t)kMix && (SLOW || q == pip::kQuickStrips)) {
-          s_mix[m] = (uint16_t)c;
-          if (MGPU_DEFER && !SLOW) {
-            // tentative match; pip_resolve_kernel walks the strip and decides (the
-            // entry's chip | record index word is written in phase 3)
-            hit = true;
-            uint64_t* pe = a.pend + ((uint64_t)tile * kMixCap + m) * kPendWords;
-            pe[0] = (uint64_t)__double_as_longlong(px);
-            pe[1] = (uint64_t)__double_as_longlong(py);
-            pe[3] = walk;
-          }
-        } else if (!SLOW) {
-          redo = true;  // list full / chip without strip index: pip_fix_kernel
-        } else {
-          hit = q == pip::kQuickStrips ? pip::chip_contains_mixed(t, ch, px, py)
-                                       : pip::chip_locate(t, ch, px, py) == pip::kInterior;
-        }
+        hit = q == pip::kQuickStrips ? pip::chip_contains_mixed(t, ch, px, py)
+                                     : pip::chip_locate(t, ch, px, py) == pip::kInterior;
       }
     }
     if (hit) atomicOr(&s_mask[li], 1u << (pj >> 10));
@@ -668,7 +672,6 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
       if (!G) {
         a.tile_count[tile] = 0;
         a.tile_where[tile] = kNoDst;
-        a.tile_pend[tile] = 0;
       }
     }
     return;
@@ -679,9 +682,6 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #ifdef MGPU_STATS
   uint32_t st_edges = 0;
 #endif
-  // (MGPU_DEFER: the streaming kernel leaves its mixed-cell candidates to
-  // pip_resolve_kernel; they are listed in phase 3, once their record index is known)
-  if (SLOW || !MGPU_DEFER)
   for (uint32_t m = threadIdx.x; m < nmix; m += kBlock) {
     const uint32_t c = s_mix[m];
     const uint32_t pj = s_cand_pj[c];
@@ -760,7 +760,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
       const int64_t p = MGPU_PT(li);
       const Range r{s_first[li], cnt, 0};
       for (uint32_t j = kMaskBits; j < cnt; j++)
-        mine += (chip_is_core(t, r, j) || (do_pip && pip::chip_contains_strips(t, r.first + j, a.x[p], a.y[p]))) ? 1 : 0;
+        mine += (chip_is_core(t, r, j) || pip::chip_contains_strips(t, r.first + j, a.x[p], a.y[p])) ? 1 : 0;
     }
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -775,20 +775,6 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     agg += v;
   }
   const uint32_t excl = wave_off + incl - mine;
-  const uint32_t npend = (MGPU_DEFER && !SLOW) ? nmix : 0u;
-  if (npend && agg > 0xFFFFu) {
-    // record indices of the pending list are 16 bits: the fix kernel redoes the tile
-    if (threadIdx.x == 0) {
-      const unsigned int q = atomicAdd(a.n_dirty, 1u);
-      a.dirty[q] = tile;
-      if (!G) {
-        a.tile_count[tile] = 0;
-        a.tile_where[tile] = kNoDst;
-        a.tile_pend[tile] = 0;
-      }
-    }
-    return;
-  }
 
   // the tile's records go to its own slot (kSlot records), or -- when it has more --
   // to space reserved in the overflow pool
@@ -801,30 +787,8 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     }
     a.tile_count[tile] = agg;
     a.tile_where[tile] = dst;
-    if (!SLOW) a.tile_pend[tile] = npend;
     if (agg) atomicAdd(&a.group_sum[tile / kScanGroup], agg);
     s_dst = dst;
-  }
-  if (!SLOW && MGPU_DEFER && npend) {
-    // pending list: each tentative record's index in the tile (point li's records
-    // start at its exclusive scan position; s_cnt is free once the streaming kernel
-    // has its masks -- it never has chips past the 32nd), the point and the chip
-    uint32_t pos = excl;
-#pragma unroll
-    for (int k = 0; k < kItems; k++) {
-      const int li = l0 + k;
-      s_cnt[li] = (uint16_t)pos;
-      pos += __popc(s_mask[li]);
-    }
-    __syncthreads();
-    uint64_t* pe = a.pend + (uint64_t)tile * kMixCap * kPendWords;
-    for (uint32_t m = threadIdx.x; m < npend; m += kBlock) {
-      const uint32_t pj = s_cand_pj[s_mix[m]];
-      const int li = pj & 1023;
-      const uint32_t j = pj >> 10;
-      const uint32_t ri = s_cnt[li] + __popc(s_mask[li] & ((1u << j) - 1u));
-      pe[m * kPendWords + 2] = (uint64_t)(s_first[li] + j) | ((uint64_t)ri << 32);
-    }
   }
   const bool staged = agg <= (uint32_t)kOutCap;
   __syncthreads();
@@ -838,7 +802,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   for (int k = 0; k < kItems; k++) {
     const int li = l0 + k;
     if (!SLOW) {
-      // every match (and tentative match) is a mask bit (s_cnt may hold record indices)
+      // every match is a mask bit
       const uint32_t first = s_first[li];
       for (uint32_t m = s_mask[li]; m; m &= m - 1) {
         const int32_t poly = t.chip_poly[first + __builtin_ctz(m)];
@@ -864,7 +828,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         hit = (m >> j) & 1;
       } else {
         const Range r{first, cnt, 0};
-        hit = chip_is_core(t, r, j) || (do_pip && pip::chip_contains_strips(t, first + j, a.x[p], a.y[p]));
+        hit = chip_is_core(t, r, j) || pip::chip_contains_strips(t, first + j, a.x[p], a.y[p]);
       }
       if (!hit) continue;
       const int32_t poly = t.chip_poly[first + j];
@@ -894,11 +858,8 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   MGPU_STAMP(4);
 }
 
-// MGPU_PERSIST=1 (not the default: measured 25% slower): a grid of resident
-// workgroups walks the tiles instead of one workgroup per tile.
-#ifndef MGPU_PERSIST
-#define MGPU_PERSIST 0
-#endif
+// One workgroup per tile (a persistent grid walking the tiles measured 25% slower in
+// round 1: workgroups that carry a tile of real work hide their dispatch).
 // 8 waves per SIMD: the tile's LDS (~4.7 KB) allows 32 workgroups per CU, and the
 // kernel is held to 64 VGPRs (it is latency-bound: the 8th wave measured -7% on C2,
 // -10% on C5)
@@ -912,33 +873,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #endif
 template <int IS>
 __global__ __launch_bounds__(kBlock) MGPU_JOIN_ATTR void pip_join_kernel(JoinArgs a) {
-#if MGPU_PERSIST
-  for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
-    join_tile<IS, false>(a, (uint32_t)tile);
-    __syncthreads();
-  }
-#else
   join_tile<IS, false>(a, blockIdx.x);
-#endif
-}
-
-// resident workgroups of pip_join_kernel<IS> on the device (persistent grid size)
-template <int IS>
-unsigned join_grid(int64_t n_tiles) {
-#if MGPU_PERSIST
-  static int resident[2] = {0, 0};
-  int& r = resident[IS == MGPU_H3 ? 0 : 1];
-  if (!r) {
-    int dev = 0, cus = 0, per = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pip_join_kernel<IS>, kBlock, 0);
-    r = cus * (per > 0 ? per : 1);
-  }
-  return (unsigned)(n_tiles < r ? n_tiles : r);
-#else
-  return (unsigned)n_tiles;
-#endif
 }
 
 // The tiles queued by pip_join_kernel, with the H3 route for their near-ties.
@@ -960,7 +895,6 @@ __global__ __launch_bounds__(kBlock) void pip_fix_kernel(JoinArgs a) {
 // writes the ordered pairs from the codes.
 constexpr int kClsBlock = 256;
 constexpr int kClsItems = kChunk / kClsBlock;  // points per thread
-constexpr int kClsBatch = 8;                   // of which in flight together
 static_assert(kClsItems * (kClsBlock / 64) == 64, "one wave scans a chunk's ballots");
 constexpr uint32_t kCodeMixed32 = 0xFFFFFFFFu;
 
@@ -974,16 +908,17 @@ struct CodeOf<MGPU_BNG> {
 };
 
 
-// Persistent: each workgroup copies the pixel block table (chip_table.h raster_blk) into
-// LDS once, then classifies chunks blockIdx.x, blockIdx.x + gridDim.x, ...; a point in a
-// uniform block takes its class from LDS, the rest load their pixel (and sub-pixel) class.
-// (512 threads: four workgroups -- 32 waves -- share a CU with their LDS tables; the
-// chunk's mixed points are ranked in point order as in split_emit_kernel)
+// One wave per chunk of kChunk points: a lane takes every 64th point of the chunk
+// (item-major, so consecutive lanes read consecutive points), and the chunk's mixed
+// points are ranked in point order by a running wave count plus the item's ballot -- no
+// workgroup barrier per chunk, no LDS scan.  The workgroup (512 threads: four share a
+// CU) copies the pixel block table (chip_table.h raster_blk) into LDS once; a point in a
+// uniform block takes its class from there, the rest load their pixel (and sub-pixel)
+// class.  Waves take chunks blockIdx.x * W + wave, then + gridDim.x * W ...
 #ifndef MGPU_CFY_BLOCK
 #define MGPU_CFY_BLOCK 512
 #endif
 constexpr int kCfyBlock = MGPU_CFY_BLOCK;
-constexpr int kCfyItems = kChunk / kCfyBlock;
 #ifndef MGPU_CFY_BATCH
 #define MGPU_CFY_BATCH 4
 #endif
@@ -991,129 +926,6 @@ constexpr int kCfyItems = kChunk / kCfyBlock;
 #define MGPU_CFY_WAVES 1  // (8 = at most 64 VGPRs: spills, slower on C2 / C5)
 #endif
 constexpr int kCfyBatch = MGPU_CFY_BATCH;
-static_assert(kCfyItems * (kCfyBlock / 64) == 64, "one wave scans a chunk's ballots");
-template <int IS>
-__global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_CFY_WAVES))) void classify_kernel(SplitArgs sa, int64_t n_chunks) {
-  using Code = typename CodeOf<IS>::T;
-  const JoinArgs& a = sa.j;
-  const ChipTableView& t = a.chips;
-  extern __shared__ uint16_t s_blk[];       // [raster_bny * raster_bnx] (IS == H3)
-  __shared__ unsigned long long s_bal[64];  // [item][wave]: the wave's mixed points
-  __shared__ uint32_t s_pos[64];
-  __shared__ uint32_t s_red[kCfyBlock / 64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool use_blk = IS == MGPU_H3 && t.raster_blk != nullptr && a.ablate != 14;  // (14: profiling, no LDS table)
-  if (use_blk) {
-    const uint32_t nb = t.raster_bnx * t.raster_bny;
-    for (uint32_t i = threadIdx.x; i < nb; i += kCfyBlock) s_blk[i] = t.raster_blk[i];
-  }
-  __syncthreads();
-  Code* codes = (Code*)sa.codes;
-  bool any_bad = false;
-  for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {
-    const int64_t c0 = ch * kChunk;
-    uint32_t pairs = 0, mixed_bits = 0;
-    for (int b = 0; b < kCfyItems; b += kCfyBatch) {
-      double bx[kCfyBatch], by[kCfyBatch];
-#pragma unroll
-      for (int k = 0; k < kCfyBatch; k++) {
-        const int64_t p = c0 + (int64_t)(b + k) * kCfyBlock + threadIdx.x;
-        bx[k] = by[k] = 0.0;
-        if (p < a.n) {
-          bx[k] = __builtin_nontemporal_load(&a.x[p]);
-          by[k] = __builtin_nontemporal_load(&a.y[p]);
-        }
-      }
-      uint32_t ri[kCfyBatch], gix[kCfyBatch], sb[kCfyBatch], bi[kCfyBatch];
-#pragma unroll
-      for (int k = 0; k < kCfyBatch; k++) {
-        ri[k] = kNoPixel;
-        gix[k] = 0;
-        sb[k] = 0;
-        bi[k] = kNoPixel;
-        const int64_t pk = c0 + (int64_t)(b + k) * kCfyBlock + threadIdx.x;
-        if (pk < a.n && pt_valid(a.valid, a.valid_off, pk)) {
-          bool ok;
-          ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &gix[k], &sb[k], use_blk ? &bi[k] : nullptr);
-          any_bad |= !ok;
-          if (a.ablate == 11) ri[k] = bx[k] == 12345.0 ? 0u : kNoPixel;  // profiling: no pixel loads
-        }
-      }
-      uint32_t cl[kCfyBatch];
-      uint64_t ge[kCfyBatch];
-#pragma unroll
-      for (int k = 0; k < kCfyBatch; k++) {
-        cl[k] = ri[k] < kRasterFull ? raster_class_blk(t, s_blk, ri[k], bi[k], sb[k])
-                                    : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
-        if (a.ablate == 15 && ri[k] < kRasterFull)  // (profiling: the LDS table only)
-          cl[k] = bi[k] != kNoPixel ? s_blk[bi[k]] : kPixMixed;
-        ge[k] = (IS == MGPU_BNG && ri[k] < kRasterFull) ? t.grid[gix[k]] : 0ull;
-      }
-#pragma unroll
-      for (int k = 0; k < kCfyBatch; k++) {
-        const int64_t p = c0 + (int64_t)(b + k) * kCfyBlock + threadIdx.x;
-        const bool valid = p < a.n;
-        bool mixed = cl[k] == kPixMixed;
-        Code code;
-        if (IS == MGPU_H3) {
-          code = (Code)cl[k];
-          if (!mixed && cl[k] != kPixEmpty) {
-            const uint32_t c = cl[k];  // the class id gives the match count (raster_pc)
-            pairs += c < t.raster_pc[0] ? 1u : c < t.raster_pc[1] ? 2u : c < t.raster_pc[2] ? 3u : c < t.raster_pc[3] ? 4u
-                     : (uint32_t)__popc((uint32_t)(t.raster_cls[c] >> 32));
-          }
-        } else {
-          const uint32_t first = (uint32_t)ge[k], m = cl[k];
-          if (!mixed && m && !(m < 256u && first < (1u << 24))) mixed = true;  // no room in the code
-          code = (Code)(mixed ? kCodeMixed32 : (m ? (first << 8) | m : 0u));
-          if (!mixed) pairs += __popc(m);
-        }
-        if (valid && a.ablate != 12) codes[p] = code;  // (12: profiling, no code stores)
-        mixed = mixed && valid;
-        const unsigned long long bal = __ballot(mixed);
-        if (lane == 0) s_bal[(b + k) * (kCfyBlock / 64) + wave] = bal;
-        if (mixed) mixed_bits |= 1u << (b + k);
-      }
-    }
-    const uint32_t wp = wave_sum_u32(pairs);
-    if (lane == 0) s_red[wave] = wp;
-    __syncthreads();
-    // mixed points ranked in point order (item-major, then wave, then lane)
-    if (wave == 0) {
-      const uint32_t v = (uint32_t)__popcll(s_bal[lane]);
-      const uint32_t incl = wave_incl_scan(v);
-      s_pos[lane] = incl - v;
-      if (lane == 63) sa.chunk_mixed[ch] = incl;
-      if (lane == 0) {
-        uint32_t tp = 0;
-        for (int w = 0; w < kCfyBlock / 64; w++) tp += s_red[w];
-        sa.chunk_pairs[ch] = tp;
-      }
-    }
-    __syncthreads();
-    for (uint32_t m = mixed_bits; m; m &= m - 1) {
-      const int it = __builtin_ctz(m);
-      const int e = it * (kCfyBlock / 64) + wave;
-      const uint32_t r = s_pos[e] + (uint32_t)__popcll(s_bal[e] & ((1ull << lane) - 1ull));
-      sa.mixed_idx[c0 + r] = (uint16_t)(it * kCfyBlock + threadIdx.x);
-    }
-    __syncthreads();  // (s_bal, s_pos, s_red reused by the next chunk)
-  }
-  count_wave(&a.counters[2], any_bad);
-}
-
-// The same classification with one wave per chunk: a lane takes every 64th point of
-// the chunk (item-major, so consecutive lanes read consecutive points), and the chunk's
-// mixed points are ranked in point order by a running wave count plus the item's ballot
-// -- no workgroup barrier per chunk, no LDS scan; the workgroup only shares the LDS copy
-// of the pixel block table.  Waves of a workgroup take chunks blockIdx.x * W + wave,
-// then + gridDim.x * W ...
-#ifndef MGPU_CFY_WAVE
-#define MGPU_CFY_WAVE 1
-#endif
-#ifndef MGPU_CFY_PF
-#define MGPU_CFY_PF 0  // (1: next batch prefetched -- 89 VGPRs, 5 waves/SIMD: C2 +20%)
-#endif
 template <int IS>
 __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_CFY_WAVES))) void classify_wave_kernel(SplitArgs sa, int64_t n_chunks) {
   using Code = typename CodeOf<IS>::T;
@@ -1123,7 +935,7 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   const ChipTableView& t = a.chips;
   extern __shared__ uint16_t s_blk[];       // [raster_bny * raster_bnx] (IS == H3)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool use_blk = IS == MGPU_H3 && t.raster_blk != nullptr && a.ablate != 14;
+  const bool use_blk = IS == MGPU_H3 && t.raster_blk != nullptr;
   if (use_blk) {
     const uint32_t nb = t.raster_bnx * t.raster_bny;
     for (uint32_t i = threadIdx.x; i < nb; i += kCfyBlock) s_blk[i] = t.raster_blk[i];
@@ -1133,8 +945,6 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   const unsigned long long below = (1ull << lane) - 1ull;
   bool any_bad = false;
   const int64_t ch_step = (int64_t)gridDim.x * kW;
-  // batch loads: the next batch's points are requested after this batch's pixel loads,
-  // so the wait for the pixels leaves them in flight (loads retire in order)
   double bx[kCfyBatch], by[kCfyBatch];
   auto load_batch = [&](int64_t ch, int b, double* X, double* Y) {
 #pragma unroll
@@ -1147,12 +957,11 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
       }
     }
   };
-  if (MGPU_CFY_PF) load_batch((int64_t)blockIdx.x * kW + wave, 0, bx, by);
   for (int64_t ch = (int64_t)blockIdx.x * kW + wave; ch < n_chunks; ch += ch_step) {
     const int64_t c0 = ch * kChunk;
     uint32_t pairs = 0, nmixed = 0;  // nmixed: wave-uniform
     for (int b = 0; b < kItems; b += kCfyBatch) {
-      if (!MGPU_CFY_PF) load_batch(ch, b, bx, by);
+      load_batch(ch, b, bx, by);
       uint32_t ri[kCfyBatch], gix[kCfyBatch], sb[kCfyBatch], bi[kCfyBatch];
 #pragma unroll
       for (int k = 0; k < kCfyBatch; k++) {
@@ -1178,12 +987,6 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
         cl[k] = ri[k] < kRasterFull ? raster_class_blk(t, s_blk, ri[k], bi[k], sb[k])
                                     : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
         ge[k] = (IS == MGPU_BNG && ri[k] < kRasterFull) ? t.grid[gix[k]] : 0ull;
-      }
-      if (MGPU_CFY_PF) {
-        if (b + kCfyBatch < kItems)
-          load_batch(ch, b + kCfyBatch, bx, by);
-        else
-          load_batch(ch + ch_step, 0, bx, by);
       }
 #pragma unroll
       for (int k = 0; k < kCfyBatch; k++) {
@@ -1355,61 +1158,6 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   }
 }
 
-// The mixed-cell candidates the streaming kernel deferred (MGPU_DEFER): one workgroup
-// per scan group of kScanGroup tiles walks all of the group's pending candidates, one
-// per lane (pip_core.h chip_contains_mixed -- the same exact walk the streaming kernel
-// would have done), and marks the tentative record of every miss dead.  The tile's
-// tile_pend entry becomes its dead-record count and the group's pair sum drops by the
-// misses.  Runs after pip_fix_kernel, before tile_scan_kernel.
-constexpr int kResolveBlock = 512;
-__global__ __launch_bounds__(kResolveBlock) void pip_resolve_kernel(JoinArgs a) {
-  __shared__ uint32_t s_po[kScanGroup + 1];
-  __shared__ uint64_t s_where[kScanGroup];
-  __shared__ uint32_t s_dead[kScanGroup];
-  const int64_t g = blockIdx.x;
-  const int64_t t0 = g * kScanGroup;
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    const int64_t t = t0 + lane;
-    const bool in = lane < kScanGroup && t < a.n_tiles;
-    const uint32_t c = in ? a.tile_pend[t] : 0u;
-    const uint32_t incl = wave_incl_scan(c);
-    if (lane < kScanGroup) {
-      s_po[lane + 1] = incl;
-      s_where[lane] = in && c ? a.tile_where[t] : kNoDst;
-      s_dead[lane] = 0;
-    }
-    if (lane == 0) s_po[0] = 0;
-  }
-  __syncthreads();
-  const uint32_t total = s_po[kScanGroup];
-  if (total == 0) return;
-  const ChipTableView& t = a.chips;
-  for (uint32_t i = threadIdx.x; i < total; i += kResolveBlock) {
-    int k = 0;
-#pragma unroll
-    for (int step = kScanGroup / 2; step >= 1; step >>= 1)
-      if (s_po[k + step] <= i) k += step;
-    const uint64_t* pe = a.pend + ((uint64_t)(t0 + k) * kMixCap + (i - s_po[k])) * kPendWords;
-    const double px = __longlong_as_double((long long)pe[0]), py = __longlong_as_double((long long)pe[1]);
-    const uint64_t w = pe[2], wk = pe[3];
-    if (!pip::chip_contains_strip(t, (uint32_t)w, (uint32_t)wk, ((wk >> 40) & 1) != 0, (uint8_t)(wk >> 32), px, py)) {
-      const uint64_t where = s_where[k];
-      if (where != kNoDst) a.recs[where + (w >> 32)] = kDeadRec;
-      atomicAdd(&s_dead[k], 1u);
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    const bool in = lane < kScanGroup && s_po[lane + 1] > s_po[lane];
-    const uint32_t d = in ? s_dead[lane] : 0u;
-    if (in) a.tile_pend[t0 + lane] = d;
-    const unsigned long long dt = wave_sum_u64(d);
-    if (lane == 0 && dt) a.group_sum[g] -= (uint32_t)dt;
-  }
-}
-
 // Output offsets, in two levels: pip_join_kernel / pip_fix_kernel add each tile's pair
 // count to its group of kScanGroup tiles; this one workgroup scans the group sums
 // (~3e3 per 1e8 points, coalesced chunks of 1024) and pair_emit_kernel adds the counts
@@ -1480,10 +1228,6 @@ __global__ __launch_bounds__(kScanBlock) void tile_scan_kernel(const uint32_t* _
   if (threadIdx.x == 0) counters[0] = tot;
 }
 
-// MGPU_NT_OUT=1: nontemporal stores of the output pairs (A/B switch)
-#ifndef MGPU_NT_OUT
-#define MGPU_NT_OUT 0
-#endif
 // Ordered output: the records of kEmitTiles consecutive tiles (their output ranges are
 // contiguous) -> out[offset of the first ...] with point ids, as one flat stream over
 // the workgroup's lanes.
@@ -1492,82 +1236,42 @@ constexpr int kEmitTiles = 4096 / kTile;  // 4 tiles of 1024 points, 16 of 256
 static_assert(kScanGroup % kEmitTiles == 0 && kEmitTiles <= 64, "emit groups inside scan groups");
 __global__ __launch_bounds__(kEmitBlock) void pair_emit_kernel(EmitArgs a, int64_t n_tiles) {
   __shared__ uint32_t s_pref[kEmitTiles + 1];
-  __shared__ uint32_t s_phys[kEmitTiles];
   __shared__ uint64_t s_where[kEmitTiles];
   __shared__ int64_t s_off;
-  __shared__ int s_anydead;
   const int64_t t0 = (int64_t)blockIdx.x * kEmitTiles;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    // this block's tiles: live counts (records minus the dead ones pip_resolve_kernel
-    // marked), slots, in-block prefix
+    // this block's tiles: counts, slots, in-block prefix
     const int64_t t = t0 + lane;
     const bool in = lane < kEmitTiles && t < n_tiles;
-    const uint32_t phys = in ? a.tile_count[t] : 0u;
-    const uint32_t dead = in ? a.tile_dead[t] : 0u;
-    if (lane < kEmitTiles) {
-      s_where[lane] = in ? a.tile_where[t] : kNoDst;
-      s_phys[lane] = phys;
-    }
-    const uint32_t incl = wave_incl_scan(phys - dead);
+    const uint32_t cnt = in ? a.tile_count[t] : 0u;
+    if (lane < kEmitTiles) s_where[lane] = in ? a.tile_where[t] : kNoDst;
+    const uint32_t incl = wave_incl_scan(cnt);
     if (lane < kEmitTiles) s_pref[lane + 1] = incl;
-    const bool anyd = __any(dead != 0);
-    if (lane == 0) {
-      s_pref[0] = 0;
-      s_anydead = anyd ? 1 : 0;
-    }
+    if (lane == 0) s_pref[0] = 0;
     // predecessors of t0 inside its scan group
     const int64_t g0 = t0 - t0 % kScanGroup;
     const int64_t j = g0 + lane;
-    unsigned long long v = (lane < kScanGroup && j < t0) ? a.tile_count[j] - a.tile_dead[j] : 0u;
+    unsigned long long v = (lane < kScanGroup && j < t0) ? a.tile_count[j] : 0u;
     v = wave_sum_u64(v);
     if (lane == 0) s_off = (int64_t)(a.group_off[t0 / kScanGroup] + v);
   }
   __syncthreads();
   const int64_t off = s_off;
-  if (!s_anydead) {
-    const uint32_t total = s_pref[kEmitTiles];
-    for (uint32_t i = threadIdx.x; i < total; i += kEmitBlock) {
-      const int64_t q = off + i;
-      if (q >= a.capacity) break;
-      int k = 0;
+  const uint32_t total = s_pref[kEmitTiles];
+  for (uint32_t i = threadIdx.x; i < total; i += kEmitBlock) {
+    const int64_t q = off + i;
+    if (q >= a.capacity) break;
+    int k = 0;
 #pragma unroll
-      for (int step = kEmitTiles / 2; step >= 1; step >>= 1)
-        if (s_pref[k + step] <= i) k += step;
-      const uint64_t where = s_where[k];
-      if (where == kNoDst) continue;  // pool exhausted: the total exceeds the capacity
-      const uint64_t r = a.recs[where + (i - s_pref[k])];
-      const int64_t p = (t0 + k) * kTile + (int64_t)(r >> 32);
-#if MGPU_NT_OUT
-      __builtin_nontemporal_store(a.point_id ? a.point_id[p] : a.id_base + p, &a.out_point[q]);
-      __builtin_nontemporal_store((int32_t)(uint32_t)r, &a.out_poly[q]);
-#else
-      a.out_point[q] = a.point_id ? a.point_id[p] : a.id_base + p;
-      a.out_poly[q] = (int32_t)(uint32_t)r;
-#endif
-    }
-    return;
-  }
-  // some tile holds dead records: a wave per tile compacts its live records in order
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int k = wave; k < kEmitTiles; k += kEmitBlock / 64) {
+    for (int step = kEmitTiles / 2; step >= 1; step >>= 1)
+      if (s_pref[k + step] <= i) k += step;
     const uint64_t where = s_where[k];
-    if (where == kNoDst) continue;
-    const uint32_t phys = s_phys[k];
-    int64_t o = off + s_pref[k];
-    for (uint32_t b = 0; b < phys; b += 64) {
-      const uint32_t i = b + lane;
-      const uint64_t r = i < phys ? a.recs[where + i] : kDeadRec;
-      const bool alive = r != kDeadRec;
-      const unsigned long long bal = __ballot(alive);
-      const int64_t q = o + __popcll(bal & ((1ull << lane) - 1ull));
-      if (alive && q < a.capacity) {
-        const int64_t p = (t0 + k) * kTile + (int64_t)(r >> 32);
-        a.out_point[q] = a.point_id ? a.point_id[p] : a.id_base + p;
-        a.out_poly[q] = (int32_t)(uint32_t)r;
-      }
-      o += __popcll(bal);
-    }
+    if (where == kNoDst) continue;  // pool exhausted: the total exceeds the capacity
+    const uint64_t r = a.recs[where + (i - s_pref[k])];
+    const int64_t p = (t0 + k) * kTile + (int64_t)(r >> 32);
+    a.out_point[q] = a.point_id ? a.point_id[p] : a.id_base + p;
+    a.out_poly[q] = (int32_t)(uint32_t)r;
   }
 }
 
@@ -2189,22 +1893,6 @@ __global__ __launch_bounds__(kBlock) MGPU_JOIN_ATTR void pip_binned_kernel(JoinA
   if (tile < n_tiles) join_tile<IS, false, true>(a, tile);
 }
 
-// MGPU_BIN_PERSIST: a resident grid (a multiple of 8 workgroups) whose workgroups walk
-// their XCD's run of tiles -- no dispatch per tile (~6 ns each, measured)
-#ifndef MGPU_BIN_PERSIST
-#define MGPU_BIN_PERSIST 0
-#endif
-template <int IS>
-__global__ __launch_bounds__(kBlock) MGPU_JOIN_ATTR void pip_binned_persist_kernel(JoinArgs a, uint32_t per_xcd,
-                                                                                   uint32_t n_tiles) {
-  const uint32_t xcd = blockIdx.x & 7u, stride = gridDim.x >> 3;
-  for (uint32_t t = blockIdx.x >> 3; t < per_xcd; t += stride) {
-    const uint32_t tile = xcd * per_xcd + t;
-    if (tile < n_tiles) join_tile<IS, false, true>(a, tile);
-    __syncthreads();
-  }
-}
-
 // The answers back in input order, per chunk of kBinChunk input points: the chunk's bin
 // runs are read run by run (consecutive lanes, consecutive slots: coalesced, one page
 // per run) and placed by perm[] into LDS, then written out in input order; the pairs of
@@ -2322,29 +2010,25 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   }
 }
 
-// input positions of a few binned slots (the near-tie audit list of a binned join)
-__global__ __launch_bounds__(256) void bin_unslot_kernel(const uint32_t* __restrict__ slot, int64_t n,
-                                                         const uint32_t* __restrict__ ts, int64_t nt,
-                                                         int64_t* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const uint32_t s = slot[i];
-    int64_t lo = 0, hi = nt;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (ts[mid] < s)
-        lo = mid + 1;
-      else
-        hi = mid;
-    }
-    if (lo < nt && ts[lo] == s) out[lo] = i;
+__global__ __launch_bounds__(256) void scatter_i64_kernel(const int64_t* __restrict__ pos, const int64_t* __restrict__ val,
+                                                          int64_t n, int64_t* __restrict__ out) {
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) out[pos[k]] = val[k];
+}
+
+__global__ __launch_bounds__(256) void gather_xy_kernel(const double* __restrict__ x, const double* __restrict__ y,
+                                                        const int64_t* __restrict__ pos, int64_t n,
+                                                        double* __restrict__ xy) {
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
+    xy[2 * k] = x[pos[k]];
+    xy[2 * k + 1] = y[pos[k]];
   }
 }
 
 // ---------------------------------------------------------------- launchers
 
 hipError_t launch_cells(int is, int res, const double* x, const double* y, int64_t n, int64_t* out,
-                        unsigned long long* counters, unsigned long long* ties, int64_t tie_cap, hipStream_t s,
-                        const uint8_t* valid, int64_t voff) {
+                        unsigned long long* counters, unsigned long long* ties, int64_t tie_cap, uint64_t* tie_queue,
+                        int64_t tq_cap, hipStream_t s, const uint8_t* valid, int64_t voff) {
   if (n <= 0) return hipSuccess;
   int64_t blocks = (n + kStreamBlock - 1) / kStreamBlock;
   if (blocks > 256 * 64) blocks = 256 * 64;
@@ -2352,11 +2036,25 @@ hipError_t launch_cells(int is, int res, const double* x, const double* y, int64
     hipLaunchKernelGGL(cells_kernel<MGPU_H3>, dim3((unsigned)blocks), dim3(kStreamBlock), 0, s, x, y, n, res, out, counters,
                        ties, tie_cap, valid, voff);
     hipLaunchKernelGGL(cells_fix_kernel, dim3(256), dim3(kStreamBlock), 0, s, x, y, n, res, out, counters, ties, tie_cap,
-                       valid, voff);
+                       tie_queue, tq_cap, valid, voff);
   } else {
     hipLaunchKernelGGL(cells_kernel<MGPU_BNG>, dim3((unsigned)blocks), dim3(kStreamBlock), 0, s, x, y, n, res, out,
                        counters, ties, tie_cap, valid, voff);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_i64(const int64_t* pos, const int64_t* val, int64_t n, int64_t* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(scatter_i64_kernel, dim3((unsigned)blocks), dim3(256), 0, s, pos, val, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_xy(const double* x, const double* y, const int64_t* pos, int64_t n, double* xy, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(gather_xy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, y, pos, n, xy);
   return hipGetLastError();
 }
 
@@ -2425,8 +2123,6 @@ hipError_t launch_valid_and(const uint8_t* a, int64_t aoff, const uint8_t* b, in
 int64_t join_tiles(int64_t n) { return (n + kTile - 1) / kTile; }
 int64_t join_tile_points() { return kTile; }
 int64_t join_slot_records() { return kSlot; }
-int64_t join_pend_cap() { return kMixCap; }
-int64_t join_pend_words() { return kPendWords; }
 
 constexpr int64_t kFixGrid = 8192;   // fix-kernel workgroups (one wave each; idle ones exit at once)
 hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s, hipEvent_t after_stream) {
@@ -2437,17 +2133,14 @@ hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t
   // workload with many border-chip candidates per point -- BNG res 3 -- dirties most tiles)
   const unsigned fix_blocks = (unsigned)(a.n_tiles < kFixGrid ? a.n_tiles : kFixGrid);
   if (is == MGPU_H3) {
-    hipLaunchKernelGGL(pip_join_kernel<MGPU_H3>, dim3(join_grid<MGPU_H3>(a.n_tiles)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(pip_join_kernel<MGPU_H3>, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, a);
     if (after_stream) hipEventRecord(after_stream, s);
     hipLaunchKernelGGL(pip_fix_kernel<MGPU_H3>, dim3(fix_blocks), dim3(kBlock), 0, s, a);
   } else {
-    hipLaunchKernelGGL(pip_join_kernel<MGPU_BNG>, dim3(join_grid<MGPU_BNG>(a.n_tiles)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(pip_join_kernel<MGPU_BNG>, dim3((unsigned)a.n_tiles), dim3(kBlock), 0, s, a);
     if (after_stream) hipEventRecord(after_stream, s);
     hipLaunchKernelGGL(pip_fix_kernel<MGPU_BNG>, dim3(fix_blocks), dim3(kBlock), 0, s, a);
   }
-  if (MGPU_DEFER)
-    hipLaunchKernelGGL(pip_resolve_kernel, dim3((unsigned)((a.n_tiles + kScanGroup - 1) / kScanGroup)),
-                       dim3(kResolveBlock), 0, s, a);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.group_sum, a.group_cand,
                      (a.n_tiles + kScanGroup - 1) / kScanGroup, e.group_off, a.counters);
   hipLaunchKernelGGL(pair_emit_kernel, dim3((unsigned)((a.n_tiles + kEmitTiles - 1) / kEmitTiles)),
@@ -2471,14 +2164,9 @@ template <int IS>
 static void launch_split_t(const SplitArgs& a, hipStream_t s, hipEvent_t after_classify, hipEvent_t after_mixed) {
   const int64_t nc = split_chunks(a.j.n);
   const size_t lds = (IS == MGPU_H3 && a.j.chips.raster_blk) ? (size_t)a.j.chips.raster_bnx * a.j.chips.raster_bny * 2 : 0;
-  if (MGPU_CFY_WAVE) {
-    const int64_t wg = (nc + kCfyBlock / 64 - 1) / (kCfyBlock / 64);
-    const int64_t grid = std::min<int64_t>(wg, (int64_t)resident_blocks((const void*)classify_wave_kernel<IS>, kCfyBlock, lds));
-    hipLaunchKernelGGL(classify_wave_kernel<IS>, dim3((unsigned)grid), dim3(kCfyBlock), lds, s, a, nc);
-  } else {
-    const int64_t grid = std::min<int64_t>(nc, (int64_t)resident_blocks((const void*)classify_kernel<IS>, kCfyBlock, lds));
-    hipLaunchKernelGGL(classify_kernel<IS>, dim3((unsigned)grid), dim3(kCfyBlock), lds, s, a, nc);
-  }
+  const int64_t wg = (nc + kCfyBlock / 64 - 1) / (kCfyBlock / 64);
+  const int64_t grid = std::min<int64_t>(wg, (int64_t)resident_blocks((const void*)classify_wave_kernel<IS>, kCfyBlock, lds));
+  hipLaunchKernelGGL(classify_wave_kernel<IS>, dim3((unsigned)grid), dim3(kCfyBlock), lds, s, a, nc);
   if (after_classify) hipEventRecord(after_classify, s);
   // (one workgroup per chunk walking its mixed tiles; one workgroup per tile measured 8x
   // slower on C2: ~6 ns per dispatched workgroup, most of them empty)
@@ -2526,16 +2214,8 @@ static void launch_binned_t(const BinArgs& a, hipStream_t s, hipEvent_t after_bi
   if (after_bin) hipEventRecord(after_bin, s);
   const int64_t nc = split_chunks(n), tiles = nc * kChunkTiles;
   const uint32_t per = a.xcd_runs ? (uint32_t)((tiles + 7) / 8) : 0u;
-  if (MGPU_BIN_PERSIST) {
-    const uint32_t per8 = (uint32_t)((tiles + 7) / 8);
-    int64_t grid = resident_blocks((const void*)pip_binned_persist_kernel<IS>, kBlock, 0) / 8 * 8;
-    grid = std::max<int64_t>(8, std::min<int64_t>(grid, 8 * (int64_t)per8));
-    hipLaunchKernelGGL(pip_binned_persist_kernel<IS>, dim3((unsigned)grid), dim3(kBlock), 0, s, a.s.j, per8,
-                       (uint32_t)tiles);
-  } else {
-    const int64_t grid = per ? 8 * (int64_t)per : tiles;
-    hipLaunchKernelGGL(pip_binned_kernel<IS>, dim3((unsigned)grid), dim3(kBlock), 0, s, a.s.j, per, (uint32_t)tiles);
-  }
+  const int64_t grid = per ? 8 * (int64_t)per : tiles;
+  hipLaunchKernelGGL(pip_binned_kernel<IS>, dim3((unsigned)grid), dim3(kBlock), 0, s, a.s.j, per, (uint32_t)tiles);
   if (after_join) hipEventRecord(after_join, s);
   const int64_t fix = tiles < kFixGrid ? tiles : kFixGrid;
   hipLaunchKernelGGL(pip_mixed_fix_kernel<IS>, dim3((unsigned)fix), dim3(kBlock), 0, s, a.s.j);
@@ -2559,13 +2239,6 @@ hipError_t launch_binned(int is, const BinArgs& a, hipStream_t s, hipEvent_t aft
 hipError_t launch_bin_emit(const BinArgs& a, hipStream_t s) {
   if (a.s.j.n <= 0) return hipSuccess;
   hipLaunchKernelGGL(bin_emit_kernel, dim3((unsigned)split_chunks(a.s.j.n)), dim3(kClsBlock), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_bin_unslot(const uint32_t* slot, int64_t n, const uint32_t* ts, int64_t nt, int64_t* out, hipStream_t s) {
-  if (n <= 0 || nt <= 0) return hipSuccess;
-  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(bin_unslot_kernel, dim3((unsigned)blocks), dim3(256), 0, s, slot, n, ts, nt, out);
   return hipGetLastError();
 }
 

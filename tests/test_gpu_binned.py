@@ -1,11 +1,9 @@
 """The binned join pipeline (spatial counting sort of the points, join over
 the binned points, answers gathered back into input order) against the oracle, through
-the C ABI.  MGPU_BIN=1 forces it on tables of any size (the planner's default takes it
-only for tables beyond the Infinity Cache, e.g. C3); MGPU_SPLIT=0 keeps the split
-pipeline of pixel-indexed tables out of the way.  Bit-exact is the bar, as everywhere."""
-import contextlib
-import os
-
+the C ABI.  The context option pipeline = MGPU_PIPELINE_BINNED forces it on tables of any
+size (the planner's default takes it only for tables beyond the Infinity Cache, e.g. C3)
+and keeps the split pipeline of pixel-indexed tables out of the way.  Bit-exact to the
+reference (the oracle with glibc's libm, as H3-Java) is the bar, as everywhere."""
 import numpy as np
 import pytest
 import torch
@@ -13,34 +11,25 @@ import torch
 import mosaic_amd as M
 import oracle as O
 from geom_util import nyc_points
-from test_gpu_parity import T, adversarial_points, oracle_join, oracle_join_cr
+from test_gpu_parity import T, adversarial_points, oracle_join
 
 pytestmark = pytest.mark.gpu
 BINNED = 2  # MGPU_PIPELINE_BINNED
 
 
-@contextlib.contextmanager
-def env(**kw):
-    old = {k: os.environ.get(k) for k in kw}
-    os.environ.update({k: str(v) for k, v in kw.items()})
-    try:
-        yield
-    finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+def opts(gpu, **kw):
+    """Context options of the default context (the one the tests' chip tables live on)."""
+    return M.default_context(gpu).options(**kw)
 
 
-def binned_join(x, y, chips, res, gpu, nb=1024, xcd=1, **kw):
-    with env(MGPU_BIN=1, MGPU_SPLIT=0, MGPU_BIN_N=nb, MGPU_BIN_XCD=xcd):
+def binned_join(x, y, chips, res, gpu, nb=512, xcd=1, **kw):
+    with opts(gpu, pipeline=BINNED, bin_count=nb, bin_xcd=xcd):
         r = M.pip_join(T(x, gpu), T(y, gpu), chips, res, **kw)
     assert r.stats["pipeline"] == BINNED
     return r
 
 
-@pytest.mark.parametrize("nb,xcd", [(1, 1), (64, 0), (1024, 1), (4096, 1)])
+@pytest.mark.parametrize("nb,xcd", [(1, 1), (64, 0), (200, 1), (512, 1)])
 def test_binned_nyc_equals_oracle(gpu, nyc_chips_r9, nb, xcd):
     """NYC zones, H3 res 9, ragged sizes (not a multiple of any chunk or tile)."""
     d = nyc_chips_r9.upload()
@@ -98,21 +87,24 @@ def test_binned_overlapping_polygons(gpu):
 
 def test_binned_adversarial_points_and_near_tie_positions(gpu, nyc_chips_r9):
     """Points on H3 cell corners (the near-tie route runs in pip_mixed_fix_kernel over the
-    binned tiles): pairs equal the correctly rounded oracle, and mgpu_last_near_ties
-    reports INPUT positions -- the same list the fused pipeline reports."""
+    binned tiles): pairs equal the reference's (the oracle with glibc's libm), nothing
+    excluded; mgpu_last_near_ties reports INPUT positions -- the same list the fused
+    pipeline reports -- and both pipelines apply the same libm overrides."""
     d = nyc_chips_r9.upload()
     x, y = adversarial_points(nyc_chips_r9)
     r = binned_join(x, y, d, 9, gpu)
     ties_b = np.sort(d.ctx.last_near_ties())
     gp, gq = r.numpy()
-    op, oq = oracle_join_cr(nyc_chips_r9, x, y)
+    op, oq = oracle_join(nyc_chips_r9, x, y)
     assert np.array_equal(gp, op) and np.array_equal(gq, oq)
-    with env(MGPU_BIN=0, MGPU_SPLIT=0):
+    with opts(gpu, pipeline=0):
         rf = M.pip_join(T(x, gpu), T(y, gpu), d, 9)
     ties_f = np.sort(d.ctx.last_near_ties())
     assert rf.stats["pipeline"] == 0
     assert len(ties_b) > 0 and np.array_equal(ties_b, ties_f)
     assert r.stats["n_near_ties"] == rf.stats["n_near_ties"]
+    assert r.stats["libm_overrides"] == rf.stats["libm_overrides"]
+    assert np.array_equal(rf.numpy()[0], op) and np.array_equal(rf.numpy()[1], oq)
 
 
 def test_binned_bng_london(gpu):
@@ -139,7 +131,7 @@ def test_binned_points_outside_and_nan(gpu, nyc_chips_r9):
     op, oq = oracle_join(nyc_chips_r9, x, y)
     assert np.array_equal(gp, op) and np.array_equal(gq, oq)
     x[5] = np.nan
-    with env(MGPU_BIN=1, MGPU_SPLIT=0):
+    with opts(gpu, pipeline=BINNED):
         with pytest.raises(M.IllegalArgumentException):
             M.pip_join(T(x, gpu), T(y, gpu), d, 9)
 
@@ -148,7 +140,7 @@ def test_binned_c3_full_table(gpu):
     """BASELINE config C3's whole table (74,000 tract-like polygons, 9.4M chips at res
     10) -- the case the binned pipeline is for -- with 2.5M points: the planner picks it
     by itself (table beyond the Infinity Cache, batch >= 2^21 points), pairs equal the
-    oracle and the fused pipeline."""
+    reference (the oracle, glibc libm) and the fused pipeline."""
     import bench_workloads as W
     P = W.tract_polygons()
     c = M.tessellate(P, M.H3IndexSystem(), 10, keep_core_geometries=False)
@@ -157,10 +149,9 @@ def test_binned_c3_full_table(gpu):
     r = M.pip_join(T(x, gpu), T(y, gpu), d, 10)
     assert r.stats["pipeline"] == BINNED
     gp, gq = r.numpy()
-    with O.h3_libm("cr"):
-        op, oq = O.pip_join(0, 10, x, y, c.cell, c.polygon_id, c.is_core, c.wkb_offsets, c.wkb)
+    op, oq = O.pip_join(0, 10, x, y, c.cell, c.polygon_id, c.is_core, c.wkb_offsets, c.wkb)
     assert np.array_equal(gp, op) and np.array_equal(gq, oq)
-    with env(MGPU_BIN=0):
+    with opts(gpu, pipeline=0):
         rf = M.pip_join(T(x, gpu), T(y, gpu), d, 10)
     assert rf.stats["pipeline"] == 0
     fp, fq = rf.numpy()

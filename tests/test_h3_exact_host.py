@@ -132,3 +132,37 @@ def test_route_on_edge_fixture():
         assert np.array_equal(O.h3_points_to_cells(lon[m], lat[m], int(r)), f["cell_glibc"][m])
         with O.h3_libm("cr"):
             assert np.array_equal(O.h3_points_to_cells(lon[m], lat[m], int(r)), f["cell_cr"][m])
+
+
+def glibc_route(lon, lat, res):
+    lon = np.ascontiguousarray(lon, np.float64)
+    lat = np.ascontiguousarray(lat, np.float64)
+    out = np.zeros(len(lon), np.int64)
+    assert _native.lib().mgpu_test_h3_glibc_host(lon.ctypes.data, lat.ctypes.data, len(lon), int(res),
+                                                 out.ctypes.data) == 0
+    return out
+
+
+def test_near_tie_resolver_equals_reference_on_edge_fixture():
+    """The library's near-tie resolver (h3_glibc.cpp: platform glibc libm, x87 long
+    double, gcc without FMA contraction -- H3-Java's JNI arithmetic) equals the fixture's
+    reference column on all 180k corner / edge points, 0 mismatches, including the points
+    where glibc misrounds a deciding argument; and the oracle's glibc mode on this host."""
+    f = np.load(os.path.join(GOLDEN, "h3_edge_points.npz"))
+    lon, lat, res = f["lon"], f["lat"], f["res"]
+    for r in np.unique(res):
+        m = res == r
+        got = glibc_route(lon[m], lat[m], int(r))
+        assert np.array_equal(got, f["cell_glibc"][m]), int(r)
+        assert np.array_equal(got, O.h3_points_to_cells(lon[m], lat[m], int(r))), int(r)
+
+
+def test_near_tie_resolver_equals_reference_global():
+    rng = np.random.default_rng(8)
+    n = 200_000
+    for res in (0, 1, 5, 9, 10, 15):
+        lon = rng.uniform(-180.0, 180.0, n)
+        lat = np.degrees(np.arcsin(rng.uniform(-1.0, 1.0, n)))
+        assert np.array_equal(glibc_route(lon, lat, res), O.h3_points_to_cells(lon, lat, res)), res
+    # H3-Java rejects non-finite input (geoToH3 returns H3_NULL)
+    assert glibc_route([np.nan, 1.0], [1.0, np.inf], 9).tolist() == [0, 0]

@@ -105,12 +105,9 @@ def test_raster_wrong_resolution_has_no_index(nyc_chips_r9):
     assert kind[0] == 4
 
 
-@pytest.fixture
-def bng_raster(monkeypatch):
-    monkeypatch.setenv("MGPU_RASTER_BNG", "1")  # BNG tables get a pixel index only on request (capi.cpp)
-
-
-def test_raster_bng_london_r4(bng_raster):
+def test_raster_bng_london_r4():
+    # (mgpu_test_raster_host builds BNG tables with their pixel index: the index is the
+    # subject here; the join path builds it only with the raster_bng option)
     import bench_workloads as W
     c = M.tessellate(W.london_districts(), M.BNGIndexSystem(), 4)
     rng = np.random.default_rng(13)
@@ -125,7 +122,7 @@ def test_raster_bng_london_r4(bng_raster):
     check_raster(c, 4, xs, ys, 0.02)
 
 
-def test_raster_bng_postcodes_r3_and_quadrant(bng_raster):
+def test_raster_bng_postcodes_r3_and_quadrant():
     z = M.Polygons.from_npz(os.path.join(ROOT, "tests", "golden", "london_postcode_zones.npz"))
     rng = np.random.default_rng(15)
     for res in (3, -4):

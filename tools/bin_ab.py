@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Binned vs fused/split join timings on one bench config (the chip table and the points
-built once; the pipeline chosen per call by the MGPU_BIN* switches): one JSON line per
+built once; the pipeline chosen per call by the context options): one JSON line per
 variant {config, variant, stream_ms, bin_ms, emit_ms, pipeline_ms, pipeline, pairs}.
 tools/bin_ab.py --config c3 [--points N] [--variants fused,bin1024,...]"""
 import argparse
@@ -16,14 +16,15 @@ sys.path.insert(0, ROOT)
 
 VARIANTS = {
     "auto": {},
-    "fused": {"MGPU_BIN": "0", "MGPU_SPLIT": "0"},
-    "bin16": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "16"},
-    "bin32": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "32"},
-    "bin64": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "64"},
-    "bin128": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "128"},
-    "bin256": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "256"},
-    "bin1024": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "1024"},
-    "bin256_noxcd": {"MGPU_BIN": "1", "MGPU_SPLIT": "0", "MGPU_BIN_N": "256", "MGPU_BIN_XCD": "0"},
+    "fused": {"pipeline": 0},
+    "split": {"pipeline": 1},
+    "bin16": {"pipeline": 2, "bin_count": 16},
+    "bin32": {"pipeline": 2, "bin_count": 32},
+    "bin64": {"pipeline": 2, "bin_count": 64},
+    "bin128": {"pipeline": 2, "bin_count": 128},
+    "bin256": {"pipeline": 2, "bin_count": 256},
+    "bin512": {"pipeline": 2, "bin_count": 512},
+    "bin256_noxcd": {"pipeline": 2, "bin_count": 256, "bin_xcd": 0},
 }
 
 
@@ -50,9 +51,7 @@ def main():
     oq = torch.empty(cap, dtype=torch.int32, device=dev)
     ref = None
     for v in a.variants.split(","):
-        saved = {k: os.environ.get(k) for k in VARIANTS[v]}
-        os.environ.update(VARIANTS[v])
-        try:
+        with ctx.options(**VARIANTS[v]):
             s, p, mx, em = [], [], [], []
             for _ in range(a.reps + 1):
                 r = M.pip_join(x, y, chips, ns.res, out=(op, oq), capacity=cap, index_system=wl["isys"])
@@ -60,12 +59,6 @@ def main():
                 p.append(r.stats["kernel_ms"])
                 mx.append(r.stats["mixed_kernel_ms"])
                 em.append(r.stats["emit_kernel_ms"])
-        finally:
-            for k, val in saved.items():
-                if val is None:
-                    del os.environ[k]
-                else:
-                    os.environ[k] = val
         # every variant's pairs equal the first one's (checksums over the full output)
         m = len(r)
         ck = (int(op[:m].sum().item()), int((oq[:m].to(torch.int64) * (torch.arange(m, device=dev) % 7919)).sum().item()))

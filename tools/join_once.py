@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Run the bench workload's join (or cells) kernel a few times -- a short target for
-rocprofv3 PMC passes.  --ablate sets MGPU_ABLATE (1 = no PIP, 2 = no probe)."""
+rocprofv3 PMC passes.  --pipeline forces one of the join's pipelines (context option)."""
 import argparse
 import os
 import sys
@@ -18,18 +18,17 @@ def main():
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2")
     ap.add_argument("--seed", type=int, default=0x20250314)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--ablate", type=int, default=0)
+    ap.add_argument("--pipeline", type=int, default=-1)
     ap.add_argument("--cells", action="store_true")
     ap.add_argument("--bng", action="store_true", help="with --cells: BNG res 4 on eastings/northings "
                     "(a pure 16 B read + 8 B write stream, used to calibrate FETCH_SIZE / WRITE_SIZE)")
     a = ap.parse_args()
-    if a.ablate:
-        os.environ["MGPU_ABLATE"] = str(a.ablate)
     import mosaic_amd as M
     import bench as B
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     ctx = M.default_context(dev)
+    ctx.set_option("pipeline", a.pipeline)
     import bench_workloads as W
     wl = B.workload(a, W, M)
     isys = wl["isys"]
