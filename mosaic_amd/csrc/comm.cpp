@@ -24,7 +24,7 @@ struct CommState {
   int rank = 0, world = 1;
   void* scratch = nullptr;  // device: the broadcast header, the gathered counts
 };
-constexpr size_t kScratch = 4096;
+constexpr size_t kScratch = 4096;  // >= the blob header + a status word; the counts
 
 CommState* state(mgpu_ctx* ctx) { return (CommState*)ctx->comm; }
 
@@ -95,39 +95,88 @@ int32_t mgpu_comm_info(mgpu_ctx* ctx, int32_t* rank, int32_t* world) {
   return MGPU_OK;
 }
 
+// Every rank issues the same collectives in the same order whatever fails locally: (1) the
+// 1 KiB header broadcast, (2) an all-reduce(min) of a status word -- each rank's "ready"
+// (root: a valid table; receivers: a valid header and the receiving allocation), and only
+// if every rank is ready (3) the bulk broadcast.  A local failure therefore never leaves
+// the other ranks blocked in a broadcast this rank skipped: all ranks see the failed
+// agreement and return an error.  A failed RCCL call aborts the communicator
+// (ncclCommAbort): later calls on the context fail instead of hanging.
+namespace {
+int32_t comm_failed(mgpu_ctx* ctx, const char* what, ncclResult_t r) {
+  CommState* c = state(ctx);
+  int32_t st = mgpu::set_error(MGPU_E_DEVICE, "%s: %s (communicator aborted)", what, ncclGetErrorString(r));
+  if (c->comm) ncclCommAbort(c->comm);
+  if (c->scratch) hipFree(c->scratch);
+  delete c;
+  ctx->comm = nullptr;
+  return st;
+}
+}  // namespace
+
 int32_t mgpu_chips_broadcast(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t root, mgpu_chips** out, void* stream) {
   if (!ctx || !ctx->comm || !out) return mgpu::set_error(MGPU_E_INVALID_ARG, "chips_broadcast: no communicator / out");
   CommState* c = state(ctx);
+  // (every rank sees the same root and world: an argument error here is the same on all)
   if (root < 0 || root >= c->world) return mgpu::set_error(MGPU_E_INVALID_ARG, "root %d of %d", root, c->world);
   const bool is_root = c->rank == root;
-  if (is_root && (!chips || chips->device != ctx->device))
-    return mgpu::set_error(MGPU_E_INVALID_ARG, "chips_broadcast: the root needs its chip table on the context's GPU");
+  *out = nullptr;
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
-  *out = nullptr;
-  // 1. the 1 KiB header, to size the receiving allocation
-  void* hdr_dev = is_root ? chips->blob : c->scratch;
-  NCCL_TRY(ncclBroadcast(hdr_dev, hdr_dev, (size_t)mgpu::kBlobHeaderSize, ncclUint8, root, c->comm, s));
+  int32_t* status = (int32_t*)((uint8_t*)c->scratch + mgpu::kBlobHeaderSize);
+  const bool root_ok = !is_root || (chips && chips->device == ctx->device && chips->blob);
+  // 1. the header (a root without a table sends zeros: no receiver accepts them)
+  void* hdr_dev = (is_root && root_ok) ? chips->blob : c->scratch;
+  if (is_root && !root_ok) (void)hipMemsetAsync(c->scratch, 0, (size_t)mgpu::kBlobHeaderSize, s);
+  ncclResult_t r = ncclBroadcast(hdr_dev, hdr_dev, (size_t)mgpu::kBlobHeaderSize, ncclUint8, root, c->comm, s);
+  if (r != ncclSuccess) return comm_failed(ctx, "ncclBroadcast(header)", r);
   int64_t bytes = 0;
+  void* dst = nullptr;
+  int32_t mine = MGPU_OK;
+  const char* why = "";
   if (is_root) {
-    bytes = (int64_t)chips->bytes;
+    if (root_ok) bytes = (int64_t)chips->bytes;
+    else mine = MGPU_E_INVALID_ARG, why = "the root needs its chip table on the context's GPU";
   } else {
     std::vector<uint8_t> h((size_t)mgpu::kBlobHeaderSize);
-    HIP_TRY(hipMemcpyAsync(h.data(), c->scratch, h.size(), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    bytes = mgpu::blob_bytes_of_header(h.data());
-    if (bytes < mgpu::kBlobHeaderSize) return mgpu::set_error(MGPU_E_INVALID_ARG, "chips_broadcast: not a chip-table blob");
+    if (hipMemcpyAsync(h.data(), c->scratch, h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      mine = MGPU_E_DEVICE, why = "reading the broadcast header";
+    } else {
+      bytes = mgpu::blob_bytes_of_header(h.data());
+      if (bytes < mgpu::kBlobHeaderSize) mine = MGPU_E_INVALID_ARG, why = "the root sent no chip-table blob";
+      else if (hipMalloc(&dst, (size_t)bytes) != hipSuccess) dst = nullptr, mine = MGPU_E_DEVICE, why = "hipMalloc of the receiving table";
+    }
   }
-  // 2. the whole blob, straight into the receiving ranks' new allocation
-  void* dst = nullptr;
-  if (!is_root) HIP_TRY(hipMalloc(&dst, (size_t)bytes));
-  void* buf = is_root ? chips->blob : dst;
-  ncclResult_t r = ncclBroadcast(buf, buf, (size_t)bytes, ncclUint8, root, c->comm, s);
+  // 2. agreement: the smallest status (errors are negative) over all ranks
+  int32_t agreed = mine;
+  if (hipMemcpyAsync(status, &mine, 4, hipMemcpyHostToDevice, s) != hipSuccess) agreed = MGPU_E_DEVICE;
+  r = ncclAllReduce(status, status, 1, ncclInt32, ncclMin, c->comm, s);
   if (r != ncclSuccess) {
     if (dst) hipFree(dst);
-    return mgpu::set_error(MGPU_E_DEVICE, "ncclBroadcast(%lld bytes): %s", (long long)bytes, ncclGetErrorString(r));
+    return comm_failed(ctx, "ncclAllReduce(status)", r);
   }
-  HIP_TRY(hipStreamSynchronize(s));
+  int32_t all = MGPU_OK;
+  if (hipMemcpyAsync(&all, status, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    all = MGPU_E_DEVICE;
+  if (agreed != MGPU_OK && all == MGPU_OK) all = agreed;
+  if (all != MGPU_OK) {
+    // every rank skips the bulk broadcast
+    if (dst) hipFree(dst);
+    if (mine != MGPU_OK) return mgpu::set_error(mine, "chips_broadcast: %s", why);
+    return mgpu::set_error(all, "chips_broadcast: another rank could not take part (status %d)", all);
+  }
+  // 3. the whole blob, straight into the receiving ranks' new allocation
+  void* buf = is_root ? chips->blob : dst;
+  r = ncclBroadcast(buf, buf, (size_t)bytes, ncclUint8, root, c->comm, s);
+  if (r != ncclSuccess) {
+    if (dst) hipFree(dst);
+    return comm_failed(ctx, "ncclBroadcast(blob)", r);
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) {
+    if (dst) hipFree(dst);
+    return mgpu::set_error(MGPU_E_DEVICE, "chips_broadcast: stream synchronize failed");
+  }
   if (is_root) return MGPU_OK;
   int32_t st = mgpu::adopt_device_blob(ctx, dst, bytes, out);
   if (st) hipFree(dst);
@@ -137,23 +186,26 @@ int32_t mgpu_chips_broadcast(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t roo
 int32_t mgpu_pair_offsets(mgpu_ctx* ctx, int64_t local_pairs, int64_t* out_offset, int64_t* out_total,
                           int64_t* out_counts, void* stream) {
   if (!ctx || !ctx->comm) return mgpu::set_error(MGPU_E_INVALID_ARG, "pair_offsets: no communicator");
-  if (local_pairs < 0) return mgpu::set_error(MGPU_E_INVALID_ARG, "pair_offsets: negative count");
   CommState* c = state(ctx);
   if ((size_t)(c->world + 1) * 8 > kScratch) return mgpu::set_error(MGPU_E_INVALID_ARG, "world too large");
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   int64_t* mine = (int64_t*)c->scratch;
   int64_t* all = mine + 1;
-  HIP_TRY(hipMemcpyAsync(mine, &local_pairs, 8, hipMemcpyHostToDevice, s));
-  NCCL_TRY(ncclAllGather(mine, all, 1, ncclInt64, c->comm, s));
+  // a negative count still takes part in the all-gather (as -1): every rank then fails
+  const int64_t v = local_pairs < 0 ? -1 : local_pairs;
+  HIP_TRY(hipMemcpyAsync(mine, &v, 8, hipMemcpyHostToDevice, s));
+  ncclResult_t r = ncclAllGather(mine, all, 1, ncclInt64, c->comm, s);
+  if (r != ncclSuccess) return comm_failed(ctx, "ncclAllGather(pair counts)", r);
   std::vector<int64_t> counts((size_t)c->world);
   HIP_TRY(hipMemcpyAsync(counts.data(), all, counts.size() * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   int64_t off = 0, tot = 0;
-  for (int r = 0; r < c->world; r++) {
-    if (r < c->rank) off += counts[r];
-    tot += counts[r];
-    if (out_counts) out_counts[r] = counts[r];
+  for (int k = 0; k < c->world; k++) {
+    if (counts[k] < 0) return mgpu::set_error(MGPU_E_INVALID_ARG, "pair_offsets: negative count on rank %d", k);
+    if (k < c->rank) off += counts[k];
+    tot += counts[k];
+    if (out_counts) out_counts[k] = counts[k];
   }
   if (out_offset) *out_offset = off;
   if (out_total) *out_total = tot;

@@ -95,11 +95,19 @@ def host_blob(table):
                                          table.wkb_offsets.ctypes.data, wkb.ctypes.data, ctypes.byref(p),
                                          ctypes.byref(nb)))
     try:
-        # (not ctypes.string_at: its size is a C int -- C3's 4.7 GB blob came back mod 2^32)
-        arr = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(int(nb.value),))
-        return arr.tobytes()
+        return host_bytes(p.value, nb.value)
     finally:
         N.lib().mgpu_host_free(p)
+
+
+def host_bytes(address, size):
+    """`size` bytes at a host address as bytes, for any size (not ctypes.string_at: its
+    size is a C int -- C3's 4.7 GB blob came back mod 2^32)."""
+    if size == 0:
+        return b""
+    arr = np.ctypeslib.as_array(ctypes.cast(ctypes.c_void_p(address), ctypes.POINTER(ctypes.c_uint8)),
+                                shape=(int(size),))
+    return arr.tobytes()
 
 
 def blob_info(blob):
@@ -116,18 +124,19 @@ def upload_host_blob(blob, ctx):
     return DeviceChips(None, ctx, handle=h)
 
 
-def broadcast_host_blob(blob, src=0, group=None):
+def broadcast_host_blob(blob, src=0, group=None, piece=1 << 30):
     """Control-plane replication of a host blob (torch.distributed, e.g. gloo): what a
-    host without RCCL (or a JVM driver) does instead of mgpu_chips_broadcast."""
+    host without RCCL (or a JVM driver) does instead of mgpu_chips_broadcast.  The blob
+    travels in pieces of at most `piece` bytes (default 1 GiB: every gloo message stays
+    well inside 32-bit sizes)."""
     import torch
     import torch.distributed as dist
     rank = dist.get_rank(group)
     size = torch.tensor([len(blob) if rank == src else 0], dtype=torch.int64)
     dist.broadcast(size, src, group=group)
     n = int(size.item())
-    # in pieces of at most 1 GiB (keeps every gloo message well inside 32-bit sizes)
     out = np.empty(n, dtype=np.uint8) if rank != src else None
-    piece = 1 << 30
+    piece = int(piece)
     for off in range(0, n, piece):
         m = min(piece, n - off)
         if rank == src:

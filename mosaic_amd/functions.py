@@ -177,7 +177,10 @@ def pip_join(x, y, chips, resolution, index_system=None, point_id=None, point_id
     Returns a JoinResult with int64 point ids and int32 polygon ids ordered by input
     position then polygon id.  ``capacity`` bounds the output (default: n + 1/8 n
     headroom; when the pairs do not fit, arrays of the exact count are allocated and
-    filled from the join's kept records by mgpu_pip_join_fetch -- the join is not redone)."""
+    filled from the join's kept records by mgpu_pip_join_fetch -- the join is not redone).
+    ``out`` = (point ids, polygon ids) preallocated: with ``capacity`` None, pairs that do
+    not fit them go to fresh arrays of the exact count the same way; an explicit
+    ``capacity`` is a hard bound (CapacityError, with the count)."""
     import torch
     isys = index_system or _H3
     res = isys.get_resolution(resolution)
@@ -209,7 +212,7 @@ def pip_join(x, y, chips, resolution, index_system=None, point_id=None, point_id
     status = N.lib().mgpu_pip_join(chips.ctx.handle, chips.handle, isys.code, res, x.data_ptr(), y.data_ptr(),
                                    pid_ptr, int(point_id_base), n, cap, ctypes.byref(cnt), op.data_ptr(),
                                    oq.data_ptr(), s, st)
-    if status == N.MGPU_E_CAPACITY and capacity is None and out is None:
+    if status == N.MGPU_E_CAPACITY and capacity is None:
         # the join's records are kept: write them into arrays of the exact size
         cap = int(cnt.value)
         op = torch.empty(cap, dtype=torch.int64, device=x.device)

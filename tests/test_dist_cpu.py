@@ -16,7 +16,7 @@ import numpy as np
 import torch.multiprocessing as mp
 
 from mosaic_amd.dist import (blob_contains, blob_info, broadcast_host_blob, gather_offsets_host, host_blob,
-                             shard_range)
+                             host_bytes, shard_range)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -46,6 +46,19 @@ def test_host_blob_roundtrip(nyc_chips_r9):
         blob_info(b[:-256])
 
 
+def test_host_bytes_beyond_32_bit_sizes():
+    """A host buffer larger than 2^32 bytes comes back whole (C3's 4.7 GB blob once came
+    back mod 2^32 through ctypes.string_at's C-int size)."""
+    n = (1 << 32) + 4099
+    buf = np.zeros(n, dtype=np.uint8)  # calloc'd: pages appear as they are touched
+    buf[-3:] = (7, 8, 9)
+    buf[(1 << 32) - 1] = 5
+    b = host_bytes(buf.ctypes.data, n)
+    assert len(b) == n and b[-3:] == bytes((7, 8, 9)) and b[(1 << 32) - 1] == 5
+    del b
+    assert host_bytes(buf.ctypes.data, 0) == b""
+
+
 def _worker(rank, world, port, x, y, chips, q):
     import torch.distributed as dist
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -59,7 +72,8 @@ def _worker(rank, world, port, x, y, chips, q):
     if rank == 0:
         t = M.ChipTable(cell, poly, core, off, wkb)
         blob = host_blob(t)
-    blob = broadcast_host_blob(blob, 0)
+    # small pieces: the chunked path (C3's 4.7 GB blob goes in 1 GiB pieces) end to end
+    blob = broadcast_host_blob(blob, 0, piece=65_537)
     info = blob_info(blob)
     # the received blob answers st_contains like the oracle on its own rows
     rng = np.random.default_rng(rank)

@@ -344,6 +344,13 @@ def test_pip_join_capacity(gpu, nyc_chips_r9):
     with pytest.raises(M.CapacityError) as ei:
         M.pip_join(T(x, gpu), T(y, gpu), nyc_chips_r9, 9, capacity=10)
     assert ei.value.required == len(op)
+    # undersized preallocated output: without a capacity the pairs go to exact-size
+    # arrays (mgpu_pip_join_fetch); with one, the bound holds
+    small = (torch.empty(10, dtype=torch.int64, device=gpu), torch.empty(10, dtype=torch.int32, device=gpu))
+    gp, gq = M.pip_join(T(x, gpu), T(y, gpu), nyc_chips_r9, 9, out=small).numpy()
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+    with pytest.raises(M.CapacityError):
+        M.pip_join(T(x, gpu), T(y, gpu), nyc_chips_r9, 9, out=small, capacity=10)
 
 
 def test_pip_join_default_capacity_grows(gpu):
@@ -676,6 +683,12 @@ def test_comm_single_rank(gpu, nyc_chips_r9):
     N.check(N.lib().mgpu_comm_unique_id(uid))
     N.check(N.lib().mgpu_comm_init(ctx.handle, uid, 0, 1))
     assert D.comm_info(ctx) == (0, 1)
+    # a root without a table: every rank (here the one) agrees on the failure after the
+    # header broadcast and skips the bulk broadcast -- an error, not a hang
+    outp = ctypes.c_void_p()
+    s = torch.cuda.current_stream(gpu).cuda_stream
+    with pytest.raises(M.IllegalArgumentException):
+        N.check(N.lib().mgpu_chips_broadcast(ctx.handle, None, 0, ctypes.byref(outp), s))
     d = nyc_chips_r9.upload(ctx)
     d2 = D.broadcast_chips(d, ctx)
     assert d2 is d
