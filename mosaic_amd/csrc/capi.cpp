@@ -63,7 +63,7 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // complete chip table there.
 constexpr uint64_t kBlobMagic = 0x4d4f534149434850ULL;  // "MOSAICHP"
 constexpr int kBlobArrays = 23;
-constexpr uint32_t kBlobVersion = 8;
+constexpr uint32_t kBlobVersion = 9;  // 9: 32-pixel rank words
 struct BlobHeader {
   uint64_t magic;
   uint32_t version, hash_mask, max_probe, n_chips, n_cells;
@@ -515,12 +515,12 @@ void build_grid(const mgpu::ChipTableView& hv, uint32_t c, const mgpu::wkb::Flat
 // Anything else is kPixMixed and takes the full path in the kernel.
 // the second level's rank table over the (ascending) mixed pixels of an n-pixel raster
 static void mixed_rank(const std::vector<uint32_t>& mixed, size_t n, std::vector<mgpu::RankWord>& rank) {
-  rank.assign((n + 63) / 64, mgpu::RankWord{0, 0});
-  for (uint32_t p : mixed) rank[p >> 6].bits |= 1ull << (p & 63);
-  uint64_t c = 0;
+  rank.assign((n + 31) / 32, mgpu::RankWord{0, 0});
+  for (uint32_t p : mixed) rank[p >> 5].bits |= 1u << (p & 31);
+  uint32_t c = 0;
   for (auto& w : rank) {
     w.base = c;
-    c += (uint64_t)__builtin_popcountll(w.bits);
+    c += (uint32_t)__builtin_popcount(w.bits);
   }
 }
 
@@ -1075,6 +1075,17 @@ int32_t read_ties(mgpu_ctx* ctx, int64_t n, std::vector<TieRec>& out) {
   if (nh) memcpy(out.data(), head + 2, (size_t)nh * 32);
   if (n > nh) HIP_TRY(hipMemcpy(out.data() + nh, ctx->tq + 2 + 4 * nh, (size_t)(n - nh) * 32, hipMemcpyDeviceToHost));
   return MGPU_OK;
+}
+
+// The reference's lattice key of every queued point (h3_glibc.cpp), by record; and the
+// (position, key) list sorted by position for the override table.
+std::vector<std::pair<int64_t, uint64_t>> libm_reference_keys(std::vector<TieRec>& ties, int res) {
+  std::sort(ties.begin(), ties.end(), [](const TieRec& a, const TieRec& b) { return a.pos < b.pos; });
+  std::vector<std::pair<int64_t, uint64_t>> out(ties.size());
+  mgpu::parallel_for((int64_t)ties.size(), 256, [&](int64_t b, int64_t e, int) {
+    for (int64_t k = b; k < e; k++) out[k] = {ties[k].pos, mgpu::h3glibc::lattice_key(ties[k].x, ties[k].y, res)};
+  });
+  return out;
 }
 
 // The reference's libm for the near-ties (h3_glibc.cpp); cells = true: keys are cell
@@ -1949,7 +1960,8 @@ static bool plan_bins(const mgpu_options& o, const mgpu_chips* chips, int32_t is
 static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
                          const double* y, const int64_t* point_id, int64_t id_base, int64_t n, int64_t capacity,
                          int64_t* out_point, int32_t* out_poly, hipStream_t s, bool timed,
-                         const uint8_t* valid = nullptr, int64_t valid_off = 0, int64_t n_ovr = 0) {
+                         const uint8_t* valid = nullptr, int64_t valid_off = 0, int64_t n_ovr = 0,
+                         int tie_host = 0) {
   if (!ctx || !chips) return fail(MGPU_E_INVALID_ARG, "ctx/chips is NULL");
   if (int32_t r = check_res(is, res)) return r;
   if (chips->index_system != is)
@@ -1987,6 +1999,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   a.tie_cap = ctx->tq_cap;
   a.ovr = ctx->ovr;
   a.n_ovr = n_ovr;
+  a.tie_host = (is == MGPU_H3 && tie_host) ? 1 : 0;
   a.pos_of = nullptr;
   mgpu::EmitArgs e;
   e.tile_count = a.tile_count;
@@ -2132,6 +2145,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   L2.emit = e;
   L2.n_tiles = tiles;
   L2.n_ovr = n_ovr;
+  L2.tie_host = a.tie_host;
   L2.pool_ok = false;
   L2.total = -1;
   L2.valid = true;
@@ -2143,6 +2157,18 @@ int32_t mgpu_last_near_ties(mgpu_ctx* ctx, int64_t* out_index, int64_t cap, int6
   *out_n = 0;
   if (!ctx->tq) return MGPU_OK;
   if (int32_t st = set_device(ctx->device)) return st;
+  if (ctx->last.valid && ctx->last.n_ovr > 0) {
+    // the last join was rerun with the reference's cell of every point its first pass
+    // queued: the override table (ascending positions) is the list
+    const int64_t n = ctx->last.n_ovr;
+    *out_n = n;
+    if (n > cap) return fail(MGPU_E_CAPACITY, "%lld near-tie points, capacity %lld", (long long)n, (long long)cap);
+    std::vector<uint64_t> hv((size_t)n * 2);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(hv.data(), ctx->ovr, hv.size() * 8, hipMemcpyDeviceToHost));
+    for (int64_t k = 0; k < n; k++) out_index[k] = (int64_t)hv[2 * k];
+    return MGPU_OK;
+  }
   uint64_t cnt = 0;
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(&cnt, ctx->tq, 8, hipMemcpyDeviceToHost));
@@ -2174,45 +2200,53 @@ int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, 
 }  // extern "C"
 
 // mgpu_pip_join with an optional validity bitmap of the points (the Arrow entry's nulls).
-// One join; then, for H3 with the reference's libm, the route's near-ties (counted in the
-// same copy as the pair count, their first kTqHead records with it) recomputed on the
-// host with the reference's arithmetic (h3_glibc.cpp).  Where that moves a point's cell
-// -- glibc misrounding an argument that decides it -- the join is run again with those
-// cells as overrides, so the output is the reference's.  A near-tie queue that overflowed
-// is grown and the join redone.
+// H3 with the reference's libm: one join in which every point whose fast projection
+// falls in its tie band is queued and joined with the fast cell (JoinArgs.tie_host);
+// the host recomputes the queued points with the reference's arithmetic (h3_glibc.cpp:
+// glibc libm + x87, as H3-Java's JNI library on this host) and, only if a cell moves
+// -- the fast path's last bits, or glibc misrounding an argument that decides it --
+// runs the join again with the reference's cell of EVERY queued point as an override
+// (the fix kernels then take the override without computing the device route).  With
+// the correctly rounded libm (option h3_libm) the fix kernels decide the ties by the
+// device route.  A near-tie queue that overflowed is grown and the join redone.
 static int32_t pip_join_sync(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
                              const double* y, const int64_t* point_id, int64_t point_id_base, int64_t n,
                              int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id, int32_t* out_polygon_id,
                              void* stream, mgpu_stats* stats, const uint8_t* valid, int64_t valid_off) {
   hipStream_t s = (hipStream_t)stream;
   const bool reference_libm = is == MGPU_H3 && ctx && ctx->opt.h3_libm == MGPU_LIBM_REFERENCE;
-  int64_t n_ovr = 0, n_ties = 0;
+  int64_t n_ovr = 0, n_ties = 0, n_moved = 0;
   uint64_t h[8] = {0};
   for (int attempt = 0;; attempt++) {
     int32_t st = join_impl(ctx, chips, is, res, x, y, point_id, point_id_base, n, capacity, out_point_id,
-                           out_polygon_id, s, true, valid, valid_off, n_ovr);
+                           out_polygon_id, s, true, valid, valid_off, n_ovr, reference_libm && n_ovr == 0);
     if (st) return st;
     HIP_TRY(hipMemcpyAsync(ctx->pin, ctx->ws, 16 * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(ctx->pin + 16, ctx->tq, (2 + 4 * kTqHead) * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(stream_wait(ctx, s));
     memcpy(h, ctx->pin, sizeof h);
-    n_ties = (int64_t)ctx->pin[16];
+    const int64_t queued = (int64_t)ctx->pin[16];
     if (h[2]) break;  // invalid coordinates: reported below
     if (attempt >= 3) return fail(MGPU_E_INTERNAL, "pip_join: near-tie resolution did not settle");
-    if (n_ties > ctx->tq_cap) {
-      if (int32_t e = ensure_tq(ctx, n_ties + n_ties / 4 + 1024)) return e;
+    if (queued > ctx->tq_cap) {
+      if (int32_t e = ensure_tq(ctx, queued + queued / 4 + 1024)) return e;
       continue;
     }
-    if (!reference_libm || n_ties == 0 || n_ovr > 0) break;
+    if (n_ovr > 0) break;  // the rerun with the reference's cells
+    n_ties = queued;
+    if (!reference_libm || n_ties == 0) break;
     std::vector<TieRec> tr;
     if (int32_t e = read_ties(ctx, n_ties, tr)) return e;
-    const auto diff = libm_second_opinion(tr, res, false);
-    if (diff.empty()) break;
-    std::vector<uint64_t> hv(2 * diff.size());
-    for (size_t k = 0; k < diff.size(); k++) hv[2 * k] = (uint64_t)diff[k].first, hv[2 * k + 1] = diff[k].second;
+    // (queued once per point: the fix kernels do not queue a tile's points again)
+    const auto ref = libm_reference_keys(tr, res);
+    n_moved = 0;
+    for (size_t k = 0; k < tr.size(); k++) n_moved += ref[k].second != tr[k].key;
+    if (n_moved == 0) break;
+    std::vector<uint64_t> hv(2 * ref.size());
+    for (size_t k = 0; k < ref.size(); k++) hv[2 * k] = (uint64_t)ref[k].first, hv[2 * k + 1] = ref[k].second;
     if (int32_t e = ensure_ovr(ctx, (int64_t)hv.size())) return e;
     HIP_TRY(hipMemcpy(ctx->ovr, hv.data(), hv.size() * 8, hipMemcpyHostToDevice));
-    n_ovr = (int64_t)diff.size();
+    n_ovr = (int64_t)ref.size();
   }
   if (out_n_pairs) *out_n_pairs = (int64_t)h[0];
   if (stats) {
@@ -2220,7 +2254,7 @@ static int32_t pip_join_sync(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is,
     stats->n_pairs = (int64_t)h[0];
     stats->n_near_ties = n_ties;
     stats->n_candidates = (int64_t)h[3];
-    stats->libm_overrides = (int32_t)n_ovr;
+    stats->libm_overrides = (int32_t)n_moved;
     float ms = 0, ms2 = 0;
     hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
     if (n > 0) hipEventElapsedTime(&ms2, ctx->ev0, ctx->ev2);

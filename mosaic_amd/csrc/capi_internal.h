@@ -60,6 +60,7 @@ struct mgpu_ctx {
     mgpu::EmitArgs emit{};
     int64_t n_tiles = 0;
     int64_t n_ovr = 0;  // libm overrides the join ran with
+    int tie_host = 0;   // near-ties queued for the host (JoinArgs.tie_host)
     bool split = false;
     mgpu::SplitArgs sargs{};
     bool binned = false;

@@ -108,9 +108,9 @@ struct DenseFace {
   uint32_t base;
 };
 
-struct alignas(16) RankWord {
-  uint64_t bits;  // pixels 64 w .. 64 w + 63 that are mixed
-  uint64_t base;  // mixed pixels before pixel 64 w
+struct alignas(8) RankWord {
+  uint32_t bits;  // pixels 32 w .. 32 w + 31 that are mixed
+  uint32_t base;  // mixed pixels before pixel 32 w
 };
 
 struct ChipTableView {
@@ -176,10 +176,11 @@ struct ChipTableView {
   // are raster_sub[b * sub_n^2 + v * sub_n + u], b = the number of mixed pixels before p
   // (lonlat: u = the truncated sub_n * fractional pixel position, clamped; BNG: (metres
   // into the pixel) / raster_sub_w).  b comes from raster_rank (a bitmap of the mixed
-  // pixels with a running count per 64-pixel word: one 16-byte load per mixed point, a
-  // table 1/8 the size of the pixel classes -- it stays in L2 beside them).
+  // pixels with a running count per 32-pixel word: one 8-byte load per mixed point, a
+  // table 1/8 the size of the pixel classes -- it stays in L2 beside them -- that the
+  // streaming kernel loads together with the pixel's class).
   uint32_t raster_sub_n, raster_sub_w;
-  const RankWord* raster_rank;  // [ceil(ny * nx / 64)], or null: no second level
+  const RankWord* raster_rank;  // [ceil(ny * nx / 32)], or null: no second level
   const uint16_t* raster_sub;
   // lonlat: blocks of 2^bshift x 2^bshift pixels, raster_blk[(iy >> bshift) * bnx + (ix >>
   // bshift)] = the class all of the block's pixels share, else kPixMixed (a table small

@@ -36,6 +36,12 @@ struct JoinArgs {
   int64_t tie_cap;
   const uint64_t* ovr;
   int64_t n_ovr;
+  // tie_host = 1 (H3 with the reference's libm, first pass): a point whose FAST projection
+  // is in its tie band is queued as above with the fast path's lattice key and joined with
+  // that cell -- no tile goes to a fix kernel for it, no device route runs; the host then
+  // recomputes every queued point with the reference's libm and, only if some cell moves,
+  // reruns the join (tie_host = 0) with an override for every queued point.
+  int tie_host;
   const uint32_t* pos_of;           // binned pipeline: input position of binned slot s (else null)
   // split pipeline (launch_split): the mixed points of chunk c are the chunk's listed
   // points c * split_chunk() + mixed_idx[c * split_chunk() + m], m < chunk_mixed[c]; their

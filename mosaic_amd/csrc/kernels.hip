@@ -221,16 +221,17 @@ __device__ __forceinline__ Range grid_range(uint64_t e) {
 }
 
 // The H3 route for a point the fast projection could not decide (fix kernels only).  A
-// near-tie of the route itself is queued for the host's libm pass; a host override (the
-// reference's libm moved the cell) replaces the route's (face, ijk).  `p` = the kernel's
-// point index (the binned slot in the binned pipeline: a.pos_of maps it to the input
-// position, which keys the queue and the overrides).
+// host override (the reference's libm decided the point) replaces the route's (face,
+// ijk) without computing it; else a near-tie of the route itself is queued for the
+// host's libm pass.  `p` = the kernel's point index (the binned slot in the binned
+// pipeline: a.pos_of maps it to the input position, which keys the queue and the
+// overrides).
+__device__ __forceinline__ int64_t input_pos(const JoinArgs& a, int64_t p) {
+  return a.pos_of ? (int64_t)a.pos_of[p] : p;
+}
 __device__ __forceinline__ void route_point(const JoinArgs& a, int64_t p, double px, double py, h3::FastHex* f,
                                                       bool* tie) {
-  h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), a.res, &f->face, &f->ijk, tie);
-  if (!*tie) return;
-  const int64_t pos = a.pos_of ? (int64_t)a.pos_of[p] : p;
-  uint64_t key = h3::lattice_key(f->face, f->ijk);
+  const int64_t pos = input_pos(a, p);
   if (a.n_ovr) {
     int64_t lo = 0, hi = a.n_ovr;
     while (lo < hi) {
@@ -241,14 +242,17 @@ __device__ __forceinline__ void route_point(const JoinArgs& a, int64_t p, double
         hi = mid;
     }
     if (lo < a.n_ovr && a.ovr[2 * lo] == (uint64_t)pos) {
-      key = a.ovr[2 * lo + 1];
+      const uint64_t key = a.ovr[2 * lo + 1];
       f->face = (int)(key >> 56);
       h3::IJK c{(int)((key >> 28) & 0xFFFFFFFULL) - (1 << 27), (int)(key & 0xFFFFFFFULL) - (1 << 27), 0};
       h3::ijk_normalize(c);
       f->ijk = c;
+      *tie = true;  // (not queued again: the override table is the run's audit list)
+      return;
     }
   }
-  if (a.tie_queue) tie_record(a.tie_queue, a.tie_cap, pos, px, py, key);
+  h3::route_face_ijk(h3::to_radians(py), h3::to_radians(px), a.res, &f->face, &f->ijk, tie);
+  if (*tie && a.tie_queue) tie_record(a.tie_queue, a.tie_cap, pos, px, py, h3::lattice_key(f->face, f->ijk));
 }
 
 template <int IS, bool SLOW>
@@ -288,11 +292,16 @@ __device__ __forceinline__ Range chip_probe(const JoinArgs& a, int64_t p, double
     if (!(px >= t.bbox[0] && px <= t.bbox[2] && py >= t.bbox[1] && py <= t.bbox[3])) return Range{0, 0, 0};
     h3::FastHex f = h3::fast_hex2d(lat, lon, res, t.k_res, t.face_mask);
     if (f.tie) {
-      if (!SLOW) {
+      if (a.tie_host) {
+        // the host decides: queued with the fast cell, joined with it (a fix kernel
+        // redoing the tile for another reason finds the point queued already)
+        if (!SLOW) tie_record(a.tie_queue, a.tie_cap, input_pos(a, p), px, py, h3::lattice_key(f.face, f.ijk));
+      } else if (!SLOW) {
         *tie = true;
         return Range{0, 0, 0};
+      } else {
+        route_point(a, p, px, py, &f, tie);
       }
-      route_point(a, p, px, py, &f, tie);
     }
     if (t.probe_mode == kProbeDense) {
       const int32_t ga = f.ijk.i - f.ijk.k, gb = f.ijk.j - f.ijk.k;
@@ -312,11 +321,14 @@ __device__ __forceinline__ Range chip_probe(const JoinArgs& a, int64_t p, double
   }
   h3::FastHex f = h3::fast_hex2d(lat, lon, res, t.k_res > 0 ? t.k_res : h3::k_of_res(res), kAllFaces);
   if (f.tie) {
-    if (!SLOW) {
+    if (a.tie_host) {
+      if (!SLOW) tie_record(a.tie_queue, a.tie_cap, input_pos(a, p), px, py, h3::lattice_key(f.face, f.ijk));
+    } else if (!SLOW) {
       *tie = true;
       return Range{0, 0, 0};
+    } else {
+      route_point(a, p, px, py, &f, tie);
     }
-    route_point(a, p, px, py, &f, tie);
   }
   return probe_range(t, h3::face_ijk_to_h3_fast(f.face, f.ijk, res));
 }
@@ -915,6 +927,10 @@ struct CodeOf<MGPU_BNG> {
 // CU) copies the pixel block table (chip_table.h raster_blk) into LDS once; a point in a
 // uniform block takes its class from there, the rest load their pixel (and sub-pixel)
 // class.  Waves take chunks blockIdx.x * W + wave, then + gridDim.x * W ...
+// (Measured and rejected, r3: a software pipeline over the wave's batches -- batch g's
+// pixel and rank loads, batch g - 1's sub-pixel loads, batch g + 1's coordinates in
+// flight before any wait: 0.806 ms vs 0.765 on C2 at batch 4 (6 waves/SIMD), 0.841 at
+// batch 2; the speculative rank loads add requests and the chain is not the limit.)
 #ifndef MGPU_CFY_BLOCK
 #define MGPU_CFY_BLOCK 512
 #endif
@@ -1022,6 +1038,7 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   }
   count_wave(&a.counters[2], any_bad);
 }
+
 
 // the mixed points of one chunk per workgroup, a tile of kTile at a time
 template <int IS>

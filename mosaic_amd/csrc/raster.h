@@ -76,10 +76,10 @@ MGPU_HDI uint32_t raster_index(const ChipTableView& t, double px, double py, boo
 MGPU_HDI uint32_t raster_class(const ChipTableView& t, uint32_t ri, uint32_t sub) {
   uint32_t cl = t.raster[ri];
   if (cl == kPixMixed && t.raster_rank) {
-    const RankWord w = t.raster_rank[ri >> 6];
-    const uint64_t bit = 1ull << (ri & 63);
+    const RankWord w = t.raster_rank[ri >> 5];
+    const uint32_t bit = 1u << (ri & 31);
     if (w.bits & bit) {
-      const uint64_t b = w.base + (uint64_t)__builtin_popcountll(w.bits & (bit - 1));
+      const uint64_t b = (uint64_t)w.base + (uint64_t)__builtin_popcount(w.bits & (bit - 1));
       cl = t.raster_sub[b * t.raster_sub_n * t.raster_sub_n + sub];
     }
   }

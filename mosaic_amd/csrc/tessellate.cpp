@@ -32,9 +32,12 @@
 // walk follows the true edges (straight in lon/lat, curved in a face's gnomonic
 // plane).  Cell geometry is H3's own h3ToGeoBoundary (h3_boundary.h), with the
 // distortion vertices of Class III cells that cross an icosahedron edge.
-// Limitations (MGPU_E_UNSUPPORTED): a cell crossing the antimeridian or containing a
-// pole (the reference's makeSafeGeometry / makePoleGeometry), a polygon more than
-// ~84 degrees from a face it touches.
+// Cells as the reference shapes them (H3IndexSystem.indexToGeometry): the cell holding
+// a pole is the cap from its boundary to the pole, a cell across the antimeridian its
+// western and eastern parts (a MULTIPOLYGON; a chip clipped from it likewise).
+// Limitations (MGPU_E_UNSUPPORTED): a polygon more than ~84 degrees from a face it
+// touches; coordinates outside [-180, 180] x [-90, 90] (the reference's alignToGrid
+// re-wraps such geometries first).
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -201,6 +204,32 @@ std::vector<std::vector<Pt>> convex_pieces(const std::vector<Pt>& cell) {
 
 // ---------------------------------------------------------------- grids
 
+// the cell holding the north / south pole at `res` (H3IndexSystem.scala:240-246:
+// geoToH3(+-90, 0, res))
+uint64_t pole_cell(bool north, int res) {
+  static uint64_t cache[2][16] = {};
+  uint64_t& c = cache[north ? 1 : 0][res & 15];
+  if (!c) {
+    bool tie = false;
+    c = mgpu::h3::point_to_cell(0.0, north ? 90.0 : -90.0, res, &tie);
+  }
+  return c;
+}
+
+// a cell's rings (Grid::boundary) as chip WKB: a Polygon, or a MultiPolygon of its parts
+void write_cell_wkb(const std::vector<std::vector<Pt>>& rings, std::vector<uint8_t>& out) {
+  std::vector<mgpu::wkb::Polygon> parts(rings.size());
+  for (size_t k = 0; k < rings.size(); k++) {
+    std::vector<double> flat;
+    for (auto& p : rings[k]) {
+      flat.push_back(p.x);
+      flat.push_back(p.y);
+    }
+    parts[k].push_back(std::move(flat));
+  }
+  mgpu::wkb::write_polygons(out, parts);
+}
+
 struct Grid {
   virtual ~Grid() {}
   // a cell whose centre is farther than this (lattice units) from every walked boundary
@@ -209,17 +238,16 @@ struct Grid {
   // whether this pass owns lattice cell (i, j) with id `id` (H3: the cell's centre lies on
   // this pass's face, and the id is the cell at that lattice position)
   virtual bool keep(int64_t, long, long) const { return true; }
-  // set when a candidate cell's geometry is outside what the builder supports
-  mutable bool unsupported = false;
   // lattice-space coordinate of an input point
   virtual Pt to_lattice(Pt p) const = 0;
   // lattice cell containing a lattice-space point
   virtual std::pair<long, long> cell_at(Pt q) const = 0;
   virtual Pt center(long i, long j) const = 0;  // lattice space
   virtual void neighbors(long i, long j, std::vector<std::pair<long, long>>& out) const = 0;
-  // cell id (0 = not representable) and its boundary in input coords (closed, ccw)
+  // cell id (0 = not representable) and its geometry in input coords: one closed ccw
+  // ring, or several (H3: a cell cut at the antimeridian); empty = no geometry
   virtual int64_t cell_id(long i, long j) const = 0;
-  virtual std::vector<Pt> boundary(long i, long j) const = 0;
+  virtual std::vector<std::vector<Pt>> boundary(long i, long j) const = 0;
   // lattice row/column iteration for the scanline: row index of a lattice y,
   // y of a row, and the column index of the cell centred at lattice x in a row
   virtual double row_y(long j) const = 0;
@@ -310,27 +338,66 @@ struct H3Grid : Grid {
     }
     return {lon * 180.0 / M_PI, lat * 180.0 / M_PI};
   }
-  // H3IndexSystem.indexToGeometry: h3ToGeoBoundary in degrees, closed (ccw)
-  std::vector<Pt> boundary(long i, long j) const override {
+  // H3IndexSystem.indexToGeometry (H3IndexSystem.scala:103-121): h3ToGeoBoundary in
+  // degrees, closed, ccw; the cell holding a pole as the cap between its boundary and
+  // the pole (makePoleGeometry, :361-384); a cell across the antimeridian cut into its
+  // western and eastern parts (makeSafeGeometry / crossesAntiMeridian, :386-410, :258-262)
+  std::vector<std::vector<Pt>> boundary(long i, long j) const override {
     const int64_t id = cell_id(i, j);
+    if (!id) return {};
     std::vector<Pt> b;
-    if (!id) return b;
     for (auto& v : mgpu::h3b::cell_boundary((uint64_t)id))
       b.push_back({mgpu::h3b::to_degrees(v.lon), mgpu::h3b::to_degrees(v.lat)});
+    const int pole = (uint64_t)id == pole_cell(true, res) ? 1 : ((uint64_t)id == pole_cell(false, res) ? -1 : 0);
+    if (pole) return {pole_cap(b, pole > 0)};
     double lo = INFINITY, hi = -INFINITY;
-    for (auto& p : b) {
-      lo = std::min(lo, p.x);
-      hi = std::max(hi, p.x);
-    }
-    if (hi - lo > 180.0 || std::fabs(mgpu::h3b::cell_center((uint64_t)id).lat) > 1.5) {
-      // antimeridian or pole cell: the reference re-shapes it (makeSafeGeometry /
-      // makePoleGeometry); not built here
-      unsupported = true;
-      return {};
+    for (auto& q : b) {
+      lo = std::min(lo, q.x);
+      hi = std::max(hi, q.x);
     }
     b.push_back(b[0]);
     if (ring_area(b) < 0) std::reverse(b.begin(), b.end());
-    return b;
+    if (!(lo < 0 && hi >= 0 && hi - lo > 180.0)) return {b};
+    // across the antimeridian: shift the western longitudes east, cut at 180
+    for (auto& q : b)
+      if (q.x < 0) q.x += 360.0;
+    if (ring_area(b) < 0) std::reverse(b.begin(), b.end());
+    static const std::vector<Pt> west{{0, -90}, {180, -90}, {180, 90}, {0, 90}, {0, -90}};
+    static const std::vector<Pt> east{{180, -90}, {360, -90}, {360, 90}, {180, 90}, {180, -90}};
+    std::vector<std::vector<Pt>> out;
+    auto w = clip_ring(b, west);
+    if (!w.empty() && std::fabs(ring_area(w)) > 0) out.push_back(std::move(w));
+    auto e = clip_ring(b, east);
+    if (!e.empty() && std::fabs(ring_area(e)) > 0) {
+      for (auto& q : e) q.x -= 360.0;
+      out.push_back(std::move(e));
+    }
+    return out;
+  }
+  // the polar cap: the boundary's vertices by longitude, the edge that crosses the
+  // antimeridian cut there, closed along the pole (ccw)
+  static std::vector<Pt> pole_cap(std::vector<Pt> v, bool north) {
+    std::sort(v.begin(), v.end(), [](const Pt& a, const Pt& b) { return a.x < b.x; });
+    const Pt a = v.back(), b{v.front().x + 360.0, v.front().y};
+    const double t = b.x > a.x ? (180.0 - a.x) / (b.x - a.x) : 0.5;
+    const double lat_x = a.y + t * (b.y - a.y);
+    std::vector<Pt> r;
+    const double pl = north ? 90.0 : -90.0;
+    if (north) {
+      r.push_back({-180.0, lat_x});
+      for (auto& q : v) r.push_back(q);
+      r.push_back({180.0, lat_x});
+      r.push_back({180.0, pl});
+      r.push_back({-180.0, pl});
+    } else {
+      r.push_back({-180.0, pl});
+      r.push_back({180.0, pl});
+      r.push_back({180.0, lat_x});
+      for (auto it = v.rbegin(); it != v.rend(); ++it) r.push_back(*it);
+      r.push_back({-180.0, lat_x});
+    }
+    r.push_back(r[0]);
+    return r;
   }
   double row_y(long j) const override { return j * mgpu::h3::kSin60; }
   long row_of(double y, bool up) const override {
@@ -368,9 +435,9 @@ struct BngGrid : Grid {
     mgpu::bng::point_to_cell((i + 0.5) * edge, (j + 0.5) * edge, res, &id);
     return id;
   }
-  std::vector<Pt> boundary(long i, long j) const override {
+  std::vector<std::vector<Pt>> boundary(long i, long j) const override {
     double x = i * edge, y = j * edge;
-    return {{x, y}, {x + edge, y}, {x + edge, y + edge}, {x, y + edge}, {x, y}};
+    return {{{x, y}, {x + edge, y}, {x + edge, y + edge}, {x, y + edge}, {x, y}}};
   }
   double row_y(long j) const override { return j + 0.5; }
   long row_of(double y, bool up) const override { return up ? (long)std::ceil(y - 0.5) : (long)std::floor(y - 0.5); }
@@ -482,17 +549,7 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
     int64_t id = g.cell_id(c.first, c.second);
     if (!id || !g.keep(id, c.first, c.second)) continue;
     Chip ch{id, pid, 1, {}};
-    if (keep_core) {
-      auto b = g.boundary(c.first, c.second);
-      std::vector<mgpu::wkb::Polygon> parts(1);
-      std::vector<double> flat;
-      for (auto& p : b) {
-        flat.push_back(p.x);
-        flat.push_back(p.y);
-      }
-      parts[0].push_back(flat);
-      mgpu::wkb::write_polygons(ch.wkb, parts);
-    }
+    if (keep_core) write_cell_wkb(g.boundary(c.first, c.second), ch.wkb);
     out.push_back(std::move(ch));
   }
   // 4. border cells: clip -- unless the boundary never came near the cell (a ring
@@ -512,52 +569,41 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
         if (point_in_ring(r, cc)) in = !in;
       if (!in) continue;
       Chip ch{cid, pid, 1, {}};
-      if (keep_core) {
-        auto b = g.boundary(c.first, c.second);
-        std::vector<mgpu::wkb::Polygon> parts(1);
-        std::vector<double> flat;
-        for (auto& p : b) {
-          flat.push_back(p.x);
-          flat.push_back(p.y);
-        }
-        parts[0].push_back(flat);
-        mgpu::wkb::write_polygons(ch.wkb, parts);
-      }
+      if (keep_core) write_cell_wkb(g.boundary(c.first, c.second), ch.wkb);
       out.push_back(std::move(ch));
       continue;
     }
-    auto cellb = g.boundary(c.first, c.second);
-    if (cellb.size() < 4) continue;
+    const auto rings = g.boundary(c.first, c.second);
+    if (rings.empty()) continue;
     double cminx = INFINITY, cminy = INFINITY, cmaxx = -INFINITY, cmaxy = -INFINITY;
-    for (auto& p : cellb) {
-      cminx = std::min(cminx, p.x);
-      cmaxx = std::max(cmaxx, p.x);
-      cminy = std::min(cminy, p.y);
-      cmaxy = std::max(cmaxy, p.y);
+    for (auto& r : rings)
+      for (auto& p : r) {
+        cminx = std::min(cminx, p.x);
+        cmaxx = std::max(cmaxx, p.x);
+        cminy = std::min(cminy, p.y);
+        cmaxy = std::max(cmaxy, p.y);
+      }
+    // every ring of the cell in convex pieces; the cell is core when each ring lies in
+    // the polygon's interior (tested from a point inside the ring's first piece)
+    std::vector<std::vector<Pt>> pieces;
+    bool inside = true;
+    for (auto& r : rings) {
+      const auto pc = convex_pieces(r);
+      Pt cc = {0, 0};
+      for (size_t k = 0; k + 1 < pc[0].size(); k++) {
+        cc.x += pc[0][k].x;
+        cc.y += pc[0][k].y;
+      }
+      cc.x /= (pc[0].size() - 1);
+      cc.y /= (pc[0].size() - 1);
+      inside = inside && cell_in_polygon(r, pc, cc, poly);
+      pieces.insert(pieces.end(), pc.begin(), pc.end());
     }
-    double cell_area = std::fabs(ring_area(cellb));
-    Pt cc = {0, 0};
-    for (size_t k = 0; k + 1 < cellb.size(); k++) {
-      cc.x += cellb[k].x;
-      cc.y += cellb[k].y;
-    }
-    cc.x /= (cellb.size() - 1);
-    cc.y /= (cellb.size() - 1);
-    const auto pieces = convex_pieces(cellb);
-    if (cell_in_polygon(cellb, pieces, cc, poly)) {
+    if (inside) {
       int64_t id = g.cell_id(c.first, c.second);
       if (!id) continue;
       Chip ch{id, pid, 1, {}};
-      if (keep_core) {
-        std::vector<mgpu::wkb::Polygon> cp(1);
-        std::vector<double> flat;
-        for (auto& p : cellb) {
-          flat.push_back(p.x);
-          flat.push_back(p.y);
-        }
-        cp[0].push_back(flat);
-        mgpu::wkb::write_polygons(ch.wkb, cp);
-      }
+      if (keep_core) write_cell_wkb(rings, ch.wkb);
       out.push_back(std::move(ch));
       continue;
     }
@@ -602,7 +648,6 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
     if (parts.empty() || area <= 0) continue;  // empty chip: dropped
     int64_t id = g.cell_id(c.first, c.second);
     if (!id) continue;
-    (void)cell_area;
     Chip ch{id, pid, 0, {}};
     mgpu::wkb::write_polygons(ch.wkb, parts);
     out.push_back(std::move(ch));
@@ -711,6 +756,14 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
       }
       if (poly.parts.empty()) continue;
       if (index_system == MGPU_H3) {
+        bool in_range = true;
+        for (auto& part : poly.parts)
+          for (auto& ring : part)
+            for (auto& q : ring) in_range = in_range && std::fabs(q.x) <= 180.0 && std::fabs(q.y) <= 90.0;
+        if (!in_range) {
+          bad_poly[p] = 2;
+          continue;
+        }
         std::vector<std::vector<Pt>> dense;
         std::vector<int> faces;
         if (!h3_faces(poly, res, dense, faces)) {
@@ -727,7 +780,6 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
             lat_rings.push_back(std::move(lr));
           }
           tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, per[p]);
-          if (g.unsupported) bad_poly[p] = 2;
         }
         // a cell reached twice (two lattice positions around a pentagon map to one id):
         // its chip is computed from the id, so the copies are equal -- keep the first
@@ -757,8 +809,8 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
                              "icosahedron face it touches); split it first", polygon_id[p]);
     if (bad_poly[p] == 2)
       return mgpu::set_error(MGPU_E_UNSUPPORTED,
-                             "tessellate: polygon %d meets an H3 cell that crosses the antimeridian or contains a "
-                             "pole (not built here)", polygon_id[p]);
+                             "tessellate: polygon %d has coordinates outside [-180, 180] x [-90, 90] (wrap them "
+                             "first, as the reference's alignToGrid does)", polygon_id[p]);
   }
   mgpu_tess* t = new mgpu_tess();
   size_t total = 0;

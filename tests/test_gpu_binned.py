@@ -86,24 +86,26 @@ def test_binned_overlapping_polygons(gpu):
 
 
 def test_binned_adversarial_points_and_near_tie_positions(gpu, nyc_chips_r9):
-    """Points on H3 cell corners (the near-tie route runs in pip_mixed_fix_kernel over the
-    binned tiles): pairs equal the reference's (the oracle with glibc's libm), nothing
-    excluded; mgpu_last_near_ties reports INPUT positions -- the same list the fused
-    pipeline reports -- and both pipelines apply the same libm overrides."""
+    """Points on H3 cell corners: pairs equal the reference's (the oracle with glibc's
+    libm), nothing excluded, in the binned and the fused pipeline.  Every point whose fast
+    projection falls in its tie band is decided by the host with the reference's libm;
+    mgpu_last_near_ties reports those INPUT positions.  The binned pipeline projects every
+    point; the fused one answers points of certified (pure) pixels without projecting
+    them -- so its list is a subset of the binned one's."""
     d = nyc_chips_r9.upload()
     x, y = adversarial_points(nyc_chips_r9)
     r = binned_join(x, y, d, 9, gpu)
-    ties_b = np.sort(d.ctx.last_near_ties())
+    ties_b = d.ctx.last_near_ties()
     gp, gq = r.numpy()
     op, oq = oracle_join(nyc_chips_r9, x, y)
     assert np.array_equal(gp, op) and np.array_equal(gq, oq)
     with opts(gpu, pipeline=0):
         rf = M.pip_join(T(x, gpu), T(y, gpu), d, 9)
-    ties_f = np.sort(d.ctx.last_near_ties())
+    ties_f = d.ctx.last_near_ties()
     assert rf.stats["pipeline"] == 0
-    assert len(ties_b) > 0 and np.array_equal(ties_b, ties_f)
-    assert r.stats["n_near_ties"] == rf.stats["n_near_ties"]
-    assert r.stats["libm_overrides"] == rf.stats["libm_overrides"]
+    assert len(ties_b) == r.stats["n_near_ties"] > 0 and len(ties_f) == rf.stats["n_near_ties"] > 0
+    assert np.array_equal(ties_b, np.unique(ties_b)) and np.array_equal(ties_f, np.unique(ties_f))
+    assert set(ties_f.tolist()) <= set(ties_b.tolist())
     assert np.array_equal(rf.numpy()[0], op) and np.array_equal(rf.numpy()[1], oq)
 
 

@@ -86,6 +86,11 @@ def test_doc_multipolygon_finer(res):
 
 
 def test_kepler_zone1_core_chips(nyc_zones):
+    """The notebook shows the first 20 rows of zone 1's chips ("only showing top 20
+    rows"), all `is_core = true` -- mosaicFill emits core chips first -- so the listing
+    has no border rows to compare; the core rows are core here too.  (The full core /
+    border split is compared with mosaicFill's construction in
+    test_mosaicfill_selection_equals_clip_*.)"""
     k = int(np.nonzero(nyc_zones.poly_id == 1)[0][0])
     c = M.tessellate(nyc_zones.select([k]), M.H3IndexSystem(), 9)
     core = set(c.cell[c.is_core.astype(bool)].tolist())
@@ -168,3 +173,196 @@ def test_cell_geometry_consistent_with_geo_to_h3(res):
 def _sphere_grid():
     lon, lat = np.meshgrid(np.linspace(-179.5, 179.5, 360), np.linspace(-89.5, 89.5, 180))
     return lon.ravel(), lat.ravel()
+
+
+
+# ---------------------------------------------------------------- mosaicFill's cell selection
+# The reference picks cells by Mosaic.mosaicFill (core/Mosaic.scala:61-99): radius r =
+# H3IndexSystem.getBufferRadius (:79-90, the largest distance from the polygon's centroid
+# to a vertex of the centroid's cell, planar degrees); core = polyfill(buffer(-r)) (cells
+# whose centre lies in the carved polygon); border = polyfill(boundary.buffer(1.01 r)
+# .simplify(0.01 r)) minus core, each clipped (getBorderChips, IndexSystem.scala:178-195:
+# is_core when the clip equals the cell, dropped when empty).  The builder here clips
+# every cell that meets the polygon instead.  Both give the same chip rows exactly when
+# (i) no chip cell lies outside core-set and band (a blind spot) and (ii) every core-set
+# cell lies wholly inside the polygon (else the reference marks a cell core that is not).
+
+def _parts(P, k):
+    for q in range(P.poly_part_off[k], P.poly_part_off[k + 1]):
+        yield [P.xy[P.ring_off[r]:P.ring_off[r + 1]] for r in range(P.part_ring_off[q], P.part_ring_off[q + 1])]
+
+
+def _area_centroid(P, k):
+    """JTS Centroid of a (multi)polygon: area-weighted ring centroids, holes subtracted."""
+    sx = sy = sa = 0.0
+    for rings in _parts(P, k):
+        for j, r in enumerate(rings):
+            x, y = r[:, 0], r[:, 1]
+            cr = x[:-1] * y[1:] - x[1:] * y[:-1]
+            a = cr.sum() / 2
+            cx, cy = ((x[:-1] + x[1:]) * cr).sum() / (6 * a), ((y[:-1] + y[1:]) * cr).sum() / (6 * a)
+            w = abs(a) * (1.0 if j == 0 else -1.0)
+            sx, sy, sa = sx + w * cx, sy + w * cy, sa + w
+    return sx / sa, sy / sa
+
+
+def _signed_distance(P, k, px, py):
+    """Distance from each point to the polygon's boundary, positive inside (even-odd)."""
+    segs = np.concatenate([np.concatenate([r[:-1], r[1:]], 1) for rings in _parts(P, k) for r in rings])
+    ax, ay, bx, by = (segs[:, i][None, :] for i in range(4))
+    X, Y = px[:, None], py[:, None]
+    dx, dy = bx - ax, by - ay
+    t = np.clip(((X - ax) * dx + (Y - ay) * dy) / np.maximum(dx * dx + dy * dy, 1e-300), 0, 1)
+    d = np.hypot(ax + t * dx - X, ay + t * dy - Y).min(1)
+    cross = ((ay > Y) != (by > Y)) & (X < (bx - ax) * (Y - ay) / np.where(by != ay, by - ay, 1) + ax)
+    inside = (cross.sum(1) % 2) == 1
+    return np.where(inside, d, -d)
+
+
+def _mosaicfill_selection(P, c, res):
+    """Per chip row: (d = signed centre distance, r, R = the cell's circumradius), and
+    the counts of rows where the two constructions could part."""
+    xy, nv, ctr = cell_geometry(c.cell)
+    R = np.array([np.hypot(*(xy[i, :nv[i]] - ctr[i]).T).max() for i in range(len(c))])
+    d = np.zeros(len(c))
+    r = np.zeros(len(c))
+    for k, pid in enumerate(P.poly_id):
+        rows = np.nonzero(c.polygon_id == pid)[0]
+        if not len(rows):
+            continue
+        gx, gy = _area_centroid(P, k)
+        cell0 = O.h3_points_to_cells(np.array([gx]), np.array([gy]), res)
+        vxy, vn, _ = cell_geometry(cell0)
+        r[rows] = np.hypot(vxy[0, :vn[0], 0] - gx, vxy[0, :vn[0], 1] - gy).max()
+        d[rows] = _signed_distance(P, k, ctr[rows, 0], ctr[rows, 1])
+    core = c.is_core.astype(bool)
+    core_set = d >= r  # polyfill(buffer(-r)): centre in the carved polygon
+    # polyfill(boundary.buffer(1.01 r).simplify(0.01 r)): the simplification moves the
+    # band's edge by at most 0.01 r, so |d| <= r is inside it for certain
+    band = np.abs(d) <= r
+    return {
+        "rows": len(c), "core": int(core.sum()),
+        "core_set": int(core_set.sum()), "band": int((band & ~core_set).sum()),
+        # (i) a chip the reference never visits
+        "blind": int((~core_set & ~band).sum()),
+        # (ii) the reference marks the cell core, the clip does not
+        "core_mismatch": int((core_set & ~core).sum()),
+        # JTS approximates buffer(-r)'s arcs by chords (8 per quadrant: <= 1.93% of r):
+        # rows within that of the carved edge whose flag the approximation could flip
+        "buffer_sensitive": int(((d >= 0.98 * r) & (d < r) & ~core).sum()),
+        "min_r_minus_R": float((r - R).min()), "max_R_over_r": float((R / r).max()),
+    }
+
+
+@pytest.mark.parametrize("res", [8, 9, 10])
+def test_mosaicfill_selection_equals_clip_nyc(nyc_zones, res):
+    """NYC taxi zones: the reference's core / border selection gives exactly this
+    builder's rows and flags -- no blind spot, no core-set cell the clip calls border,
+    none near the buffer's chord approximation -- because every chip cell's circumradius
+    stays below the polygon's r (r is at least the centroid cell's nearest-vertex
+    distance; cell size varies by < 1% across a zone)."""
+    c = M.tessellate(nyc_zones, M.H3IndexSystem(), res)
+    s = _mosaicfill_selection(nyc_zones, c, res)
+    print("NYC res %d:" % res, s)
+    assert s["blind"] == 0 and s["core_mismatch"] == 0 and s["buffer_sensitive"] == 0, s
+    assert s["core_set"] <= s["core"] and s["core_set"] + s["band"] >= s["rows"]
+
+
+def test_mosaicfill_selection_equals_clip_tracts():
+    """The C3 tract-like polygons at res 10 (a 400-tract sample): the same equivalence."""
+    import bench_workloads as W
+    T = W.tract_polygons(n_cells=2000, extent=(-74.5, 40.5, -74.0, 41.0), seed=3)
+    P = T.select(range(0, len(T), 5))
+    c = M.tessellate(P, M.H3IndexSystem(), 10)
+    s = _mosaicfill_selection(P, c, 10)
+    print("tracts res 10:", s)
+    assert s["blind"] == 0 and s["core_mismatch"] == 0 and s["buffer_sensitive"] == 0, s
+
+
+# ---------------------------------------------------------------- antimeridian and poles
+def _wkb_parts_x(w):
+    """The x ranges of the parts of a Polygon / MultiPolygon WKB (little or big endian)."""
+    import struct
+    bo = "<" if w[0] == 1 else ">"
+    typ = struct.unpack(bo + "I", w[1:5])[0]
+    def poly(pos):
+        nr = struct.unpack(bo + "I", w[pos:pos + 4])[0]
+        pos += 4
+        xs = []
+        for _ in range(nr):
+            npt = struct.unpack(bo + "I", w[pos:pos + 4])[0]
+            pos += 4
+            pts = np.frombuffer(w[pos:pos + 16 * npt], dtype=bo + "f8").reshape(-1, 2)
+            xs.append(pts[:, 0])
+            pos += 16 * npt
+        allx = np.concatenate(xs)
+        return (allx.min(), allx.max()), pos
+    if typ == 3:
+        return [poly(5)[0]]
+    n = struct.unpack(bo + "I", w[5:9])[0]
+    pos, out = 9, []
+    for _ in range(n):
+        r, pos = poly(pos + 5)
+        out.append(r)
+    return out
+
+
+@pytest.mark.parametrize("res", [2, 3, 4])
+def test_antimeridian_cells(res):
+    """A Fiji-like MULTIPOLYGON on both sides of the antimeridian: cells across it are
+    cut into western and eastern parts (makeSafeGeometry, H3IndexSystem.scala:386-410),
+    so a chip there is a MULTIPOLYGON with one part each side; chips of a cell never
+    repeat, chip areas add up to the polygon's, and the join over the chips finds only
+    true containments (the rest: chips' straight lon/lat edges against the true cells)."""
+    P = M.Polygons.from_lists([(7, [
+        [[(177.5, -18.5), (180.0, -18.5), (180.0, -15.5), (177.5, -15.5), (177.5, -18.5)]],
+        [[(-180.0, -18.5), (-178.0, -18.5), (-178.0, -15.5), (-180.0, -15.5), (-180.0, -18.5)]]])])
+    c = M.tessellate(P, M.H3IndexSystem(), res)
+    _check_invariants(P, c)
+    split = 0
+    for i in range(len(c)):
+        w = _wkb(c, i)
+        if not w:
+            continue
+        parts = _wkb_parts_x(w)
+        assert all(lo >= -180.0 and hi <= 180.0 for lo, hi in parts)
+        if len(parts) == 2 and min(p[0] for p in parts) < 0 < max(p[1] for p in parts):
+            split += 1
+    assert split >= 1  # cells straddle the antimeridian at these resolutions
+    rng = np.random.default_rng(60 + res)
+    x = np.concatenate([rng.uniform(177.0, 180.0, 3000), rng.uniform(-180.0, -177.5, 3000)])
+    y = rng.uniform(-19.0, -15.0, 6000)
+    pts, polys = O.pip_join(0, res, x, y, c.cell, c.polygon_id, c.is_core, c.wkb_offsets, c.wkb)
+    got = set(zip(pts.tolist(), polys.tolist()))
+    want = brute_force_pairs(P, x, y, O)
+    assert got <= want and len(got) > 0.97 * len(want)
+
+
+@pytest.mark.parametrize("res", [1, 2, 3])
+def test_polar_cap_cells(res):
+    """A polar cap (lat >= 84, every longitude): the cell holding the pole is the cap
+    between its boundary and the pole (makePoleGeometry, H3IndexSystem.scala:361-384), the
+    cells across the antimeridian are cut; chip areas add up to the cap's area in lon/lat,
+    the pole's cell is a chip, and the join over the chips finds only true containments.
+    Near a pole a cell's straight lon/lat edges stray far from its true (geodesic)
+    border, so geoToH3 sends some points to a cell whose chip does not hold them -- as in
+    the reference, whose chips are the same lon/lat polygons; the share shrinks with the
+    cell size (measured: 86% of the cap's points matched at res 1, 98% at 2, 99% at 3)."""
+    for north in (True, False):
+        s = 1 if north else -1
+        lat0 = 84.0 * s
+        ring = [(-180.0, lat0), (180.0, lat0), (180.0, 90.0 * s), (-180.0, 90.0 * s), (-180.0, lat0)]
+        if not north:
+            ring = ring[::-1]
+        P = M.Polygons.from_lists([(3, [[ring]])])
+        c = M.tessellate(P, M.H3IndexSystem(), res)
+        _check_invariants(P, c)
+        pole = int(O.h3_points_to_cells(np.array([0.0]), np.array([90.0 * s]), res)[0])
+        assert pole in set(c.cell.tolist())
+        rng = np.random.default_rng(70 + res)
+        x = rng.uniform(-180, 180, 5000)
+        y = s * rng.uniform(84.0, 90.0, 5000)
+        pts, polys = O.pip_join(0, res, x, y, c.cell, c.polygon_id, c.is_core, c.wkb_offsets, c.wkb)
+        got = set(zip(pts.tolist(), polys.tolist()))
+        want = brute_force_pairs(P, x, y, O)
+        assert got <= want and len(got) > {1: 0.8, 2: 0.95, 3: 0.98}[res] * len(want), (north, len(got), len(want))

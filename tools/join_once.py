@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--pipeline", type=int, default=-1)
     ap.add_argument("--cells", action="store_true")
+    ap.add_argument("--cache", default=None, help="npz of the tessellated chip table (written when absent): "
+                    "PMC passes of a large config tessellate once")
     ap.add_argument("--bng", action="store_true", help="with --cells: BNG res 4 on eastings/northings "
                     "(a pure 16 B read + 8 B write stream, used to calibrate FETCH_SIZE / WRITE_SIZE)")
     a = ap.parse_args()
@@ -32,7 +34,16 @@ def main():
     import bench_workloads as W
     wl = B.workload(a, W, M)
     isys = wl["isys"]
-    chips = M.tessellate(wl["polygons"], isys, a.res, keep_core_geometries=wl.get("keep_core", True)).upload(ctx)
+    import numpy as np
+    if a.cache and os.path.exists(a.cache):
+        z = np.load(a.cache)
+        table = M.ChipTable(z["cell"], z["polygon_id"], z["is_core"], z["wkb_offsets"], z["wkb"], isys.code)
+    else:
+        table = M.tessellate(wl["polygons"], isys, a.res, keep_core_geometries=wl.get("keep_core", True))
+        if a.cache:
+            np.savez(a.cache, cell=table.cell, polygon_id=table.polygon_id, is_core=table.is_core,
+                     wkb_offsets=table.wkb_offsets, wkb=table.wkb)
+    chips = table.upload(ctx)
     x, y = wl["points"](a.points, 0, dev)
     cap = int(a.points * wl["pairs_per_point"]) + 1024
     op = torch.empty(cap, dtype=torch.int64, device=dev)
