@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive measurement")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
+                    help="context option (mgpu_ctx_set_option, include/mosaic_gpu.h) set before the chip table "
+                         "is uploaded, e.g. raster_bng=1 or pipeline=0; repeatable")
     return ap.parse_args()
 
 
@@ -256,6 +259,9 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo")  # control plane only
     ctx = M.default_context(dev)
+    for kv in a.option:
+        k, v = kv.split("=", 1)
+        ctx.set_option(k, int(v))
     if world > 1 and not rehearsal:
         D.init_comm(ctx)
     import bench_workloads as W
@@ -364,6 +370,7 @@ def main():
         "config": {"workload": wl["workload"] % (n, a.res),
                    "points_per_gpu": n, "polygons": len(zones.poly_part_off) - 1, "chips": info["chips"],
                    "chip_cells": info["cells"], "index_system": isys.name, "resolution": a.res,
+                   **({"options": dict(kv.split("=", 1) for kv in a.option)} if a.option else {}),
                    "parallelism": ("points sharded x%d, chip table replicated (%s)"
                                    % (world, "gloo host blob: a protocol rehearsal, not a measurement" if rehearsal
                                       else "RCCL broadcast") if world > 1 else "one GPU")},

@@ -40,7 +40,7 @@ extern "C" {
 #define MGPU_E_CAPACITY -5          /* output arrays too small; the required count is returned */
 #define MGPU_E_DEVICE -6            /* HIP runtime error */
 #define MGPU_E_INTERNAL -7          /* kernel protocol failure (look-back timeout) */
-#define MGPU_E_UNSUPPORTED -8       /* input outside what the device path builds (H3 kRing near pentagons) */
+#define MGPU_E_UNSUPPORTED -8       /* input outside what the device path builds (geometry types, huge polygons) */
 #define MGPU_E_EMPTY -9             /* IllegalStateException (JTS: getX / getY of an empty Point) */
 
 #define MGPU_H3 0
@@ -185,7 +185,7 @@ int32_t mgpu_bng_format_device(mgpu_ctx* ctx, const int64_t* cells, int64_t n, c
  * in the reference's order.  H3: H3IndexSystem.kRing / kLoop, H3IndexSystem.scala:
  * 182-205 (H3 v3.7 kRing spiral / hexRing order; a walk that meets a pentagon takes H3's
  * _kRingInternal hash-set order, and kLoop Mosaic's kRing(k) diff kRing(k - 1) in Scala
- * HashSet order -- built for k <= 64, MGPU_E_UNSUPPORTED beyond).  Cell i's list
+ * HashSet order, any k).  Cell i's list
  * is out_cells[out_offsets[i] .. out_offsets[i + 1]); device pointers; *out_total =
  * entries needed (MGPU_E_CAPACITY when above `capacity`).  0 <= k <= 1024. */
 int32_t mgpu_grid_kring(mgpu_ctx* ctx, int32_t index_system, const int64_t* cells, int64_t n, int32_t k,

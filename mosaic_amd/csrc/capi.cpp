@@ -1380,9 +1380,6 @@ int32_t mgpu_grid_kring(mgpu_ctx* ctx, int32_t index_system, const int64_t* cell
   } free_scratch{scratch};
   int64_t batch = 0;
   if (n_fb) {
-    if (k > mgpu::kring_fallback_max_k())
-      return fail(MGPU_E_UNSUPPORTED, "grid_kring: %lld H3 cells reach a pentagon within k = %d; pentagon "
-                  "neighbourhoods are built for k <= %d", (long long)n_fb, k, mgpu::kring_fallback_max_k());
     const int64_t words = mgpu::kring_fallback_words(k);
     batch = std::max<int64_t>(1, std::min<int64_t>(n_fb, ((int64_t)256 << 20) / 8 / words));
     HIP_TRY(hipMalloc(&scratch, (size_t)batch * words * 8));
@@ -2018,6 +2015,8 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   a.mixed_idx = nullptr;
   a.mixed_res = nullptr;
   a.chunk_mixed = nullptr;
+  a.extra = nullptr;
+  a.n_extra = nullptr;
   a.poly_answers = 0;
   HIP_TRY(hipMemsetAsync(base, 0, kWsCounters, s));
   HIP_TRY(hipMemsetAsync(ctx->tq, 0, 16, s));
@@ -2037,6 +2036,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     };
     const size_t o_codes = carve((size_t)nc * C * 4), o_idx = carve((size_t)nc * C * 2), o_res = carve((size_t)nc * C * 8);
     const size_t o_pairs = carve(nc * 4), o_mixed = carve(nc * 4), o_cand = carve(nc * 4), o_off = carve(nc * 8);
+    const size_t o_extra = carve((size_t)nc * (C / mgpu::join_tile_points()) * 4);
     if (off > ctx->split_bytes) {
       if (ctx->split_ws) HIP_TRY(hipFree(ctx->split_ws));
       ctx->split_ws = nullptr;
@@ -2050,6 +2050,8 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     sa.chunk_pairs = (uint32_t*)(sb + o_pairs);
     sa.chunk_mixed = (uint32_t*)(sb + o_mixed);
     sa.chunk_off = (uint64_t*)(sb + o_off);
+    a.extra = sa.extra = (uint32_t*)(sb + o_extra);
+    a.n_extra = (uint32_t*)(a.counters + 7);  // (zeroed with the counters)
     a.group_sum = sa.chunk_pairs;
     a.group_cand = (uint32_t*)(sb + o_cand);
     a.mixed_idx = sa.mixed_idx;

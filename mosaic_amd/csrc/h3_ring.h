@@ -209,15 +209,13 @@ MGPU_HD int64_t hex_ring(uint64_t h, int k, int64_t* out) {
 }
 
 // H3 C _kRingInternal from h with k rings into the hash set tab[max_kring(k)] (zeroed
-// here) with dist[] -- the same depth-first order as the recursion (an explicit stack of
-// depth k + 1: stk[], nxt[] of kMaxFallbackK + 2 entries).  Returns false if the set
-// overflowed (only possible with inconsistent tables; H3 would not terminate).
-constexpr int kMaxFallbackK = 64;
-MGPU_HD bool kring_hash(uint64_t h, int k, uint64_t* tab, int32_t* dist) {
+// here) with dist[] -- the same depth-first order as the recursion, on an explicit stack
+// of depth k + 1 held in the caller's scratch (stk[k + 2], nxt[k + 2]: any k).  Returns
+// false if the set overflowed (only possible with inconsistent tables; H3 would not
+// terminate).
+MGPU_HD bool kring_hash(uint64_t h, int k, uint64_t* tab, int32_t* dist, uint64_t* stk, int8_t* nxt) {
   const int64_t m = max_kring(k);
   for (int64_t i = 0; i < m; i++) tab[i] = 0, dist[i] = 0;
-  uint64_t stk[kMaxFallbackK + 2];
-  int nxt[kMaxFallbackK + 2];
   int depth = 0;
   stk[0] = h;
   nxt[0] = -1;

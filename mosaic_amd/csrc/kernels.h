@@ -50,6 +50,11 @@ struct JoinArgs {
   const uint16_t* mixed_idx;
   uint64_t* mixed_res;
   const uint32_t* chunk_mixed;
+  // a chunk with more than one tile of mixed points queues its further tiles here (for
+  // pip_mixed_more_kernel): extra[0 .. *n_extra), capacity chunks * (tiles per chunk - 1)
+  uint32_t* extra;
+  uint32_t* n_extra;
+
   const uint8_t* valid;             // null points (Arrow validity bitmap at bit offset valid_off), or null
   int64_t valid_off;
   int poly_answers;                 // binned pipeline: a one-match answer is (polygon id | 1 << 32)
@@ -68,6 +73,7 @@ struct SplitArgs {
   uint32_t* chunk_pairs;            // [chunks] (= j.group_sum)
   uint32_t* chunk_mixed;            // [chunks]
   uint16_t* mixed_idx;              // [chunks * split_chunk()]
+  uint32_t* extra;                  // [chunks * split_chunk() / join_tile_points()] (j.extra)
   uint64_t* chunk_off;              // [chunks] written by the scan
   const int64_t* point_id;
   int64_t id_base;

@@ -406,13 +406,14 @@ constexpr int kChunkTiles = kChunk / kGTile;
 constexpr int kGCandCap = 3 * kTile;
 constexpr int kGMixCap = kTile;
 
+
 // One tile (see the phase comment above).  SLOW = false: the streaming kernel; a
 // tile with a near-tie point is queued for pip_fix_kernel and abandoned after phase 1.
 // SLOW = true: the fix kernel; near-ties go through the H3 route.
 // G = true: the split pipeline's mixed points -- tile = chunk * kChunkTiles + t covers
 // list positions [t * kTile, ...) of the chunk's mixed list; the phases are the same,
 // the result is each point's (first chip, match mask) in mixed_res (no pair records).
-template <int IS, bool SLOW, bool G = false>
+template <int IS, bool SLOW, int G = 0>
 __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile) {
   __shared__ uint32_t s_ncand, s_nmix;
   __shared__ uint32_t s_wave_tot[kBlock / 64];
@@ -421,7 +422,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   __shared__ uint16_t s_cnt[kTile];     // chips of the point's cell (0: none)
   // phases 1-2: candidate list; phase 3: output staging (same bytes)
   constexpr int kCap = G ? kGCandCap : kCandCap, kMix = G ? kGMixCap : kMixCap;
-  __shared__ __attribute__((aligned(16))) uint8_t s_buf[G ? kStash * 16 + kGCandCap * 2 + kGMixCap * 2 : kOutCap * 6];
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[G ? kStash * 16 + kCap * 2 + kMix * 2 : kOutCap * 6];
   // candidate c = chip s_first[li] + j of point li, s_cand_pj[c] = li | j << 10; the
   // first kStash candidates also keep the point's coordinates (no re-read in phase 2)
   double2* s_cand_xy = (double2*)s_buf;                             // [kStash]
@@ -429,25 +430,25 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   uint16_t* s_mix = (uint16_t*)(s_buf + kStash * 16 + kCap * 2);  // [kMix] candidate index
   int32_t* s_out_poly = (int32_t*)s_buf;                          // [kOutCap]
   uint16_t* s_out_li = (uint16_t*)(s_buf + kOutCap * 4);          // [kOutCap]
-  __shared__ uint16_t s_gidx[G ? kTile : 1];  // G: the point's index within its chunk
+  // G == 2 (the split pipeline): the tile's slice of its chunk's mixed list, each item's
+  // point index within the chunk; G == 1 (binned): the chunk's points in order
+  __shared__ uint16_t s_gidx[G == 2 ? kTile : 1];
 
-  // G: the tile's slice of its chunk's mixed list
   const uint32_t chunk = G ? tile / kChunkTiles : 0u;
-  const int64_t gbase = (int64_t)chunk * kChunk;         // first point of the chunk
+  const int64_t gbase = (int64_t)chunk * kChunk;                        // first point of the chunk
   const int64_t lbase = gbase + (int64_t)(tile % kChunkTiles) * kGTile;  // first list position
   uint32_t gcount = 0;
   if (G) {
-    // (the binned pipeline: no mixed list -- every point of the chunk, in order)
-    const bool listed = a.mixed_idx != nullptr;
     const int64_t left = a.n - gbase;
-    const uint32_t nm = listed ? a.chunk_mixed[chunk] : (uint32_t)(left <= 0 ? 0 : (left < kChunk ? left : kChunk));
+    const uint32_t nm = G == 2 ? a.chunk_mixed[chunk] : (uint32_t)(left <= 0 ? 0 : (left < kChunk ? left : kChunk));
     const uint32_t t0 = (tile % kChunkTiles) * kGTile;
     if (nm <= t0) return;
     gcount = nm - t0 < (uint32_t)kGTile ? nm - t0 : (uint32_t)kGTile;
-    for (uint32_t li = threadIdx.x; li < (uint32_t)kTile; li += kBlock)
-      s_gidx[li] = li < gcount ? (listed ? a.mixed_idx[lbase + li] : (uint16_t)(t0 + li)) : (uint16_t)0;
+    if (G == 2)
+      for (uint32_t li = threadIdx.x; li < (uint32_t)kTile; li += kBlock)
+        s_gidx[li] = li < gcount ? a.mixed_idx[lbase + li] : (uint16_t)0;
   }
-#define MGPU_PT(li) (G ? gbase + (int64_t)s_gidx[li] : (int64_t)tile * kTile + (li))
+#define MGPU_PT(li) (G == 2 ? gbase + (int64_t)s_gidx[li] : G == 1 ? lbase + (li) : (int64_t)tile * kTile + (li))
 #define MGPU_VALID(li) (G ? (uint32_t)(li) < gcount : (int64_t)tile * kTile + (li) < a.n)
 
 #ifdef MGPU_STAMPS
@@ -734,29 +735,33 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   MGPU_STAMP(3);
   if (G) {
     // the split pipeline: each listed point's answer, and the chunk's pair count
-    uint32_t mine = 0;
     // the binned pipeline: one match is answered by its polygon id (the chip is local
     // here; in input order, where the emit runs, every lookup would be a random line);
     // the lane's lookups are issued together, then its answers stored
     uint64_t v[kItems];
+    uint32_t mine[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
       const uint32_t li = threadIdx.x + k * kBlock;
       v[k] = 0;
+      mine[k] = 0;
       if (li < gcount) {
         const uint32_t m = s_mask[li];
         v[k] = (uint64_t)s_first[li] | ((uint64_t)m << 32);
         if (a.poly_answers && m && !(m & (m - 1)))
           v[k] = (uint64_t)(uint32_t)t.chip_poly[s_first[li] + __builtin_ctz(m)] | (1ull << 32);
-        mine += __popc(m);
+        mine[k] = __popc(m);
       }
     }
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
       const uint32_t li = threadIdx.x + k * kBlock;
-      if (li < gcount) a.mixed_res[lbase + li] = v[k];
+      if (li < gcount) a.mixed_res[lbase + li] = v[k];  // (the slot: the list position / binned point)
     }
-    const unsigned long long tot = wave_sum_u64(mine);
+    uint32_t tm = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; k++) tm += mine[k];
+    const unsigned long long tot = wave_sum_u64(tm);
     if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&a.group_sum[chunk], (uint32_t)tot);
     return;
   }
@@ -1040,21 +1045,36 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
 }
 
 
-// the mixed points of one chunk per workgroup, a tile of kTile at a time
+// The mixed points of one chunk per workgroup: its first tile of kTile; a chunk with
+// more queues its further tiles for pip_mixed_more_kernel (a loop over tiles here pinned
+// 23 more VGPRs: 5 waves/SIMD instead of 7).  (Measured and rejected, r3: the chunks'
+// lists packed into full tiles walked by a resident grid -- C2 mixed 0.22 -> 0.35 ms,
+// C5 0.60 -> 0.87: a full tile's phases take longer, and fewer tiles are in flight.)
 template <int IS>
 __global__ __launch_bounds__(kBlock) MGPU_JOIN_ATTR void pip_mixed_kernel(JoinArgs a) {
   const uint32_t nm = a.chunk_mixed[blockIdx.x];
-  for (uint32_t t = 0; t * kGTile < nm; t++) {
-    join_tile<IS, false, true>(a, blockIdx.x * kChunkTiles + t);
+  if (threadIdx.x == 0 && nm > (uint32_t)kGTile) {
+    const uint32_t more = (nm - 1) / kGTile;
+    const uint32_t q = atomicAdd(a.n_extra, more);
+    for (uint32_t t = 0; t < more; t++) a.extra[q + t] = blockIdx.x * kChunkTiles + 1 + t;
+  }
+  join_tile<IS, false, 2>(a, blockIdx.x * kChunkTiles);
+}
+
+template <int IS>
+__global__ __launch_bounds__(kBlock) void pip_mixed_more_kernel(JoinArgs a) {
+  const uint32_t n = *a.n_extra;
+  for (uint32_t q = blockIdx.x; q < n; q += gridDim.x) {
+    join_tile<IS, false, 2>(a, a.extra[q]);
     __syncthreads();
   }
 }
 
-template <int IS>
+template <int IS, int G>
 __global__ __launch_bounds__(kBlock) void pip_mixed_fix_kernel(JoinArgs a) {
   const uint32_t nd = *a.n_dirty;
   for (uint32_t q = blockIdx.x; q < nd; q += gridDim.x) {
-    join_tile<IS, true, true>(a, a.dirty[q]);
+    join_tile<IS, true, G>(a, a.dirty[q]);
     __syncthreads();
   }
 }
@@ -1565,7 +1585,8 @@ __global__ __launch_bounds__(kFmtBlock) void kring_count_kernel(int is, const in
 // walks whose hash set overflowed (inconsistent tables; never expected).
 __host__ __device__ constexpr int64_t kring_fb_words(int k) {
   return 2 * (3 * (int64_t)k * (k + 1) + 1) + (3 * (int64_t)k * (k + 1) + 2) / 2 +
-         (k > 0 ? (3 * (int64_t)(k - 1) * k + 1) + (3 * (int64_t)(k - 1) * k + 2) / 2 : 0) + 2;
+         (k > 0 ? (3 * (int64_t)(k - 1) * k + 1) + (3 * (int64_t)(k - 1) * k + 2) / 2 : 0) + 2 +
+         (k + 2) + (k + 2 + 7) / 8;  // + the walk's stack (cells, next direction)
 }
 __global__ __launch_bounds__(64) void kring_fallback_kernel(const int64_t* __restrict__ cells, const uint32_t* __restrict__ fb_idx,
                                                             int64_t j0, int64_t j1, int k, int loop_only,
@@ -1583,10 +1604,12 @@ __global__ __launch_bounds__(64) void kring_fallback_kernel(const int64_t* __res
   uint64_t* tab2 = tab + m + (m + 1) / 2;
   int32_t* dist2 = (int32_t*)(tab2 + m2);
   int64_t* list = (int64_t*)(tab2 + m2 + (m2 + 1) / 2);
+  uint64_t* stk = tab + kring_fb_words(k) - ((k + 2) + (k + 2 + 7) / 8);
+  int8_t* nxt = (int8_t*)(stk + k + 2);
   bool ok = true;
   int64_t cnt = 0;
   if (!loop_only) {  // (here the spiral failed: H3's _kRingInternal)
-    ok = h3ring::kring_hash(h, k, tab, dist);
+    ok = h3ring::kring_hash(h, k, tab, dist, stk, nxt);
     for (int64_t q = 0; q < m; q++)
       if (tab[q]) list[cnt++] = (int64_t)tab[q];
   } else {
@@ -1597,14 +1620,14 @@ __global__ __launch_bounds__(64) void kring_fallback_kernel(const int64_t* __res
       for (int64_t q = 0; q < m; q++) tab[q] = 0;
       for (int64_t q = 0; q < ma; q++) h3ring::hash_insert(tab, m, (uint64_t)list[q]);
     } else {
-      ok = h3ring::kring_hash(h, k, tab, dist);
+      ok = h3ring::kring_hash(h, k, tab, dist, stk, nxt);
     }
     const int64_t ms = h3ring::kring(h, k - 1, list);
     if (ms >= 0) {
       for (int64_t q = 0; q < m2; q++) tab2[q] = 0;
       for (int64_t q = 0; q < ms; q++) h3ring::hash_insert(tab2, m2, (uint64_t)list[q]);
     } else {
-      ok = ok && h3ring::kring_hash(h, k - 1, tab2, dist2);
+      ok = ok && h3ring::kring_hash(h, k - 1, tab2, dist2, stk, nxt);
     }
     cnt = ok ? h3ring::kloop_diff(tab, m, tab2, m2, list) : 0;
   }
@@ -1663,14 +1686,13 @@ hipError_t launch_kring_count(int is, const int64_t* cells, int64_t n, int k, in
 }
 
 int64_t kring_fallback_words(int k) { return kring_fb_words(k); }
-int32_t kring_fallback_max_k() { return h3ring::kMaxFallbackK; }
+int32_t kring_fallback_max_k() { return 1024; }  // (the entry's own bound on k)
 
 hipError_t launch_kring_fallback(const int64_t* cells, const uint32_t* fb_idx, int64_t j0, int64_t j1, int k,
                                  int loop_only, int64_t* mc, int64_t* chunk, const int64_t* offsets, int64_t* out,
                                  int64_t capacity, uint64_t* scratch, int write, unsigned long long* counters,
                                  hipStream_t s) {
   if (j1 <= j0) return hipSuccess;
-  if (k > h3ring::kMaxFallbackK) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kring_fallback_kernel, dim3((unsigned)((j1 - j0 + 63) / 64)), dim3(64), 0, s, cells, fb_idx, j0, j1,
                      k, loop_only, mc, chunk, offsets, out, capacity, scratch, write, counters);
   return hipGetLastError();
@@ -1775,26 +1797,47 @@ __global__ __launch_bounds__(256) void bin_colscan_kernel(BinArgs b, int64_t n_c
 }
 
 // one workgroup: each bin's total, the bins' exclusive scan (slots are bin-major), then
-// gsum[group][bin] = the first slot of the bin's points of that group of chunks
-__global__ __launch_bounds__(kBinBlock) void bin_base_kernel(BinArgs b, int64_t n_groups) {
-  __shared__ uint32_t s_w[kBinBlock / 64];
+// gsum[group][bin] = the first slot of the bin's points of that group of chunks.  Each
+// bin's column of group sums is cut into kBaseBlock / bins parts, one thread each (one
+// thread per bin walked ~400 groups serially: 83 us per 1e8 points on C3).
+constexpr int kBaseBlock = 1024;
+__global__ __launch_bounds__(kBaseBlock) void bin_base_kernel(BinArgs b, int64_t n_groups) {
+  __shared__ uint32_t s_part[kBaseBlock];
+  __shared__ uint32_t s_base[kBinMax];
+  __shared__ uint32_t s_w[kBaseBlock / 64];
   const int nb = b.nbx * b.nby;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int bin = threadIdx.x;
+  const int parts = kBaseBlock / nb > 0 ? kBaseBlock / nb : 1;
+  const int bin = threadIdx.x / parts, part = threadIdx.x % parts;
+  const int64_t per = (n_groups + parts - 1) / parts;
+  const int64_t g0 = part * per, g1 = g0 + per < n_groups ? g0 + per : n_groups;
   uint32_t mine = 0;
   if (bin < nb)
-    for (int64_t g = 0; g < n_groups; g++) mine += b.gsum[g * nb + bin];
-  const uint32_t incl = wave_incl_scan(mine);
+    for (int64_t g = g0; g < g1; g++) mine += b.gsum[g * nb + bin];
+  s_part[threadIdx.x] = mine;
+  __syncthreads();
+  // the bins' totals, scanned (thread t < nb: bin t)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t tot = 0;
+  if ((int)threadIdx.x < nb)
+    for (int q = 0; q < parts; q++) tot += s_part[threadIdx.x * parts + q];
+  const uint32_t incl = wave_incl_scan(tot);
   if (lane == 63) s_w[wave] = incl;
   __syncthreads();
-  uint32_t run = incl - mine;
-  for (int w = 0; w < wave; w++) run += s_w[w];
-  if (bin < nb)
-    for (int64_t g = 0; g < n_groups; g++) {
+  if ((int)threadIdx.x < nb) {
+    uint32_t run = incl - tot;
+    for (int w = 0; w < wave; w++) run += s_w[w];
+    s_base[threadIdx.x] = run;
+  }
+  __syncthreads();
+  if (bin < nb) {
+    uint32_t run = s_base[bin];
+    for (int q = 0; q < part; q++) run += s_part[bin * parts + q];
+    for (int64_t g = g0; g < g1; g++) {
       const uint32_t v = b.gsum[g * nb + bin];
       b.gsum[g * nb + bin] = run;
       run += v;
     }
+  }
 }
 
 // The chunk's bin runs: s_off[bin] = its first binned slot, s_loc[bin] = its first
@@ -1907,7 +1950,7 @@ __global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
 template <int IS>
 __global__ __launch_bounds__(kBlock) MGPU_JOIN_ATTR void pip_binned_kernel(JoinArgs a, uint32_t per_xcd, uint32_t n_tiles) {
   const uint32_t tile = per_xcd ? (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3) : blockIdx.x;
-  if (tile < n_tiles) join_tile<IS, false, true>(a, tile);
+  if (tile < n_tiles) join_tile<IS, false, 1>(a, tile);
 }
 
 // The answers back in input order, per chunk of kBinChunk input points: the chunk's bin
@@ -2188,8 +2231,10 @@ static void launch_split_t(const SplitArgs& a, hipStream_t s, hipEvent_t after_c
   // (one workgroup per chunk walking its mixed tiles; one workgroup per tile measured 8x
   // slower on C2: ~6 ns per dispatched workgroup, most of them empty)
   hipLaunchKernelGGL(pip_mixed_kernel<IS>, dim3((unsigned)nc), dim3(kBlock), 0, s, a.j);
+  const int64_t more = std::min<int64_t>(nc, (int64_t)resident_blocks((const void*)pip_mixed_more_kernel<IS>, kBlock, 0));
+  hipLaunchKernelGGL(pip_mixed_more_kernel<IS>, dim3((unsigned)more), dim3(kBlock), 0, s, a.j);
   const int64_t fix = nc * kChunkTiles < kFixGrid ? nc * kChunkTiles : kFixGrid;
-  hipLaunchKernelGGL(pip_mixed_fix_kernel<IS>, dim3((unsigned)fix), dim3(kBlock), 0, s, a.j);
+  hipLaunchKernelGGL((pip_mixed_fix_kernel<IS, 2>), dim3((unsigned)fix), dim3(kBlock), 0, s, a.j);
   if (after_mixed) hipEventRecord(after_mixed, s);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.chunk_pairs, a.j.group_cand, nc,
                      a.chunk_off, a.j.counters);
@@ -2226,7 +2271,7 @@ static void launch_binned_t(const BinArgs& a, hipStream_t s, hipEvent_t after_bi
   const int64_t n = a.s.j.n, K = bin_chunks(n), G = bin_groups(n), nb = (int64_t)a.nbx * a.nby;
   hipLaunchKernelGGL(bin_hist_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
   hipLaunchKernelGGL(bin_colscan_kernel, dim3((unsigned)((nb + 255) / 256), (unsigned)G), dim3(256), 0, s, a, K);
-  hipLaunchKernelGGL(bin_base_kernel, dim3(1), dim3(kBinBlock), 0, s, a, G);
+  hipLaunchKernelGGL(bin_base_kernel, dim3(1), dim3(kBaseBlock), 0, s, a, G);
   hipLaunchKernelGGL(bin_scatter_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
   if (after_bin) hipEventRecord(after_bin, s);
   const int64_t nc = split_chunks(n), tiles = nc * kChunkTiles;
@@ -2235,7 +2280,7 @@ static void launch_binned_t(const BinArgs& a, hipStream_t s, hipEvent_t after_bi
   hipLaunchKernelGGL(pip_binned_kernel<IS>, dim3((unsigned)grid), dim3(kBlock), 0, s, a.s.j, per, (uint32_t)tiles);
   if (after_join) hipEventRecord(after_join, s);
   const int64_t fix = tiles < kFixGrid ? tiles : kFixGrid;
-  hipLaunchKernelGGL(pip_mixed_fix_kernel<IS>, dim3((unsigned)fix), dim3(kBlock), 0, s, a.s.j);
+  hipLaunchKernelGGL((pip_mixed_fix_kernel<IS, 1>), dim3((unsigned)fix), dim3(kBlock), 0, s, a.s.j);
   hipLaunchKernelGGL(bin_gather_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.s.chunk_pairs, a.s.j.group_cand, nc,
                      a.s.chunk_off, a.s.j.counters);

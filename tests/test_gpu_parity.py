@@ -236,6 +236,17 @@ def test_h3_kring_kloop_pentagons_equal_oracle(gpu, res):
     assert_h3_rings_equal_oracle(gpu, pents + near, ks=(0, 1, 2, 3, 4), tag="pentagons r%d" % res)
 
 
+def test_h3_kring_kloop_pentagons_large_k(gpu):
+    """k beyond 64 near pentagons (the walk's stack lives in scratch, any k the entry
+    accepts): four res-5 pentagons (polar 4 and 117 among them) and a neighbour, k = 65
+    and 80, ring and loop, == the oracle.  (A walk is one lane's depth-first search: k =
+    100 over 14 cells took ~2.5 min.)"""
+    pents = h3_pentagon_cells(5)
+    pick = [p for p in pents if ((p >> 45) & 127) in (4, 117)] + [p for p in pents if ((p >> 45) & 127) not in (4, 117)][:2]
+    near = [O.h3_k_ring(pick[0], 1)[1]]
+    assert_h3_rings_equal_oracle(gpu, pick + near, ks=(65, 80), tag="pentagons large k")
+
+
 def test_index_system_scalar_k_ring_k_loop(gpu):
     """IndexSystem.kRing / kLoop (scalar surface of the mirror) == the oracle, H3 and BNG."""
     import numpy as np

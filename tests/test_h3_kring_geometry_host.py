@@ -70,3 +70,67 @@ def test_kring_rings_are_graph_distances(res):
         assert all(_adjacent(keys[loop[i]], keys[loop[(i + 1) % len(loop)]]) for i in range(len(loop)))
         checked += 1
     assert checked > 50 and (res > 3 or crossings > 5)
+
+
+def _geo_neighbours(cells, res):
+    """Each cell's neighbours from geometry alone: a point just outside the midpoint of
+    every boundary edge (h3ToGeoBoundary, distortion vertices included), indexed by
+    geoToH3 -- faceIjkBaseCells + faceNeighbors, not the neighbour tables."""
+    xy, nv, ctr = cell_geometry(np.asarray(cells, dtype=np.int64))
+
+    def unit(lon, lat):
+        lo, la = np.radians(lon), np.radians(lat)
+        return np.stack([np.cos(la) * np.cos(lo), np.cos(la) * np.sin(lo), np.sin(la)], -1)
+
+    out = {}
+    for i, h in enumerate(cells):
+        v = unit(xy[i, :nv[i], 0], xy[i, :nv[i], 1])
+        c = unit(ctr[i, 0], ctr[i, 1])
+        m = v + np.roll(v, -1, 0)
+        m /= np.linalg.norm(m, axis=1)[:, None]
+        p = m + 0.05 * (m - c)
+        p /= np.linalg.norm(p, axis=1)[:, None]
+        lon, lat = np.degrees(np.arctan2(p[:, 1], p[:, 0])), np.degrees(np.arcsin(p[:, 2]))
+        nb = set(int(x) for x in O.h3_points_to_cells(lon, lat, res)) - {int(h)}
+        out[int(h)] = nb
+    return out
+
+
+@pytest.mark.parametrize("res,kmax", [(1, 3), (2, 4), (3, 5), (5, 5), (8, 4)])
+def test_pentagon_krings_are_geometric_balls(res, kmax):
+    """Around pentagons -- the polar ones 4 and 117 among them -- kRing(h, k) (H3's
+    _kRingInternal hash-set walk) is exactly the set of cells within k steps of h over
+    geometric adjacency, and kLoop(h, k) the cells at exactly k steps; for the pentagon
+    itself and for cells next to it, k = 1..kmax.  Adjacency comes from cell geometry and
+    geoToH3 only (no neighbour table).  (This pins the sets; the lists' order -- the
+    walk's hash-set order -- follows the derived direction tables.)"""
+    unused = sum(7 << (3 * (15 - r)) for r in range(res + 1, 16))
+    pents = [(1 << 59) | (res << 52) | (b << 45) | unused for b in sorted(H3_PENTAGON_BASE_CELLS)]
+    nbr_cache = {}
+
+    def neighbours(cells):
+        need = [c for c in cells if c not in nbr_cache]
+        if need:
+            nbr_cache.update(_geo_neighbours(need, res))
+        return {c: nbr_cache[c] for c in cells}
+
+    checked = 0
+    for p in pents:
+        starts = [p] + sorted(neighbours([p])[p])[:2]
+        for h in starts:
+            dist = {h: 0}
+            frontier = [h]
+            for step in range(1, kmax + 1):
+                nxt = []
+                for u, nb in neighbours(frontier).items():
+                    for v in nb:
+                        if v not in dist:
+                            dist[v] = step
+                            nxt.append(v)
+                frontier = nxt
+                ball = {v for v, d in dist.items() if d <= step}
+                ring = O.h3_k_ring(h, step)
+                assert set(ring) == ball and len(ring) == len(ball), (hex(h), step)
+                assert set(O.h3_k_loop(h, step)) == {v for v, d in dist.items() if d == step}, (hex(h), step)
+                checked += 1
+    assert checked == 12 * 3 * kmax
