@@ -139,23 +139,41 @@ int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t index_system, int32_t res,
                              int64_t* out_cell, void* stream, mgpu_stats* stats);
 
 /* grid_pointascellid on a geometry column (PointIndexGeom.scala:33-47: GeometryAPI.geometry
- * (GeometryAPI.scala:81-89) decodes BinaryType as WKB, StringType as WKT, then getCentroid,
- * then pointToIndex).  Rows are data[offsets[i] .. offsets[i + 1]) (the Arrow binary /
- * utf8 layout); POINT and MULTIPOINT geometries (WKB big- or little-endian, EWKB / ISO
- * Z, M; WKT with Java Double.parseDouble rounding) -- other types return
- * MGPU_E_UNSUPPORTED, malformed rows MGPU_E_WKB (JTS ParseException), empty points
- * MGPU_E_EMPTY.  `valid` (optional Arrow bitmap, bit offset valid_offset): null rows are
+ * (GeometryAPI.scala:81-89) decodes BinaryType as WKB, StringType as WKT, HexType as
+ * hex WKB, JSONType as GeoJSON, then getCentroid -- JTS Centroid: area-weighted for
+ * polygons, length-weighted for lines, the mean of points -- then pointToIndex).  Rows
+ * are data[offsets[i] .. offsets[i + 1]) (the Arrow binary / utf8 layout).  WKB / HEX:
+ * every geometry type (big- or little-endian, EWKB / ISO Z, M, nested collections);
+ * WKT (Java Double.parseDouble rounding) and GeoJSON: POINT and MULTIPOINT, other types
+ * return MGPU_E_UNSUPPORTED.  Malformed rows MGPU_E_WKB (JTS ParseException), empty
+ * geometries MGPU_E_EMPTY.  `valid` (optional Arrow bitmap, bit offset valid_offset): null rows are
  * null out -- out_cell 0 and a 0 bit in out_valid ((n + 7) / 8 bytes, optional).
  * mgpu_points_from_geometry stops at the point (x, y; NaN for null rows).  Device
  * pointers; synchronises `stream`. */
 #define MGPU_GEOM_WKB 0
 #define MGPU_GEOM_WKT 1
+#define MGPU_GEOM_HEX 2     /* HexType: WKB as hex text (WKBReader.hexToBytes) */
+#define MGPU_GEOM_GEOJSON 3 /* JSONType: GeoJSON text (GeoJsonReader) */
 int32_t mgpu_points_from_geometry(mgpu_ctx* ctx, int32_t format, const uint8_t* data, const int64_t* offsets,
                                   const uint8_t* valid, int64_t valid_offset, int64_t n, double* out_x, double* out_y,
                                   void* stream);
 int32_t mgpu_geometry_to_cells(mgpu_ctx* ctx, int32_t index_system, int32_t res, int32_t format, const uint8_t* data,
                                const int64_t* offsets, const uint8_t* valid, int64_t valid_offset, int64_t n,
                                int64_t* out_cell, uint8_t* out_valid, void* stream, mgpu_stats* stats);
+
+/* grid_pointascellid on Mosaic's InternalGeometryType column (InternalGeometry.scala:
+ * typeId, boundaries, holes; MosaicGeometryJTS.fromInternal, MosaicGeometryJTS.scala:343-357)
+ * flattened as nested lists: row i's parts [row_part[i], row_part[i + 1]), part q's
+ * rings [part_ring[q], part_ring[q + 1]) (the boundary, then its holes), ring k's points
+ * xy[2 ring_off[k] .. 2 ring_off[k + 1]) -- the Arrow layout of list<list<list<x, y>>>.
+ * type_id: POINT 1, MULTIPOINT 2, LINESTRING 3, MULTILINESTRING 4, POLYGON 5,
+ * MULTIPOLYGON 6 (GeometryTypeEnum); others MGPU_E_UNSUPPORTED.  Centroid, validity and
+ * errors as mgpu_geometry_to_cells.  Device pointers; synchronises `stream`. */
+int32_t mgpu_internal_geometry_to_cells(mgpu_ctx* ctx, int32_t index_system, int32_t res, int64_t n,
+                                        const int32_t* type_id, const int64_t* row_part, const int64_t* part_ring,
+                                        const int64_t* ring_off, const double* xy, const uint8_t* valid,
+                                        int64_t valid_offset, int64_t* out_cell, uint8_t* out_valid, void* stream,
+                                        mgpu_stats* stats);
 
 /* Host-pointer convenience form (copies over PCIe). */
 int32_t mgpu_points_to_cells_host(mgpu_ctx* ctx, int32_t index_system, int32_t res,
@@ -354,6 +372,11 @@ int32_t mgpu_test_h3_glibc_host(const double* lon, const double* lat, int64_t n,
 int32_t mgpu_test_h3_boundary_host(const int64_t* cells, int64_t n, double* out_lonlat, int32_t* out_nverts,
                                    double* out_center);
 int32_t mgpu_test_decode_point(int32_t format, const uint8_t* data, int64_t len, double* x, double* y);
+/* TEST ONLY: the centroids of n InternalGeometryType rows (layout of
+ * mgpu_internal_geometry_to_cells) on the host; status[i] 0 ok, 1 malformed, 2 unsupported,
+ * 3 empty. */
+int32_t mgpu_test_internal_centroid(int64_t n, const int32_t* type_id, const int64_t* row_part, const int64_t* part_ring,
+                                    const int64_t* ring_off, const double* xy, double* x, double* y, int32_t* status);
 
 /* TEST ONLY -- st_contains(chip row, point) evaluated on a HOST blob (the join's
  * classification grid + strip path), to check on the CPU that a shipped blob is a

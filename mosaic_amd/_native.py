@@ -40,10 +40,12 @@ EXPORTS = (
     "mgpu_geometry_to_cells_arrow", "mgpu_pip_join_arrow", "mgpu_test_parse_number", "mgpu_test_decode_point",
     "mgpu_test_h3_elementary_host", "mgpu_test_h3_route_host", "mgpu_test_h3_boundary_host",
     "mgpu_ctx_set_option", "mgpu_ctx_get_option", "mgpu_build_opts_default", "mgpu_chips_host_blob_ex",
-    "mgpu_test_h3_glibc_host",
+    "mgpu_test_h3_glibc_host", "mgpu_internal_geometry_to_cells", "mgpu_test_internal_centroid",
 )
 MGPU_GEOM_WKB = 0
 MGPU_GEOM_WKT = 1
+MGPU_GEOM_HEX = 2
+MGPU_GEOM_GEOJSON = 3
 MGPU_COMM_ID_BYTES = 128
 MGPU_PIPELINE_AUTO = -1
 MGPU_PIPELINE_FUSED = 0
@@ -167,6 +169,9 @@ def lib():
         "mgpu_chips_host_blob_ex": (I32, [I32, I64, P, P, P, P, P, ctypes.POINTER(BuildOpts), ctypes.POINTER(P),
                                           ctypes.POINTER(I64)]),
         "mgpu_test_h3_glibc_host": (I32, [P, P, I64, I32, P]),
+        "mgpu_internal_geometry_to_cells": (I32, [P, I32, I32, I64, P, P, P, P, P, P, I64, P, P, P,
+                                                  ctypes.POINTER(MgpuStats)]),
+        "mgpu_test_internal_centroid": (I32, [I64, P, P, P, P, P, P, P, P]),
     }
     for name, (rt, args) in sig.items():
         f = getattr(L, name)

@@ -2503,22 +2503,30 @@ static int32_t ensure_scratch(mgpu_ctx* ctx, size_t bytes) {
 }
 
 // decode into (x, y) and check the decode counters
+// the decode kernels' counters -> the reference's exception classes
+static int32_t decode_status(mgpu_ctx* ctx, int32_t format, hipStream_t s) {
+  static const char* names[] = {"WKB", "WKT", "hex WKB", "GeoJSON", "internal geometry"};
+  unsigned long long h[8] = {0};
+  HIP_TRY(hipMemcpyAsync(h, ctx->ws, sizeof h, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const char* name = names[format >= 0 && format <= 4 ? format : 0];
+  if (h[4]) return fail(MGPU_E_WKB, "%llu rows are not well-formed %s", h[4], name);
+  if (h[5])
+    return fail(MGPU_E_UNSUPPORTED, "%llu %s rows are of a geometry type whose centroid is not built for this format",
+                h[5], name);
+  if (h[6]) return fail(MGPU_E_EMPTY, "getX called on empty Point (%llu rows: empty geometries)", h[6]);
+  return MGPU_OK;
+}
+
 static int32_t decode_points(mgpu_ctx* ctx, int32_t format, const uint8_t* data, const void* offsets, int off32,
                              const uint8_t* valid, int64_t voff, int64_t n, double* x, double* y, hipStream_t s) {
-  if (format != MGPU_GEOM_WKB && format != MGPU_GEOM_WKT) return fail(MGPU_E_INVALID_ARG, "geometry format %d", format);
+  if (format < MGPU_GEOM_WKB || format > MGPU_GEOM_GEOJSON) return fail(MGPU_E_INVALID_ARG, "geometry format %d", format);
   if (n < 0 || (n > 0 && (!data || !offsets || !x || !y))) return fail(MGPU_E_INVALID_ARG, "bad geometry arrays");
   if (int32_t st = ensure_ws(ctx, 1)) return st;
   auto* counters = (unsigned long long*)ctx->ws;
   HIP_TRY(hipMemsetAsync(counters, 0, kWsCounters, s));
   HIP_TRY(mgpu::launch_decode_points(format, data, offsets, off32, valid, voff, n, x, y, counters, s));
-  unsigned long long h[8] = {0};
-  HIP_TRY(hipMemcpyAsync(h, counters, sizeof h, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  if (h[4]) return fail(MGPU_E_WKB, "%llu rows are not well-formed %s", h[4], format == MGPU_GEOM_WKB ? "WKB" : "WKT");
-  if (h[5])
-    return fail(MGPU_E_UNSUPPORTED, "%llu rows are neither POINT nor MULTIPOINT (their centroid is not built here)", h[5]);
-  if (h[6]) return fail(MGPU_E_EMPTY, "getX called on empty Point (%llu rows)", h[6]);
-  return MGPU_OK;
+  return decode_status(ctx, format, s);
 }
 
 extern "C" {
@@ -2576,6 +2584,33 @@ int32_t mgpu_geometry_to_cells(mgpu_ctx* ctx, int32_t index_system, int32_t res,
                                int64_t* out_cell, uint8_t* out_valid, void* stream, mgpu_stats* stats) {
   return geometry_cells(ctx, index_system, res, format, data, offsets, 0, valid, valid_offset, n, out_cell, out_valid,
                         (hipStream_t)stream, stats);
+}
+
+int32_t mgpu_internal_geometry_to_cells(mgpu_ctx* ctx, int32_t index_system, int32_t res, int64_t n,
+                                        const int32_t* type_id, const int64_t* row_part, const int64_t* part_ring,
+                                        const int64_t* ring_off, const double* xy, const uint8_t* valid,
+                                        int64_t valid_offset, int64_t* out_cell, uint8_t* out_valid, void* stream,
+                                        mgpu_stats* stats) {
+  if (!ctx) return fail(MGPU_E_INVALID_ARG, "ctx is NULL");
+  if (int32_t r = check_res(index_system, res)) return r;
+  if (n < 0 || (n > 0 && (!out_cell || !type_id || !row_part || !part_ring || !ring_off || !xy)))
+    return fail(MGPU_E_INVALID_ARG, "bad internal geometry arrays");
+  if (int32_t st = set_device(ctx->device)) return st;
+  hipStream_t s = (hipStream_t)stream;
+  if (int32_t st = ensure_ws(ctx, 1)) return st;
+  if (int32_t st = ensure_scratch(ctx, (size_t)std::max<int64_t>(n, 1) * 16)) return st;
+  double* x = (double*)ctx->scratch;
+  double* y = x + std::max<int64_t>(n, 1);
+  HIP_TRY(hipMemsetAsync(ctx->ws, 0, kWsCounters, s));
+  HIP_TRY(mgpu::launch_decode_internal(type_id, row_part, part_ring, ring_off, xy, valid, valid_offset, n, x, y,
+                                       (unsigned long long*)ctx->ws, s));
+  if (int32_t st = decode_status(ctx, 4, s)) return st;
+  if (int32_t st = cells_impl(ctx, index_system, res, x, y, n, out_cell, s, valid, valid_offset, stats)) return st;
+  if (out_valid) {
+    HIP_TRY(mgpu::launch_valid_and(valid, valid_offset, nullptr, 0, n, out_valid, s));
+    HIP_TRY(stream_wait(ctx, s));
+  }
+  return MGPU_OK;
 }
 
 int32_t mgpu_geometry_to_cells_arrow(mgpu_ctx* ctx, int32_t index_system, int32_t res,
@@ -2683,8 +2718,20 @@ int32_t mgpu_test_h3_glibc_host(const double* lon, const double* lat, int64_t n,
 }
 
 int32_t mgpu_test_decode_point(int32_t format, const uint8_t* data, int64_t len, double* x, double* y) {
-  return format == MGPU_GEOM_WKB ? mgpu::geom::wkb_centroid(data, len, x, y)
-                                 : mgpu::geom::wkt_centroid((const char*)data, len, x, y);
+  switch (format) {
+    case MGPU_GEOM_WKB: return mgpu::geom::wkb_centroid(data, len, x, y);
+    case MGPU_GEOM_WKT: return mgpu::geom::wkt_centroid((const char*)data, len, x, y);
+    case MGPU_GEOM_HEX: return mgpu::geom::hex_centroid((const char*)data, len, x, y);
+    case MGPU_GEOM_GEOJSON: return mgpu::geom::json_centroid((const char*)data, len, x, y);
+  }
+  return mgpu::geom::kDecUnsupported;
+}
+
+int32_t mgpu_test_internal_centroid(int64_t n, const int32_t* type_id, const int64_t* row_part, const int64_t* part_ring,
+                                    const int64_t* ring_off, const double* xy, double* x, double* y, int32_t* status) {
+  for (int64_t i = 0; i < n; i++)
+    status[i] = mgpu::geom::internal_centroid(type_id[i], row_part[i], row_part[i + 1], part_ring, ring_off, xy, &x[i], &y[i]);
+  return MGPU_OK;
 }
 
 }  // extern "C"

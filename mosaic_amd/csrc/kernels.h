@@ -155,6 +155,9 @@ hipError_t launch_gather_xy(const double* x, const double* y, const int64_t* pos
 // the point (centroid) of each POINT / MULTIPOINT geometry, WKB (format 0) or WKT (1),
 // rows data[offsets[i] .. offsets[i + 1]); null rows (valid bitmap) -> NaN.  counters[4..6]
 // += malformed / unsupported type / empty rows
+hipError_t launch_decode_internal(const int32_t* type_id, const int64_t* row_part, const int64_t* part_ring,
+                                  const int64_t* ring_off, const double* xy, const uint8_t* valid, int64_t voff,
+                                  int64_t n, double* x, double* y, unsigned long long* counters, hipStream_t s);
 hipError_t launch_decode_points(int format, const uint8_t* data, const void* offsets, int off32, const uint8_t* valid,
                                 int64_t voff, int64_t n, double* x, double* y, unsigned long long* counters,
                                 hipStream_t s);

@@ -38,9 +38,12 @@ def grid_longlatascellid(lon, lat, resolution, index_system=None, ctx=None, stre
 
 
 class GeometryColumn:
-    """A WKB (BinaryType) or WKT (StringType) geometry column in device memory, laid out
-    as Arrow lays out binary / utf8: one byte buffer, int64 offsets (n + 1), optional
-    validity bitmap (LSB first, 1 = present)."""
+    """A geometry column in device memory as Arrow lays out binary / utf8: one byte buffer,
+    int64 offsets (n + 1), optional validity bitmap (LSB first, 1 = present).  Format:
+    MGPU_GEOM_WKB (BinaryType), _WKT (StringType), _HEX (HexType: hex WKB text) or
+    _GEOJSON (JSONType), GeometryAPI.geometry's input types (GeometryAPI.scala:81-89)."""
+
+    FORMATS = {"wkb": N.MGPU_GEOM_WKB, "wkt": N.MGPU_GEOM_WKT, "hex": N.MGPU_GEOM_HEX, "geojson": N.MGPU_GEOM_GEOJSON}
 
     def __init__(self, fmt, data, offsets, valid=None):
         self.format, self.data, self.offsets, self.valid = fmt, data, offsets, valid
@@ -49,13 +52,14 @@ class GeometryColumn:
         return self.offsets.numel() - 1
 
     @staticmethod
-    def from_rows(rows, device="cuda"):
-        """Python rows (bytes: WKB, str: WKT, None: null) -> device column."""
+    def from_rows(rows, device="cuda", fmt=None):
+        """Python rows (bytes: WKB, str: WKT unless `fmt` says "hex" / "geojson", None:
+        null) -> device column."""
         import torch
         kinds = {type(r) for r in rows if r is not None}
         if len(kinds) > 1:
-            raise N.IllegalArgumentException(N.MGPU_E_INVALID_ARG, "mixed WKB and WKT rows")
-        fmt = N.MGPU_GEOM_WKT if kinds == {str} else N.MGPU_GEOM_WKB
+            raise N.IllegalArgumentException(N.MGPU_E_INVALID_ARG, "mixed binary and text rows")
+        code = GeometryColumn.FORMATS[fmt] if fmt else (N.MGPU_GEOM_WKT if kinds == {str} else N.MGPU_GEOM_WKB)
         bs = [b"" if r is None else (r.encode() if isinstance(r, str) else bytes(r)) for r in rows]
         off = np.zeros(len(bs) + 1, np.int64)
         off[1:] = np.cumsum([len(b) for b in bs])
@@ -64,17 +68,67 @@ class GeometryColumn:
         if any(r is None for r in rows):
             valid = np.packbits(np.array([r is not None for r in rows], bool), bitorder="little")
             valid = torch.from_numpy(valid).to(device)
-        return GeometryColumn(fmt, torch.from_numpy(data.copy()).to(device), torch.from_numpy(off).to(device), valid)
+        return GeometryColumn(code, torch.from_numpy(data.copy()).to(device), torch.from_numpy(off).to(device), valid)
+
+
+class InternalGeometryColumn:
+    """Mosaic's InternalGeometryType column (InternalGeometry.scala: typeId, boundaries,
+    holes) flattened as nested lists in device memory (mgpu_internal_geometry_to_cells):
+    type_id[n]; row_part[n + 1]; part_ring[P + 1] (each part's boundary, then its holes);
+    ring_off[R + 1]; xy[2 V]."""
+
+    def __init__(self, type_id, row_part, part_ring, ring_off, xy):
+        self.type_id, self.row_part, self.part_ring, self.ring_off, self.xy = type_id, row_part, part_ring, ring_off, xy
+
+    def __len__(self):
+        return self.type_id.numel()
+
+    @staticmethod
+    def from_rows(rows, device="cuda"):
+        """rows: (type_id, parts), parts = [[ring, ring, ...], ...] (boundary first), a
+        ring a list of (x, y)."""
+        import torch
+        tid, rp, pr, ro, xy = [], [0], [0], [0], []
+        for t, parts in rows:
+            tid.append(t)
+            for part in parts:
+                for ring in part:
+                    xy.extend(ring)
+                    ro.append(len(xy))
+                pr.append(len(ro) - 1)
+            rp.append(len(pr) - 1)
+        T = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(device)
+        return InternalGeometryColumn(T(tid, np.int32), T(rp, np.int64), T(pr, np.int64), T(ro, np.int64),
+                                      T(np.array(xy, np.float64).reshape(-1, 2) if xy else np.zeros((1, 2)), np.float64))
 
 
 def grid_pointascellid(points, resolution, index_system=None, ctx=None, stream=None, stats=False):
     """grid_pointascellid (PointIndexGeom.scala:33-47): the cell of each row's centroid.
 
-    ``points``: a GeometryColumn (WKB / WKT POINT or MULTIPOINT rows decoded on the GPU;
-    null rows give cell 0 -- returned with the validity bitmap as (cells, valid)), an
-    (n, 2) float64 tensor, or an (x, y) pair (a point's centroid is the point itself,
-    MosaicGeometryJTS.scala:60-64).  Other geometry types raise MGPU_E_UNSUPPORTED, an
-    empty point IllegalStateException (JTS getX on an empty point)."""
+    ``points``: a GeometryColumn (WKB / HEX rows of any type, WKT / GeoJSON POINT or
+    MULTIPOINT rows, decoded on the GPU and reduced to JTS's centroid; null rows give
+    cell 0 -- returned with the validity bitmap as (cells, valid)), an
+    InternalGeometryColumn, an (n, 2) float64 tensor, or an (x, y) pair (a point's
+    centroid is the point itself, MosaicGeometryJTS.scala:60-64).  Types a format does
+    not build raise MGPU_E_UNSUPPORTED, an empty geometry IllegalStateException (JTS getX
+    on an empty point)."""
+    if isinstance(points, InternalGeometryColumn):
+        import ctypes
+        import torch
+        from .context import default_context
+        isys = index_system or _H3
+        res = isys.get_resolution(resolution)
+        dev = points.type_id.device
+        ctx = ctx or default_context(dev)
+        n = len(points)
+        cells = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        st = N.MgpuStats()
+        s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        N.check(N.lib().mgpu_internal_geometry_to_cells(ctx.handle, isys.code, res, n, points.type_id.data_ptr(),
+                                                        points.row_part.data_ptr(), points.part_ring.data_ptr(),
+                                                        points.ring_off.data_ptr(), points.xy.data_ptr(), None, 0,
+                                                        cells.data_ptr(), None, s, ctypes.byref(st)))
+        return (cells[:n], st.as_dict()) if stats else cells[:n]
     if isinstance(points, GeometryColumn):
         import ctypes
         import torch

@@ -114,7 +114,7 @@ def test_wkb_points():
     assert decode(N.MGPU_GEOM_WKB, wkb_point(float("nan"), float("nan")))[0] == 3  # POINT EMPTY
     assert decode(N.MGPU_GEOM_WKB, wkb_point(1.0, 2.0)[:-1])[0] == 1  # truncated
     assert decode(N.MGPU_GEOM_WKB, b"")[0] == 1
-    assert decode(N.MGPU_GEOM_WKB, struct.pack("<BII", 1, 3, 0))[0] == 2  # polygon: unsupported
+    assert decode(N.MGPU_GEOM_WKB, struct.pack("<BII", 1, 3, 0))[0] == 3  # POLYGON EMPTY
     pts = [(1.0, 2.0), (3.0, 5.0), (-4.0, 0.5)]
     mp = struct.pack("<BII", 1, 4, len(pts)) + b"".join(wkb_point(*p) for p in pts)
     st, x, y = decode(N.MGPU_GEOM_WKB, mp)
@@ -137,3 +137,174 @@ def test_wkt_points():
     st, x, y = decode(W, "MULTIPOINT (1 2, 3 5, 5 8)")
     assert st == 0 and (x, y) == (3.0, 5.0)
     assert decode(W, "MULTIPOINT EMPTY")[0] == 3
+
+
+# ---------------------------------------------------------------- centroids of any geometry
+# The reference takes JTS's Centroid of whatever the row holds (PointIndexGeom.scala:
+# 33-47); the oracle is oracle/jts_centroid.py's restatement of JTS 1.20 Centroid.
+import sys  # noqa: E402
+import os  # noqa: E402
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import jts_centroid as JC  # noqa: E402
+
+
+def _w_seq(bo, pts, z):
+    b = struct.pack(bo + "I", len(pts))
+    for p in pts:
+        b += struct.pack(bo + "dd", *p) + (struct.pack(bo + "d", 7.0) if z else b"")
+    return b
+
+
+def w_geom(kind, data, le=True, z=False):
+    """WKB of ('point', p) / ('line', pts) / ('poly', rings) / ('multi...', [parts]) /
+    ('collection', [(kind, data), ...])."""
+    bo = "<" if le else ">"
+    codes = {"point": 1, "line": 2, "poly": 3, "mpoint": 4, "mline": 5, "mpoly": 6, "collection": 7}
+    t = codes[kind] + (1000 if z else 0)
+    b = struct.pack(bo + "BI", 1 if le else 0, t)
+    if kind == "point":
+        return b + struct.pack(bo + "dd", *data) + (struct.pack(bo + "d", 7.0) if z else b"")
+    if kind == "line":
+        return b + _w_seq(bo, data, z)
+    if kind == "poly":
+        return b + struct.pack(bo + "I", len(data)) + b"".join(_w_seq(bo, r, z) for r in data)
+    sub = {"mpoint": "point", "mline": "line", "mpoly": "poly"}.get(kind)
+    parts = [(sub, d) for d in data] if sub else data
+    return b + struct.pack(bo + "I", len(parts)) + b"".join(w_geom(k, d, not le if kind == "collection" else le, z)
+                                                           for k, d in parts)
+
+
+def _star(rng, cx, cy, r, k, ccw=True):
+    ang = np.sort(rng.uniform(0, 2 * np.pi, k))
+    rad = rng.uniform(0.4 * r, r, k)
+    pts = [(float(cx + q * np.cos(a)), float(cy + q * np.sin(a))) for a, q in zip(ang, rad)]
+    pts.append(pts[0])
+    return pts if ccw else pts[::-1]
+
+
+def _random_geoms(seed, n):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        cx, cy = rng.uniform(-170, 170), rng.uniform(-80, 80)
+        kind = ["poly", "mpoly", "line", "mline", "mpoint", "collection", "point"][i % 7]
+        shell = _star(rng, cx, cy, rng.uniform(0.01, 2.0), int(rng.integers(3, 40)), bool(rng.random() < 0.5))
+        hole = _star(rng, cx, cy, 0.2 * abs(shell[0][0] - cx) + 1e-4, 6, bool(rng.random() < 0.5))
+        if kind == "poly":
+            out.append((kind, [shell, hole] if rng.random() < 0.5 else [shell]))
+        elif kind == "mpoly":
+            other = _star(rng, cx + 5, cy, 1.0, 9, bool(rng.random() < 0.5))
+            out.append((kind, [[shell, hole], [other]]))
+        elif kind == "line":
+            out.append((kind, shell[:-1]))
+        elif kind == "mline":
+            out.append((kind, [shell[:5], hole[:4]]))
+        elif kind == "mpoint":
+            out.append((kind, shell[:7]))
+        elif kind == "collection":
+            out.append((kind, [("point", shell[0]), ("line", hole[:4]), ("poly", [shell]),
+                               ("collection", [("mpoint", hole[:3])])]))
+        else:
+            out.append((kind, shell[0]))
+    return out
+
+
+def test_centroid_any_wkb_equals_jts_restatement():
+    """WKB of every type (both byte orders, ISO Z, nested collections) and the same rows
+    as hex text (upper / lower case): the decoder's centroid equals the JTS Centroid
+    restatement bit for bit."""
+    for le in (True, False):
+        for g in _random_geoms(11 if le else 12, 140):
+            w = w_geom(*g, le=le, z=(g[0] == "poly" and le))
+            want = JC.centroid_wkb(w)
+            st, x, y = decode(N.MGPU_GEOM_WKB, w)
+            assert st == 0 and (x, y) == want, (g[0], (x, y), want)
+            for hx in (w.hex(), w.hex().upper()):
+                assert decode(N.MGPU_GEOM_HEX, hx) == (0, x, y)
+
+
+def test_centroid_special_cases():
+    """Flat / degenerate rings, zero-length lines (their first point), empty members,
+    malformed rings and hex text."""
+    sq = [(0.0, 0.0), (2.0, 0.0), (2.0, 2.0), (0.0, 2.0), (0.0, 0.0)]
+    flat = [(0.0, 1.0), (3.0, 1.0), (1.0, 1.0), (0.0, 1.0)]  # zero area: the lines decide
+    for g in [("poly", [sq]), ("poly", [sq[::-1]]), ("poly", [flat]), ("line", [(1.0, 1.0), (1.0, 1.0)]),
+              ("mpoly", [[sq], [[(5.0, 5.0), (6.0, 5.0), (6.0, 6.0), (5.0, 5.0)]]]),
+              ("collection", [("poly", []), ("point", (3.0, 4.0))]),
+              ("mline", [[(0.0, 0.0), (3.0, 4.0)], [(1.0, 1.0), (1.0, 1.0)]])]:
+        w = w_geom(*g)
+        assert decode(N.MGPU_GEOM_WKB, w)[1:] == JC.centroid_wkb(w), g
+    assert decode(N.MGPU_GEOM_WKB, w_geom("poly", [sq]))[1:] == (1.0, 1.0)
+    assert decode(N.MGPU_GEOM_WKB, w_geom("collection", []))[0] == 3  # empty
+    assert decode(N.MGPU_GEOM_WKB, w_geom("line", [(1.0, 1.0)]))[0] == 1  # one-point line
+    assert decode(N.MGPU_GEOM_WKB, w_geom("poly", [sq[:-1]]))[0] == 1  # ring not closed
+    assert decode(N.MGPU_GEOM_WKB, w_geom("poly", [sq[:2] + sq[:1]]))[0] == 1  # a LinearRing needs 4 points
+    assert decode(N.MGPU_GEOM_HEX, w_geom("point", (1.0, 2.0)).hex() + "0")[0] == 0  # odd last char ignored
+    assert decode(N.MGPU_GEOM_HEX, "01zz")[0] == 1
+
+
+def test_hypot_port():
+    """StrictMath.hypot (fdlibm) as the decoder ports it: equal to the oracle's port, and
+    within an ulp of the exact value."""
+    from decimal import Decimal, getcontext
+    getcontext().prec = 60
+    rng = np.random.default_rng(3)
+    for a, b in zip(rng.standard_normal(400) * 10.0 ** rng.integers(-300, 300, 400), rng.standard_normal(400)):
+        h = JC.hypot(float(a), float(b))
+        exact = (Decimal(float(a)) ** 2 + Decimal(float(b)) ** 2).sqrt()
+        assert abs(Decimal(h) - exact) <= Decimal(np.spacing(h))
+
+
+def test_geojson_points():
+    J = N.MGPU_GEOM_GEOJSON
+    assert decode(J, '{"type": "Point", "coordinates": [-73.956758, 40.769978]}') == (0, -73.956758, 40.769978)
+    assert decode(J, '{"coordinates":[1,2,3],"type":"Point","crs":{"type":"name","properties":{"name":"x"}}}') == (0, 1.0, 2.0)
+    st, x, y = decode(J, '{"type":"MultiPoint","coordinates":[[1,2],[3,5],[5,8]]}')
+    assert st == 0 and (x, y) == (3.0, 5.0)
+    assert decode(J, '{"type":"Point","coordinates":[]}')[0] == 3
+    assert decode(J, '{"type":"MultiPoint","coordinates":[]}')[0] == 3
+    assert decode(J, '{"type":"Polygon","coordinates":[[[0,0],[1,0],[1,1],[0,0]]]}')[0] == 2
+    assert decode(J, '{"type":"Point","coordinates":[1]}')[0] == 1
+    assert decode(J, '{"type":"Blob"}')[0] == 1
+
+
+def _internal_rows(geoms):
+    """InternalGeometryType rows (type id, boundaries + holes) of the WKB test shapes."""
+    rows = []
+    for kind, d in geoms:
+        if kind == "point":
+            rows.append((1, [[[d]]]))
+        elif kind == "mpoint":
+            rows.append((2, [[list(d)]]))
+        elif kind == "line":
+            rows.append((3, [[list(d)]]))
+        elif kind == "mline":
+            rows.append((4, [[list(l)] for l in d]))
+        elif kind == "poly":
+            rows.append((5, [list(d)]))
+        elif kind == "mpoly":
+            rows.append((6, [list(p) for p in d]))
+    return rows
+
+
+def test_internal_geometry_centroids_equal_wkb():
+    """The InternalGeometryType layout gives the same centroid as the WKB of the same shape."""
+    geoms = [g for g in _random_geoms(13, 120) if g[0] != "collection"]
+    rows = _internal_rows(geoms)
+    tid, rp, pr, ro, xy = [], [0], [0], [0], []
+    for t, parts in rows:
+        tid.append(t)
+        for part in parts:
+            for ring in part:
+                xy.extend(ring)
+                ro.append(len(xy))
+            pr.append(len(ro) - 1)
+        rp.append(len(pr) - 1)
+    A = lambda a, dt: np.ascontiguousarray(a, dtype=dt)
+    tid, rp, pr, ro, xy = A(tid, np.int32), A(rp, np.int64), A(pr, np.int64), A(ro, np.int64), A(xy, np.float64)
+    n = len(tid)
+    x, y, st = np.zeros(n), np.zeros(n), np.zeros(n, np.int32)
+    P = lambda a: ctypes.c_void_p(a.ctypes.data)
+    N.check(N.lib().mgpu_test_internal_centroid(n, P(tid), P(rp), P(pr), P(ro), P(xy), P(x), P(y), P(st)))
+    for i, g in enumerate(geoms):
+        assert st[i] == 0 and (x[i], y[i]) == JC.centroid_wkb(w_geom(*g)), (i, g[0])

@@ -122,3 +122,34 @@ def test_pip_join_arrow_rejects_host_arrays(gpu, nyc_chips_r9):
     yc.struct.device_type = 1  # ARROW_DEVICE_CPU
     with pytest.raises(M.IllegalArgumentException):
         A.pip_join_arrow(xc, yc, d, 9)
+
+
+def test_centroids_of_any_geometry_on_gpu(gpu):
+    """Polygons (holes, both orientations), multipolygons, lines, collections as WKB, the
+    same rows as hex text, as Mosaic's InternalGeometryType layout, and GeoJSON points:
+    the device cells equal the oracle's cells of the JTS Centroid restatement
+    (oracle/jts_centroid.py); a POLYGON EMPTY row raises as getX on the empty centroid
+    (PointIndexBehaviors.scala:134-137)."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import jts_centroid as JC
+    from test_geom_host import _internal_rows, _random_geoms, w_geom
+    geoms = _random_geoms(21, 3000)
+    wkbs = [w_geom(*g, le=(i % 2 == 0)) for i, g in enumerate(geoms)]
+    cx, cy = np.array([JC.centroid_wkb(w) for w in wkbs]).T
+    for res in (5, 9, 12):
+        want = O.h3_points_to_cells(cx, cy, res)
+        got = M.grid_pointascellid(M.GeometryColumn.from_rows(wkbs, gpu), res).cpu().numpy()
+        assert np.array_equal(got, want), res
+        hexes = [w.hex() if i % 3 else w.hex().upper() for i, w in enumerate(wkbs)]
+        got = M.grid_pointascellid(M.GeometryColumn.from_rows(hexes, gpu, fmt="hex"), res).cpu().numpy()
+        assert np.array_equal(got, want), res
+    sel = [i for i, g in enumerate(geoms) if g[0] != "collection"]
+    col = M.InternalGeometryColumn.from_rows(_internal_rows([geoms[i] for i in sel]), gpu)
+    got = M.grid_pointascellid(col, 9).cpu().numpy()
+    assert np.array_equal(got, O.h3_points_to_cells(cx[sel], cy[sel], 9))
+    js = ['{"type": "Point", "coordinates": [%r, %r]}' % (float(a), float(b)) for a, b in zip(cx[:500], cy[:500])]
+    got = M.grid_pointascellid(M.GeometryColumn.from_rows(js, gpu, fmt="geojson"), 9).cpu().numpy()
+    assert np.array_equal(got, O.h3_points_to_cells(cx[:500], cy[:500], 9))
+    with pytest.raises(M.IllegalStateException):
+        M.grid_pointascellid(M.GeometryColumn.from_rows([struct.pack("<BII", 1, 3, 0)], gpu), 5)
