@@ -372,6 +372,11 @@ int32_t mgpu_test_h3_glibc_host(const double* lon, const double* lat, int64_t n,
 int32_t mgpu_test_h3_boundary_host(const int64_t* cells, int64_t n, double* out_lonlat, int32_t* out_nverts,
                                    double* out_center);
 int32_t mgpu_test_decode_point(int32_t format, const uint8_t* data, int64_t len, double* x, double* y);
+/* TEST ONLY (profiling): the last join's 16 workspace counters (pairs, near-ties, invalid
+ * points, candidates, ...; builds with -DMGPU_STAMPS add per-phase clock ticks of the
+ * join tiles at [10..14]).  Waits for the device. */
+int32_t mgpu_test_join_counters(mgpu_ctx* ctx, uint64_t* out16);
+
 /* TEST ONLY: the centroids of n InternalGeometryType rows (layout of
  * mgpu_internal_geometry_to_cells) on the host; status[i] 0 ok, 1 malformed, 2 unsupported,
  * 3 empty. */

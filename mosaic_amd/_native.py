@@ -40,7 +40,7 @@ EXPORTS = (
     "mgpu_geometry_to_cells_arrow", "mgpu_pip_join_arrow", "mgpu_test_parse_number", "mgpu_test_decode_point",
     "mgpu_test_h3_elementary_host", "mgpu_test_h3_route_host", "mgpu_test_h3_boundary_host",
     "mgpu_ctx_set_option", "mgpu_ctx_get_option", "mgpu_build_opts_default", "mgpu_chips_host_blob_ex",
-    "mgpu_test_h3_glibc_host", "mgpu_internal_geometry_to_cells", "mgpu_test_internal_centroid",
+    "mgpu_test_h3_glibc_host", "mgpu_internal_geometry_to_cells", "mgpu_test_internal_centroid", "mgpu_test_join_counters",
 )
 MGPU_GEOM_WKB = 0
 MGPU_GEOM_WKT = 1
@@ -172,6 +172,7 @@ def lib():
         "mgpu_internal_geometry_to_cells": (I32, [P, I32, I32, I64, P, P, P, P, P, P, I64, P, P, P,
                                                   ctypes.POINTER(MgpuStats)]),
         "mgpu_test_internal_centroid": (I32, [I64, P, P, P, P, P, P, P, P]),
+        "mgpu_test_join_counters": (I32, [P, P]),
     }
     for name, (rt, args) in sig.items():
         f = getattr(L, name)

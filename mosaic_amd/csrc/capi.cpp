@@ -62,8 +62,8 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // offsets, so a byte copy of the blob on another GPU (RCCL broadcast) is a
 // complete chip table there.
 constexpr uint64_t kBlobMagic = 0x4d4f534149434850ULL;  // "MOSAICHP"
-constexpr int kBlobArrays = 24;
-constexpr uint32_t kBlobVersion = 10;  // 9: 32-pixel rank words; 10: class -> first polygon
+constexpr int kBlobArrays = 23;
+constexpr uint32_t kBlobVersion = 9;  // 9: 32-pixel rank words
 struct BlobHeader {
   uint64_t magic;
   uint32_t version, hash_mask, max_probe, n_chips, n_cells;
@@ -144,7 +144,6 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.raster_bnx = h.raster_bnx;
   v.raster_bny = h.raster_bny;
   v.raster_blk = h.raster_bshift ? (const uint16_t*)(base + h.off[22]) : nullptr;
-  v.raster_cls_poly = (const int32_t*)(base + h.off[23]);
   return v;
 }
 
@@ -532,7 +531,6 @@ struct Raster {
   double x0 = 0, y0 = 0, inv_dx = 0, inv_dy = 0;
   std::vector<uint16_t> cells;
   std::vector<uint64_t> cls;
-  std::vector<int32_t> cls_poly;  // per class: the polygon of its first match (-1: none)
   uint32_t pc[4] = {0, 0, 0, 0};
   // second level: ref[pixel] = 1 + block of a refined mixed pixel (0: none); block b's
   // sub_n x sub_n sub-pixel classes at sub[b * sub_n^2 ..] (BNG: sub-pixel edge sub_w metres)
@@ -717,11 +715,6 @@ void raster_classes(const mgpu::ChipTableView& hv, const std::vector<uint64_t>& 
     }
     const int32_t c = cls_of[answer_key[v]];
     if (c >= 0) slot(i) = (uint16_t)c;
-  }
-  R.cls_poly.assign(R.cls.size(), -1);
-  for (size_t c = 1; c < R.cls.size(); c++) {
-    const uint64_t v = R.cls[c];
-    if (v >> 32) R.cls_poly[c] = hv.chip_poly[(uint32_t)v + __builtin_ctzll(v >> 32)];
   }
   auto pc = [](uint64_t v) { return __builtin_popcountll(v >> 32); };
   for (int k = 0; k < 4; k++) {
@@ -1670,7 +1663,6 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
       {raster.rank.data(), raster.rank.size() * sizeof(mgpu::RankWord), 0},
       {raster.sub.data(), raster.sub.size() * 2, 0},
       {raster.blk.data(), raster.blk.size() * 2, 0},
-      {raster.cls_poly.data(), raster.cls_poly.size() * 4, 0},
   };
   size_t total = kBlobHeaderBytes;
   BlobHeader hdr{};
@@ -2733,6 +2725,16 @@ int32_t mgpu_test_decode_point(int32_t format, const uint8_t* data, int64_t len,
     case MGPU_GEOM_GEOJSON: return mgpu::geom::json_centroid((const char*)data, len, x, y);
   }
   return mgpu::geom::kDecUnsupported;
+}
+
+int32_t mgpu_test_join_counters(mgpu_ctx* ctx, uint64_t* out16) {
+  if (!ctx || !out16) return fail(MGPU_E_INVALID_ARG, "bad arguments");
+  memset(out16, 0, 16 * 8);
+  if (!ctx->ws) return MGPU_OK;
+  if (int32_t st = set_device(ctx->device)) return st;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out16, ctx->ws, 16 * 8, hipMemcpyDeviceToHost));
+  return MGPU_OK;
 }
 
 int32_t mgpu_test_internal_centroid(int64_t n, const int32_t* type_id, const int64_t* row_part, const int64_t* part_ring,

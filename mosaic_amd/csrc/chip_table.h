@@ -172,7 +172,6 @@ struct ChipTableView {
                                // matches for raster_pc[k - 1] <= c < raster_pc[k] (k < 4)
   const uint16_t* raster;      // [ny * nx] classes
   const uint64_t* raster_cls;  // [classes]
-  const int32_t* raster_cls_poly;  // [classes] the polygon of the class's first match
   // second level: every mixed pixel p is cut into sub_n x sub_n sub-pixels whose classes
   // are raster_sub[b * sub_n^2 + v * sub_n + u], b = the number of mixed pixels before p
   // (lonlat: u = the truncated sub_n * fractional pixel position, clamped; BNG: (metres

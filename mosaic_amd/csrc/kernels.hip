@@ -1145,15 +1145,6 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
     if (IS == MGPU_H3) return t.raster_cls[(uint32_t)c];
     return (uint64_t)((uint32_t)c >> 8) | ((uint64_t)((uint32_t)c & 0xFFu) << 32);
   };
-  // an H3 class's pair count from its id (classes are ordered by match count, as
-  // classify_kernel counts them): no table load below the fifth threshold
-  auto pure_pairs = [&](uint32_t c) -> uint32_t {
-    return c < t.raster_pc[0]   ? 1u
-           : c < t.raster_pc[1] ? 2u
-           : c < t.raster_pc[2] ? 3u
-           : c < t.raster_pc[3] ? 4u
-                                : (uint32_t)__popc((uint32_t)(t.raster_cls[c] >> 32));
-  };
   uint32_t nmix = 0;
 #pragma unroll
   for (int k = 0; k < kClsItems; k++) nmix += code(k) == kMixed;
@@ -1166,7 +1157,7 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
     if (c == kMixed)
       npair += __popc((uint32_t)(a.mixed_res[c0 + r++] >> 32));
     else if (c != 0)
-      npair += IS == MGPU_H3 ? pure_pairs((uint32_t)c) : (uint32_t)__popc((uint32_t)c & 0xFFu);
+      npair += IS == MGPU_H3 ? (uint32_t)__popc((uint32_t)(pure(c) >> 32)) : (uint32_t)__popc((uint32_t)c & 0xFFu);
   }
   uint32_t total;
   const uint32_t off0 = chunk_excl_scan(npair, s_w[1], &total);
@@ -1178,15 +1169,6 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
 #pragma unroll
       for (int k = 0; k < kClsItems; k++) {
         const Code c = code(k);
-        if (IS == MGPU_H3 && c != 0 && (uint32_t)c < t.raster_pc[0]) {
-          // one match: the class's polygon in one load
-          if (q >= w0 && q < w0 + kEmitWin) {
-            s_poly[q - w0] = (uint32_t)t.raster_cls_poly[(uint32_t)c];
-            s_pt[q - w0] = (uint16_t)(threadIdx.x * kClsItems + k);
-          }
-          q++;
-          continue;
-        }
         uint64_t v = 0;
         if (c == kMixed)
           v = a.mixed_res[c0 + r++];
