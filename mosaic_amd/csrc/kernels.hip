@@ -181,15 +181,29 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 #endif
 constexpr int kCandCap = MGPU_CANDCAP;
 constexpr int kMixCap = kTile / 2;  // mixed-cell candidates (phase 2b), after the list in s_buf
+// Candidates whose point coordinates phase 1 leaves in LDS (the rest re-read them in
+// phases 2 / 2b), per join_tile mode -- A/B r3 (profiles/r3_stash_ab.txt): the fused
+// kernel 320 (BNG res 3's 1.25 candidates per point re-read most coordinates at 80:
+// C4 r3 join 3.69 -> 2.80 ms, r4 1.75 -> 1.73), the binned join 160 (C3 3.29 -> 3.17),
+// the split pipeline's mixed tiles 80 (160 and more: C5 +4%)
+#ifndef MGPU_STASH_FUSED
+#define MGPU_STASH_FUSED 320
+#endif
+#ifndef MGPU_STASH_BINNED
+#define MGPU_STASH_BINNED 160
+#endif
+#ifndef MGPU_STASH_MIXED
+#define MGPU_STASH_MIXED 80
+#endif
+template <int G>
+constexpr int stash_of() {
+  return G == 2 ? MGPU_STASH_MIXED : G == 1 ? MGPU_STASH_BINNED : MGPU_STASH_FUSED;
+}
 #ifndef MGPU_OUTCAP
-#define MGPU_OUTCAP 448
+#define MGPU_OUTCAP 1072
 #endif
-constexpr int kOutCap = MGPU_OUTCAP;  // pairs a tile stages in LDS
-#ifndef MGPU_STASH
-#define MGPU_STASH 80
-#endif
-constexpr int kStash = MGPU_STASH;  // candidates whose coordinates phase 1 leaves in LDS
-static_assert(kCandCap * 2 + kMixCap * 2 + kStash * 16 <= kOutCap * 6, "phase 1-2 lists fit the staging buffer");
+constexpr int kOutCap = MGPU_OUTCAP;  // pairs a tile stages in LDS (the fused lists' bytes)
+static_assert(kCandCap * 2 + kMixCap * 2 + stash_of<0>() * 16 <= kOutCap * 6, "phase 1-2 lists fit the staging buffer");
 constexpr int kMaskBits = 32;
 // A tile reserves kSlot records in its slot; more go to the overflow pool.
 constexpr int kSlot = 2 * kTile;
@@ -343,7 +357,7 @@ __device__ __forceinline__ bool chip_is_core(const ChipTableView& t, const Range
 // Phase 1 for one point: its core chips match at once; every border chip becomes a
 // candidate (chip, point, slot j) in the tile's LDS list (a full list: the fast kernel
 // abandons the tile, the fix kernel evaluates the candidate on the spot).
-template <bool SLOW, int CAND_CAP = kCandCap>
+template <bool SLOW, int CAND_CAP, int STASH>
 __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, const Range& r, double px, double py,
                                             bool& any_tie, uint32_t* s_ncand, uint16_t* s_cand_pj,
                                             double2* s_cand_xy, uint32_t* s_first, uint16_t* s_cnt,
@@ -364,7 +378,7 @@ __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, cons
       const uint32_t j = __builtin_ctz(b);
       if (j0 < (uint32_t)CAND_CAP) {
         s_cand_pj[j0] = (uint16_t)(li | (j << 10));
-        if (j0 < (uint32_t)kStash) s_cand_xy[j0] = make_double2(px, py);
+        if (j0 < (uint32_t)STASH) s_cand_xy[j0] = make_double2(px, py);
       } else if (!SLOW) {
         any_tie = true;  // list full: the fix kernel evaluates such tiles
       } else if (pip::chip_contains_strips(t, r.first + j, px, py)) {
@@ -425,6 +439,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   __shared__ uint16_t s_cnt[kTile];     // chips of the point's cell (0: none)
   // phases 1-2: candidate list; phase 3: output staging (same bytes)
   constexpr int kCap = G ? kGCandCap : kCandCap, kMix = G ? kGMixCap : kMixCap;
+  constexpr int kStash = stash_of<G>();
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[G ? kStash * 16 + kCap * 2 + kMix * 2 : kOutCap * 6];
   // candidate c = chip s_first[li] + j of point li, s_cand_pj[c] = li | j << 10; the
   // first kStash candidates also keep the point's coordinates (no re-read in phase 2)
@@ -557,7 +572,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         Range r = chip_probe<IS, SLOW>(a, base + li, px, py, &ok, &tie, &gi);
         if (gi != kNoEntry) r = grid_range(t.grid[gi]);
         any_tie |= tie;
-        phase1_item<SLOW, kCap>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
+        phase1_item<SLOW, kCap, kStash>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
       }
     }
   } else if (IS == MGPU_H3 && !SLOW && MGPU_P1_BATCH) {
@@ -601,7 +616,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         px = a.x[MGPU_PT(li)];
         py = a.y[MGPU_PT(li)];
       }
-      phase1_item<SLOW, kCap>(t, li, r[k], px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
+      phase1_item<SLOW, kCap, kStash>(t, li, r[k], px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
     }
   } else if (IS == MGPU_BNG) {
     // the cell is a few integer ops: the lane's four points load together, then
@@ -636,7 +651,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
       if (gi[k] != kNoEntry) r[k] = grid_range(ge[k]);
-      phase1_item<SLOW, kCap>(t, k * kBlock + threadIdx.x, r[k], bx[k], by[k], any_tie, &s_ncand, s_cand_pj,
+      phase1_item<SLOW, kCap, kStash>(t, k * kBlock + threadIdx.x, r[k], bx[k], by[k], any_tie, &s_ncand, s_cand_pj,
                         s_cand_xy, s_first, s_cnt, s_mask);
     }
   } else {
@@ -665,7 +680,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         any_bad |= !ok;
         any_tie |= tie;
       }
-      phase1_item<SLOW, kCap>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
+      phase1_item<SLOW, kCap, kStash>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
     }
   }
   count_wave(&a.counters[2], any_bad);
@@ -923,8 +938,8 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 
 // One workgroup per tile (a persistent grid walking the tiles measured 25% slower in
 // round 1: workgroups that carry a tile of real work hide their dispatch).
-// 8 waves per SIMD: the tile's LDS (~4.7 KB) allows 32 workgroups per CU, and the
-// kernel is held to 64 VGPRs (it is latency-bound: the 8th wave measured -7% on C2,
+// 8 waves per SIMD: the kernel is held to 64 VGPRs (the fused tile's LDS, ~9 KB with its
+// 320-candidate stash, allows 17 workgroups per CU; the binned tile's ~7 KB, 22) (it is latency-bound: the 8th wave measured -7% on C2,
 // -10% on C5)
 #ifndef MGPU_WAVES_PER_EU
 #define MGPU_WAVES_PER_EU 8

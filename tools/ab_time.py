@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--configs", default="c2,c4,c5")
     ap.add_argument("--points", type=int, default=100_000_000)
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--res", type=int, default=None)
     a = ap.parse_args()
     import mosaic_amd as M
     import bench as B
@@ -27,7 +28,7 @@ def main():
     ctx = M.default_context(dev)
     ctx.reserve(a.points)
     for c in a.configs.split(","):
-        ns = argparse.Namespace(config=c, res=None, seed=0x20250314, points=a.points)
+        ns = argparse.Namespace(config=c, res=a.res, seed=0x20250314, points=a.points)
         wl = B.workload(ns, W, M)
         chips = M.tessellate(wl["polygons"], wl["isys"], ns.res).upload(ctx)
         x, y = wl["points"](a.points, 0, dev)
