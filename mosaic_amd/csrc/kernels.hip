@@ -181,13 +181,15 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 #endif
 constexpr int kCandCap = MGPU_CANDCAP;
 constexpr int kMixCap = kTile / 2;  // mixed-cell candidates (phase 2b), after the list in s_buf
-// Candidates whose point coordinates phase 1 leaves in LDS (the rest re-read them in
-// phases 2 / 2b), per join_tile mode -- A/B r3 (profiles/r3_stash_ab.txt): the fused
-// kernel 320 (BNG res 3's 1.25 candidates per point re-read most coordinates at 80:
-// C4 r3 join 3.69 -> 2.80 ms, r4 1.75 -> 1.73), the binned join 160 (C3 3.29 -> 3.17),
-// the split pipeline's mixed tiles 80 (160 and more: C5 +4%)
+// Coordinates phase 1 leaves in LDS for phases 2 / 2b (the rest are re-read), per
+// join_tile mode -- A/B r3 (profiles/r3_stash_ab.txt): the fused kernel keeps every
+// point with a candidate (BNG res 3's 1.25 candidates per point re-read most coordinates
+// with 80 candidate entries: C4 r3 join 3.69 ms per 1e8, 320 entries 2.78, per point
+// 2.55; r4 1.75 / 1.71 / 1.67); the binned join the first 160 candidates (C3 3.29 ->
+// 3.17; 256 and more cost it occupancy), the split pipeline's mixed tiles 80 (160 and
+// more: C5 +4%)
 #ifndef MGPU_STASH_FUSED
-#define MGPU_STASH_FUSED 320
+#define MGPU_STASH_FUSED 0
 #endif
 #ifndef MGPU_STASH_BINNED
 #define MGPU_STASH_BINNED 160
@@ -195,12 +197,18 @@ constexpr int kMixCap = kTile / 2;  // mixed-cell candidates (phase 2b), after t
 #ifndef MGPU_STASH_MIXED
 #define MGPU_STASH_MIXED 80
 #endif
+// (MGPU_STASH_FUSED 0: the fused kernel keeps EVERY point of the tile that has a
+// candidate, by point -- kTile entries, no re-read at all)
 template <int G>
 constexpr int stash_of() {
-  return G == 2 ? MGPU_STASH_MIXED : G == 1 ? MGPU_STASH_BINNED : MGPU_STASH_FUSED;
+  return G == 2 ? MGPU_STASH_MIXED : G == 1 ? MGPU_STASH_BINNED : (MGPU_STASH_FUSED ? MGPU_STASH_FUSED : kTile);
+}
+template <int G>
+constexpr bool point_stash() {
+  return G == 0 && MGPU_STASH_FUSED == 0;
 }
 #ifndef MGPU_OUTCAP
-#define MGPU_OUTCAP 1072
+#define MGPU_OUTCAP 896
 #endif
 constexpr int kOutCap = MGPU_OUTCAP;  // pairs a tile stages in LDS (the fused lists' bytes)
 static_assert(kCandCap * 2 + kMixCap * 2 + stash_of<0>() * 16 <= kOutCap * 6, "phase 1-2 lists fit the staging buffer");
@@ -357,7 +365,7 @@ __device__ __forceinline__ bool chip_is_core(const ChipTableView& t, const Range
 // Phase 1 for one point: its core chips match at once; every border chip becomes a
 // candidate (chip, point, slot j) in the tile's LDS list (a full list: the fast kernel
 // abandons the tile, the fix kernel evaluates the candidate on the spot).
-template <bool SLOW, int CAND_CAP, int STASH>
+template <bool SLOW, int CAND_CAP, int STASH, bool PT_STASH = false>
 __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, const Range& r, double px, double py,
                                             bool& any_tie, uint32_t* s_ncand, uint16_t* s_cand_pj,
                                             double2* s_cand_xy, uint32_t* s_first, uint16_t* s_cnt,
@@ -372,13 +380,14 @@ __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, cons
     if (t.chip_flags[r.first + j] & kChipCore) border &= ~(1u << j);
   uint32_t mask = lowm & ~border;
   if (border) {
+    if (PT_STASH) s_cand_xy[li] = make_double2(px, py);
     const uint32_t nb = __popc(border);
     uint32_t j0 = atomicAdd(s_ncand, nb);
     for (uint32_t b = border; b; b &= b - 1) {
       const uint32_t j = __builtin_ctz(b);
       if (j0 < (uint32_t)CAND_CAP) {
         s_cand_pj[j0] = (uint16_t)(li | (j << 10));
-        if (j0 < (uint32_t)STASH) s_cand_xy[j0] = make_double2(px, py);
+        if (!PT_STASH && j0 < (uint32_t)STASH) s_cand_xy[j0] = make_double2(px, py);
       } else if (!SLOW) {
         any_tie = true;  // list full: the fix kernel evaluates such tiles
       } else if (pip::chip_contains_strips(t, r.first + j, px, py)) {
@@ -572,7 +581,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         Range r = chip_probe<IS, SLOW>(a, base + li, px, py, &ok, &tie, &gi);
         if (gi != kNoEntry) r = grid_range(t.grid[gi]);
         any_tie |= tie;
-        phase1_item<SLOW, kCap, kStash>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
+        phase1_item<SLOW, kCap, kStash, point_stash<G>()>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
       }
     }
   } else if (IS == MGPU_H3 && !SLOW && MGPU_P1_BATCH) {
@@ -616,7 +625,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         px = a.x[MGPU_PT(li)];
         py = a.y[MGPU_PT(li)];
       }
-      phase1_item<SLOW, kCap, kStash>(t, li, r[k], px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
+      phase1_item<SLOW, kCap, kStash, point_stash<G>()>(t, li, r[k], px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
     }
   } else if (IS == MGPU_BNG) {
     // the cell is a few integer ops: the lane's four points load together, then
@@ -651,7 +660,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
       if (gi[k] != kNoEntry) r[k] = grid_range(ge[k]);
-      phase1_item<SLOW, kCap, kStash>(t, k * kBlock + threadIdx.x, r[k], bx[k], by[k], any_tie, &s_ncand, s_cand_pj,
+      phase1_item<SLOW, kCap, kStash, point_stash<G>()>(t, k * kBlock + threadIdx.x, r[k], bx[k], by[k], any_tie, &s_ncand, s_cand_pj,
                         s_cand_xy, s_first, s_cnt, s_mask);
     }
   } else {
@@ -680,7 +689,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         any_bad |= !ok;
         any_tie |= tie;
       }
-      phase1_item<SLOW, kCap, kStash>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
+      phase1_item<SLOW, kCap, kStash, point_stash<G>()>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
     }
   }
   count_wave(&a.counters[2], any_bad);
@@ -716,8 +725,8 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     const uint32_t ch = s_first[li] + (pj >> 10);
     const int64_t p = MGPU_PT(li);
     double px, py;
-    if (c < (uint32_t)kStash) {
-      const double2 q = s_cand_xy[c];
+    if (point_stash<G>() || c < (uint32_t)kStash) {
+      const double2 q = s_cand_xy[point_stash<G>() ? (uint32_t)li : c];
       px = q.x;
       py = q.y;
     } else {
@@ -763,8 +772,8 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     const uint32_t ch = s_first[li] + (pj >> 10);
     const int64_t p = MGPU_PT(li);
     double px, py;
-    if (c < (uint32_t)kStash) {
-      const double2 q = s_cand_xy[c];
+    if (point_stash<G>() || c < (uint32_t)kStash) {
+      const double2 q = s_cand_xy[point_stash<G>() ? (uint32_t)li : c];
       px = q.x;
       py = q.y;
     } else {
@@ -938,8 +947,8 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 
 // One workgroup per tile (a persistent grid walking the tiles measured 25% slower in
 // round 1: workgroups that carry a tile of real work hide their dispatch).
-// 8 waves per SIMD: the kernel is held to 64 VGPRs (the fused tile's LDS, ~9 KB with its
-// 320-candidate stash, allows 17 workgroups per CU; the binned tile's ~7 KB, 22) (it is latency-bound: the 8th wave measured -7% on C2,
+// 8 waves per SIMD: the kernel is held to 64 VGPRs (the fused tile's LDS, ~8 KB with its
+// per-point stash, allows 20 workgroups per CU; the binned tile's ~7 KB, 22) (it is latency-bound: the 8th wave measured -7% on C2,
 // -10% on C5)
 #ifndef MGPU_WAVES_PER_EU
 #define MGPU_WAVES_PER_EU 8
