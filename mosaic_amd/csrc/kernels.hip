@@ -173,9 +173,6 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 // candidates are abandoned by the streaming kernel after phase 1 and redone by
 // pip_fix_kernel, which evaluates list overflows on the spot and chips past the
 // 32nd of a cell in phase 3.
-#ifndef MGPU_P1_BATCH
-#define MGPU_P1_BATCH 0
-#endif
 #ifndef MGPU_CANDCAP
 #define MGPU_CANDCAP 512  // (256: BNG res 3's 1.25 candidates per point sent most tiles to the fix kernel)
 #endif
@@ -583,49 +580,6 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         any_tie |= tie;
         phase1_item<SLOW, kCap, kStash, point_stash<G>()>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
       }
-    }
-  } else if (IS == MGPU_H3 && !SLOW && MGPU_P1_BATCH) {
-    // all four projections first, then the four grid entries in flight together (the
-    // one-ahead form below waits for each entry before projecting the next point)
-    double bx[kItems], by[kItems];
-#pragma unroll
-    for (int k = 0; k < kItems; k++) {
-      const int li = k * kBlock + threadIdx.x;
-      bx[k] = by[k] = 0.0;
-      if (MGPU_VALID(li)) {
-        const int64_t p = MGPU_PT(li);
-        // (mode 2 reads the points again after the probes: cached loads)
-        bx[k] = MGPU_P1_BATCH == 2 ? a.x[p] : MGPU_LDPT(&a.x[p]);
-        by[k] = MGPU_P1_BATCH == 2 ? a.y[p] : MGPU_LDPT(&a.y[p]);
-      }
-    }
-    Range r[kItems];
-    uint32_t gi[kItems];
-#pragma unroll
-    for (int k = 0; k < kItems; k++) {
-      r[k] = Range{0, 0, 0};
-      gi[k] = kNoEntry;
-      const int li = k * kBlock + threadIdx.x;
-      if (MGPU_VALID(li) && pt_valid(a.valid, a.valid_off, MGPU_PT(li))) {
-        bool ok, tie;
-        r[k] = chip_probe<IS, SLOW>(a, MGPU_PT(li), bx[k], by[k], &ok, &tie, &gi[k]);
-        any_bad |= !ok;
-        any_tie |= tie;
-      }
-    }
-    uint64_t ge[kItems];
-#pragma unroll
-    for (int k = 0; k < kItems; k++) ge[k] = gi[k] != kNoEntry ? t.grid[gi[k]] : 0;
-#pragma unroll
-    for (int k = 0; k < kItems; k++) {
-      if (gi[k] != kNoEntry) r[k] = grid_range(ge[k]);
-      const int li = k * kBlock + threadIdx.x;
-      double px = bx[k], py = by[k];
-      if (MGPU_P1_BATCH == 2 && r[k].count) {
-        px = a.x[MGPU_PT(li)];
-        py = a.y[MGPU_PT(li)];
-      }
-      phase1_item<SLOW, kCap, kStash, point_stash<G>()>(t, li, r[k], px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
     }
   } else if (IS == MGPU_BNG) {
     // the cell is a few integer ops: the lane's four points load together, then
