@@ -185,6 +185,9 @@ constexpr int kMixCap = kTile / 2;  // mixed-cell candidates (phase 2b), after t
 // 2.55; r4 1.75 / 1.71 / 1.67); the binned join the first 160 candidates (C3 3.29 ->
 // 3.17; 256 and more cost it occupancy), the split pipeline's mixed tiles 80 (160 and
 // more: C5 +4%)
+#ifndef MGPU_SPLIT_WALK
+#define MGPU_SPLIT_WALK 1  // (A/B r3, profiles/r3_split_walk_ab.txt: C3 binned join -3.8%, C4 r4 -1.6%)
+#endif
 #ifndef MGPU_STASH_FUSED
 #define MGPU_STASH_FUSED 0
 #endif
@@ -718,6 +721,45 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   const uint32_t nmix = s_nmix < (uint32_t)kMix ? s_nmix : (uint32_t)kMix;
 #ifdef MGPU_STATS
   uint32_t st_edges = 0;
+#endif
+#if MGPU_SPLIT_WALK
+  // few walks (binned tiles: ~16): a group of 4 (<= 16 walks) or 2 (<= 32) lanes shares
+  // each walk, every lane taking every L-th block of the strip's edges; the partial
+  // ring bits combine by OR / XOR across the group
+  if (!SLOW && kBlock == 64 && nmix > 0 && nmix <= 32) {
+    const uint32_t lg = nmix <= 16 ? 2u : 1u;
+    const uint32_t lane = threadIdx.x, m = lane >> lg, sub = lane & ((1u << lg) - 1u);
+    uint32_t bnd = 0, par = 0, pj = 0, ch = 0;
+    int li = 0;
+    bool one = false;
+    uint8_t fl = 0;
+    double px = 0.0, py = 0.0;
+    if (m < nmix) {
+      const uint32_t c = s_mix[m];
+      pj = s_cand_pj[c];
+      li = pj & 1023;
+      ch = s_first[li] + (pj >> 10);
+      if (point_stash<G>() || c < (uint32_t)kStash) {
+        const double2 q = s_cand_xy[point_stash<G>() ? (uint32_t)li : c];
+        px = q.x;
+        py = q.y;
+      } else {
+        px = a.x[MGPU_PT(li)];
+        py = a.y[MGPU_PT(li)];
+      }
+      const ChipHdr& H = t.chip_hdr[ch];
+      const uint32_t strip = H.strip_base + (uint32_t)strip_of(py, H.env[1], H.inv_h, (int)H.n_strips);
+      one = H.single_ring != 0;
+      fl = H.flags;
+      pip::strip_bits(t, strip, one, px, py, sub * MGPU_EDGE_STEP, MGPU_EDGE_STEP << lg, &bnd, &par);
+    }
+    for (uint32_t o = 1; o < (1u << lg); o <<= 1) {
+      bnd |= (uint32_t)__shfl_xor((int)bnd, (int)o);
+      par ^= (uint32_t)__shfl_xor((int)par, (int)o);
+    }
+    if (m < nmix && sub == 0 && pip::strip_verdict(t, ch, one, fl, bnd, par, px, py))
+      atomicOr(&s_mask[li], 1u << (pj >> 10));
+  } else
 #endif
   for (uint32_t m = threadIdx.x; m < nmix; m += kBlock) {
     const uint32_t c = s_mix[m];

@@ -237,8 +237,13 @@ MGPU_HDI bool chip_contains_mixed(const ChipTableView& t, uint32_t c, double px,
   return chip_contains_strip(t, c, H.strip_base + (uint32_t)s, H.single_ring != 0, H.flags, px, py, stat_edges);
 }
 
-MGPU_HDI bool chip_contains_strip(const ChipTableView& t, uint32_t c, uint32_t strip, bool one_ring, uint8_t fl,
-                                  double px, double py, uint32_t* stat_edges) {
+// RayCrossingCounter over the edges of strip `strip` (MGPU_EDGE_STEP records in flight
+// per step): the blocks of MGPU_EDGE_STEP edges first, first + stride, ... (in edges; a
+// lane group splitting one walk takes first = lane * STEP, stride = lanes * STEP), each
+// ring's boundary / parity bits OR-ed / XOR-ed into *bnd / *par -- order-free, so the
+// lanes' partial bits combine by OR / XOR.
+MGPU_HDI void strip_bits(const ChipTableView& t, uint32_t strip, bool one_ring, double px, double py, uint32_t first,
+                         uint32_t stride, uint32_t* bnd_out, uint32_t* par_out, uint32_t* stat_edges = nullptr) {
   const uint32_t eb = t.strip_edge[strip], ee = t.strip_edge[strip + 1];
   if (stat_edges) *stat_edges = ee - eb;
   const double4* E4 = (const double4*)t.edges;
@@ -246,7 +251,7 @@ MGPU_HDI bool chip_contains_strip(const ChipTableView& t, uint32_t c, uint32_t s
 #ifndef MGPU_EDGE_STEP
 #define MGPU_EDGE_STEP 2
 #endif
-  for (uint32_t e = eb; e < ee; e += MGPU_EDGE_STEP) {
+  for (uint32_t e = eb + first; e < ee; e += stride) {
     const uint32_t l = ee - 1;
     int bits[MGPU_EDGE_STEP];
     double4 R[MGPU_EDGE_STEP];
@@ -263,6 +268,14 @@ MGPU_HDI bool chip_contains_strip(const ChipTableView& t, uint32_t c, uint32_t s
       if (bits[k] & 2) par ^= rb;
     }
   }
+  *bnd_out = bnd;
+  *par_out = par;
+}
+
+// PointLocator over the rings' RayCrossingCounter verdicts (strip_bits of the point's
+// strip): contains() of chip c
+MGPU_HDI bool strip_verdict(const ChipTableView& t, uint32_t c, bool one_ring, uint8_t fl, uint32_t bnd, uint32_t par,
+                            double px, double py) {
   // one polygon, one ring (its envelope is the chip's): RayCrossingCounter's verdict
   if (one_ring) return !(bnd & 1) && (par & 1);
   const uint32_t pb = t.chip_part[c], pe = t.chip_part[c + 1];
@@ -298,6 +311,13 @@ MGPU_HDI bool chip_contains_strip(const ChipTableView& t, uint32_t c, uint32_t s
   if (!(fl & kChipMulti)) return single == kInterior;
   if (n_bnd & 1) return false;
   return n_bnd > 0 || is_in;
+}
+
+MGPU_HDI bool chip_contains_strip(const ChipTableView& t, uint32_t c, uint32_t strip, bool one_ring, uint8_t fl,
+                                  double px, double py, uint32_t* stat_edges) {
+  uint32_t bnd, par;
+  strip_bits(t, strip, one_ring, px, py, 0, MGPU_EDGE_STEP, &bnd, &par, stat_edges);
+  return strip_verdict(t, c, one_ring, fl, bnd, par, px, py);
 }
 
 // Geometry.contains(point) for sorted chip `c` -- the same decision as chip_locate()
