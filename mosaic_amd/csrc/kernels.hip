@@ -727,7 +727,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   // each walk, every lane taking every L-th block of the strip's edges; the partial
   // ring bits combine by OR / XOR across the group
   if (!SLOW && kBlock == 64 && nmix > 0 && nmix <= 32) {
-    const uint32_t lg = nmix <= 16 ? 2u : 1u;
+    const uint32_t lg = nmix <= 16 ? 2u : 1u;  // (8 lanes at <= 8 walks: no gain, r3)
     const uint32_t lane = threadIdx.x, m = lane >> lg, sub = lane & ((1u << lg) - 1u);
     uint32_t bnd = 0, par = 0, pj = 0, ch = 0;
     int li = 0;
