@@ -7,8 +7,8 @@ TAG=${1:-t}
 CFG=${2:-c2}
 OUT=gpurun_out/traffic_$TAG; mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/join_fetch -o run -- python3 -u tools/join_once.py --config $CFG > $OUT/join_fetch.log 2>&1 &&
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/join_write -o run -- python3 -u tools/join_once.py --config $CFG > $OUT/join_write.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/join_fetch -o run -- python3 -u tools/join_once.py --config $CFG --cache /tmp/mgpu_cache_$CFG.npz > $OUT/join_fetch.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/join_write -o run -- python3 -u tools/join_once.py --config $CFG --cache /tmp/mgpu_cache_$CFG.npz > $OUT/join_write.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/bng_fetch -o run -- python3 -u tools/join_once.py --cells --bng > $OUT/bng_fetch.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/bng_write -o run -- python3 -u tools/join_once.py --cells --bng > $OUT/bng_write.log 2>&1
 rc=$?
