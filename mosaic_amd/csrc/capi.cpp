@@ -2077,7 +2077,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
       return o_;
     };
     const size_t o_perm = carve((size_t)n * 4), o_rorig = carve((size_t)n * 8);
-    const size_t o_bx = carve((size_t)n * 8), o_by = carve((size_t)n * 8), o_slot = carve((size_t)n * 4),
+    const size_t o_bx = carve((size_t)n * 8), o_by = carve((size_t)n * 8),
                  o_pre = carve((size_t)K * nb * 4), o_res = carve((size_t)nc * C * 8), o_cnt = carve((size_t)K * nb * 4),
                  o_gs = carve((size_t)G * nb * 4), o_pairs = carve(nc * 4), o_off = carve(nc * 8),
                  o_gperm = carve(nc * 4), o_gcand = carve(nc * 4);
@@ -2093,7 +2093,6 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     ba.y = y;
     ba.bx = (double*)(bb + o_bx);
     ba.by = (double*)(bb + o_by);
-    ba.slot = (uint32_t*)(bb + o_slot);
     ba.pre = (uint32_t*)(bb + o_pre);
     ba.perm = (uint32_t*)(bb + o_perm);
     ba.res = (uint64_t*)(bb + o_rorig);

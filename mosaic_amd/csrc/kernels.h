@@ -91,8 +91,8 @@ hipError_t launch_split_emit(int is, const SplitArgs& a, hipStream_t s);
 // by bin instead of at random, then the answers are gathered back into input order.
 //   bin_hist_kernel     per chunk of bin_chunk() points: the chunk's bin counts
 //   bin_colscan_kernel  + bin_base_kernel: counts -> run offsets (bin-major, chunk-minor)
-//   bin_scatter_kernel  x, y -> their binned slots (sorted by bin in LDS, written as runs);
-//                       slot[i] kept for the gather
+//   bin_scatter_kernel  x, y -> their binned slots (sorted by bin in LDS, written as runs),
+//                       perm[slot] = the input position
 //   pip_binned_kernel   join_tile's phases over the binned points, tiles dealt to the XCDs
 //                       in contiguous runs (one bin's chips stay in one L2); answers
 //                       (first chip | match mask << 32) per slot in j.mixed_res
@@ -108,7 +108,6 @@ struct BinArgs {
   const double* y;
   double* bx;                       // [n] binned copies
   double* by;
-  uint32_t* slot;                   // [n] binned slot of input point i
   uint32_t* perm;                   // [n] input point of binned slot s
   uint64_t* res;                    // [n] the answers (first chip | match mask << 32) in input order
   uint32_t* cnt;                    // [bin chunks * nb] bin counts per chunk of bin_chunk() points

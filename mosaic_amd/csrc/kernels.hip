@@ -1944,7 +1944,7 @@ __device__ __forceinline__ uint32_t bin_at(const uint32_t* s_loc, int nb, uint32
 }
 
 // Per chunk: each point's rank among the chunk's points of its bin (LDS atomics -- any
-// order inside a bin will do: perm[slot] and slot[i] record where each point went), the
+// order inside a bin will do: perm[slot] records where each point came from), the
 // chunk's points sorted by bin in LDS, then written as contiguous runs (one per bin) by
 // consecutive lanes: whole cache lines, not one scattered 8-byte store per point.
 __global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
@@ -1981,7 +1981,6 @@ __global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
       lps[q] = s_loc[bi] + r;
       s_val[lps[q]] = px[q];
       s_li[lps[q]] = (uint16_t)(q * kBinBlock + threadIdx.x);
-      b.slot[p] = s_off[bi] + r;
     }
   }
   __syncthreads();
