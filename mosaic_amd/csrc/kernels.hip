@@ -2288,7 +2288,10 @@ int64_t join_tiles(int64_t n) { return (n + kTile - 1) / kTile; }
 int64_t join_tile_points() { return kTile; }
 int64_t join_slot_records() { return kSlot; }
 
-constexpr int64_t kFixGrid = 8192;   // fix-kernel workgroups (one wave each; idle ones exit at once)
+#ifndef MGPU_FIX_GRID
+#define MGPU_FIX_GRID 8192
+#endif
+constexpr int64_t kFixGrid = MGPU_FIX_GRID;  // fix-kernel workgroups (one wave each; idle ones exit at once)
 hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s, hipEvent_t after_stream) {
   if (a.n_tiles <= 0) return hipSuccess;
   // BNG has no near-ties, but its tiles still go dirty on a cell of more than 32
