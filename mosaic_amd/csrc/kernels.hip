@@ -185,6 +185,16 @@ constexpr int kMixCap = kTile / 2;  // mixed-cell candidates (phase 2b), after t
 // 2.55; r4 1.75 / 1.71 / 1.67); the binned join the first 160 candidates (C3 3.29 ->
 // 3.17; 256 and more cost it occupancy), the split pipeline's mixed tiles 80 (160 and
 // more: C5 +4%)
+// intermediate arrays written once and read once by a later kernel (classify codes, the
+// binned coordinates / perm, the gathered answers): non-temporal stores (A/B r3)
+#ifndef MGPU_NT_INTER
+#define MGPU_NT_INTER 0
+#endif
+#if MGPU_NT_INTER
+#define MGPU_ST_INTER(v, ptr) __builtin_nontemporal_store((v), (ptr))
+#else
+#define MGPU_ST_INTER(v, ptr) (*(ptr) = (v))
+#endif
 #ifndef MGPU_SPLIT_WALK
 #define MGPU_SPLIT_WALK 1  // (A/B r3, profiles/r3_split_walk_ab.txt: C3 binned join -3.8%, C4 r4 -1.6%)
 #endif
@@ -1094,7 +1104,7 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
           code = (Code)(mixed ? kCodeMixed32 : (m ? (first << 8) | m : 0u));
           if (!mixed) pairs += __popc(m);
         }
-        if (valid) codes[p] = code;
+        if (valid) MGPU_ST_INTER(code, &codes[p]);
         mixed = mixed && valid;
         const unsigned long long bal = __ballot(mixed);
         if (mixed) sa.mixed_idx[c0 + nmixed + (uint32_t)__popcll(bal & below)] = (uint16_t)((b + k) * 64 + lane);
@@ -2010,8 +2020,8 @@ __global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
     if (lp < m) {
       const uint32_t bi = bin_at(s_loc, nb, lp);
       sls[q] = s_off[bi] + (lp - s_loc[bi]);
-      b.bx[sls[q]] = s_val[lp];
-      b.perm[sls[q]] = (uint32_t)(c0 + s_li[lp]);
+      MGPU_ST_INTER(s_val[lp], &b.bx[sls[q]]);
+      MGPU_ST_INTER((uint32_t)(c0 + s_li[lp]), &b.perm[sls[q]]);
     }
   }
   __syncthreads();
@@ -2021,7 +2031,7 @@ __global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < kBinItems; q++)
-    if (sls[q] != 0xFFFFFFFFu) b.by[sls[q]] = s_val[q * kBinBlock + threadIdx.x];
+    if (sls[q] != 0xFFFFFFFFu) MGPU_ST_INTER(s_val[q * kBinBlock + threadIdx.x], &b.by[sls[q]]);
 }
 
 // the join over the binned points: join_tile's phases (G mode, no mixed list: every
@@ -2064,7 +2074,7 @@ __global__ __launch_bounds__(kBinBlock) void bin_gather_kernel(BinArgs b) {
   for (int i = wave * kPerWave + lane; i < (wave + 1) * kPerWave; i += 64)
     if ((uint32_t)i < m) {
       const uint64_t v = s_v[i];
-      b.res[c0 + i] = v;
+      MGPU_ST_INTER(v, &b.res[c0 + i]);
       np += __popc((uint32_t)(v >> 32));
     }
   np = wave_sum_u32(np);
