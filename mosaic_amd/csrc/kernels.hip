@@ -1177,11 +1177,14 @@ __device__ __forceinline__ uint32_t chunk_excl_scan(uint32_t v, uint32_t* s_w, u
 }
 
 constexpr int kEmitWin = 2048;  // pairs staged at a time
-// the ordered pairs are written once and read by the caller later: non-temporal stores
-// keep them from evicting the tables (A/B r3, profiles/r3_emit_nt_ab.txt: C2 emit 0.362 ->
-// 0.328 ms, C5 0.397 -> 0.355)
+// the split emit's ordered pairs with non-temporal stores (A/B r3, profiles/r3_emit_nt_ab.txt:
+// C2 emit 0.362 -> 0.328 ms, C5 0.397 -> 0.355); bin_emit_kernel / pair_emit_kernel with
+// plain stores (non-temporal: C3 emit +0.09 ms, C4 +0.06)
 #ifndef MGPU_EMIT_NT
 #define MGPU_EMIT_NT 1
+#endif
+#ifndef MGPU_EMIT_NT_OTHER
+#define MGPU_EMIT_NT_OTHER 0
 #endif
 #ifndef MGPU_EMIT_WAVES
 #define MGPU_EMIT_WAVES 5  // (8: 64 VGPRs, spills; 5: none, A/B equal or better)
@@ -1394,7 +1397,7 @@ __global__ __launch_bounds__(kEmitBlock) void pair_emit_kernel(EmitArgs a, int64
     if (where == kNoDst) continue;  // pool exhausted: the total exceeds the capacity
     const uint64_t r = a.recs[where + (i - s_pref[k])];
     const int64_t p = (t0 + k) * kTile + (int64_t)(r >> 32);
-#if MGPU_EMIT_NT
+#if MGPU_EMIT_NT_OTHER
     __builtin_nontemporal_store(a.point_id ? a.point_id[p] : a.id_base + p, &a.out_point[q]);
     __builtin_nontemporal_store((int32_t)(uint32_t)r, &a.out_poly[q]);
 #else
@@ -2154,7 +2157,7 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
       const uint64_t q = base + w0 + i;
       if ((int64_t)q >= sa.capacity) break;
       const int64_t p = c0 + s_pt[i];
-#if MGPU_EMIT_NT
+#if MGPU_EMIT_NT_OTHER
       __builtin_nontemporal_store(sa.point_id ? sa.point_id[p] : sa.id_base + p, &sa.out_point[q]);
       __builtin_nontemporal_store((int32_t)s_poly[i], &sa.out_poly[q]);
 #else
