@@ -302,15 +302,26 @@ int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t index_syst
 int32_t mgpu_pip_join_fetch(mgpu_ctx* ctx, int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id,
                             int32_t* out_polygon_id, void* stream);
 
-/* Asynchronous form: the pair count is left in device memory (*d_n_pairs, one
- * int64) and nothing synchronises -- graph-capturable once mgpu_ctx_reserve has
- * sized the workspace and one call of the same size has grown the split / binned
- * pipeline's buffers.  Without a host step, H3 near-ties keep the device's correctly
- * rounded cells: mgpu_last_near_ties lists them for the caller to audit. */
+/* Asynchronous form, in two calls.  mgpu_pip_join_async enqueues the join on `stream`
+ * and returns at once: the pair count is left in device memory (*d_n_pairs, one int64)
+ * -- graph-capturable once mgpu_ctx_reserve has sized the workspace and one call of the
+ * same size has grown the split / binned pipeline's buffers.  As in the synchronous
+ * call, H3 points inside the fast path's tie band are joined with the fast cell and
+ * queued; mgpu_pip_join_finish (same context, no other call on it in between) waits
+ * for the stream, recomputes the queued points with the reference's libm (option
+ * h3_libm; H3IndexSystem.scala:168-170 -> H3-Java's glibc) and, only when that moves a
+ * cell, reruns the join into the same output arrays and *d_n_pairs.  The pairs equal
+ * mgpu_pip_join's once mgpu_pip_join_finish has returned MGPU_OK (or MGPU_E_CAPACITY,
+ * with *out_n_pairs the count: mgpu_pip_join_fetch then writes them all); before it, a
+ * batch with near-ties may hold the fast cell at those points.  BNG joins and the
+ * correctly rounded mode have no host step, but the call is still required.
+ * mgpu_pip_join_finish: MGPU_E_INVALID_ARG when no asynchronous join is pending (another
+ * call on the context ended it). */
 int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t index_system, int32_t res,
                             const double* x, const double* y, const int64_t* point_id, int64_t point_id_base,
                             int64_t n, int64_t capacity, int64_t* d_n_pairs, int64_t* out_point_id,
                             int32_t* out_polygon_id, void* stream);
+int32_t mgpu_pip_join_finish(mgpu_ctx* ctx, int64_t* out_n_pairs, mgpu_stats* stats);
 int32_t mgpu_ctx_reserve(mgpu_ctx* ctx, int64_t max_points);
 
 /* Parity audit (no reference counterpart): the input positions of the H3 near-tie
@@ -340,6 +351,26 @@ typedef struct mgpu_tess mgpu_tess;
 int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, const int32_t* polygon_id,
                         const int64_t* poly_part_off, const int64_t* part_ring_off, const int64_t* ring_off,
                         const double* xy, int32_t keep_core_geometries, mgpu_tess** out);
+/* The is_core rule (mgpu_tessellate uses MGPU_CORE_MOSAICFILL):
+ *   MGPU_CORE_MOSAICFILL  the reference's: core iff the cell is in polyfill(buffer(-r))
+ *                         (Mosaic.scala:71-93, getCoreChips IndexSystem.scala:208-213: its
+ *                         centre inside the polygon at distance >= r = getBufferRadius from
+ *                         the boundary); a border-set cell is never core -- getBorderChips'
+ *                         equalsExact (IndexSystem.scala:186-188) compares JTS overlay's
+ *                         clockwise shell with indexToGeometry's counter-clockwise cell --
+ *                         so a cell the polygon holds whole but outside the core set is a
+ *                         border chip whose geometry is the whole cell; chip cells beyond
+ *                         the border band are dropped (never visited by the reference);
+ *   MGPU_CORE_CLIP        every cell the polygon holds whole is core.
+ * mgpu_tess_result_stats: out6 = {rows, core rows, whole cells flagged border (demoted),
+ * partly covered cells flagged core (promoted), dropped, rows within the JTS buffer /
+ * simplification tolerance bands (ambiguous)}. */
+#define MGPU_CORE_MOSAICFILL 0
+#define MGPU_CORE_CLIP 1
+int32_t mgpu_tessellate_ex(int32_t index_system, int32_t res, int64_t n_polys, const int32_t* polygon_id,
+                           const int64_t* poly_part_off, const int64_t* part_ring_off, const int64_t* ring_off,
+                           const double* xy, int32_t keep_core_geometries, int32_t core_rule, mgpu_tess** out);
+int32_t mgpu_tess_result_stats(const mgpu_tess* t, int64_t* out6);
 int32_t mgpu_tess_result_sizes(const mgpu_tess* t, int64_t* n_chips, int64_t* wkb_bytes);
 int32_t mgpu_tess_result_copy(const mgpu_tess* t, int64_t* cell, int32_t* polygon_id, uint8_t* is_core,
                               int64_t* wkb_offsets, uint8_t* wkb);

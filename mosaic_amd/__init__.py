@@ -11,16 +11,16 @@ from ._native import (CapacityError, IllegalArgumentException, IllegalStateExcep
                       EXPORTS, LIB_PATH)
 from .chips import ChipTable, DeviceChips, Polygons, tessellate
 from .context import GpuContext, MosaicContext, default_context
-from .functions import (GeometryColumn, InternalGeometryColumn, JoinResult, grid_cellkloop, grid_cellkring, grid_longlatascellid, grid_pointascellid,
-                        grid_tessellateexplode, pip_join, st_contains)
+from .functions import (AsyncJoin, GeometryColumn, InternalGeometryColumn, JoinResult, grid_cellkloop, grid_cellkring, grid_longlatascellid, grid_pointascellid,
+                        grid_tessellateexplode, pip_join, pip_join_async, st_contains)
 from .index_system import BNGIndexSystem, H3IndexSystem, IndexSystem, get_index_system
 
 __version__ = "0.1.0"
 
 __all__ = [
-    "BNGIndexSystem", "CapacityError", "ChipTable", "DeviceChips", "EXPORTS", "GeometryColumn", "GpuContext", "InternalGeometryColumn", "H3IndexSystem",
+    "AsyncJoin", "BNGIndexSystem", "CapacityError", "ChipTable", "DeviceChips", "EXPORTS", "GeometryColumn", "GpuContext", "InternalGeometryColumn", "H3IndexSystem",
     "IllegalArgumentException", "IllegalStateException", "IndexSystem", "JoinResult", "LIB_PATH",
     "MosaicContext", "MosaicGpuError", "Polygons", "default_context", "get_index_system", "grid_cellkloop",
     "grid_cellkring", "grid_longlatascellid",
-    "grid_pointascellid", "grid_tessellateexplode", "pip_join", "st_contains", "tessellate",
+    "grid_pointascellid", "grid_tessellateexplode", "pip_join", "pip_join_async", "st_contains", "tessellate",
 ]

@@ -151,17 +151,28 @@ class Polygons:
         return self.xy[:, 0].min(), self.xy[:, 1].min(), self.xy[:, 0].max(), self.xy[:, 1].max()
 
 
-def tessellate(polygons, index_system, resolution, keep_core_geometries=True):
-    """grid_tessellateexplode over a polygon set -> ChipTable (host C++ builder)."""
+CORE_RULES = {"mosaicfill": 0, "clip": 1}
+
+
+def tessellate(polygons, index_system, resolution, keep_core_geometries=True, core_rule="mosaicfill"):
+    """grid_tessellateexplode over a polygon set -> ChipTable (host C++ builder).
+
+    ``core_rule``: "mosaicfill" (default, the reference's: core iff the cell is in
+    polyfill(buffer(-r)); a border-set cell the polygon holds whole is a border chip of the
+    whole cell) or "clip" (every wholly covered cell is core) -- include/mosaic_gpu.h
+    MGPU_CORE_*.  The table's ``core_stats`` = rows, core rows, demoted, promoted, dropped,
+    ambiguous (mgpu_tess_result_stats)."""
     res = index_system.get_resolution(resolution)
     L = N.lib()
     h = ctypes.c_void_p()
     p = polygons
-    st = L.mgpu_tessellate(index_system.code, res, len(p), p.poly_id.ctypes.data, p.poly_part_off.ctypes.data,
-                           p.part_ring_off.ctypes.data, p.ring_off.ctypes.data, p.xy.ctypes.data,
-                           1 if keep_core_geometries else 0, ctypes.byref(h))
+    st = L.mgpu_tessellate_ex(index_system.code, res, len(p), p.poly_id.ctypes.data, p.poly_part_off.ctypes.data,
+                              p.part_ring_off.ctypes.data, p.ring_off.ctypes.data, p.xy.ctypes.data,
+                              1 if keep_core_geometries else 0, CORE_RULES[core_rule], ctypes.byref(h))
     N.check(st, "tessellation failed")
     try:
+        stats = np.zeros(6, np.int64)
+        N.check(L.mgpu_tess_result_stats(h, stats.ctypes.data))
         n, b = ctypes.c_int64(), ctypes.c_int64()
         N.check(L.mgpu_tess_result_sizes(h, ctypes.byref(n), ctypes.byref(b)))
         cell = np.zeros(n.value, np.int64)
@@ -173,4 +184,6 @@ def tessellate(polygons, index_system, resolution, keep_core_geometries=True):
                                         wkb.ctypes.data))
     finally:
         L.mgpu_tess_destroy(h)
-    return ChipTable(cell, pid, core, off, wkb[:b.value], index_system.code)
+    t = ChipTable(cell, pid, core, off, wkb[:b.value], index_system.code)
+    t.core_stats = dict(zip(("rows", "core", "demoted", "promoted", "dropped", "ambiguous"), stats.tolist()))
+    return t

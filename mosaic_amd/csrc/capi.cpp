@@ -1005,6 +1005,7 @@ WsLayout ws_layout(int64_t n_tiles, int64_t pool) {
 
 int32_t ensure_ws(mgpu_ctx* ctx, int64_t n_tiles, int64_t pool = 0) {
   ctx->last.valid = false;  // every call that uses the workspace ends the last join's lifetime
+  ctx->last.async_pending = false;
   size_t need = ws_layout(n_tiles, pool).total;
   if (need <= ctx->ws_bytes) return MGPU_OK;
   if (ctx->ws) HIP_TRY(hipFree(ctx->ws));
@@ -2150,6 +2151,10 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   L2.pool_ok = false;
   L2.total = -1;
   L2.valid = true;
+  L2.stream = (void*)s;
+  L2.capacity = capacity;
+  L2.out_point = out_point;
+  L2.out_poly = out_poly;
   return MGPU_OK;
 }
 
@@ -2186,18 +2191,6 @@ int32_t mgpu_last_near_ties(mgpu_ctx* ctx, int64_t* out_index, int64_t cap, int6
   return MGPU_OK;
 }
 
-int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
-                            const double* y, const int64_t* point_id, int64_t point_id_base, int64_t n,
-                            int64_t capacity, int64_t* d_n_pairs, int64_t* out_point_id, int32_t* out_polygon_id,
-                            void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  int32_t st = join_impl(ctx, chips, is, res, x, y, point_id, point_id_base, n, capacity, out_point_id, out_polygon_id,
-                         s, false);
-  if (st) return st;
-  if (d_n_pairs) HIP_TRY(hipMemcpyAsync(d_n_pairs, ctx->ws, 8, hipMemcpyDeviceToDevice, s));
-  return MGPU_OK;
-}
-
 }  // extern "C"
 
 // mgpu_pip_join with an optional validity bitmap of the points (the Arrow entry's nulls).
@@ -2210,36 +2203,63 @@ int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, 
 // (the fix kernels then take the override without computing the device route).  With
 // the correctly rounded libm (option h3_libm) the fix kernels decide the ties by the
 // device route.  A near-tie queue that overflowed is grown and the join redone.
-static int32_t pip_join_sync(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
-                             const double* y, const int64_t* point_id, int64_t point_id_base, int64_t n,
-                             int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id, int32_t* out_polygon_id,
-                             void* stream, mgpu_stats* stats, const uint8_t* valid, int64_t valid_off) {
-  hipStream_t s = (hipStream_t)stream;
-  const bool reference_libm = is == MGPU_H3 && ctx && ctx->opt.h3_libm == MGPU_LIBM_REFERENCE;
+// One join's arguments (the synchronous call's, or an asynchronous call's kept until
+// mgpu_pip_join_finish).
+struct JoinCall {
+  const mgpu_chips* chips;
+  int32_t is, res;
+  const double *x, *y;
+  const int64_t* point_id;
+  int64_t id_base, n, capacity;
+  int64_t* out_point;
+  int32_t* out_poly;
+  hipStream_t s;
+  const uint8_t* valid;
+  int64_t valid_off;
+  int64_t* d_n_pairs;  // the asynchronous form's device count (or null)
+};
+
+static int32_t launch_call(mgpu_ctx* ctx, const JoinCall& c, bool timed, int64_t n_ovr, int tie_host) {
+  int32_t st = join_impl(ctx, c.chips, c.is, c.res, c.x, c.y, c.point_id, c.id_base, c.n, c.capacity, c.out_point,
+                         c.out_poly, c.s, timed, c.valid, c.valid_off, n_ovr, tie_host);
+  if (st) return st;
+  if (c.d_n_pairs) HIP_TRY(hipMemcpyAsync(c.d_n_pairs, ctx->ws, 8, hipMemcpyDeviceToDevice, c.s));
+  return MGPU_OK;
+}
+
+// After a join's first launch (near-ties queued for the host when reference_libm): read
+// its counters; grow an overflowed near-tie queue and launch again; recompute the queued
+// points with the reference's libm and, only if a cell moves, launch once more with the
+// reference's cell of every queued point as an override.  Overflow relaunches are bounded
+// separately from the one override pass, so a completed pass is never reported as a
+// failure.  Fills out_n_pairs / stats and the context's record of the last join.
+static int32_t settle_join(mgpu_ctx* ctx, const JoinCall& c, bool timed, bool reference_libm, int64_t* out_n_pairs,
+                           mgpu_stats* stats) {
+  const hipStream_t s = c.s;
   int64_t n_ovr = 0, n_ties = 0, n_moved = 0;
+  int overflows = 0;
   uint64_t h[8] = {0};
-  for (int attempt = 0;; attempt++) {
-    int32_t st = join_impl(ctx, chips, is, res, x, y, point_id, point_id_base, n, capacity, out_point_id,
-                           out_polygon_id, s, true, valid, valid_off, n_ovr, reference_libm && n_ovr == 0);
-    if (st) return st;
+  for (;;) {
     HIP_TRY(hipMemcpyAsync(ctx->pin, ctx->ws, 16 * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(ctx->pin + 16, ctx->tq, (2 + 4 * kTqHead) * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(stream_wait(ctx, s));
     memcpy(h, ctx->pin, sizeof h);
     const int64_t queued = (int64_t)ctx->pin[16];
     if (h[2]) break;  // invalid coordinates: reported below
-    if (attempt >= 3) return fail(MGPU_E_INTERNAL, "pip_join: near-tie resolution did not settle");
     if (queued > ctx->tq_cap) {
+      // the queue is sized from this pass's count, so one regrowth holds the next pass
+      if (++overflows > 2) return fail(MGPU_E_INTERNAL, "pip_join: the near-tie queue overflowed %d times", overflows);
       if (int32_t e = ensure_tq(ctx, queued + queued / 4 + 1024)) return e;
+      if (int32_t e = launch_call(ctx, c, timed, n_ovr, reference_libm && n_ovr == 0)) return e;
       continue;
     }
-    if (n_ovr > 0) break;  // the rerun with the reference's cells
+    if (n_ovr > 0) break;  // the pass with the reference's cells
     n_ties = queued;
     if (!reference_libm || n_ties == 0) break;
     std::vector<TieRec> tr;
     if (int32_t e = read_ties(ctx, n_ties, tr)) return e;
     // (queued once per point: the fix kernels do not queue a tile's points again)
-    const auto ref = libm_reference_keys(tr, res);
+    const auto ref = libm_reference_keys(tr, c.res);
     n_moved = 0;
     for (size_t k = 0; k < tr.size(); k++) n_moved += ref[k].second != tr[k].key;
     if (n_moved == 0) break;
@@ -2248,7 +2268,10 @@ static int32_t pip_join_sync(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is,
     if (int32_t e = ensure_ovr(ctx, (int64_t)hv.size())) return e;
     HIP_TRY(hipMemcpy(ctx->ovr, hv.data(), hv.size() * 8, hipMemcpyHostToDevice));
     n_ovr = (int64_t)ref.size();
+    if (int32_t e = launch_call(ctx, c, timed, n_ovr, 0)) return e;
   }
+  const int32_t is = c.is;
+  const int64_t n = c.n, capacity = c.capacity;
   if (out_n_pairs) *out_n_pairs = (int64_t)h[0];
   if (stats) {
     stats->n_points = n;
@@ -2257,12 +2280,16 @@ static int32_t pip_join_sync(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is,
     stats->n_candidates = (int64_t)h[3];
     stats->libm_overrides = (int32_t)n_moved;
     float ms = 0, ms2 = 0;
-    hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
-    if (n > 0) hipEventElapsedTime(&ms2, ctx->ev0, ctx->ev2);
+    if (timed) {
+      hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+      if (n > 0) hipEventElapsedTime(&ms2, ctx->ev0, ctx->ev2);
+    }
     stats->kernel_ms = ms;
     stats->stream_kernel_ms = ms2;
     stats->mixed_kernel_ms = stats->emit_kernel_ms = 0;
-    if (ctx->last.split && n > 0) {
+    if (!timed) {
+      // (an asynchronous join records no events)
+    } else if (ctx->last.split && n > 0) {
       float m3 = 0;
       hipEventElapsedTime(&m3, ctx->ev0, ctx->ev3);
       stats->mixed_kernel_ms = m3 - ms2;
@@ -2293,6 +2320,17 @@ static int32_t pip_join_sync(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is,
   return MGPU_OK;
 }
 
+static int32_t pip_join_sync(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
+                             const double* y, const int64_t* point_id, int64_t point_id_base, int64_t n,
+                             int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id, int32_t* out_polygon_id,
+                             void* stream, mgpu_stats* stats, const uint8_t* valid, int64_t valid_off) {
+  const JoinCall c{chips, is, res, x, y, point_id, point_id_base, n, capacity, out_point_id, out_polygon_id,
+                   (hipStream_t)stream, valid, valid_off, nullptr};
+  const bool reference_libm = is == MGPU_H3 && ctx && ctx->opt.h3_libm == MGPU_LIBM_REFERENCE;
+  if (int32_t st = launch_call(ctx, c, true, 0, reference_libm)) return st;
+  return settle_join(ctx, c, true, reference_libm, out_n_pairs, stats);
+}
+
 extern "C" {
 
 int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
@@ -2301,6 +2339,34 @@ int32_t mgpu_pip_join(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_
                       mgpu_stats* stats) {
   return pip_join_sync(ctx, chips, is, res, x, y, point_id, point_id_base, n, capacity, out_n_pairs, out_point_id,
                        out_polygon_id, stream, stats, nullptr, 0);
+}
+
+// The asynchronous form: the same first launch as the synchronous call (H3 near-ties
+// queued with the fast cell), nothing waits; mgpu_pip_join_finish settles it.
+int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int32_t res, const double* x,
+                            const double* y, const int64_t* point_id, int64_t point_id_base, int64_t n,
+                            int64_t capacity, int64_t* d_n_pairs, int64_t* out_point_id, int32_t* out_polygon_id,
+                            void* stream) {
+  const JoinCall c{chips, is, res, x, y, point_id, point_id_base, n, capacity, out_point_id, out_polygon_id,
+                   (hipStream_t)stream, nullptr, 0, d_n_pairs};
+  const bool reference_libm = is == MGPU_H3 && ctx && ctx->opt.h3_libm == MGPU_LIBM_REFERENCE;
+  if (int32_t st = launch_call(ctx, c, false, 0, reference_libm)) return st;
+  ctx->last.async_pending = true;
+  ctx->last.d_n_pairs = d_n_pairs;
+  return MGPU_OK;
+}
+
+int32_t mgpu_pip_join_finish(mgpu_ctx* ctx, int64_t* out_n_pairs, mgpu_stats* stats) {
+  if (!ctx) return fail(MGPU_E_INVALID_ARG, "ctx is NULL");
+  auto& L = ctx->last;
+  if (!L.valid || !L.async_pending)
+    return fail(MGPU_E_INVALID_ARG, "pip_join_finish: no asynchronous join pending on this context");
+  if (int32_t st = set_device(ctx->device)) return st;
+  const JoinCall c{L.chips, L.is, L.res, L.x, L.y, L.point_id, L.id_base, L.n, L.capacity, L.out_point, L.out_poly,
+                   (hipStream_t)L.stream, nullptr, 0, L.d_n_pairs};
+  const bool reference_libm = L.tie_host != 0;
+  L.async_pending = false;
+  return settle_join(ctx, c, false, reference_libm, out_n_pairs, stats);
 }
 
 int32_t mgpu_pip_join_fetch(mgpu_ctx* ctx, int64_t capacity, int64_t* out_n_pairs, int64_t* out_point_id,

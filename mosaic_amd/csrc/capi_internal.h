@@ -65,6 +65,14 @@ struct mgpu_ctx {
     mgpu::SplitArgs sargs{};
     bool binned = false;
     mgpu::BinArgs bargs{};
+    // an mgpu_pip_join_async call waiting for mgpu_pip_join_finish (its H3 near-ties
+    // are queued for the host's libm pass); any other call on the context ends it
+    bool async_pending = false;
+    int64_t* d_n_pairs = nullptr;
+    void* stream = nullptr;
+    int64_t capacity = 0;
+    int64_t* out_point = nullptr;
+    int32_t* out_poly = nullptr;
   } last;
 };
 

@@ -230,6 +230,67 @@ void write_cell_wkb(const std::vector<std::vector<Pt>>& rings, std::vector<uint8
   mgpu::wkb::write_polygons(out, parts);
 }
 
+// the polar cap: the boundary's vertices by longitude, the edge that crosses the
+// antimeridian cut there, closed along the pole (ccw)
+std::vector<Pt> pole_cap(std::vector<Pt> v, bool north) {
+  std::sort(v.begin(), v.end(), [](const Pt& a, const Pt& b) { return a.x < b.x; });
+  const Pt a = v.back(), b{v.front().x + 360.0, v.front().y};
+  const double t = b.x > a.x ? (180.0 - a.x) / (b.x - a.x) : 0.5;
+  const double lat_x = a.y + t * (b.y - a.y);
+  std::vector<Pt> r;
+  const double pl = north ? 90.0 : -90.0;
+  if (north) {
+    r.push_back({-180.0, lat_x});
+    for (auto& q : v) r.push_back(q);
+    r.push_back({180.0, lat_x});
+    r.push_back({180.0, pl});
+    r.push_back({-180.0, pl});
+  } else {
+    r.push_back({-180.0, pl});
+    r.push_back({180.0, pl});
+    r.push_back({180.0, lat_x});
+    for (auto it = v.rbegin(); it != v.rend(); ++it) r.push_back(*it);
+    r.push_back({-180.0, lat_x});
+  }
+  r.push_back(r[0]);
+  return r;
+}
+
+// H3IndexSystem.indexToGeometry (H3IndexSystem.scala:103-121): h3ToGeoBoundary in
+// degrees, closed, ccw; the cell holding a pole as the cap between its boundary and
+// the pole (makePoleGeometry, :361-384); a cell across the antimeridian cut into its
+// western and eastern parts (makeSafeGeometry / crossesAntiMeridian, :386-410, :258-262)
+std::vector<std::vector<Pt>> h3_cell_rings(uint64_t id, int res) {
+  std::vector<Pt> b;
+  for (auto& v : mgpu::h3b::cell_boundary(id))
+    b.push_back({mgpu::h3b::to_degrees(v.lon), mgpu::h3b::to_degrees(v.lat)});
+  const int pole = id == pole_cell(true, res) ? 1 : (id == pole_cell(false, res) ? -1 : 0);
+  if (pole) return {pole_cap(b, pole > 0)};
+  double lo = INFINITY, hi = -INFINITY;
+  for (auto& q : b) {
+    lo = std::min(lo, q.x);
+    hi = std::max(hi, q.x);
+  }
+  b.push_back(b[0]);
+  if (ring_area(b) < 0) std::reverse(b.begin(), b.end());
+  if (!(lo < 0 && hi >= 0 && hi - lo > 180.0)) return {b};
+  // across the antimeridian: shift the western longitudes east, cut at 180
+  for (auto& q : b)
+    if (q.x < 0) q.x += 360.0;
+  if (ring_area(b) < 0) std::reverse(b.begin(), b.end());
+  static const std::vector<Pt> west{{0, -90}, {180, -90}, {180, 90}, {0, 90}, {0, -90}};
+  static const std::vector<Pt> east{{180, -90}, {360, -90}, {360, 90}, {180, 90}, {180, -90}};
+  std::vector<std::vector<Pt>> out;
+  auto w = clip_ring(b, west);
+  if (!w.empty() && std::fabs(ring_area(w)) > 0) out.push_back(std::move(w));
+  auto e = clip_ring(b, east);
+  if (!e.empty() && std::fabs(ring_area(e)) > 0) {
+    for (auto& q : e) q.x -= 360.0;
+    out.push_back(std::move(e));
+  }
+  return out;
+}
+
 struct Grid {
   virtual ~Grid() {}
   // a cell whose centre is farther than this (lattice units) from every walked boundary
@@ -248,6 +309,8 @@ struct Grid {
   // ring, or several (H3: a cell cut at the antimeridian); empty = no geometry
   virtual int64_t cell_id(long i, long j) const = 0;
   virtual std::vector<std::vector<Pt>> boundary(long i, long j) const = 0;
+  // the cell's centre in input coords (H3: h3ToGeo; BNG: the square's centre)
+  virtual Pt center_input(long i, long j, int64_t id) const = 0;
   // lattice row/column iteration for the scanline: row index of a lattice y,
   // y of a row, and the column index of the cell centred at lattice x in a row
   virtual double row_y(long j) const = 0;
@@ -338,66 +401,14 @@ struct H3Grid : Grid {
     }
     return {lon * 180.0 / M_PI, lat * 180.0 / M_PI};
   }
-  // H3IndexSystem.indexToGeometry (H3IndexSystem.scala:103-121): h3ToGeoBoundary in
-  // degrees, closed, ccw; the cell holding a pole as the cap between its boundary and
-  // the pole (makePoleGeometry, :361-384); a cell across the antimeridian cut into its
-  // western and eastern parts (makeSafeGeometry / crossesAntiMeridian, :386-410, :258-262)
   std::vector<std::vector<Pt>> boundary(long i, long j) const override {
     const int64_t id = cell_id(i, j);
     if (!id) return {};
-    std::vector<Pt> b;
-    for (auto& v : mgpu::h3b::cell_boundary((uint64_t)id))
-      b.push_back({mgpu::h3b::to_degrees(v.lon), mgpu::h3b::to_degrees(v.lat)});
-    const int pole = (uint64_t)id == pole_cell(true, res) ? 1 : ((uint64_t)id == pole_cell(false, res) ? -1 : 0);
-    if (pole) return {pole_cap(b, pole > 0)};
-    double lo = INFINITY, hi = -INFINITY;
-    for (auto& q : b) {
-      lo = std::min(lo, q.x);
-      hi = std::max(hi, q.x);
-    }
-    b.push_back(b[0]);
-    if (ring_area(b) < 0) std::reverse(b.begin(), b.end());
-    if (!(lo < 0 && hi >= 0 && hi - lo > 180.0)) return {b};
-    // across the antimeridian: shift the western longitudes east, cut at 180
-    for (auto& q : b)
-      if (q.x < 0) q.x += 360.0;
-    if (ring_area(b) < 0) std::reverse(b.begin(), b.end());
-    static const std::vector<Pt> west{{0, -90}, {180, -90}, {180, 90}, {0, 90}, {0, -90}};
-    static const std::vector<Pt> east{{180, -90}, {360, -90}, {360, 90}, {180, 90}, {180, -90}};
-    std::vector<std::vector<Pt>> out;
-    auto w = clip_ring(b, west);
-    if (!w.empty() && std::fabs(ring_area(w)) > 0) out.push_back(std::move(w));
-    auto e = clip_ring(b, east);
-    if (!e.empty() && std::fabs(ring_area(e)) > 0) {
-      for (auto& q : e) q.x -= 360.0;
-      out.push_back(std::move(e));
-    }
-    return out;
+    return h3_cell_rings((uint64_t)id, res);
   }
-  // the polar cap: the boundary's vertices by longitude, the edge that crosses the
-  // antimeridian cut there, closed along the pole (ccw)
-  static std::vector<Pt> pole_cap(std::vector<Pt> v, bool north) {
-    std::sort(v.begin(), v.end(), [](const Pt& a, const Pt& b) { return a.x < b.x; });
-    const Pt a = v.back(), b{v.front().x + 360.0, v.front().y};
-    const double t = b.x > a.x ? (180.0 - a.x) / (b.x - a.x) : 0.5;
-    const double lat_x = a.y + t * (b.y - a.y);
-    std::vector<Pt> r;
-    const double pl = north ? 90.0 : -90.0;
-    if (north) {
-      r.push_back({-180.0, lat_x});
-      for (auto& q : v) r.push_back(q);
-      r.push_back({180.0, lat_x});
-      r.push_back({180.0, pl});
-      r.push_back({-180.0, pl});
-    } else {
-      r.push_back({-180.0, pl});
-      r.push_back({180.0, pl});
-      r.push_back({180.0, lat_x});
-      for (auto it = v.rbegin(); it != v.rend(); ++it) r.push_back(*it);
-      r.push_back({-180.0, lat_x});
-    }
-    r.push_back(r[0]);
-    return r;
+  Pt center_input(long, long, int64_t id) const override {
+    const auto c = mgpu::h3b::cell_center((uint64_t)id);
+    return {mgpu::h3b::to_degrees(c.lon), mgpu::h3b::to_degrees(c.lat)};
   }
   double row_y(long j) const override { return j * mgpu::h3::kSin60; }
   long row_of(double y, bool up) const override {
@@ -439,6 +450,7 @@ struct BngGrid : Grid {
     double x = i * edge, y = j * edge;
     return {{{x, y}, {x + edge, y}, {x + edge, y + edge}, {x, y + edge}, {x, y}}};
   }
+  Pt center_input(long i, long j, int64_t) const override { return {(i + 0.5) * edge, (j + 0.5) * edge}; }
   double row_y(long j) const override { return j + 0.5; }
   long row_of(double y, bool up) const override { return up ? (long)std::ceil(y - 0.5) : (long)std::floor(y - 0.5); }
   double col_x(long i, long) const override { return i + 0.5; }
@@ -453,6 +465,146 @@ struct Chip {
   uint8_t core;
   std::vector<uint8_t> wkb;
 };
+
+// ---------------------------------------------------------------- mosaicFill's core set
+// The reference flags a chip core in two places (core/Mosaic.scala:61-99):
+//  * getCoreChips (IndexSystem.scala:208-213): every cell of polyfill(buffer(-r)) -- a
+//    cell whose centre lies in the polygon carved by r = getBufferRadius (H3IndexSystem.
+//    scala:79-90: the largest planar distance from the polygon's centroid to a vertex of
+//    the centroid's cell; BNGIndexSystem.scala:151-154: edge * sqrt(2) / 2), i.e. whose
+//    centre is inside the polygon at distance >= r from its boundary;
+//  * getBorderChips (IndexSystem.scala:178-195): isCore = coerced.equals(indexGeom), JTS
+//    equalsExact (MosaicGeometryJTS.scala:209-212) of the OverlayNG intersection (or its
+//    difference with the cell boundary, coerceChipGeometry :293-303) against the cell from
+//    indexToGeometry.  JTS overlay builds result shells clockwise (OverlayEdgeRing: a ring
+//    is a hole iff it is counter-clockwise) while indexToGeometry's cells are H3's
+//    counter-clockwise boundary (BNG: the counter-clockwise square), so the two rings are
+//    never exactly equal: a border-set cell is never core, even when the polygon holds all
+//    of it -- its chip is then the whole cell (written clockwise here, as OverlayNG would).
+// Cells neither in the core set nor in polyfill(boundary.buffer(1.01 r).simplify(0.01 r))
+// are never visited by the reference (a blind spot: dropped).  CoreRule decides each row
+// by its centre's signed distance d to the polygon boundary; rows within the bands where
+// JTS's chord approximation of the buffers (8 segments per quadrant: <= 1.93% of r) and
+// the 1% simplification could decide otherwise are counted as ambiguous.
+struct SegIndex {
+  double x0 = 0, y0 = 0, s = 1, inv = 1;
+  long nx = 0, ny = 0;
+  std::vector<uint32_t> start, items;
+  std::vector<Pt> a, b;
+
+  void build(const Polygon& poly, double cell) {
+    double minx = INFINITY, miny = INFINITY, maxx = -INFINITY, maxy = -INFINITY;
+    for (auto& part : poly.parts)
+      for (auto& ring : part)
+        for (size_t i = 0; i + 1 < ring.size(); i++) {
+          a.push_back(ring[i]);
+          b.push_back(ring[i + 1]);
+          minx = std::min(minx, ring[i].x);
+          maxx = std::max(maxx, ring[i].x);
+          miny = std::min(miny, ring[i].y);
+          maxy = std::max(maxy, ring[i].y);
+        }
+    if (a.empty()) return;
+    s = std::max({cell, (maxx - minx) / 512.0, (maxy - miny) / 512.0, 1e-300});
+    inv = 1.0 / s;
+    x0 = minx;
+    y0 = miny;
+    nx = (long)((maxx - minx) * inv) + 1;
+    ny = (long)((maxy - miny) * inv) + 1;
+    start.assign((size_t)(nx * ny + 1), 0);
+    auto range = [&](size_t k, long* i0, long* i1, long* j0, long* j1) {
+      *i0 = col(std::min(a[k].x, b[k].x));
+      *i1 = col(std::max(a[k].x, b[k].x));
+      *j0 = row(std::min(a[k].y, b[k].y));
+      *j1 = row(std::max(a[k].y, b[k].y));
+    };
+    for (int pass = 0; pass < 2; pass++) {
+      std::vector<uint32_t> fill;
+      if (pass) {
+        for (size_t q = 1; q < start.size(); q++) start[q] += start[q - 1];
+        items.assign(start.back(), 0);
+        fill.assign(start.begin(), start.end() - 1);
+      }
+      for (size_t k = 0; k < a.size(); k++) {
+        long i0, i1, j0, j1;
+        range(k, &i0, &i1, &j0, &j1);
+        for (long j = j0; j <= j1; j++)
+          for (long i = i0; i <= i1; i++) {
+            const size_t q = (size_t)(j * nx + i);
+            if (pass) items[fill[q]++] = (uint32_t)k;
+            else start[q + 1]++;
+          }
+      }
+    }
+  }
+  long col(double x) const { return std::min(std::max((long)std::floor((x - x0) * inv), 0L), nx - 1); }
+  long row(double y) const { return std::min(std::max((long)std::floor((y - y0) * inv), 0L), ny - 1); }
+  static double seg_dist(Pt p, Pt u, Pt v) {
+    const double dx = v.x - u.x, dy = v.y - u.y, l2 = dx * dx + dy * dy;
+    double t = l2 > 0 ? ((p.x - u.x) * dx + (p.y - u.y) * dy) / l2 : 0.0;
+    t = std::min(1.0, std::max(0.0, t));
+    return std::hypot(u.x + t * dx - p.x, u.y + t * dy - p.y);
+  }
+  // distance from p to the nearest boundary segment, or INFINITY when none is within q
+  double min_dist(Pt p, double q) const {
+    if (a.empty()) return INFINITY;
+    double best = INFINITY;
+    for (long j = row(p.y - q); j <= row(p.y + q); j++)
+      for (long i = col(p.x - q); i <= col(p.x + q); i++) {
+        const size_t c = (size_t)(j * nx + i);
+        for (uint32_t k = start[c]; k < start[c + 1]; k++) best = std::min(best, seg_dist(p, a[items[k]], b[items[k]]));
+      }
+    return best <= q ? best : INFINITY;
+  }
+  // even-odd inside test of p (half-open crossing rule), from p's bucket row to the right;
+  // a crossing is counted in the bucket holding its x, so a segment in several buckets
+  // counts once
+  bool inside(Pt p) const {
+    if (a.empty() || p.y < y0 || p.y > y0 + ny * s) return false;
+    const long j = row(p.y);
+    bool in = false;
+    for (long i = col(p.x); i < nx; i++) {
+      const double bx0 = x0 + i * s, bx1 = i + 1 < nx ? x0 + (i + 1) * s : INFINITY;
+      const size_t c = (size_t)(j * nx + i);
+      for (uint32_t k = start[c]; k < start[c + 1]; k++) {
+        const Pt u = a[items[k]], v = b[items[k]];
+        if ((u.y > p.y) == (v.y > p.y)) continue;
+        const double xi = (v.x - u.x) * (p.y - u.y) / (v.y - u.y) + u.x;
+        if (p.x < xi && xi >= std::max(bx0, p.x) && xi < bx1) in = !in;
+      }
+    }
+    return in;
+  }
+};
+
+struct CoreStats {
+  int64_t demoted = 0, promoted = 0, dropped = 0, ambiguous = 0;
+};
+
+struct CoreRule {
+  double r = 0;
+  SegIndex seg;
+  CoreStats st;
+  enum Verdict { kCore, kBorder, kDrop };
+  // the reference's flag of a chip cell with centre c; inside: the clip's knowledge (1 in,
+  // 0 out, -1 unknown)
+  Verdict decide(Pt c, int inside) {
+    const double q = 1.1 * r;
+    double d = seg.min_dist(c, q);
+    const bool in = inside >= 0 ? inside == 1 : seg.inside(c);
+    if (!in) d = -d;
+    if (std::fabs(d - r) <= 0.02 * r || std::fabs(-d - 1.01 * r) <= 0.03 * r) st.ambiguous++;
+    if (d >= r) return kCore;
+    if (-d > 1.04 * r) return kDrop;
+    return kBorder;
+  }
+};
+
+// Grid::boundary's rings reversed (clockwise shells, as JTS overlay returns them)
+std::vector<std::vector<Pt>> reversed(std::vector<std::vector<Pt>> rings) {
+  for (auto& r : rings) std::reverse(r.begin(), r.end());
+  return rings;
+}
 
 struct PairHash {
   size_t operator()(const std::pair<long, long>& p) const { return std::hash<long>()(p.first * 1000003L ^ p.second); }
@@ -495,7 +647,21 @@ bool cell_in_polygon(const std::vector<Pt>& cellb, const std::vector<std::vector
 
 // `lat_rings`: every ring in the grid's lattice space (densified for H3)
 void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<std::vector<Pt>>& lat_rings, int32_t pid,
-                        bool keep_core, std::vector<Chip>& out) {
+                        bool keep_core, CoreRule* rule, std::vector<Chip>& out) {
+  // a cell the polygon holds whole: core -- unless mosaicFill's rule (rule != null) puts
+  // it in the border set (then its chip is the whole cell, not core)
+  auto whole = [&](int64_t id, long i, long j, const std::vector<std::vector<Pt>>* rings) {
+    if (rule && rule->decide(g.center_input(i, j, id), 1) != CoreRule::kCore) {
+      rule->st.demoted++;
+      Chip ch{id, pid, 0, {}};
+      write_cell_wkb(reversed(rings ? *rings : g.boundary(i, j)), ch.wkb);
+      out.push_back(std::move(ch));
+      return;
+    }
+    Chip ch{id, pid, 1, {}};
+    if (keep_core) write_cell_wkb(rings ? *rings : g.boundary(i, j), ch.wkb);
+    out.push_back(std::move(ch));
+  };
   // 2. border cells: walk every edge in lattice space; per cell the smallest distance
   // from its centre to a walked sample (samples <= 0.2 apart)
   std::unordered_map<std::pair<long, long>, float, PairHash> border;
@@ -548,9 +714,7 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
   for (auto& c : interior) {
     int64_t id = g.cell_id(c.first, c.second);
     if (!id || !g.keep(id, c.first, c.second)) continue;
-    Chip ch{id, pid, 1, {}};
-    if (keep_core) write_cell_wkb(g.boundary(c.first, c.second), ch.wkb);
-    out.push_back(std::move(ch));
+    whole(id, c.first, c.second, nullptr);
   }
   // 4. border cells: clip -- unless the boundary never came near the cell (a ring
   // neighbour of a walked cell): then it lies wholly inside or outside, decided by its
@@ -568,9 +732,7 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
       for (auto& r : lat_rings)
         if (point_in_ring(r, cc)) in = !in;
       if (!in) continue;
-      Chip ch{cid, pid, 1, {}};
-      if (keep_core) write_cell_wkb(g.boundary(c.first, c.second), ch.wkb);
-      out.push_back(std::move(ch));
+      whole(cid, c.first, c.second, nullptr);
       continue;
     }
     const auto rings = g.boundary(c.first, c.second);
@@ -600,11 +762,7 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
       pieces.insert(pieces.end(), pc.begin(), pc.end());
     }
     if (inside) {
-      int64_t id = g.cell_id(c.first, c.second);
-      if (!id) continue;
-      Chip ch{id, pid, 1, {}};
-      if (keep_core) write_cell_wkb(rings, ch.wkb);
-      out.push_back(std::move(ch));
+      whole(cid, c.first, c.second, &rings);
       continue;
     }
     // (a concave cell is clipped piece by piece: the chip is then a MULTIPOLYGON whose
@@ -646,9 +804,24 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
       if (shell_ok) parts.push_back(std::move(out_part));
     }
     if (parts.empty() || area <= 0) continue;  // empty chip: dropped
-    int64_t id = g.cell_id(c.first, c.second);
-    if (!id) continue;
-    Chip ch{id, pid, 0, {}};
+    if (rule) {
+      // mosaicFill's sets: a cell whose centre is deep enough inside is in the core set
+      // (its chip is the whole cell, core, even where the polygon does not cover it); one
+      // whose centre is beyond the border band is never visited
+      const auto v = rule->decide(g.center_input(c.first, c.second, cid), -1);
+      if (v == CoreRule::kDrop) {
+        rule->st.dropped++;
+        continue;
+      }
+      if (v == CoreRule::kCore) {
+        rule->st.promoted++;
+        Chip ch{cid, pid, 1, {}};
+        if (keep_core) write_cell_wkb(rings, ch.wkb);
+        out.push_back(std::move(ch));
+        continue;
+      }
+    }
+    Chip ch{cid, pid, 0, {}};
     mgpu::wkb::write_polygons(ch.wkb, parts);
     out.push_back(std::move(ch));
   }
@@ -723,14 +896,71 @@ bool h3_faces(const Polygon& poly, int res, std::vector<std::vector<Pt>>& dense,
 
 struct mgpu_tess {
   std::vector<Chip> chips;
+  CoreStats core_stats;
 };
+
+namespace {
+
+// getBufferRadius (H3IndexSystem.scala:79-90): the centroid's cell at `res`; its shell
+// points' largest distance to the centroid (planar degrees) -- or, when indexToGeometry
+// gives several parts (a cell across the antimeridian), the length of the longest part
+// boundary, as the reference's second case computes it
+double h3_buffer_radius(const Polygon& poly, int res) {
+  double sx = 0, sy = 0, sa = 0;
+  for (auto& part : poly.parts)
+    for (size_t k = 0; k < part.size(); k++) {
+      const auto& r = part[k];
+      double a = 0, cx = 0, cy = 0;
+      for (size_t i = 0; i + 1 < r.size(); i++) {
+        const double cr = r[i].x * r[i + 1].y - r[i + 1].x * r[i].y;
+        a += cr;
+        cx += (r[i].x + r[i + 1].x) * cr;
+        cy += (r[i].y + r[i + 1].y) * cr;
+      }
+      if (a == 0) continue;
+      const double w = std::fabs(a / 2) * (k == 0 ? 1.0 : -1.0);
+      sx += w * cx / (3 * a);
+      sy += w * cy / (3 * a);
+      sa += w;
+    }
+  if (!(sa > 0)) return 0;
+  double gx = sx / sa, gy = sy / sa;
+  if (gx > 180) gx = -180 + std::fmod(gx, 180.0);
+  else if (gx < -180) gx = 180 - std::fmod(gx, 180.0);
+  bool tie = false;
+  const uint64_t id = mgpu::h3::point_to_cell(gx, gy, res, &tie);
+  if (!id) return 0;
+  const auto rings = h3_cell_rings(id, res);
+  double r = 0;
+  if (rings.size() == 1) {
+    for (auto& q : rings[0]) r = std::max(r, std::hypot(q.x - gx, q.y - gy));
+  } else {
+    for (auto& ring : rings) {
+      double len = 0;
+      for (size_t i = 0; i + 1 < ring.size(); i++) len += std::hypot(ring[i + 1].x - ring[i].x, ring[i + 1].y - ring[i].y);
+      r = std::max(r, len);
+    }
+  }
+  return r;
+}
+
+}  // namespace
 
 extern "C" {
 
 int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, const int32_t* polygon_id,
                         const int64_t* poly_part_off, const int64_t* part_ring_off, const int64_t* ring_off,
                         const double* xy, int32_t keep_core_geometries, mgpu_tess** out) {
+  return mgpu_tessellate_ex(index_system, res, n_polys, polygon_id, poly_part_off, part_ring_off, ring_off, xy,
+                            keep_core_geometries, MGPU_CORE_MOSAICFILL, out);
+}
+
+int32_t mgpu_tessellate_ex(int32_t index_system, int32_t res, int64_t n_polys, const int32_t* polygon_id,
+                           const int64_t* poly_part_off, const int64_t* part_ring_off, const int64_t* ring_off,
+                           const double* xy, int32_t keep_core_geometries, int32_t core_rule, mgpu_tess** out) {
   if (!out || n_polys < 0) return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellate: bad arguments");
+  if (core_rule != MGPU_CORE_MOSAICFILL && core_rule != MGPU_CORE_CLIP)
+    return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellate: unknown core rule %d", core_rule);
   if (int32_t st = mgpu_check_resolution(index_system, res)) return st;
   if (index_system == MGPU_BNG && res == -1)
     // 500km ids depend on the easting letter only: no square cells to clip
@@ -739,6 +969,7 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
   // then concatenate in input order (the output does not depend on the schedule)
   std::vector<std::vector<Chip>> per(n_polys);
   std::vector<uint8_t> bad_poly(n_polys, 0);
+  std::vector<CoreStats> pstats(n_polys);
   mgpu::parallel_for(n_polys, 64, [&](int64_t pb, int64_t pe, int) {
     for (int64_t p = pb; p < pe; p++) {
       Polygon poly;
@@ -755,6 +986,17 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
         if (!rings.empty()) poly.parts.push_back(std::move(rings));
       }
       if (poly.parts.empty()) continue;
+      // mosaicFill's core set (CoreRule) unless the clip rule was asked for
+      CoreRule rule_storage;
+      CoreRule* rule = nullptr;
+      if (core_rule == MGPU_CORE_MOSAICFILL) {
+        rule_storage.r = index_system == MGPU_H3 ? h3_buffer_radius(poly, res)
+                                                 : BngGrid(res).edge * std::sqrt(2.0) / 2.0;
+        if (rule_storage.r > 0) {
+          rule_storage.seg.build(poly, rule_storage.r);
+          rule = &rule_storage;
+        }
+      }
       if (index_system == MGPU_H3) {
         bool in_range = true;
         for (auto& part : poly.parts)
@@ -779,7 +1021,7 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
             for (auto& q : r) lr.push_back(g.to_lattice(q));
             lat_rings.push_back(std::move(lr));
           }
-          tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, per[p]);
+          tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, rule, per[p]);
         }
         // a cell reached twice (two lattice positions around a pentagon map to one id):
         // its chip is computed from the id, so the copies are equal -- keep the first
@@ -798,8 +1040,9 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
             for (auto& q : ring) lr.push_back(g.to_lattice(q));
             lat_rings.push_back(std::move(lr));
           }
-        tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, per[p]);
+        tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, rule, per[p]);
       }
+      if (rule) pstats[p] = rule->st;
     }
   });
   for (int64_t p = 0; p < n_polys; p++) {
@@ -813,6 +1056,12 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
                              "first, as the reference's alignToGrid does)", polygon_id[p]);
   }
   mgpu_tess* t = new mgpu_tess();
+  for (auto& q : pstats) {
+    t->core_stats.demoted += q.demoted;
+    t->core_stats.promoted += q.promoted;
+    t->core_stats.dropped += q.dropped;
+    t->core_stats.ambiguous += q.ambiguous;
+  }
   size_t total = 0;
   for (auto& v : per) total += v.size();
   t->chips.reserve(total);
@@ -847,6 +1096,19 @@ int32_t mgpu_tess_result_copy(const mgpu_tess* t, int64_t* cell, int32_t* polygo
     off += (int64_t)c.wkb.size();
   }
   wkb_offsets[t->chips.size()] = off;
+  return MGPU_OK;
+}
+
+int32_t mgpu_tess_result_stats(const mgpu_tess* t, int64_t* out6) {
+  if (!t || !out6) return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellation result is NULL");
+  int64_t core = 0;
+  for (auto& c : t->chips) core += c.core;
+  out6[0] = (int64_t)t->chips.size();
+  out6[1] = core;
+  out6[2] = t->core_stats.demoted;
+  out6[3] = t->core_stats.promoted;
+  out6[4] = t->core_stats.dropped;
+  out6[5] = t->core_stats.ambiguous;
   return MGPU_OK;
 }
 

@@ -275,3 +275,53 @@ def pip_join(x, y, chips, resolution, index_system=None, point_id=None, point_id
     N.check(status, required=cnt.value)
     m = int(cnt.value)
     return JoinResult(op[:m], oq[:m], st.as_dict())
+
+
+class AsyncJoin:
+    """A join enqueued by pip_join_async: ``finish()`` settles it (mgpu_pip_join_finish:
+    the stream's wait, the H3 near-ties recomputed with the reference's libm, a rerun only
+    when a cell moves) and returns the JoinResult.  ``count`` is the device-side pair
+    count (one int64 tensor) the enqueued work leaves before finish."""
+
+    def __init__(self, ctx, op, oq, count, keep):
+        self._ctx, self._op, self._oq, self.count, self._keep = ctx, op, oq, count, keep
+        self._done = None
+
+    def finish(self):
+        import ctypes
+        if self._done is not None:
+            return self._done
+        cnt = ctypes.c_int64()
+        st = N.MgpuStats()
+        status = N.lib().mgpu_pip_join_finish(self._ctx.handle, ctypes.byref(cnt), st)
+        N.check(status, required=cnt.value)
+        m = int(cnt.value)
+        self._done = JoinResult(self._op[:m], self._oq[:m], st.as_dict())
+        return self._done
+
+
+def pip_join_async(x, y, chips, resolution, index_system=None, point_id=None, point_id_base=0, capacity=None,
+                   stream=None):
+    """mgpu_pip_join_async: enqueue the join on the stream (nothing waits); the pairs
+    equal pip_join's after ``finish()`` (include/mosaic_gpu.h).  ``capacity`` is a hard
+    bound here (CapacityError from finish, with the count)."""
+    import torch
+    isys = index_system or _H3
+    res = isys.get_resolution(resolution)
+    if isinstance(chips, ChipTable):
+        chips = chips.upload()
+    _check_points(x, y)
+    n = x.numel()
+    pid_ptr = None
+    if point_id is not None:
+        point_id = point_id.contiguous()
+        pid_ptr = point_id.data_ptr()
+    s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+    cap = int(capacity if capacity is not None else max(16, n + n // 8))
+    op = torch.empty(cap, dtype=torch.int64, device=x.device)
+    oq = torch.empty(cap, dtype=torch.int32, device=x.device)
+    count = torch.zeros(1, dtype=torch.int64, device=x.device)
+    N.check(N.lib().mgpu_pip_join_async(chips.ctx.handle, chips.handle, isys.code, res, x.data_ptr(), y.data_ptr(),
+                                        pid_ptr, int(point_id_base), n, cap, count.data_ptr(), op.data_ptr(),
+                                        oq.data_ptr(), s))
+    return AsyncJoin(chips.ctx, op, oq, count, (x, y, point_id, chips))

@@ -416,6 +416,38 @@ def test_pip_join_adversarial_points(gpu, nyc_chips_r9):
     assert np.array_equal(gp, op) and np.array_equal(gq, oq)
 
 
+def test_pip_join_async_adversarial_points(gpu, nyc_chips_r9):
+    """mgpu_pip_join_async + mgpu_pip_join_finish on the adversarial points: the pairs
+    equal the reference (glibc) oracle's -- which differ from the correctly rounded
+    oracle's on this set (21 cells move) -- and the synchronous join's, in both libm
+    modes; finish without a pending join, or after another call ended it, raises."""
+    c = nyc_chips_r9
+    x, y = adversarial_points(c)
+    op, oq = oracle_join(c, x, y)
+    with O.h3_libm("cr"):
+        cp, cq = oracle_join(c, x, y)
+    assert not (len(op) == len(cp) and np.array_equal(op, cp) and np.array_equal(oq, cq))
+    xt, yt = T(x, gpu), T(y, gpu)
+    sync = M.pip_join(xt, yt, c, 9)
+    aj = M.pip_join_async(xt, yt, c, 9)
+    r = aj.finish()
+    gp, gq = r.numpy()
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+    assert int(aj.count.item()) == len(op)
+    assert r.stats["n_near_ties"] == sync.stats["n_near_ties"] > 0
+    assert r.stats["libm_overrides"] == sync.stats["libm_overrides"]
+    ctx = M.default_context(gpu)
+    with ctx.options(h3_libm=1):  # MGPU_LIBM_CORRECTLY_ROUNDED
+        gp2, gq2 = M.pip_join_async(xt, yt, c, 9).finish().numpy()
+    assert np.array_equal(gp2, cp) and np.array_equal(gq2, cq)
+    with pytest.raises(M.IllegalArgumentException):
+        aj2 = M.pip_join_async(xt, yt, c, 9)
+        M.pip_join(xt, yt, c, 9)  # another call on the context ends the pending join
+        aj2.finish()
+    with pytest.raises(M.IllegalArgumentException):
+        M.AsyncJoin(ctx, None, None, None, None).finish()
+
+
 def test_pip_join_bng_equals_oracle(gpu):
     from test_host import _bng_synthetic
     P = _bng_synthetic(seed=21, n=40)

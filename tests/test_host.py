@@ -82,7 +82,7 @@ def test_tessellation_covers_each_zone_exactly(nyc_zones, nyc_chips_r9):
     """MosaicExplodeBehaviors.scala:415-457 (issue 382): the chips of a polygon
     add up to the polygon's area; chips never overlap (one chip per cell)."""
     c = nyc_chips_r9
-    assert len(c) > 10000 and c.is_core.sum() > 3000
+    assert len(c) > 10000 and c.is_core.sum() > 2000
     for pid in (1, 2, 43, 132, 138, 161, 230, 263):
         k = int(np.nonzero(nyc_zones.poly_id == pid)[0][0])
         rows = np.nonzero(c.polygon_id == pid)[0]

@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 import mosaic_amd as M
+from geom_util import nyc_points
 import oracle as O
 from mosaic_amd import _native
 from geom_util import brute_force_pairs, polygons_area, wkb_area, wkt_to_parts
@@ -79,24 +80,29 @@ def test_doc_multipolygon_res0():
 @pytest.mark.parametrize("res", [1, 2, 3])
 def test_doc_multipolygon_finer(res):
     P = M.Polygons.from_lists([(1, wkt_to_parts(DOC_WKT))])
-    c = M.tessellate(P, M.H3IndexSystem(), res)
+    c = M.tessellate(P, M.H3IndexSystem(), res, core_rule="clip")
     _check_invariants(P, c)
     # (H3 children are not nested in their parents' boundaries, so no parent invariant)
     assert len(c) > {1: 20, 2: 100, 3: 500}[res]
 
 
 def test_kepler_zone1_core_chips(nyc_zones):
-    """The notebook shows the first 20 rows of zone 1's chips ("only showing top 20
-    rows"), all `is_core = true` -- mosaicFill emits core chips first -- so the listing
-    has no border rows to compare; the core rows are core here too.  (The full core /
-    border split is compared with mosaicFill's construction in
-    test_mosaicfill_selection_equals_clip_*.)"""
+    """The notebook shows the first 20 rows of zone 1's res-9 chips ("only showing top 20
+    rows"), all `is_core = true` -- mosaicFill emits core chips first.  The listing comes
+    from a Mosaic older than the one under /root/reference (before v0.3.11's issue-360
+    change of the tessellation, CHANGELOG.md): its core rows include cells whose centre
+    lies only 0.60 r from the boundary (r = 0.4.3's getBufferRadius, 0.0041 deg here), so
+    0.4.3's polyfill(buffer(-r)) does not produce them; every one of them is at least 1.05
+    circumradii deep, i.e. wholly inside -- the clip rule's core set holds them all.  The
+    listing pins no border row either way (test_mosaicfill_rule_*)."""
     k = int(np.nonzero(nyc_zones.poly_id == 1)[0][0])
-    c = M.tessellate(nyc_zones.select([k]), M.H3IndexSystem(), 9)
-    core = set(c.cell[c.is_core.astype(bool)].tolist())
-    # the reference's core set polyfills the polygon shrunk by a cell radius: a subset of
-    # the cells that lie wholly inside
-    assert set(KEPLER_ZONE1_RES9_CORE) <= core
+    P = nyc_zones.select([k])
+    clip = M.tessellate(P, M.H3IndexSystem(), 9, core_rule="clip")
+    assert set(KEPLER_ZONE1_RES9_CORE) <= set(clip.cell[clip.is_core.astype(bool)].tolist())
+    mf = M.tessellate(P, M.H3IndexSystem(), 9)
+    assert sorted(mf.cell.tolist()) == sorted(clip.cell.tolist())
+    missing = set(KEPLER_ZONE1_RES9_CORE) - set(mf.cell[mf.is_core.astype(bool)].tolist())
+    assert len(missing) == 7  # the listing's cells 0.60-0.94 r deep (an older radius)
 
 
 def _star(cx, cy, r0, r1, k, seed):
@@ -120,8 +126,11 @@ def test_multi_face_polygons_join_equals_brute_force():
         (3, _star(pent[1, 0], pent[1, 1], 0.5, 2.0, 25, 3)),
         (4, _star(-40.0, -30.0, 6.0, 12.0, 50, 4)),           # large, several faces
     ])
+    # (geometric invariants of the clip: chips tile the polygon.  mosaicFill's rule at
+    # these coarse resolutions promotes / drops cells whose size differs from the
+    # centroid cell's -- test_mosaicfill_rule_coarse_cells)
     for res in (2, 3, 4, 5):
-        c = M.tessellate(P, M.H3IndexSystem(), res)
+        c = M.tessellate(P, M.H3IndexSystem(), res, core_rule="clip")
         _check_invariants(P, c)
     rng = np.random.default_rng(5)
     xs, ys = [], []
@@ -251,32 +260,111 @@ def _mosaicfill_selection(P, c, res):
         # rows within that of the carved edge whose flag the approximation could flip
         "buffer_sensitive": int(((d >= 0.98 * r) & (d < r) & ~core).sum()),
         "min_r_minus_R": float((r - R).min()), "max_R_over_r": float((R / r).max()),
+        "_d": d, "_r": r,
     }
 
 
-@pytest.mark.parametrize("res", [8, 9, 10])
-def test_mosaicfill_selection_equals_clip_nyc(nyc_zones, res):
-    """NYC taxi zones: the reference's core / border selection gives exactly this
-    builder's rows and flags -- no blind spot, no core-set cell the clip calls border,
-    none near the buffer's chord approximation -- because every chip cell's circumradius
-    stays below the polygon's r (r is at least the centroid cell's nearest-vertex
-    distance; cell size varies by < 1% across a zone)."""
-    c = M.tessellate(nyc_zones, M.H3IndexSystem(), res)
-    s = _mosaicfill_selection(nyc_zones, c, res)
-    print("NYC res %d:" % res, s)
-    assert s["blind"] == 0 and s["core_mismatch"] == 0 and s["buffer_sensitive"] == 0, s
-    assert s["core_set"] <= s["core"] and s["core_set"] + s["band"] >= s["rows"]
+def _assert_rule(P, res, expect=None):
+    """The default (mosaicFill) table against an independent restatement of its sets: the
+    same rows as the clip; core exactly where the centre is >= r inside (polyfill(buffer
+    (-r)), d and r computed here in numpy); the clip's whole cells outside that set are the
+    demoted rows; the ambiguity count = rows within 2% of r (JTS's buffer chords)."""
+    clip = M.tessellate(P, M.H3IndexSystem(), res, core_rule="clip")
+    mf = M.tessellate(P, M.H3IndexSystem(), res)
+    assert np.array_equal(clip.cell, mf.cell) and np.array_equal(clip.polygon_id, mf.polygon_id)
+    s = _mosaicfill_selection(P, clip, res)
+    d, r = s.pop("_d"), s.pop("_r")
+    core_set = d >= r
+    exact = np.abs(d - r) > 1e-9 * r
+    assert np.array_equal(mf.is_core.astype(bool)[exact], core_set[exact])
+    assert s["blind"] == 0 and s["core_mismatch"] == 0, s
+    whole = clip.is_core.astype(bool)
+    st = mf.core_stats
+    assert st["demoted"] == int((whole & ~mf.is_core.astype(bool)).sum()) and st["promoted"] == st["dropped"] == 0
+    assert st["ambiguous"] == int((np.abs(d - r) <= 0.02 * r).sum()), (st, s)
+    for i in np.nonzero(whole & ~mf.is_core.astype(bool))[0][:50]:
+        # a demoted row's chip is the whole cell, written clockwise (JTS overlay's shell)
+        w = _wkb(mf, i)
+        assert w and wkb_area(w) == pytest.approx(wkb_area(_wkb(clip, i)), rel=1e-12)
+    print("res %d:" % res, st, s)
+    if expect:
+        assert (st["rows"], st["core"], st["demoted"], st["ambiguous"]) == expect, st
+    return clip, mf
 
 
-def test_mosaicfill_selection_equals_clip_tracts():
-    """The C3 tract-like polygons at res 10 (a 400-tract sample): the same equivalence."""
+@pytest.mark.parametrize("res,expect", [(8, (2795, 29, 125, 7)), (9, (11890, 2227, 1715, 126)),
+                                        (10, (64041, 34251, 7475, 636))])
+def test_mosaicfill_rule_nyc(nyc_zones, res, expect):
+    """NYC taxi zones: mosaicFill's flags (core set = polyfill(buffer(-r))) vs the clip's
+    (every wholly covered cell): the same rows; at res 9, 1,715 of 3,942 whole cells are
+    border chips under the reference's rule; 126 rows are within JTS's chord tolerance of
+    r (their flag is parity unpinned)."""
+    _assert_rule(nyc_zones, res, expect)
+
+
+def test_mosaicfill_rule_tracts():
+    """The C3 tract-like polygons at res 10 (a 400-tract sample): the same checks."""
     import bench_workloads as W
     T = W.tract_polygons(n_cells=2000, extent=(-74.5, 40.5, -74.0, 41.0), seed=3)
-    P = T.select(range(0, len(T), 5))
-    c = M.tessellate(P, M.H3IndexSystem(), 10)
-    s = _mosaicfill_selection(P, c, 10)
-    print("tracts res 10:", s)
-    assert s["blind"] == 0 and s["core_mismatch"] == 0 and s["buffer_sensitive"] == 0, s
+    _assert_rule(T.select(range(0, len(T), 5)), 10)
+
+
+def test_mosaicfill_rule_pairs_on_adversarial_points(nyc_zones):
+    """How much the rule changes the join (the oracle, same inputs): on the NYC r9
+    adversarial fixture -- points on chip vertices and edge midpoints -- the clip table's
+    pairs are a superset of mosaicFill's; every extra pair is a point on the boundary of
+    a whole cell the reference keeps as a border chip (st_contains is false on it).  On
+    uniform points the two tables give the same pairs."""
+    import struct
+    from test_gpu_parity import adversarial_points
+    clip = M.tessellate(nyc_zones, M.H3IndexSystem(), 9, core_rule="clip")
+    mf = M.tessellate(nyc_zones, M.H3IndexSystem(), 9)
+    x, y = adversarial_points(clip)
+    a = set(zip(*[v.tolist() for v in O.pip_join(0, 9, x, y, clip.cell, clip.polygon_id, clip.is_core,
+                                                   clip.wkb_offsets, clip.wkb)]))
+    b = set(zip(*[v.tolist() for v in O.pip_join(0, 9, x, y, mf.cell, mf.polygon_id, mf.is_core,
+                                                   mf.wkb_offsets, mf.wkb)]))
+    extra = a - b
+    print("adversarial points %d: clip %d pairs, mosaicFill %d, clip-only %d, mosaicFill-only %d"
+          % (len(x), len(a), len(b), len(extra), len(b - a)))
+    assert b <= a and len(extra) > 0
+    demoted = {(int(c), int(p)) for c, p, w, m in zip(clip.cell, clip.polygon_id, clip.is_core, mf.is_core) if w and not m}
+    cells = O.h3_points_to_cells(x, y, 9)
+    assert all((int(cells[i]), pid) in demoted for i, pid in extra)
+    u, v = nyc_points(300_000, 12)
+    pa = O.pip_join(0, 9, u, v, clip.cell, clip.polygon_id, clip.is_core, clip.wkb_offsets, clip.wkb)
+    pb = O.pip_join(0, 9, u, v, mf.cell, mf.polygon_id, mf.is_core, mf.wkb_offsets, mf.wkb)
+    assert all(np.array_equal(p, q) for p, q in zip(pa, pb))
+
+
+def test_mosaicfill_rule_coarse_cells():
+    """Where chip cells differ in size from the polygon's centroid cell (coarse
+    resolutions, multi-face polygons) mosaicFill's sets cover the polygon imperfectly:
+    a cell whose centre is >= r deep is core although it sticks out (promoted), one
+    beyond the border band is never visited (dropped).  The join over such a table
+    differs from true containment only inside those cells."""
+    _, _, pent = cell_geometry([(1 << 59) | (bc << 45) | 0x1FFFFFFFFFFF for bc in (14,)])
+    P = M.Polygons.from_lists([(2, _star(pent[0, 0], pent[0, 1], 1.0, 3.0, 30, 2)),
+                               (4, _star(-40.0, -30.0, 6.0, 12.0, 50, 4))])
+    res = 4
+    clip = M.tessellate(P, M.H3IndexSystem(), res, core_rule="clip")
+    mf = M.tessellate(P, M.H3IndexSystem(), res)
+    st = mf.core_stats
+    print(st)
+    assert st["promoted"] + st["dropped"] > 0
+    changed = set(zip(clip.cell.tolist(), clip.polygon_id.tolist())) ^ set(zip(mf.cell.tolist(), mf.polygon_id.tolist()))
+    rng = np.random.default_rng(9)
+    x = np.concatenate([rng.uniform(-52, -28, 8000), rng.uniform(pent[0, 0] - 3, pent[0, 0] + 3, 4000)])
+    y = np.concatenate([rng.uniform(-42, -18, 8000), rng.uniform(pent[0, 1] - 3, pent[0, 1] + 3, 4000)])
+    got = set(zip(*[v.tolist() for v in O.pip_join(0, res, x, y, mf.cell, mf.polygon_id, mf.is_core, mf.wkb_offsets,
+                                                   mf.wkb)]))
+    want = set(zip(*[v.tolist() for v in O.pip_join(0, res, x, y, clip.cell, clip.polygon_id, clip.is_core,
+                                                      clip.wkb_offsets, clip.wkb)]))
+    cells = O.h3_points_to_cells(x, y, res)
+    clip_core = {(int(c), int(p)) for c, p, k in zip(clip.cell, clip.polygon_id, clip.is_core) if k}
+    mf_core = {(int(c), int(p)) for c, p, k in zip(mf.cell, mf.polygon_id, mf.is_core) if k}
+    moved = (clip_core ^ mf_core) | changed
+    assert all((int(cells[i]), pid) in moved for i, pid in got ^ want)
 
 
 # ---------------------------------------------------------------- antimeridian and poles
@@ -317,7 +405,7 @@ def test_antimeridian_cells(res):
     P = M.Polygons.from_lists([(7, [
         [[(177.5, -18.5), (180.0, -18.5), (180.0, -15.5), (177.5, -15.5), (177.5, -18.5)]],
         [[(-180.0, -18.5), (-178.0, -18.5), (-178.0, -15.5), (-180.0, -15.5), (-180.0, -18.5)]]])])
-    c = M.tessellate(P, M.H3IndexSystem(), res)
+    c = M.tessellate(P, M.H3IndexSystem(), res, core_rule="clip")
     _check_invariants(P, c)
     split = 0
     for i in range(len(c)):
@@ -355,7 +443,7 @@ def test_polar_cap_cells(res):
         if not north:
             ring = ring[::-1]
         P = M.Polygons.from_lists([(3, [[ring]])])
-        c = M.tessellate(P, M.H3IndexSystem(), res)
+        c = M.tessellate(P, M.H3IndexSystem(), res, core_rule="clip")
         _check_invariants(P, c)
         pole = int(O.h3_points_to_cells(np.array([0.0]), np.array([90.0 * s]), res)[0])
         assert pole in set(c.cell.tolist())
