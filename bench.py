@@ -269,18 +269,33 @@ def main():
     isys, zones = wl["isys"], wl["polygons"]
     log("config %s: %d polygons" % (a.config, len(zones)))
     table = None
+    setup = {"tessellate_s": 0.0, "upload_s": 0.0, "broadcast_s": 0.0}
     if rank == 0:
+        # setup (grid_tessellateexplode's chip table, built once per polygon
+        # set): the host tessellator, the blob build + upload, the replication
+        t = time.perf_counter()
         table = M.tessellate(zones, isys, a.res, keep_core_geometries=wl.get("keep_core", True))
-        log("tessellated: %d chips" % len(table))
+        setup["tessellate_s"] = time.perf_counter() - t
+        log("tessellated: %d chips (%.2f s)" % (len(table), setup["tessellate_s"]))
+        t = time.perf_counter()
         chips = table.upload(ctx)
-        log("chip table uploaded")
+        torch.cuda.synchronize(dev)
+        setup["upload_s"] = time.perf_counter() - t
+        log("chip table uploaded (%.2f s)" % setup["upload_s"])
     else:
         chips = None
-    if world > 1 and not rehearsal:
-        chips = D.broadcast_chips(chips, ctx)
-    elif world > 1:
-        blob = D.broadcast_host_blob(D.host_blob(table) if rank == 0 else None, 0)
-        chips = chips if rank == 0 else D.upload_host_blob(blob, ctx)
+    if world > 1:
+        dist.barrier()
+        t = time.perf_counter()
+        if not rehearsal:
+            chips = D.broadcast_chips(chips, ctx)
+        else:
+            blob = D.broadcast_host_blob(D.host_blob(table) if rank == 0 else None, 0)
+            chips = chips if rank == 0 else D.upload_host_blob(blob, ctx)
+        torch.cuda.synchronize(dev)
+        tb = torch.tensor([time.perf_counter() - t], dtype=torch.float64)
+        dist.all_reduce(tb, op=dist.ReduceOp.MAX)
+        setup["broadcast_s"] = float(tb.item())
     info = chips.info()
 
     n = a.points
@@ -385,6 +400,10 @@ def main():
         "kernels_ms": ({"classify": stream_ms, "mixed": float(np.mean(mms)), "emit": float(np.mean(ems))} if split
                        else {"bin": float(np.mean(mms)), "pip_binned": stream_ms, "emit": float(np.mean(ems))} if binned
                        else {"pip_join": stream_ms, "rest": pipeline_ms - stream_ms}),
+        # once per chip table, outside the timed steps (rank 0 builds, every rank receives)
+        "setup_s": dict(setup, total_s=sum(setup.values()),
+                        core_rule="mosaicfill", chip_stats=(table.core_stats if table is not None else None),
+                        blob_bytes=info.get("bytes")),
         "pairs_per_gpu": pairs,
         "pairs_total": total_pairs,
         "near_ties": ties,

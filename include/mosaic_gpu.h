@@ -266,6 +266,11 @@ int32_t mgpu_comm_destroy(mgpu_ctx* ctx);
 int32_t mgpu_chips_broadcast(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t root, mgpu_chips** out, void* stream);
 int32_t mgpu_pair_offsets(mgpu_ctx* ctx, int64_t local_pairs, int64_t* out_offset, int64_t* out_total,
                           int64_t* out_counts, void* stream);
+/* TEST ONLY: a receiving rank's side of mgpu_chips_broadcast without RCCL -- the header
+ * read from the device buffer dev_blob, the receiving allocation (fail_alloc != 0 forces
+ * it to fail), the blob copied in, the table adopted -- so a corrupt header or a failed
+ * allocation can be shown to return an error (it does not wait on anything). */
+int32_t mgpu_test_receive_blob(mgpu_ctx* ctx, const void* dev_blob, int32_t fail_alloc, mgpu_chips** out);
 
 /* st_contains(chip.wkb, point) for explicit (chip row, point) pairs
  * (ST_Contains.scala:21-44 -> MosaicGeometryJTS.contains, MosaicGeometryJTS.scala:197).

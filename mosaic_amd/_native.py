@@ -41,6 +41,7 @@ EXPORTS = (
     "mgpu_test_h3_elementary_host", "mgpu_test_h3_route_host", "mgpu_test_h3_boundary_host",
     "mgpu_ctx_set_option", "mgpu_ctx_get_option", "mgpu_build_opts_default", "mgpu_chips_host_blob_ex",
     "mgpu_test_h3_glibc_host", "mgpu_internal_geometry_to_cells", "mgpu_test_internal_centroid", "mgpu_test_join_counters",
+    "mgpu_test_receive_blob",
 )
 MGPU_GEOM_WKB = 0
 MGPU_GEOM_WKT = 1
@@ -176,6 +177,7 @@ def lib():
                                                   ctypes.POINTER(MgpuStats)]),
         "mgpu_test_internal_centroid": (I32, [I64, P, P, P, P, P, P, P, P]),
         "mgpu_test_join_counters": (I32, [P, P]),
+        "mgpu_test_receive_blob": (I32, [P, P, I32, ctypes.POINTER(P)]),
     }
     for name, (rt, args) in sig.items():
         f = getattr(L, name)

@@ -85,7 +85,8 @@ class DeviceChips:
     def info(self):
         a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         N.check(N.lib().mgpu_chips_info(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
-        return {"chips": a.value, "cells": b.value, "vertices": c.value}
+        p, n = self.device_blob()
+        return {"chips": a.value, "cells": b.value, "vertices": c.value, "bytes": n}
 
     def close(self):
         if self.handle:

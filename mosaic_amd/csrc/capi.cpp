@@ -230,6 +230,10 @@ double angle_between(const double* a, const double* b) {
 // nothing; inside it, only faces that can be nearest somewhere in the box are
 // tested (65 x 65 sampling with a 2-Lipschitz margin).  Returns false (caller keeps
 // cell-id probing) for mixed resolutions, res < 5, or pentagon base cells.
+// H3's maxDimByCIIres: the face triangle at Class II resolution r is normalized
+// i + j + k <= this
+constexpr int64_t kMaxDimCII[17] = {2, -1, 14, -1, 98, -1, 686, -1, 4802, -1, 33614, -1, 235298, -1, 1647086, -1, 11529602};
+
 bool build_lattice(const std::vector<mgpu::HashSlot>& cells, std::vector<std::pair<uint64_t, uint32_t>>& keys,
                    int* res_out, uint32_t* face_mask, double bbox[4]) {
   namespace H = mgpu::h3;
@@ -269,7 +273,18 @@ bool build_lattice(const std::vector<mgpu::HashSlot>& cells, std::vector<std::pa
         ang[f] = angle_between(v, H3T_FACE_CENTER_POINT[f]);
         amin = std::min(amin, ang[f]);
       }
-      for (int f = 0; f < 20; f++) {
+      // a cell deep inside its home face (the only face within 3 rho, every lattice
+      // position within hex distance 3 of its own strictly inside the face triangle --
+      // normalized i + j + k below the face's maxDim, for Class III compared after the
+      // aperture-7 step to the next Class II resolution, which at most quadruples the sum)
+      // is reached at its own position only: positions inside one face are distinct cells
+      int near = 0;
+      for (int f = 0; f < 20; f++) near += ang[f] <= amin + 3 * rho;
+      const int64_t sum = (int64_t)ijk.i + ijk.j + ijk.k;
+      const bool interior = near == 1 && ang[face] <= amin + 3 * rho &&
+                            ((res & 1) ? 4 * (sum + 6) < kMaxDimCII[res + 1] : sum + 6 < kMaxDimCII[res]);
+      if (interior) tk.push_back({H::lattice_key(face, ijk), (uint32_t)ci});
+      for (int f = 0; f < 20 && !interior; f++) {
         if (ang[f] > amin + 3 * rho) continue;
         const double(*F)[3] = H3T_FACE_FRAME[f][res & 1];
         double dc = v[0] * F[2][0] + v[1] * F[2][1] + v[2] * F[2][2];
@@ -372,59 +387,87 @@ struct Strips {
 };
 
 void build_strips(int64_t n_chips, std::vector<uint8_t>& cflags, const std::vector<uint32_t>& cpart,
-                  const std::vector<double>& cenv, const mgpu::wkb::Flat& geo, Strips& st) {
+                  const std::vector<double>& cenv, const mgpu::wkb::Flat& geo, Strips& st, int64_t G) {
   st.chip_strip.assign(n_chips + 1, 0);
   st.chip_sy.assign(2 * (size_t)n_chips, 0.0);
-  std::vector<std::vector<uint32_t>> bucket;
-  for (int64_t c = 0; c < n_chips; c++) {
-    st.chip_strip[c] = (uint32_t)(st.strip_edge.size() - 1);
-    uint8_t fl = cflags[c];
-    if (fl & (mgpu::kChipCore | mgpu::kChipEmpty | mgpu::kChipNoGeom | mgpu::kChipRect)) {
-      if (!(fl & (mgpu::kChipEmpty | mgpu::kChipNoGeom | mgpu::kChipRect))) cflags[c] |= mgpu::kChipNoStrips;
-      continue;
-    }
-    const uint32_t r0 = geo.part_ring[cpart[c]], r1 = geo.part_ring[cpart[c + 1]];
-    if (r1 - r0 > (uint32_t)mgpu::kStripRings) {
-      cflags[c] |= mgpu::kChipNoStrips;
-      continue;
-    }
-    int64_t E = 0;
-    for (uint32_t r = r0; r < r1; r++) {
-      uint32_t nv = geo.ring_vtx[r + 1] - geo.ring_vtx[r];
-      if (nv >= 2) E += nv - 1;
-    }
-    int S = (int)std::min<int64_t>(mgpu::kMaxStrips, std::max<int64_t>(1, E / 2));
-    const double y0 = cenv[4 * c + 1], H = cenv[4 * c + 3] - y0;
-    if (!(H > 0)) S = 1;
-    const double inv_h = (H > 0) ? (double)S / H : 0.0;
-    st.chip_sy[2 * c] = y0;
-    st.chip_sy[2 * c + 1] = inv_h;
-    bucket.assign(S, {});
+  // chunks of G chips in parallel, each into its own strip / edge lists (chip_strip then
+  // local), concatenated with the offsets shifted
+  const int64_t NC = (n_chips + G - 1) / G;
+  std::vector<Strips> cs(NC);
+  mgpu::parallel_for(NC, 1, [&](int64_t kb, int64_t ke, int) {
+    std::vector<std::vector<uint32_t>> bucket;
     std::vector<double> rec;
     std::vector<uint8_t> rring;
-    uint32_t k = 0;
-    for (uint32_t r = r0; r < r1; r++) {
-      const uint32_t vb = geo.ring_vtx[r], ve = geo.ring_vtx[r + 1];
-      for (uint32_t i = vb + 1; i < ve; i++) {
-        const double p1x = geo.vtx[2 * i], p1y = geo.vtx[2 * i + 1];
-        const double p2x = geo.vtx[2 * i - 2], p2y = geo.vtx[2 * i - 1];
-        rec.insert(rec.end(), {p1x, p1y, p2x, p2y});
-        rring.push_back((uint8_t)(r - r0));
-        const int sa = mgpu::strip_of(std::min(p1y, p2y), y0, inv_h, S);
-        const int sb = mgpu::strip_of(std::max(p1y, p2y), y0, inv_h, S);
-        for (int q = sa; q <= sb; q++) bucket[q].push_back(k);
-        k++;
+    for (int64_t kc = kb; kc < ke; kc++) {
+      Strips& L = cs[kc];
+      for (int64_t c = kc * G; c < std::min(n_chips, (kc + 1) * G); c++) {
+        st.chip_strip[c] = (uint32_t)(L.strip_edge.size() - 1);
+        uint8_t fl = cflags[c];
+        if (fl & (mgpu::kChipCore | mgpu::kChipEmpty | mgpu::kChipNoGeom | mgpu::kChipRect)) {
+          if (!(fl & (mgpu::kChipEmpty | mgpu::kChipNoGeom | mgpu::kChipRect))) cflags[c] |= mgpu::kChipNoStrips;
+          continue;
+        }
+        const uint32_t r0 = geo.part_ring[cpart[c]], r1 = geo.part_ring[cpart[c + 1]];
+        if (r1 - r0 > (uint32_t)mgpu::kStripRings) {
+          cflags[c] |= mgpu::kChipNoStrips;
+          continue;
+        }
+        int64_t E = 0;
+        for (uint32_t r = r0; r < r1; r++) {
+          uint32_t nv = geo.ring_vtx[r + 1] - geo.ring_vtx[r];
+          if (nv >= 2) E += nv - 1;
+        }
+        int S = (int)std::min<int64_t>(mgpu::kMaxStrips, std::max<int64_t>(1, E / 2));
+        const double y0 = cenv[4 * c + 1], H = cenv[4 * c + 3] - y0;
+        if (!(H > 0)) S = 1;
+        const double inv_h = (H > 0) ? (double)S / H : 0.0;
+        st.chip_sy[2 * c] = y0;
+        st.chip_sy[2 * c + 1] = inv_h;
+        bucket.assign(S, {});
+        rec.clear();
+        rring.clear();
+        uint32_t k = 0;
+        for (uint32_t r = r0; r < r1; r++) {
+          const uint32_t vb = geo.ring_vtx[r], ve = geo.ring_vtx[r + 1];
+          for (uint32_t i = vb + 1; i < ve; i++) {
+            const double p1x = geo.vtx[2 * i], p1y = geo.vtx[2 * i + 1];
+            const double p2x = geo.vtx[2 * i - 2], p2y = geo.vtx[2 * i - 1];
+            rec.insert(rec.end(), {p1x, p1y, p2x, p2y});
+            rring.push_back((uint8_t)(r - r0));
+            const int sa = mgpu::strip_of(std::min(p1y, p2y), y0, inv_h, S);
+            const int sb = mgpu::strip_of(std::max(p1y, p2y), y0, inv_h, S);
+            for (int q = sa; q <= sb; q++) bucket[q].push_back(k);
+            k++;
+          }
+        }
+        for (int q = 0; q < S; q++) {
+          for (uint32_t e : bucket[q]) {
+            L.edges.insert(L.edges.end(), rec.begin() + 4 * e, rec.begin() + 4 * e + 4);
+            L.edge_ring.push_back(rring[e]);
+          }
+          L.strip_edge.push_back((uint32_t)L.edge_ring.size());
+        }
       }
     }
-    for (int q = 0; q < S; q++) {
-      for (uint32_t e : bucket[q]) {
-        st.edges.insert(st.edges.end(), rec.begin() + 4 * e, rec.begin() + 4 * e + 4);
-        st.edge_ring.push_back(rring[e]);
-      }
-      st.strip_edge.push_back((uint32_t)st.edge_ring.size());
-    }
+  });
+  std::vector<size_t> s0(NC + 1, 0), e0(NC + 1, 0);
+  for (int64_t k = 0; k < NC; k++) {
+    s0[k + 1] = s0[k] + cs[k].strip_edge.size() - 1;
+    e0[k + 1] = e0[k] + cs[k].edge_ring.size();
   }
-  st.chip_strip[n_chips] = (uint32_t)(st.strip_edge.size() - 1);
+  st.strip_edge.assign(s0[NC] + 1, 0);
+  st.edges.resize(4 * e0[NC]);
+  st.edge_ring.resize(e0[NC]);
+  mgpu::parallel_for(NC, 1, [&](int64_t kb, int64_t ke, int) {
+    for (int64_t k = kb; k < ke; k++) {
+      const Strips& L = cs[k];
+      for (size_t q = 1; q < L.strip_edge.size(); q++) st.strip_edge[s0[k] + q] = (uint32_t)(L.strip_edge[q] + e0[k]);
+      std::copy(L.edges.begin(), L.edges.end(), st.edges.begin() + 4 * e0[k]);
+      std::copy(L.edge_ring.begin(), L.edge_ring.end(), st.edge_ring.begin() + e0[k]);
+      for (int64_t c = k * G; c < std::min(n_chips, (k + 1) * G); c++) st.chip_strip[c] += (uint32_t)s0[k];
+    }
+  });
+  st.chip_strip[n_chips] = (uint32_t)s0[NC];
 }
 
 // Does segment a-b meet the closed box [x0, x1] x [y0, y1]?  (The callers widen the
@@ -479,18 +522,62 @@ void build_grid(const mgpu::ChipTableView& hv, uint32_t c, const mgpu::wkb::Flat
         }
     }
   }
+  // The rest: PointLocator's verdict at the cell centre, which lies at a positive distance
+  // from every edge (its widened cell meets none), so RayCrossingCounter's per-ring
+  // crossing parity there is the count of the ring's edges that straddle the centre's
+  // row (half-open, as countSegment) and cross it to the right of the centre -- computed
+  // per row for the row's 16 centres at once instead of a ring walk per centre.  A part
+  // is entered when its shell's parity is odd and no hole's is; the chip when some part
+  // is (a point on no boundary: the Mod-2 rule does not arise).
+  std::vector<double> xs;
+  std::vector<uint32_t> ring_first;  // per ring of the chip: its first crossing in xs
   for (int gy = 0; gy < kGrid; gy++) {
     uint32_t row = 0;
-    for (int gx = 0; gx < kGrid; gx++) {
-      uint32_t v = st[gy][gx];
-      if (v != kCellMixed) {
-        const double cxp = e0 + (gx + 0.5) / h.sx, cyp = e1 + (gy + 0.5) / h.sy;
-        const int loc = pip::chip_locate(hv, c, cxp, cyp);
-        v = loc == pip::kInterior ? kCellIn : (loc == pip::kExterior ? kCellOut : kCellMixed);
+    bool any = false;
+    for (int gx = 0; gx < kGrid && !any; gx++) any = st[gy][gx] != kCellMixed;
+    if (any) {
+      const double cyp = e1 + (gy + 0.5) / h.sy;
+      xs.clear();
+      ring_first.clear();
+      for (uint32_t r = r0; r < r1; r++) {
+        ring_first.push_back((uint32_t)xs.size());
+        for (uint32_t i = geo.ring_vtx[r] + 1; i < geo.ring_vtx[r + 1]; i++) {
+          const double p1x = geo.vtx[2 * i], p1y = geo.vtx[2 * i + 1], p2x = geo.vtx[2 * i - 2], p2y = geo.vtx[2 * i - 1];
+          if (((p1y > cyp) && (p2y <= cyp)) || ((p2y > cyp) && (p1y <= cyp)))
+            xs.push_back(p1x + (cyp - p1y) * (p2x - p1x) / (p2y - p1y));
+        }
+        std::sort(xs.begin() + ring_first.back(), xs.end());
       }
-      row |= v << (2 * gx);
+      ring_first.push_back((uint32_t)xs.size());
+      for (int gx = 0; gx < kGrid; gx++) {
+        uint32_t v = st[gy][gx];
+        if (v != kCellMixed) {
+          const double cxp = e0 + (gx + 0.5) / h.sx;
+          auto odd = [&](uint32_t r) {  // ring r (index within the chip): crossings right of cxp
+            const auto b = xs.begin() + ring_first[r], e = xs.begin() + ring_first[r + 1];
+            return ((e - std::upper_bound(b, e, cxp)) & 1) != 0;
+          };
+          bool in = false;
+          for (uint32_t p = hv.chip_part[c]; p < hv.chip_part[c + 1] && !in; p++) {
+            const uint32_t rb = hv.part_ring[p], re = hv.part_ring[p + 1];
+            if (re == rb || geo.ring_vtx[rb + 1] == geo.ring_vtx[rb] || !odd(rb - r0)) continue;
+            bool hole = false;
+            for (uint32_t q = rb + 1; q < re && !hole; q++) hole = odd(q - r0);
+            in = !hole;
+          }
+          v = in ? kCellIn : kCellOut;
+#ifdef MGPU_GRID_VERIFY
+          const int loc = pip::chip_locate(hv, c, cxp, cyp);
+          if (loc != (in ? pip::kInterior : pip::kExterior)) {
+            fprintf(stderr, "grid verify: chip %u cell (%d, %d) row parity %d, PointLocator %d\n", c, gx, gy, (int)in, loc);
+            abort();
+          }
+#endif
+        }
+        row |= v << (2 * gx);
+      }
     }
-    h.grid[gy] = row;
+    h.grid[gy] = any ? row : 0xAAAAAAAAu;
   }
 }
 
@@ -1434,11 +1521,83 @@ int32_t mgpu_points_to_cells_host(mgpu_ctx* ctx, int32_t is, int32_t res, const 
 
 }  // extern "C"
 
+#ifdef MGPU_BLOB_TIMING
+#define BLOB_T0() auto blob_t = std::chrono::steady_clock::now()
+#define BLOB_MARK(what)                                                                                   \
+  do {                                                                                                    \
+    const auto now = std::chrono::steady_clock::now();                                                    \
+    fprintf(stderr, "[blob] %-10s %.3f s\n", what, std::chrono::duration<double>(now - blob_t).count()); \
+    blob_t = now;                                                                                         \
+  } while (0)
+#else
+#define BLOB_T0() \
+  do {            \
+  } while (0)
+#define BLOB_MARK(what) \
+  do {                  \
+  } while (0)
+#endif
+// The host blob: malloc'd and filled without a zero pass (build_blob writes every byte)
+struct HostBlob {
+  uint8_t* p = nullptr;
+  size_t n = 0;
+  HostBlob() = default;
+  HostBlob(const HostBlob&) = delete;
+  HostBlob& operator=(const HostBlob&) = delete;
+  ~HostBlob() { free(p); }
+  bool alloc(size_t bytes) {
+    free(p);
+    p = (uint8_t*)malloc(bytes);
+    n = p ? bytes : 0;
+    return p != nullptr;
+  }
+  uint8_t* data() const { return p; }
+  size_t size() const { return n; }
+  uint8_t* release() {
+    uint8_t* q = p;
+    p = nullptr;
+    n = 0;
+    return q;
+  }
+};
+
+// chips per chunk of the parallel blob-build phases (fixed: the result never depends on
+// the thread count or schedule)
+constexpr int64_t kBlobChunk = 1 << 14;
+
+// std::sort of v by cmp (a strict total order) on the host threads: chunks sorted in
+// parallel, then pairwise merge rounds
+template <class T, class Cmp>
+static void parallel_sort(std::vector<T>& v, Cmp cmp) {
+  const int64_t n = (int64_t)v.size();
+  const int64_t P = mgpu::parallel_slots(n, 1 << 16);
+  if (P <= 1) {
+    std::sort(v.begin(), v.end(), cmp);
+    return;
+  }
+  std::vector<int64_t> b(P + 1);
+  for (int64_t k = 0; k <= P; k++) b[k] = n * k / P;
+  mgpu::parallel_for(P, 1, [&](int64_t kb, int64_t ke, int) {
+    for (int64_t k = kb; k < ke; k++) std::sort(v.begin() + b[k], v.begin() + b[k + 1], cmp);
+  });
+  std::vector<T> tmp(v.size());
+  for (int64_t w = 1; w < P; w *= 2) {
+    const int64_t jobs = (P + 2 * w - 1) / (2 * w);
+    mgpu::parallel_for(jobs, 1, [&](int64_t jb, int64_t je, int) {
+      for (int64_t j = jb; j < je; j++) {
+        const int64_t lo = b[2 * w * j], mid = b[std::min(P, 2 * w * j + w)], hi = b[std::min(P, 2 * w * j + 2 * w)];
+        std::merge(v.begin() + lo, v.begin() + mid, v.begin() + mid, v.begin() + hi, tmp.begin() + lo, cmp);
+      }
+    });
+    v.swap(tmp);
+  }
+}
+
 // The whole chip table as one host blob (header + arrays, chip_table.h); uploaded as
 // is by mgpu_chips_upload, evaluated in place by mgpu_test_chip_contains_host.
 static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
                           const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb,
-                          std::vector<uint8_t>& host, BlobHeader& hdr_out, const mgpu_build_opts& bo) {
+                          HostBlob& host, BlobHeader& hdr_out, const mgpu_build_opts& bo) {
   if (index_system != MGPU_H3 && index_system != MGPU_BNG)
     return fail(MGPU_E_INVALID_ARG, "unknown index system %d (0 = H3, 1 = BNG)", index_system);
   if (n_chips < 0 || n_chips > (int64_t)std::numeric_limits<int32_t>::max())
@@ -1446,13 +1605,20 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   if (n_chips > 0 && (!cell || !polygon_id || !is_core || !wkb_offsets))
     return fail(MGPU_E_INVALID_ARG, "chip arrays are NULL");
 
+  BLOB_T0();
+  // chips sorted by (cell, polygon id, input row): chunks sorted in parallel, merged in
+  // parallel rounds
   std::vector<int64_t> order(n_chips);
   for (int64_t i = 0; i < n_chips; i++) order[i] = i;
-  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+  parallel_sort(order, [&](int64_t a, int64_t b) {
     if (cell[a] != cell[b]) return cell[a] < cell[b];
-    return polygon_id[a] < polygon_id[b];
+    if (polygon_id[a] != polygon_id[b]) return polygon_id[a] < polygon_id[b];
+    return a < b;
   });
+  BLOB_MARK("sort");
 
+  // the chips' WKB parsed in parallel: each chunk of sorted chips into its own flat
+  // geometry, then the chunks concatenated with their offsets shifted
   mgpu::wkb::Flat geo;  // parts / rings / vertices of all chips, in sorted order
   std::vector<int32_t> cpoly(n_chips);
   std::vector<uint8_t> cflags(n_chips);
@@ -1460,36 +1626,77 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   std::vector<double> cenv(4 * (size_t)n_chips);
   std::vector<int64_t> crow(n_chips);
   std::vector<uint32_t> row2chip(n_chips);
-  for (int64_t s = 0; s < n_chips; s++) {
-    int64_t i = order[s];
-    cpoly[s] = polygon_id[i];
-    crow[s] = i;
-    row2chip[i] = (uint32_t)s;
-    cpart[s] = (uint32_t)geo.part_ring.size() - 1;
-    uint8_t fl = is_core[i] ? mgpu::kChipCore : 0;
-    int64_t b = wkb_offsets[i], e = wkb_offsets[i + 1];
-    if (e < b) return fail(MGPU_E_INVALID_ARG, "wkb_offsets not ascending at row %lld", (long long)i);
-    double env[4] = {INFINITY, INFINITY, -INFINITY, -INFINITY};
-    if (e == b) {
-      if (!is_core[i]) return fail(MGPU_E_WKB, "border chip row %lld has NULL geometry", (long long)i);
-      fl |= mgpu::kChipNoGeom;
-    } else {
-      mgpu::wkb::GeomInfo gi;
-      std::string msg;
-      if (!mgpu::wkb::parse(wkb + b, (size_t)(e - b), geo, gi, msg))
-        return fail(MGPU_E_WKB, "chip row %lld: %s", (long long)i, msg.c_str());
-      if (gi.multi) fl |= mgpu::kChipMulti;
-      if (gi.n_points == 0) fl |= mgpu::kChipEmpty;
-      if (gi.rectangle) fl |= mgpu::kChipRect;
-      env[0] = gi.env[0];
-      env[1] = gi.env[1];
-      env[2] = gi.env[2];
-      env[3] = gi.env[3];
+  {
+    const int64_t G = kBlobChunk, NC = (n_chips + G - 1) / G;
+    std::vector<mgpu::wkb::Flat> cf(NC);
+    std::vector<int32_t> cst(NC, MGPU_OK);
+    std::vector<std::string> cmsg(NC);
+    mgpu::parallel_for(NC, 1, [&](int64_t kb, int64_t ke, int) {
+      for (int64_t k = kb; k < ke; k++) {
+        mgpu::wkb::Flat& f = cf[k];
+        for (int64_t s = k * G; s < std::min(n_chips, (k + 1) * G) && cst[k] == MGPU_OK; s++) {
+          const int64_t i = order[s];
+          cpoly[s] = polygon_id[i];
+          crow[s] = i;
+          row2chip[i] = (uint32_t)s;
+          cpart[s] = (uint32_t)f.part_ring.size() - 1;  // (local: shifted below)
+          uint8_t fl = is_core[i] ? mgpu::kChipCore : 0;
+          const int64_t b = wkb_offsets[i], e = wkb_offsets[i + 1];
+          double env[4] = {INFINITY, INFINITY, -INFINITY, -INFINITY};
+          if (e < b) {
+            cst[k] = MGPU_E_INVALID_ARG;
+            cmsg[k] = "wkb_offsets not ascending at row " + std::to_string(i);
+          } else if (e == b) {
+            if (!is_core[i]) {
+              cst[k] = MGPU_E_WKB;
+              cmsg[k] = "border chip row " + std::to_string(i) + " has NULL geometry";
+            }
+            fl |= mgpu::kChipNoGeom;
+          } else {
+            mgpu::wkb::GeomInfo gi;
+            std::string msg;
+            if (!mgpu::wkb::parse(wkb + b, (size_t)(e - b), f, gi, msg)) {
+              cst[k] = MGPU_E_WKB;
+              cmsg[k] = "chip row " + std::to_string(i) + ": " + msg;
+            }
+            if (gi.multi) fl |= mgpu::kChipMulti;
+            if (gi.n_points == 0) fl |= mgpu::kChipEmpty;
+            if (gi.rectangle) fl |= mgpu::kChipRect;
+            for (int q = 0; q < 4; q++) env[q] = gi.env[q];
+          }
+          cflags[s] = fl;
+          for (int q = 0; q < 4; q++) cenv[4 * s + q] = env[q];
+        }
+      }
+    });
+    for (int64_t k = 0; k < NC; k++)  // the first failing row in sorted order
+      if (cst[k] != MGPU_OK) return fail(cst[k], "%s", cmsg[k].c_str());
+    // chunk k's parts, rings and vertices start after those of chunks < k
+    std::vector<size_t> p0(NC + 1, 0), r0(NC + 1, 0), v0(NC + 1, 0);
+    for (int64_t k = 0; k < NC; k++) {
+      p0[k + 1] = p0[k] + cf[k].part_ring.size() - 1;
+      r0[k + 1] = r0[k] + cf[k].ring_vtx.size() - 1;
+      v0[k + 1] = v0[k] + cf[k].vtx.size() / 2;
     }
-    cflags[s] = fl;
-    for (int k = 0; k < 4; k++) cenv[4 * s + k] = env[k];
+    geo.part_ring.assign(p0[NC] + 1, 0);
+    geo.ring_vtx.assign(r0[NC] + 1, 0);
+    geo.ring_env.resize(4 * r0[NC]);
+    geo.vtx.resize(2 * v0[NC]);
+    mgpu::parallel_for(NC, 1, [&](int64_t kb, int64_t ke, int) {
+      for (int64_t k = kb; k < ke; k++) {
+        const mgpu::wkb::Flat& f = cf[k];
+        for (size_t q = 1; q < f.part_ring.size(); q++) geo.part_ring[p0[k] + q] = (uint32_t)(f.part_ring[q] + r0[k]);
+        for (size_t q = 1; q < f.ring_vtx.size(); q++) geo.ring_vtx[r0[k] + q] = (uint32_t)(f.ring_vtx[q] + v0[k]);
+        std::copy(f.ring_env.begin(), f.ring_env.end(), geo.ring_env.begin() + 4 * r0[k]);
+        std::copy(f.vtx.begin(), f.vtx.end(), geo.vtx.begin() + 2 * v0[k]);
+        for (int64_t s = k * G; s < std::min(n_chips, (k + 1) * G); s++) cpart[s] += (uint32_t)p0[k];
+      }
+    });
+    if (r0[NC] > 0xFFFFFFFFull || v0[NC] > 0xFFFFFFFFull)
+      return fail(MGPU_E_UNSUPPORTED, "chip table too large (%zu rings, %zu vertices)", r0[NC], v0[NC]);
   }
   cpart[n_chips] = (uint32_t)geo.part_ring.size() - 1;
+  BLOB_MARK("parse");
 
   // cell hash over the distinct cells
   std::vector<mgpu::HashSlot> distinct;
@@ -1504,8 +1711,10 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     distinct.push_back(mgpu::HashSlot{c, (uint32_t)s, (uint16_t)(e - s), core});
     s = e;
   }
+  BLOB_MARK("distinct");
   Strips strips;
-  build_strips(n_chips, cflags, cpart, cenv, geo, strips);
+  build_strips(n_chips, cflags, cpart, cenv, geo, strips, kBlobChunk);
+  BLOB_MARK("strips");
   std::vector<mgpu::ChipHdr> chdr(n_chips);
   {
     // host view of the flattened geometry for the grid classification
@@ -1534,6 +1743,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     }
     });
   }
+  BLOB_MARK("headers");
   // H3: probe by lattice key when possible (chip_table.h)
   int32_t probe_mode = mgpu::kProbeCellId, lres = -1;
   uint32_t face_mask = (1u << 20) - 1;
@@ -1555,6 +1765,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     entries = distinct;
     if (index_system == MGPU_H3 && !distinct.empty()) lres = (int32_t)((distinct[0].cell >> 52) & 15);
   }
+  BLOB_MARK("lattice");
   // dense lattice grid when the chip cells' (a, b) boxes are compact: one load per
   // point instead of a hash probe sequence (misses -- most points -- included)
   std::vector<uint64_t> grid;
@@ -1603,6 +1814,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   uint32_t bng_edge = 0;
   if (index_system == MGPU_BNG && build_bng_dense(distinct, &lres, &dense[0], &bng_edge, grid))
     probe_mode = mgpu::kProbeDense;
+  BLOB_MARK("dense");
   // pixel index over the dense grid (chip_table.h, build_raster_*)
   Raster raster;
   if (probe_mode == mgpu::kProbeDense) {
@@ -1620,6 +1832,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
                   : build_raster_bng(hv, dense[0], bng_edge, grid, raster, bo);
     if (!ok) raster = Raster{};
   }
+  BLOB_MARK("raster");
   uint32_t cap = 16;
   while (cap < 2 * entries.size()) cap <<= 1;
   std::vector<mgpu::HashSlot> slots(cap, mgpu::HashSlot{0, 0, 0, 0});
@@ -1634,6 +1847,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     max_probe = std::max(max_probe, k);
   }
 
+  BLOB_MARK("hash");
   // one blob
   struct Part {
     const void* src;
@@ -1706,10 +1920,32 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     total = align_up(total + std::max<size_t>(parts[k].bytes, 1), 256);
   }
   hdr.blob_bytes = total;
-  host.assign(total, 0);
-  memcpy(host.data(), &hdr, sizeof hdr);
-  for (auto& p : parts)
-    if (p.bytes) memcpy(host.data() + p.off, p.src, p.bytes);
+  if (!host.alloc(total)) return fail(MGPU_E_INTERNAL, "out of host memory (%zu bytes)", total);
+  // the header, each array and the zero padding behind it, in pieces of <= 64 MiB on the
+  // host threads
+  struct Piece {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t bytes, zero;
+  };
+  std::vector<Piece> pieces;
+  pieces.push_back({host.data(), (const uint8_t*)&hdr, sizeof hdr, kBlobHeaderBytes - sizeof hdr});
+  for (size_t k = 0; k < parts.size(); k++) {
+    const size_t end = k + 1 < parts.size() ? parts[k + 1].off : total;
+    const size_t pad = end - parts[k].off - parts[k].bytes;
+    for (size_t o = 0; o < parts[k].bytes; o += (64u << 20)) {
+      const size_t b = std::min(parts[k].bytes - o, (size_t)64 << 20);
+      pieces.push_back({host.data() + parts[k].off + o, (const uint8_t*)parts[k].src + o, b, 0});
+    }
+    pieces.push_back({host.data() + parts[k].off + parts[k].bytes, nullptr, 0, pad});
+  }
+  mgpu::parallel_for((int64_t)pieces.size(), 1, [&](int64_t qb, int64_t qe, int) {
+    for (int64_t q = qb; q < qe; q++) {
+      if (pieces[q].bytes) memcpy(pieces[q].dst, pieces[q].src, pieces[q].bytes);
+      if (pieces[q].zero) memset(pieces[q].dst + pieces[q].bytes, 0, pieces[q].zero);
+    }
+  });
+  BLOB_MARK("assemble");
   hdr_out = hdr;
   return MGPU_OK;
 }
@@ -1792,15 +2028,12 @@ int32_t mgpu_chips_host_blob_ex(int32_t index_system, int64_t n_chips, const int
     if (int32_t st = check_build_opts(*opts)) return st;
     bo = *opts;
   }
-  std::vector<uint8_t> host;
+  HostBlob host;
   BlobHeader hdr;
   if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr, bo))
     return st;
-  uint8_t* p = (uint8_t*)malloc(host.size());
-  if (!p) return fail(MGPU_E_INTERNAL, "out of host memory (%zu bytes)", host.size());
-  memcpy(p, host.data(), host.size());
-  *out = p;
   *bytes = (int64_t)host.size();
+  *out = host.release();  // (malloc'd: mgpu_host_free)
   return MGPU_OK;
 }
 
@@ -1842,7 +2075,7 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
                           const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
                           const uint8_t* wkb, mgpu_chips** out) {
   if (!ctx || !out) return fail(MGPU_E_INVALID_ARG, "ctx/out is NULL");
-  std::vector<uint8_t> host;
+  HostBlob host;
   BlobHeader hdr;
   if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr,
                               build_opts_of(ctx)))
@@ -2463,7 +2696,7 @@ int32_t mgpu_test_chip_contains_host(int32_t index_system, int64_t n_chips, cons
                                      const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
                                      const uint8_t* wkb, int64_t n, const int64_t* chip_row, const double* x,
                                      const double* y, int8_t* out_join_path, int8_t* out_point_locator) {
-  std::vector<uint8_t> host;
+  HostBlob host;
   BlobHeader hdr;
   mgpu_build_opts bo;
   mgpu_build_opts_default(&bo);
@@ -2495,7 +2728,7 @@ int32_t mgpu_test_raster_host(int32_t index_system, int32_t res, int64_t n_chips
                               const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
                               const uint8_t* wkb, int64_t n, const double* x, const double* y, int8_t* out_kind,
                               uint32_t* out_first, uint32_t* out_mask, int32_t* out_chip_poly) {
-  std::vector<uint8_t> host;
+  HostBlob host;
   BlobHeader hdr;
   mgpu_build_opts bo;  // (the BNG pixel index too: this hook tests the index itself)
   mgpu_build_opts_default(&bo);

@@ -112,7 +112,53 @@ int32_t comm_failed(mgpu_ctx* ctx, const char* what, ncclResult_t r) {
   ctx->comm = nullptr;
   return st;
 }
+
+// A receiving rank's side of step 1: read the broadcast header, size and allocate the
+// receiving table.  Returns its status (MGPU_OK or the error class, *why the reason);
+// fail_alloc (test hook only) makes the allocation fail.
+int32_t receiver_prepare(const void* hdr_dev, hipStream_t s, bool fail_alloc, int64_t* bytes, void** dst,
+                         const char** why) {
+  *bytes = 0;
+  *dst = nullptr;
+  std::vector<uint8_t> h((size_t)mgpu::kBlobHeaderSize);
+  if (hipMemcpyAsync(h.data(), hdr_dev, h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    *why = "reading the broadcast header";
+    return MGPU_E_DEVICE;
+  }
+  *bytes = mgpu::blob_bytes_of_header(h.data());
+  if (*bytes < mgpu::kBlobHeaderSize) {
+    *why = "the root sent no chip-table blob";
+    return MGPU_E_INVALID_ARG;
+  }
+  if (fail_alloc || hipMalloc(dst, (size_t)*bytes) != hipSuccess) {
+    *dst = nullptr;
+    *why = "hipMalloc of the receiving table";
+    return MGPU_E_DEVICE;
+  }
+  return MGPU_OK;
+}
 }  // namespace
+
+// TEST ONLY: the receiving rank's path without RCCL -- header read, allocation (forced to
+// fail with fail_alloc), the blob's bytes copied in as the bulk broadcast would, adoption.
+int32_t mgpu_test_receive_blob(mgpu_ctx* ctx, const void* dev_blob, int32_t fail_alloc, mgpu_chips** out) {
+  if (!ctx || !dev_blob || !out) return mgpu::set_error(MGPU_E_INVALID_ARG, "receive_blob: NULL argument");
+  *out = nullptr;
+  HIP_TRY(hipSetDevice(ctx->device));
+  int64_t bytes = 0;
+  void* dst = nullptr;
+  const char* why = "";
+  if (int32_t st = receiver_prepare(dev_blob, nullptr, fail_alloc != 0, &bytes, &dst, &why))
+    return mgpu::set_error(st, "chips_broadcast: %s", why);
+  if (hipMemcpy(dst, dev_blob, (size_t)bytes, hipMemcpyDeviceToDevice) != hipSuccess) {
+    hipFree(dst);
+    return mgpu::set_error(MGPU_E_DEVICE, "receive_blob: copy");
+  }
+  int32_t st = mgpu::adopt_device_blob(ctx, dst, bytes, out);
+  if (st) hipFree(dst);
+  return st;
+}
 
 int32_t mgpu_chips_broadcast(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t root, mgpu_chips** out, void* stream) {
   if (!ctx || !ctx->comm || !out) return mgpu::set_error(MGPU_E_INVALID_ARG, "chips_broadcast: no communicator / out");
@@ -138,19 +184,15 @@ int32_t mgpu_chips_broadcast(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t roo
     if (root_ok) bytes = (int64_t)chips->bytes;
     else mine = MGPU_E_INVALID_ARG, why = "the root needs its chip table on the context's GPU";
   } else {
-    std::vector<uint8_t> h((size_t)mgpu::kBlobHeaderSize);
-    if (hipMemcpyAsync(h.data(), c->scratch, h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess) {
-      mine = MGPU_E_DEVICE, why = "reading the broadcast header";
-    } else {
-      bytes = mgpu::blob_bytes_of_header(h.data());
-      if (bytes < mgpu::kBlobHeaderSize) mine = MGPU_E_INVALID_ARG, why = "the root sent no chip-table blob";
-      else if (hipMalloc(&dst, (size_t)bytes) != hipSuccess) dst = nullptr, mine = MGPU_E_DEVICE, why = "hipMalloc of the receiving table";
-    }
+    mine = receiver_prepare(c->scratch, s, false, &bytes, &dst, &why);
   }
-  // 2. agreement: the smallest status (errors are negative) over all ranks
+  // 2. agreement: the smallest status (errors are negative) over all ranks.  The status
+  // word is first set negative on the stream, so a failed copy of `mine` still
+  // contributes a failure (never a stale OK from an earlier call)
   int32_t agreed = mine;
-  if (hipMemcpyAsync(status, &mine, 4, hipMemcpyHostToDevice, s) != hipSuccess) agreed = MGPU_E_DEVICE;
+  if (hipMemsetAsync(status, 0x80, 4, s) != hipSuccess ||
+      hipMemcpyAsync(status, &mine, 4, hipMemcpyHostToDevice, s) != hipSuccess)
+    agreed = MGPU_E_DEVICE;
   r = ncclAllReduce(status, status, 1, ncclInt32, ncclMin, c->comm, s);
   if (r != ncclSuccess) {
     if (dst) hipFree(dst);
@@ -192,9 +234,11 @@ int32_t mgpu_pair_offsets(mgpu_ctx* ctx, int64_t local_pairs, int64_t* out_offse
   hipStream_t s = (hipStream_t)stream;
   int64_t* mine = (int64_t*)c->scratch;
   int64_t* all = mine + 1;
-  // a negative count still takes part in the all-gather (as -1): every rank then fails
+  // a negative count still takes part in the all-gather (as -1): every rank then fails.
+  // The slot is set to -1 on the stream first, so a failed copy also contributes -1
+  // instead of returning before the collective the other ranks wait in
   const int64_t v = local_pairs < 0 ? -1 : local_pairs;
-  HIP_TRY(hipMemcpyAsync(mine, &v, 8, hipMemcpyHostToDevice, s));
+  if (hipMemsetAsync(mine, 0xFF, 8, s) == hipSuccess) (void)hipMemcpyAsync(mine, &v, 8, hipMemcpyHostToDevice, s);
   ncclResult_t r = ncclAllGather(mine, all, 1, ncclInt64, c->comm, s);
   if (r != ncclSuccess) return comm_failed(ctx, "ncclAllGather(pair counts)", r);
   std::vector<int64_t> counts((size_t)c->world);

@@ -97,6 +97,17 @@ struct WkbSeq {
   MGPU_DEC double y(int64_t i) const { return rd_f64(*b, o + 8 * dims * i + 8, le); }
 };
 
+// A coordinate sequence as JTS's non-strict WKBReader repairs it: n points, those past the
+// read ones copies of the first (rings: createClosedRing) or of the last (a one-point
+// LineString: extend -- the same point)
+template <class S>
+struct Repaired {
+  S s;
+  uint32_t n;
+  MGPU_DEC double x(int64_t i) const { return s.x(i < (int64_t)s.n ? i : 0); }
+  MGPU_DEC double y(int64_t i) const { return s.y(i < (int64_t)s.n ? i : 0); }
+};
+
 // Orientation.isCCW(CoordinateSequence) of JTS 1.20: the first highest point reached by
 // a rising segment, the next lower point after it; a pointed cap by its orientation
 // index, a flat cap by the direction of its top; flat or degenerate rings are not CCW
@@ -287,8 +298,9 @@ MGPU_DEC int wkb_centroid_any(const B& p, int64_t len, double* x, double* y) {
         o += 4 + (int64_t)8 * d * q.n;
         if (o > len) return kDecMalformed;
         if (t == 2) {
-          if (q.n == 1) return kDecMalformed;  // (JTS: a LineString of one point)
-          if (q.n) c.add_line(q);
+          // WKBReader (not strict, its default) extends a one-point LineString with its
+          // last point (CoordinateSequences.extend): a zero-length line
+          if (q.n) c.add_line(Repaired<WkbSeq<B>>{q, q.n == 1 ? 2u : q.n});
           continue;
         }
         if (q.n == 0) {
@@ -301,8 +313,11 @@ MGPU_DEC int wkb_centroid_any(const B& p, int64_t len, double* x, double* y) {
           }
           continue;
         }
-        if (q.n < 4 || q.x(0) != q.x(q.n - 1) || q.y(0) != q.y(q.n - 1)) return kDecMalformed;  // LinearRing
-        c.add_ring(q, r == 0);
+        // WKBReader (not strict) repairs a ring that is not one (CoordinateSequences.
+        // ensureValidRing): fewer than 4 points are padded to 4 with the first point, an
+        // open ring is closed with it
+        const bool closed = q.x(0) == q.x(q.n - 1) && q.y(0) == q.y(q.n - 1);
+        c.add_ring(Repaired<WkbSeq<B>>{q, q.n <= 3 ? 4u : (closed ? q.n : q.n + 1)}, r == 0);
       }
     } else if (t >= 4 && t <= 7) {
       if (o + 4 > len) return kDecMalformed;

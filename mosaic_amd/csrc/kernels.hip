@@ -1079,10 +1079,22 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
       }
       uint32_t cl[kCfyBatch];
       uint64_t ge[kCfyBatch];
+#ifndef MGPU_CFY_ABLATE
+#define MGPU_CFY_ABLATE 0  // profiling only (wrong answers): 1 no lookups, 2 LDS blocks only, 3 no sub-pixels
+#endif
 #pragma unroll
       for (int k = 0; k < kCfyBatch; k++) {
+#if MGPU_CFY_ABLATE == 1
+        cl[k] = ri[k] < kRasterFull ? (ri[k] & 1) : kPixEmpty;
+#elif MGPU_CFY_ABLATE == 2
+        cl[k] = ri[k] < kRasterFull && bi[k] != kNoPixel && s_blk[bi[k]] != kPixMixed ? s_blk[bi[k]] : kPixEmpty;
+#elif MGPU_CFY_ABLATE == 3
+        cl[k] = ri[k] < kRasterFull ? (bi[k] != kNoPixel && s_blk[bi[k]] != kPixMixed ? s_blk[bi[k]] : t.raster[ri[k]])
+                                    : kPixEmpty;
+#else
         cl[k] = ri[k] < kRasterFull ? raster_class_blk(t, s_blk, ri[k], bi[k], sb[k])
                                     : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
+#endif
         ge[k] = (IS == MGPU_BNG && ri[k] < kRasterFull) ? t.grid[gix[k]] : 0ull;
       }
 #pragma unroll

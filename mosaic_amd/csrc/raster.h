@@ -73,10 +73,20 @@ MGPU_HDI uint32_t raster_index(const ChipTableView& t, double px, double py, boo
 
 // The class of pixel ri (a raster_index result below kRasterFull), refined by its
 // second level when the pixel is mixed.
+#ifndef MGPU_RANK_SPEC
+#define MGPU_RANK_SPEC 0
+#endif
 MGPU_HDI uint32_t raster_class(const ChipTableView& t, uint32_t ri, uint32_t sub) {
+#if MGPU_RANK_SPEC
+  // the rank word loads beside the pixel's class (no second round trip for mixed pixels)
+  const RankWord w = t.raster_rank ? t.raster_rank[ri >> 5] : RankWord{0u, 0u};
+  uint32_t cl = t.raster[ri];
+  if (cl == kPixMixed) {
+#else
   uint32_t cl = t.raster[ri];
   if (cl == kPixMixed && t.raster_rank) {
     const RankWord w = t.raster_rank[ri >> 5];
+#endif
     const uint32_t bit = 1u << (ri & 31);
     if (w.bits & bit) {
       const uint64_t b = (uint64_t)w.base + (uint64_t)__builtin_popcount(w.bits & (bit - 1));

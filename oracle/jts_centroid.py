@@ -180,6 +180,19 @@ class Centroid:
         return None
 
 
+def _ensure_valid_ring(pts):
+    """JTS WKBReader, not strict (its default): CoordinateSequences.ensureValidRing --
+    fewer than 4 points padded to 4 with the first, an open ring closed with it."""
+    n = len(pts)
+    if n == 0:
+        return pts
+    if n <= 3:
+        return list(pts) + [pts[0]] * (4 - n)
+    if pts[0][0] == pts[-1][0] and pts[0][1] == pts[-1][1]:
+        return pts
+    return list(pts) + [pts[0]]
+
+
 def _read(b, o, c):
     """One WKB geometry at o into the accumulator; returns the next offset."""
     le = b[o] == 1
@@ -211,6 +224,8 @@ def _read(b, o, c):
         return o + 8 * d
     if t == 2:
         pts, o = seq(o)
+        if len(pts) == 1:  # non-strict WKBReader: CoordinateSequences.extend to 2 points
+            pts = pts * 2
         if pts:
             c.segments(pts)
         return o
@@ -220,7 +235,7 @@ def _read(b, o, c):
         rings = []
         for _ in range(nr):
             pts, o = seq(o)
-            rings.append(pts)
+            rings.append(_ensure_valid_ring(pts))
         if rings and rings[0]:
             for k, r in enumerate(rings):
                 if r:

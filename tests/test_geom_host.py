@@ -225,7 +225,7 @@ def test_centroid_any_wkb_equals_jts_restatement():
 
 def test_centroid_special_cases():
     """Flat / degenerate rings, zero-length lines (their first point), empty members,
-    malformed rings and hex text."""
+    rings and lines the non-strict WKBReader repairs, and hex text."""
     sq = [(0.0, 0.0), (2.0, 0.0), (2.0, 2.0), (0.0, 2.0), (0.0, 0.0)]
     flat = [(0.0, 1.0), (3.0, 1.0), (1.0, 1.0), (0.0, 1.0)]  # zero area: the lines decide
     for g in [("poly", [sq]), ("poly", [sq[::-1]]), ("poly", [flat]), ("line", [(1.0, 1.0), (1.0, 1.0)]),
@@ -236,9 +236,16 @@ def test_centroid_special_cases():
         assert decode(N.MGPU_GEOM_WKB, w)[1:] == JC.centroid_wkb(w), g
     assert decode(N.MGPU_GEOM_WKB, w_geom("poly", [sq]))[1:] == (1.0, 1.0)
     assert decode(N.MGPU_GEOM_WKB, w_geom("collection", []))[0] == 3  # empty
-    assert decode(N.MGPU_GEOM_WKB, w_geom("line", [(1.0, 1.0)]))[0] == 1  # one-point line
-    assert decode(N.MGPU_GEOM_WKB, w_geom("poly", [sq[:-1]]))[0] == 1  # ring not closed
-    assert decode(N.MGPU_GEOM_WKB, w_geom("poly", [sq[:2] + sq[:1]]))[0] == 1  # a LinearRing needs 4 points
+    # JTS 1.20's WKBReader is not strict by default: it repairs a one-point line (extended
+    # to two) and rings that are not rings (ensureValidRing: closed, padded to 4 points);
+    # the oracle restates the same repair
+    for g in [("line", [(1.0, 1.0)]), ("poly", [sq[:-1]]), ("poly", [sq[:2] + sq[:1]]), ("poly", [sq[:3]]),
+              ("poly", [sq, [(0.5, 0.5), (1.0, 0.5), (1.0, 1.0)]]), ("mline", [[(2.0, 3.0)], [(0.0, 0.0), (3.0, 4.0)]])]:
+        w = w_geom(*g)
+        st, x, y = decode(N.MGPU_GEOM_WKB, w)
+        assert st == 0 and (x, y) == JC.centroid_wkb(w), (g, (x, y), JC.centroid_wkb(w))
+    assert decode(N.MGPU_GEOM_WKB, w_geom("line", [(1.0, 1.0)]))[1:] == (1.0, 1.0)
+    assert decode(N.MGPU_GEOM_WKB, w_geom("poly", [sq[:-1]]))[1:] == (1.0, 1.0)  # closed: the square
     assert decode(N.MGPU_GEOM_HEX, w_geom("point", (1.0, 2.0)).hex() + "0")[0] == 0  # odd last char ignored
     assert decode(N.MGPU_GEOM_HEX, "01zz")[0] == 1
 

@@ -744,3 +744,28 @@ def test_comm_single_rank(gpu, nyc_chips_r9):
     r2 = M.pip_join(T(x, gpu), T(y, gpu), b, 9).numpy()
     assert np.array_equal(r1[0], r2[0]) and np.array_equal(r1[1], r2[1])
     ctx.close()
+
+
+def test_broadcast_receiver_path(gpu, nyc_chips_r9):
+    """The receiving rank's side of mgpu_chips_broadcast (mgpu_test_receive_blob: the same
+    header check, allocation and adoption, the bulk copy done locally): a valid blob joins
+    like the original; a corrupt header and a failed allocation return errors at once."""
+    import ctypes
+    from mosaic_amd import _native as N
+    from mosaic_amd import dist as D
+    ctx = M.default_context(gpu)
+    d = nyc_chips_r9.upload(ctx)
+    blob = torch.from_numpy(np.frombuffer(D.host_blob(nyc_chips_r9), np.uint8).copy()).to(gpu)
+    out = ctypes.c_void_p()
+    N.check(N.lib().mgpu_test_receive_blob(ctx.handle, blob.data_ptr(), 0, ctypes.byref(out)))
+    got = M.DeviceChips(None, ctx, handle=out)
+    x, y = nyc_points(50_000, 37)
+    r1 = M.pip_join(T(x, gpu), T(y, gpu), d, 9).numpy()
+    r2 = M.pip_join(T(x, gpu), T(y, gpu), got, 9).numpy()
+    assert np.array_equal(r1[0], r2[0]) and np.array_equal(r1[1], r2[1])
+    bad = blob.clone()
+    bad[:8] = 0  # no magic: "the root sent no chip-table blob"
+    st = N.lib().mgpu_test_receive_blob(ctx.handle, bad.data_ptr(), 0, ctypes.byref(out))
+    assert st == N.MGPU_E_INVALID_ARG and "no chip-table blob" in N.last_error()
+    st = N.lib().mgpu_test_receive_blob(ctx.handle, blob.data_ptr(), 1, ctypes.byref(out))
+    assert st == N.MGPU_E_DEVICE and "hipMalloc" in N.last_error()
