@@ -139,8 +139,10 @@ def test_h3_neighbor_tables_consistent_away_from_pentagons():
     """Derived base-cell neighbour tables (tools/gen_h3_neighbors.py): at every
     resolution, cells whose 2-neighbourhood stays among hexagon base cells have 19
     distinct kRing(2) ids, mutual kRing(1) adjacency, and hexRing(2) == kRing(2)'s
-    outer 12 (same cyclic order, started at the cell two steps in I).  (Pentagon neighbourhoods are checked by tools/h3_pentagon_diag.py;
-    the device path refuses them.)"""
+    outer 12 (same cyclic order, started at the cell two steps in I).  (Pentagon neighbourhoods,
+    which the device path walks as H3 does, are checked against the oracle by
+    test_gpu_parity.py's pentagon kRing tests and as geometric balls by
+    test_h3_kring_geometry_host.py.)"""
     pent = {4, 14, 24, 38, 49, 58, 63, 72, 83, 97, 107, 117}
     rng = np.random.default_rng(7)
     tested = 0
