@@ -143,9 +143,11 @@ int32_t mgpu_points_to_cells(mgpu_ctx* ctx, int32_t index_system, int32_t res,
  * hex WKB, JSONType as GeoJSON, then getCentroid -- JTS Centroid: area-weighted for
  * polygons, length-weighted for lines, the mean of points -- then pointToIndex).  Rows
  * are data[offsets[i] .. offsets[i + 1]) (the Arrow binary / utf8 layout).  WKB / HEX:
- * every geometry type (big- or little-endian, EWKB / ISO Z, M, nested collections);
- * WKT (Java Double.parseDouble rounding) and GeoJSON: POINT and MULTIPOINT, other types
- * return MGPU_E_UNSUPPORTED.  Malformed rows MGPU_E_WKB (JTS ParseException), empty
+ * every geometry type (big- or little-endian, EWKB / ISO Z, M, nested collections; the
+ * rings and one-point lines JTS's non-strict WKBReader repairs are repaired); WKT (Java
+ * Double.parseDouble rounding; WKTReader) and GeoJSON (GeoJsonReader): every type, Z / M
+ * ignored, collections nested up to 8 deep, strict rings.  Malformed rows MGPU_E_WKB (JTS
+ * ParseException / IllegalArgumentException), empty
  * geometries MGPU_E_EMPTY.  `valid` (optional Arrow bitmap, bit offset valid_offset): null rows are
  * null out -- out_cell 0 and a 0 bit in out_valid ((n + 7) / 8 bytes, optional).
  * mgpu_points_from_geometry stops at the point (x, y; NaN for null rows).  Device

@@ -394,48 +394,6 @@ MGPU_DEC void wkt_dims(const char* s, int64_t len, int64_t* i) {
   if (!keyword(s, len, i, "zm") && !keyword(s, len, i, "z")) keyword(s, len, i, "m");
 }
 
-// centroid of a WKT POINT / MULTIPOINT
-MGPU_DEC int wkt_centroid(const char* s, int64_t len, double* x, double* y) {
-  int64_t i = 0;
-  skip_ws(s, len, &i);
-  if (keyword(s, len, &i, "point")) {
-    wkt_dims(s, len, &i);
-    skip_ws(s, len, &i);
-    if (keyword(s, len, &i, "empty")) return kDecEmpty;
-    if (!wkt_char(s, len, &i, '(') || !wkt_coord(s, len, &i, x, y) || !wkt_char(s, len, &i, ')')) return kDecMalformed;
-    return kDecOk;
-  }
-  if (keyword(s, len, &i, "multipoint")) {
-    wkt_dims(s, len, &i);
-    skip_ws(s, len, &i);
-    if (keyword(s, len, &i, "empty")) return kDecEmpty;
-    if (!wkt_char(s, len, &i, '(')) return kDecMalformed;
-    double sx = 0.0, sy = 0.0;
-    uint32_t cnt = 0;
-    for (;;) {
-      skip_ws(s, len, &i);
-      double px, py;
-      if (keyword(s, len, &i, "empty")) {
-      } else if (wkt_char(s, len, &i, '(')) {  // MULTIPOINT ((x y), ...)
-        if (!wkt_coord(s, len, &i, &px, &py) || !wkt_char(s, len, &i, ')')) return kDecMalformed;
-        sx += px, sy += py, cnt++;
-      } else {  // MULTIPOINT (x y, ...)
-        if (!wkt_coord(s, len, &i, &px, &py)) return kDecMalformed;
-        sx += px, sy += py, cnt++;
-      }
-      if (wkt_char(s, len, &i, ',')) continue;
-      if (wkt_char(s, len, &i, ')')) break;
-      return kDecMalformed;
-    }
-    if (!cnt) return kDecEmpty;
-    *x = sx / cnt;
-    *y = sy / cnt;
-    return kDecOk;
-  }
-  return kDecUnsupported;
-}
-
-
 // ---------------------------------------------------------------- GeoJSON (JTS GeoJsonReader)
 // A value at *i skipped (string, number, literal, array, object); false if malformed
 MGPU_DEC bool json_skip(const char* s, int64_t len, int64_t* i) {
@@ -501,60 +459,269 @@ MGPU_DEC bool json_position(const char* s, int64_t len, int64_t* i, double* x, d
     return wkt_char(s, len, i, ']') && *n >= 2;
   }
 }
-MGPU_DEC int json_centroid(const char* s, int64_t len, double* x, double* y) {
-  int64_t i = 0;
-  if (!wkt_char(s, len, &i, '{')) return kDecMalformed;
-  int64_t type_b = -1, type_e = -1, coord = -1;
-  if (!wkt_char(s, len, &i, '}')) {
-    for (;;) {
-      skip_ws(s, len, &i);
-      const int64_t kb = i;
-      if (!json_skip(s, len, &i)) return kDecMalformed;
-      const int64_t ke = i;
-      if (!wkt_char(s, len, &i, ':')) return kDecMalformed;
-      skip_ws(s, len, &i);
-      const int64_t vb = i;
-      if (!json_skip(s, len, &i)) return kDecMalformed;
-      if (json_str_is(s, len, kb, ke, "type")) type_b = vb, type_e = i;
-      if (json_str_is(s, len, kb, ke, "coordinates")) coord = vb;
-      if (wkt_char(s, len, &i, ',')) continue;
-      if (wkt_char(s, len, &i, '}')) break;
-      return kDecMalformed;
+// A coordinate sequence in text -- WKT "(x y, x y, ...)" (J = false) or GeoJSON
+// "[[x, y], [x, y], ...]" (J = true) -- whose opening bracket is at offset b, n points,
+// read by a forward cursor (the Centroid and isCCW walks visit points in order, stepping
+// back one at most; an earlier point restarts the cursor).  Validated by text_seq_scan.
+template <bool J>
+struct TextSeq {
+  const char* s;
+  int64_t len, b;
+  uint32_t n;
+  mutable int64_t k = -1, pos = 0;
+  mutable double cx = 0, cy = 0, px = 0, py = 0;
+  MGPU_DEC void step() const {
+    if (k < 0) pos = b + 1;
+    else wkt_char(s, len, &pos, ',');
+    px = cx, py = cy;
+    if (J) {
+      int m;
+      json_position(s, len, &pos, &cx, &cy, &m);
+    } else {
+      wkt_coord(s, len, &pos, &cx, &cy);
     }
+    k++;
   }
-  if (type_b < 0 || s[type_b] != '"') return kDecMalformed;
-  const bool point = json_str_is(s, len, type_b, type_e, "Point");
-  const bool multi = json_str_is(s, len, type_b, type_e, "MultiPoint");
-  if (!point && !multi) {
-    const char* known[] = {"LineString", "MultiLineString", "Polygon", "MultiPolygon", "GeometryCollection"};
-    for (const char* k : known)
-      if (json_str_is(s, len, type_b, type_e, k)) return kDecUnsupported;
-    return kDecMalformed;
+  MGPU_DEC void seek(int64_t i) const {
+    if (i < k - 1) k = -1;
+    while (k < i) step();
   }
-  if (coord < 0) return kDecMalformed;
-  int64_t j = coord;
-  int n;
-  if (point) {
-    if (!json_position(s, len, &j, x, y, &n)) return kDecMalformed;
-    return n ? kDecOk : kDecEmpty;
+  MGPU_DEC double x(int64_t i) const {
+    seek(i);
+    return i == k ? cx : px;
   }
-  if (!wkt_char(s, len, &j, '[')) return kDecMalformed;
-  double sx = 0.0, sy = 0.0;
-  int64_t cnt = 0;
-  if (!wkt_char(s, len, &j, ']')) {
-    for (;;) {
-      double px, py;
-      if (!json_position(s, len, &j, &px, &py, &n)) return kDecMalformed;
-      if (n) sx += px, sy += py, cnt++;
-      if (wkt_char(s, len, &j, ',')) continue;
-      if (wkt_char(s, len, &j, ']')) break;
-      return kDecMalformed;
+  MGPU_DEC double y(int64_t i) const {
+    seek(i);
+    return i == k ? cy : py;
+  }
+};
+
+// The sequence at *i ("(" coords ")" / "[" positions "]"): its offset and point count,
+// *i past it; the first and last points (rings: closure).  False if malformed (GeoJSON: a
+// position with fewer than two numbers; "[]" is an empty sequence).
+template <bool J>
+MGPU_DEC bool text_seq_scan(const char* s, int64_t len, int64_t* i, TextSeq<J>* q, double* x0, double* y0,
+                            double* x1, double* y1) {
+  skip_ws(s, len, i);
+  q->s = s, q->len = len, q->b = *i, q->n = 0;
+  if (!wkt_char(s, len, i, J ? '[' : '(')) return false;
+  if (J && wkt_char(s, len, i, ']')) return true;
+  for (;;) {
+    double x, y;
+    if (J) {
+      int m;
+      if (!json_position(s, len, i, &x, &y, &m) || m < 2) return false;
+    } else if (!wkt_coord(s, len, i, &x, &y)) {
+      return false;
     }
+    if (q->n == 0) *x0 = x, *y0 = y;
+    *x1 = x, *y1 = y;
+    q->n++;
+    if (wkt_char(s, len, i, ',')) continue;
+    return wkt_char(s, len, i, J ? ']' : ')');
   }
-  if (!cnt) return kDecEmpty;
-  *x = sx / cnt;
-  *y = sy / cnt;
+}
+
+// A LineString / LinearRing sequence into the accumulator, as JTS's WKTReader and
+// GeoJsonReader build them (strict: a LineString of one point and a ring that is not
+// closed or has fewer than 4 points throw -- malformed)
+template <bool J>
+MGPU_DEC int text_line(const char* s, int64_t len, int64_t* i, Centroid& c) {
+  TextSeq<J> q;
+  double x0, y0, x1, y1;
+  if (!text_seq_scan<J>(s, len, i, &q, &x0, &y0, &x1, &y1)) return kDecMalformed;
+  if (q.n == 1) return kDecMalformed;
+  if (q.n) c.add_line(q);
   return kDecOk;
+}
+template <bool J>
+MGPU_DEC int text_polygon(const char* s, int64_t len, int64_t* i, Centroid& c) {
+  if (!wkt_char(s, len, i, J ? '[' : '(')) return kDecMalformed;
+  if (J && wkt_char(s, len, i, ']')) return kDecOk;  // an empty polygon
+  for (int r = 0;; r++) {
+    TextSeq<J> q;
+    double x0, y0, x1, y1;
+    if (!text_seq_scan<J>(s, len, i, &q, &x0, &y0, &x1, &y1)) return kDecMalformed;
+    if (q.n == 0) {
+      if (r == 0) return kDecMalformed;  // (an empty shell with holes)
+    } else {
+      if (q.n < 4 || x0 != x1 || y0 != y1) return kDecMalformed;
+      c.add_ring(q, r == 0);
+    }
+    if (wkt_char(s, len, i, ',')) continue;
+    return wkt_char(s, len, i, J ? ']' : ')') ? kDecOk : kDecMalformed;
+  }
+}
+
+// JTS Centroid of a WKT geometry (WKTReader: every type, Z / M / ZM, EMPTY members,
+// collections nested up to 8 deep)
+MGPU_DEC int wkt_centroid(const char* s, int64_t len, double* x, double* y) {
+  Centroid c;
+  int64_t i = 0;
+  int depth = 0;  // open GEOMETRYCOLLECTION levels
+  for (;;) {
+    skip_ws(s, len, &i);
+    int t = 0;
+    if (keyword(s, len, &i, "point")) t = 1;
+    else if (keyword(s, len, &i, "linestring")) t = 2;
+    else if (keyword(s, len, &i, "linearring")) t = 8;
+    else if (keyword(s, len, &i, "polygon")) t = 3;
+    else if (keyword(s, len, &i, "multipoint")) t = 4;
+    else if (keyword(s, len, &i, "multilinestring")) t = 5;
+    else if (keyword(s, len, &i, "multipolygon")) t = 6;
+    else if (keyword(s, len, &i, "geometrycollection")) t = 7;
+    else return depth == 0 && i < len && (s[i] | 32) >= 'a' && (s[i] | 32) <= 'z' ? kDecUnsupported : kDecMalformed;
+    wkt_dims(s, len, &i);
+    skip_ws(s, len, &i);
+    if (!keyword(s, len, &i, "empty")) {
+      int st = kDecOk;
+      if (t == 1) {
+        double px, py;
+        if (!wkt_char(s, len, &i, '(') || !wkt_coord(s, len, &i, &px, &py) || !wkt_char(s, len, &i, ')')) return kDecMalformed;
+        c.add_point(px, py);
+      } else if (t == 2) {
+        st = text_line<false>(s, len, &i, c);
+      } else if (t == 8) {  // a LinearRing: closed, at least 4 points; its centroid is a line's
+        TextSeq<false> q;
+        double x0, y0, x1, y1;
+        if (!text_seq_scan<false>(s, len, &i, &q, &x0, &y0, &x1, &y1) || q.n < 4 || x0 != x1 || y0 != y1) return kDecMalformed;
+        c.add_line(q);
+      } else if (t == 3) {
+        st = text_polygon<false>(s, len, &i, c);
+      } else if (t == 7) {
+        if (!wkt_char(s, len, &i, '(')) return kDecMalformed;
+        if (depth == 8) return kDecUnsupported;
+        depth++;
+        continue;  // its first member
+      } else {
+        if (!wkt_char(s, len, &i, '(')) return kDecMalformed;
+        for (;;) {
+          skip_ws(s, len, &i);
+          if (keyword(s, len, &i, "empty")) {
+          } else if (t == 4) {
+            double px, py;
+            const bool paren = wkt_char(s, len, &i, '(');  // MULTIPOINT ((x y), ...) or (x y, ...)
+            if (!wkt_coord(s, len, &i, &px, &py) || (paren && !wkt_char(s, len, &i, ')'))) return kDecMalformed;
+            c.add_point(px, py);
+          } else {
+            st = t == 5 ? text_line<false>(s, len, &i, c) : text_polygon<false>(s, len, &i, c);
+            if (st) return st;
+          }
+          if (wkt_char(s, len, &i, ',')) continue;
+          if (wkt_char(s, len, &i, ')')) break;
+          return kDecMalformed;
+        }
+      }
+      if (st) return st;
+    }
+    // one geometry done: close the collections it ends
+    bool next = false;
+    while (depth > 0 && !next) {
+      if (wkt_char(s, len, &i, ',')) next = true;
+      else if (wkt_char(s, len, &i, ')')) depth--;
+      else return kDecMalformed;
+    }
+    if (!next) break;
+  }
+  return c.result(x, y);
+}
+
+
+// The members "type" (its string's extent), "coordinates" and "geometries" (value
+// offsets, -1 if absent) of the GeoJSON object at *i; *i past it
+MGPU_DEC bool json_object(const char* s, int64_t len, int64_t* i, int64_t* type_b, int64_t* type_e, int64_t* coord,
+                          int64_t* geoms) {
+  *type_b = *type_e = *coord = *geoms = -1;
+  if (!wkt_char(s, len, i, '{')) return false;
+  if (wkt_char(s, len, i, '}')) return true;
+  for (;;) {
+    skip_ws(s, len, i);
+    const int64_t kb = *i;
+    if (!json_skip(s, len, i)) return false;
+    const int64_t ke = *i;
+    if (!wkt_char(s, len, i, ':')) return false;
+    skip_ws(s, len, i);
+    const int64_t vb = *i;
+    if (!json_skip(s, len, i)) return false;
+    if (json_str_is(s, len, kb, ke, "type")) *type_b = vb, *type_e = *i;
+    if (json_str_is(s, len, kb, ke, "coordinates")) *coord = vb;
+    if (json_str_is(s, len, kb, ke, "geometries")) *geoms = vb;
+    if (wkt_char(s, len, i, ',')) continue;
+    return wkt_char(s, len, i, '}');
+  }
+}
+
+// JTS Centroid of a GeoJSON geometry (GeoJsonReader: every type, members in any order,
+// GeometryCollection "geometries" nested up to 8 deep)
+MGPU_DEC int json_centroid(const char* s, int64_t len, double* x, double* y) {
+  Centroid c;
+  int64_t stack[8];  // per open collection: the offset of its next member
+  int depth = 0;
+  int64_t at = 0;
+  for (;;) {
+    int64_t tb, te, coord, geoms;
+    if (!json_object(s, len, &at, &tb, &te, &coord, &geoms)) return kDecMalformed;
+    if (tb < 0 || s[tb] != '"') return kDecMalformed;
+    int t = 0;
+    const char* names[] = {"Point", "LineString", "Polygon", "MultiPoint", "MultiLineString", "MultiPolygon",
+                           "GeometryCollection"};
+    for (int k = 0; k < 7 && !t; k++)
+      if (json_str_is(s, len, tb, te, names[k])) t = k + 1;
+    if (!t) return kDecMalformed;
+    if (t == 7) {
+      if (geoms < 0) return kDecMalformed;
+      int64_t j = geoms;
+      if (!wkt_char(s, len, &j, '[')) return kDecMalformed;
+      if (!wkt_char(s, len, &j, ']')) {
+        if (depth == 8) return kDecUnsupported;
+        stack[depth++] = at;
+        at = j;
+        continue;  // its first member
+      }
+    } else {
+      if (coord < 0) return kDecMalformed;
+      int64_t j = coord;
+      int st = kDecOk;
+      if (t == 1) {
+        double px, py;
+        int m;
+        if (!json_position(s, len, &j, &px, &py, &m) || m == 1) return kDecMalformed;
+        if (m) c.add_point(px, py);
+      } else if (t == 2) {
+        st = text_line<true>(s, len, &j, c);
+      } else if (t == 3) {
+        st = text_polygon<true>(s, len, &j, c);
+      } else {
+        if (!wkt_char(s, len, &j, '[')) return kDecMalformed;
+        if (!wkt_char(s, len, &j, ']')) {
+          for (;;) {
+            if (t == 4) {
+              double px, py;
+              int m;
+              if (!json_position(s, len, &j, &px, &py, &m) || m == 1) return kDecMalformed;
+              if (m) c.add_point(px, py);
+            } else {
+              st = t == 5 ? text_line<true>(s, len, &j, c) : text_polygon<true>(s, len, &j, c);
+              if (st) return st;
+            }
+            if (wkt_char(s, len, &j, ',')) continue;
+            if (wkt_char(s, len, &j, ']')) break;
+            return kDecMalformed;
+          }
+        }
+      }
+      if (st) return st;
+    }
+    // one member done: the next one of its collection, or close collections
+    bool next = false;
+    while (depth > 0 && !next) {
+      if (wkt_char(s, len, &at, ',')) next = true;
+      else if (wkt_char(s, len, &at, ']')) at = stack[--depth];
+      else return kDecMalformed;
+    }
+    if (!next) break;
+  }
+  return c.result(x, y);
 }
 
 // ---------------------------------------------------------------- Mosaic's InternalGeometryType

@@ -131,7 +131,8 @@ def test_wkt_points():
     assert decode(W, "POINT EMPTY")[0] == 3
     assert decode(W, "POINT (1)")[0] == 1
     assert decode(W, "POINT (1 2")[0] == 1
-    assert decode(W, "LINESTRING (1 2, 3 4)")[0] == 2
+    assert decode(W, "LINESTRING (1 2, 3 4)") == (0, 2.0, 3.0)
+    assert decode(W, "CIRCULARSTRING (1 2, 3 4, 5 6)")[0] == 2  # (no JTS WKT type)
     st, x, y = decode(W, "MULTIPOINT ((1 2), (3 5))")
     assert st == 0 and (x, y) == (2.0, 3.5)
     st, x, y = decode(W, "MULTIPOINT (1 2, 3 5, 5 8)")
@@ -270,7 +271,8 @@ def test_geojson_points():
     assert st == 0 and (x, y) == (3.0, 5.0)
     assert decode(J, '{"type":"Point","coordinates":[]}')[0] == 3
     assert decode(J, '{"type":"MultiPoint","coordinates":[]}')[0] == 3
-    assert decode(J, '{"type":"Polygon","coordinates":[[[0,0],[1,0],[1,1],[0,0]]]}')[0] == 2
+    st, x, y = decode(J, '{"type":"Polygon","coordinates":[[[0,0],[3,0],[0,3],[0,0]]]}')
+    assert st == 0 and (x, y) == (1.0, 1.0)
     assert decode(J, '{"type":"Point","coordinates":[1]}')[0] == 1
     assert decode(J, '{"type":"Blob"}')[0] == 1
 
@@ -315,3 +317,75 @@ def test_internal_geometry_centroids_equal_wkb():
     N.check(N.lib().mgpu_test_internal_centroid(n, P(tid), P(rp), P(pr), P(ro), P(xy), P(x), P(y), P(st)))
     for i, g in enumerate(geoms):
         assert st[i] == 0 and (x[i], y[i]) == JC.centroid_wkb(w_geom(*g)), (i, g[0])
+
+
+# ---------------------------------------------------------------- WKT / GeoJSON of every type
+def _wkt(kind, d, z=False):
+    """WKT text of the _random_geoms shapes (repr: the shortest round-tripping decimals)."""
+    zs = " Z" if z else ""
+    c = lambda p: "%r %r" % p + (" 7.0" if z else "")  # noqa: E731
+    seq = lambda pts: "(" + ", ".join(c(p) for p in pts) + ")"  # noqa: E731
+    poly = lambda rings: "(" + ", ".join(seq(r) for r in rings) + ")"  # noqa: E731
+    if kind == "point":
+        return "POINT%s (%s)" % (zs, c(d))
+    if kind == "line":
+        return "LINESTRING%s %s" % (zs, seq(d))
+    if kind == "poly":
+        return "POLYGON%s %s" % (zs, poly(d))
+    if kind == "mpoint":
+        return "MULTIPOINT%s (%s)" % (zs, ", ".join("(%s)" % c(p) for p in d))
+    if kind == "mline":
+        return "MULTILINESTRING%s (%s)" % (zs, ", ".join(seq(l) for l in d))
+    if kind == "mpoly":
+        return "MULTIPOLYGON%s (%s)" % (zs, ", ".join(poly(q) for q in d))
+    return "GEOMETRYCOLLECTION%s (%s)" % (zs, ", ".join(_wkt(k, v, z) for k, v in d))
+
+
+def _json(kind, d):
+    pos = lambda p: "[%r, %r]" % p  # noqa: E731
+    seq = lambda pts: "[" + ", ".join(pos(p) for p in pts) + "]"  # noqa: E731
+    poly = lambda rings: "[" + ", ".join(seq(r) for r in rings) + "]"  # noqa: E731
+    names = {"point": "Point", "line": "LineString", "poly": "Polygon", "mpoint": "MultiPoint",
+             "mline": "MultiLineString", "mpoly": "MultiPolygon"}
+    if kind == "collection":
+        return '{"geometries": [%s], "type": "GeometryCollection"}' % ", ".join(_json(k, v) for k, v in d)
+    coords = {"point": lambda: pos(d), "line": lambda: seq(d), "poly": lambda: poly(d), "mpoint": lambda: seq(d),
+              "mline": lambda: "[" + ", ".join(seq(l) for l in d) + "]",
+              "mpoly": lambda: "[" + ", ".join(poly(q) for q in d) + "]"}[kind]()
+    return '{"type": "%s", "coordinates": %s}' % (names[kind], coords)
+
+
+def test_centroid_any_wkt_geojson_equals_jts_restatement():
+    """grid_pointascellid on WKT (StringType) and GeoJSON (JSONType) rows of every geometry
+    type -- GeometryAPI.geometry (GeometryAPI.scala:81-89) reads them with JTS's WKTReader /
+    GeoJsonReader, PointIndexGeom takes getCentroid -- equals the JTS Centroid restatement of
+    the same geometry (as WKB) bit for bit; Z coordinates are ignored."""
+    for seed in (21, 22):
+        for g in _random_geoms(seed, 140):
+            want = JC.centroid_wkb(w_geom(*g))
+            assert decode(N.MGPU_GEOM_WKT, _wkt(*g))[1:] == want, (g[0], _wkt(*g)[:80])
+            assert decode(N.MGPU_GEOM_WKT, _wkt(*g, z=True))[1:] == want
+            assert decode(N.MGPU_GEOM_GEOJSON, _json(*g))[1:] == want, (g[0], _json(*g)[:80])
+
+
+def test_text_geometry_special_cases():
+    """EMPTY members, strict rings (WKTReader / GeoJsonReader throw where WKBReader
+    repairs), nesting."""
+    W, J = N.MGPU_GEOM_WKT, N.MGPU_GEOM_GEOJSON
+    assert decode(W, "POLYGON EMPTY")[0] == 3
+    assert decode(W, "GEOMETRYCOLLECTION EMPTY")[0] == 3
+    assert decode(W, "GEOMETRYCOLLECTION (POINT EMPTY, LINESTRING EMPTY)")[0] == 3
+    assert decode(W, "GEOMETRYCOLLECTION (POINT (1 2), GEOMETRYCOLLECTION (POINT (3 4)))") == (0, 2.0, 3.0)
+    assert decode(W, "MULTIPOLYGON (EMPTY, ((0 0, 3 0, 0 3, 0 0)))") == (0, 1.0, 1.0)
+    assert decode(W, "POLYGON ((0 0, 3 0, 0 3))")[0] == 1        # not closed
+    assert decode(W, "POLYGON ((0 0, 3 0, 0 0))")[0] == 1        # fewer than 4 points
+    assert decode(W, "LINESTRING (1 2)")[0] == 1                 # one point
+    assert decode(W, "LINEARRING (0 0, 3 0, 0 3, 0 0)")[0] == 0
+    assert decode(W, "POLYGON ((0 0, 3 0, 0 3, 0 0)")[0] == 1    # truncated
+    assert decode(W, "GEOMETRYCOLLECTION (POINT (1 2)")[0] == 1
+    assert decode(J, '{"type":"Polygon","coordinates":[[[0,0],[1,0],[1,1]]]}')[0] == 1
+    assert decode(J, '{"type":"LineString","coordinates":[[0,0]]}')[0] == 1
+    assert decode(J, '{"type":"GeometryCollection","geometries":[]}')[0] == 3
+    assert decode(J, '{"type":"GeometryCollection","geometries":[{"type":"Point","coordinates":[1,2]},'
+                     '{"type":"GeometryCollection","geometries":[{"type":"Point","coordinates":[3,4]}]}]}') == (0, 2.0, 3.0)
+    assert decode(J, '{"type":"Polygon","coordinates":[]}')[0] == 3

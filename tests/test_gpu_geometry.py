@@ -126,7 +126,7 @@ def test_pip_join_arrow_rejects_host_arrays(gpu, nyc_chips_r9):
 
 def test_centroids_of_any_geometry_on_gpu(gpu):
     """Polygons (holes, both orientations), multipolygons, lines, collections as WKB, the
-    same rows as hex text, as Mosaic's InternalGeometryType layout, and GeoJSON points:
+    same rows as hex text, as Mosaic's InternalGeometryType layout, as WKT and as GeoJSON:
     the device cells equal the oracle's cells of the JTS Centroid restatement
     (oracle/jts_centroid.py); a POLYGON EMPTY row raises as getX on the empty centroid
     (PointIndexBehaviors.scala:134-137)."""
@@ -151,5 +151,12 @@ def test_centroids_of_any_geometry_on_gpu(gpu):
     js = ['{"type": "Point", "coordinates": [%r, %r]}' % (float(a), float(b)) for a, b in zip(cx[:500], cy[:500])]
     got = M.grid_pointascellid(M.GeometryColumn.from_rows(js, gpu, fmt="geojson"), 9).cpu().numpy()
     assert np.array_equal(got, O.h3_points_to_cells(cx[:500], cy[:500], 9))
+    # every type as WKT (StringType) and GeoJSON (JSONType) text: the device's text readers
+    from test_geom_host import _json, _wkt
+    want = O.h3_points_to_cells(cx, cy, 9)
+    for fmt, rows in (("wkt", [_wkt(*g, z=(i % 5 == 0)) for i, g in enumerate(geoms)]),
+                      ("geojson", [_json(*g) for g in geoms])):
+        got = M.grid_pointascellid(M.GeometryColumn.from_rows(rows, gpu, fmt=fmt), 9).cpu().numpy()
+        assert np.array_equal(got, want), fmt
     with pytest.raises(M.IllegalStateException):
         M.grid_pointascellid(M.GeometryColumn.from_rows([struct.pack("<BII", 1, 3, 0)], gpu), 5)

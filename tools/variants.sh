@@ -1,13 +1,19 @@
 #!/bin/bash
 # Build profiling variants of libmosaic_gpu.so: tools/variants.sh NAME "-DFOO=1" [NAME "-D..."]...
-# Each lands in build/variants/NAME/libmosaic_gpu.so (select with MOSAIC_AMD_LIB).
+# Each lands in build/variants/NAME/libmosaic_gpu.so (select with MOSAIC_AMD_LIB).  The
+# variants' kernels.hip compiles run in parallel; the host objects are the tree's.
 set -e
 cd "$(dirname "$0")/../mosaic_amd/csrc"
+make -s
+CXXFLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wno-unused-result -Wno-unused-value"
+pids=()
+names=()
 while [ $# -ge 2 ]; do
   d=../../build/variants/$1; mkdir -p $d
-  rm -f kernels.o
-  make -s OUT=$d/libmosaic_gpu.so KFLAGS="$2" $d/libmosaic_gpu.so
-  rm -f kernels.o
+  (/opt/rocm/bin/hipcc --offload-arch=gfx950 $CXXFLAGS $2 -c kernels.hip -o $d/kernels.o 2> $d/build.log &&
+   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $d/libmosaic_gpu.so $d/kernels.o capi.o comm.o tessellate.o \
+     bng_format.o h3_glibc.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib && rm -f $d/kernels.o) &
+  pids+=($!); names+=($1)
   shift 2
 done
-make -s
+for i in "${!pids[@]}"; do wait ${pids[$i]} || { echo "variant ${names[$i]} failed"; exit 1; }; done
