@@ -274,6 +274,25 @@ int32_t mgpu_pair_offsets(mgpu_ctx* ctx, int64_t local_pairs, int64_t* out_offse
  * allocation can be shown to return an error (it does not wait on anything). */
 int32_t mgpu_test_receive_blob(mgpu_ctx* ctx, const void* dev_blob, int32_t fail_alloc, mgpu_chips** out);
 
+/* The grid-ring neighbour join of SpatialKNN for point landmarks and point candidates, one
+ * iteration (models/knn/GridRingNeighbours.scala: transform :121 and resultTransform;
+ * SpatialKNN.scala's per-iteration filter): each landmark's cells -- kRing(cell, k)
+ * (loop_only = 0: iteration 1's grid_geometrykringexplode) or kLoop(cell, k) (loop_only =
+ * 1: iteration k's grid_geometrykloopexplode) of pointToIndex(landmark) -- joined with the
+ * candidates' cells (grid_tessellateexplode of a point: its one chip); every (landmark,
+ * candidate) sharing a cell is a pair once, self matches (identical coordinates) dropped,
+ * distance = st_distance (JTS Coordinate.distance: Math.hypot), pairs with distance <=
+ * max_distance (< 0: no threshold), per landmark ordered by (distance, candidate index)
+ * and cut to the first max_per_left (0: all; SpatialKNN's neighbour_number <= k).  Output:
+ * out_left = left_id_base + landmark index, out_right = candidate index, out_dist; landmarks
+ * in order.  Device pointers; synchronises `stream`; MGPU_E_CAPACITY with *out_n when the
+ * pairs exceed `capacity`. */
+int32_t mgpu_ring_join(mgpu_ctx* ctx, int32_t index_system, int32_t res, int32_t k, int32_t loop_only,
+                       const double* left_x, const double* left_y, int64_t n_left, const double* right_x,
+                       const double* right_y, int64_t n_right, int64_t left_id_base, int32_t max_per_left,
+                       double max_distance, int64_t capacity, int64_t* out_n, int64_t* out_left, int64_t* out_right,
+                       double* out_dist, void* stream);
+
 /* st_contains(chip.wkb, point) for explicit (chip row, point) pairs
  * (ST_Contains.scala:21-44 -> MosaicGeometryJTS.contains, MosaicGeometryJTS.scala:197).
  * out[i] = 1 / 0, or -1 when the chip's geometry is NULL.  Device pointers.

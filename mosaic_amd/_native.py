@@ -41,7 +41,7 @@ EXPORTS = (
     "mgpu_test_h3_elementary_host", "mgpu_test_h3_route_host", "mgpu_test_h3_boundary_host",
     "mgpu_ctx_set_option", "mgpu_ctx_get_option", "mgpu_build_opts_default", "mgpu_chips_host_blob_ex",
     "mgpu_test_h3_glibc_host", "mgpu_internal_geometry_to_cells", "mgpu_test_internal_centroid", "mgpu_test_join_counters",
-    "mgpu_test_receive_blob",
+    "mgpu_test_receive_blob", "mgpu_ring_join",
 )
 MGPU_GEOM_WKB = 0
 MGPU_GEOM_WKT = 1
@@ -178,6 +178,8 @@ def lib():
         "mgpu_test_internal_centroid": (I32, [I64, P, P, P, P, P, P, P, P]),
         "mgpu_test_join_counters": (I32, [P, P]),
         "mgpu_test_receive_blob": (I32, [P, P, I32, ctypes.POINTER(P)]),
+        "mgpu_ring_join": (I32, [P, I32, I32, I32, I32, P, P, I64, P, P, I64, I64, I32, ctypes.c_double, I64,
+                                 ctypes.POINTER(I64), P, P, P, P]),
     }
     for name, (rt, args) in sig.items():
         f = getattr(L, name)

@@ -8,9 +8,9 @@
 // org.locationtech.jts.algorithm.Centroid (restated below: area-weighted triangle fans
 // from the first shell point for polygons, length-weighted segment midpoints for lines,
 // the mean of the points otherwise; one accumulator over all components in order).
-// WKB / HEX: every geometry type; WKT and GeoJSON: POINT / MULTIPOINT (other types
-// report unsupported).  An empty geometry has no centroid (JTS: empty point, getX
-// throws) and is reported as such.
+// Every geometry type in all four encodings (WKB / HEX with the non-strict WKBReader's
+// ring repairs; WKT and GeoJSON with their readers' strict rings).  An empty geometry has
+// no centroid (JTS: empty point, getX throws) and is reported as such.
 #pragma once
 #include <stdint.h>
 
@@ -360,7 +360,7 @@ MGPU_DEC bool keyword(const char* s, int64_t len, int64_t* i, const char* kw) {
   *i = j;
   return true;
 }
-MGPU_DEC bool wkt_number(const char* s, int64_t len, int64_t* i, double* v) {
+__attribute__((noinline)) MGPU_DEC bool wkt_number(const char* s, int64_t len, int64_t* i, double* v) {
   skip_ws(s, len, i);
   const int64_t rest = len - *i;
   const int n = dec::parse_number(s + *i, rest > 512 ? 512 : (int)rest, v);
@@ -470,7 +470,9 @@ struct TextSeq {
   uint32_t n;
   mutable int64_t k = -1, pos = 0;
   mutable double cx = 0, cy = 0, px = 0, py = 0;
-  MGPU_DEC void step() const {
+  // (out of line: the centroid walks call it from many places, and the decimal parser
+  // inlined into each made the device code of the decode kernel ~4x larger)
+  __attribute__((noinline)) MGPU_DEC void step() const {
     if (k < 0) pos = b + 1;
     else wkt_char(s, len, &pos, ',');
     px = cx, py = cy;
@@ -482,15 +484,15 @@ struct TextSeq {
     }
     k++;
   }
-  MGPU_DEC void seek(int64_t i) const {
+  __attribute__((noinline)) MGPU_DEC void seek(int64_t i) const {
     if (i < k - 1) k = -1;
     while (k < i) step();
   }
-  MGPU_DEC double x(int64_t i) const {
+  __attribute__((noinline)) MGPU_DEC double x(int64_t i) const {
     seek(i);
     return i == k ? cx : px;
   }
-  MGPU_DEC double y(int64_t i) const {
+  __attribute__((noinline)) MGPU_DEC double y(int64_t i) const {
     seek(i);
     return i == k ? cy : py;
   }

@@ -1,0 +1,329 @@
+// The grid-ring neighbour join of SpatialKNN (models/knn/GridRingNeighbours.scala,
+// SpatialKNN.scala) for point landmarks and point candidates, one iteration on the GPU.
+//
+// Reference, one iteration (GridRingNeighbours.transform, :121, and resultTransform):
+//   left  = the landmark's cells: iteration 1 grid_geometrykringexplode(geom, res, 1) --
+//           for a point, kRing(pointToIndex(point), 1) (Mosaic.geometryKRing,
+//           core/Mosaic.scala:123-128: a point is one border chip); iteration k > 1
+//           grid_geometrykloopexplode(geom, res, k) -- kLoop(cell, k) minus kRing(cell,
+//           k - 1), i.e. kLoop(cell, k) (Mosaic.geometryKLoop :142-156)
+//   right = the candidates' chips, grid_tessellateexplode(keepCoreGeometries = false)
+//           (SpatialKNN.transform :~160): for a point one chip at pointToIndex(point)
+//           (Mosaic.pointChip :48-59)
+//   join  = left cell == right chip index_id; st_intersects_agg is true for a left chip
+//           wrapped with isCore = true (ST_IntersectsAgg.update), so every (landmark,
+//           candidate) sharing a cell is a pair, once; distance = st_distance (JTS
+//           Coordinate.distance, Math.hypot); self matches (the same geometry) dropped;
+//           neighbour_number = row_number over (landmark, distance ascending);
+//           SpatialKNN keeps neighbour_number <= kNeighbours and distance <= threshold.
+// Here: cells of both sides by mgpu_points_to_cells (the reference's cells, near-ties
+// included), ring lists by mgpu_grid_kring (H3's pentagon handling included), the
+// candidates in an open-addressing hash of their cells (each slot heads a list of its
+// candidates), one thread per landmark probing its ring cells; pairs per landmark
+// ordered by (distance, candidate index) -- the reference's window leaves distance ties
+// unordered; this order is the oracle's.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "capi_internal.h"
+#include "geom_decode.h"
+
+namespace {
+
+#define RJ_TRY(expr)                                                                                     \
+  do {                                                                                                   \
+    hipError_t _e = (expr);                                                                              \
+    if (_e != hipSuccess) return mgpu::set_error(MGPU_E_DEVICE, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+struct RjArgs {
+  const double *lx, *ly, *rx, *ry;
+  const int64_t* ring;        // ring cells of every landmark, [ring_off[i], ring_off[i + 1])
+  const int64_t* ring_off;    // [n_left + 1]
+  const uint64_t* slot_cell;  // candidate-cell hash: the cell (0: empty slot)
+  const int64_t* slot_head;   // its first candidate (a list through next[])
+  const int64_t* next;        // [n_right] the next candidate of the same cell (-1: end)
+  uint64_t mask;              // slots - 1
+  int64_t n_left;
+  double max_dist;            // < 0: no threshold
+};
+
+__device__ __forceinline__ uint64_t rj_hash(uint64_t c) {
+  c ^= c >> 33;
+  c *= 0xff51afd7ed558ccdULL;
+  c ^= c >> 33;
+  return c;
+}
+
+// the candidates into the hash: slot of the cell (claimed by CAS), candidate pushed on its
+// list (the list order does not matter: segments are sorted afterwards)
+__global__ __launch_bounds__(256) void rj_insert_kernel(const int64_t* __restrict__ rc, int64_t n, uint64_t* slot_cell,
+                                                        unsigned long long* slot_head, int64_t* __restrict__ next,
+                                                        uint64_t mask) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t c = (uint64_t)rc[j];
+  uint64_t h = rj_hash(c) & mask;
+  for (;;) {
+    const unsigned long long prev = atomicCAS((unsigned long long*)&slot_cell[h], 0ull, (unsigned long long)c);
+    if (prev == 0ull || prev == c) break;
+    h = (h + 1) & mask;
+  }
+  next[j] = (int64_t)atomicExch(&slot_head[h], (unsigned long long)j);
+}
+
+__device__ __forceinline__ bool same_bits(double a, double b) {
+  return __double_as_longlong(a) == __double_as_longlong(b);
+}
+
+// per landmark: the candidates sharing one of its ring cells, minus itself (the same
+// coordinates: the reference's hash of the same geometry), within the threshold --
+// counted (WRITE = false) or written from off[i] (WRITE = true)
+template <bool WRITE>
+__global__ __launch_bounds__(256) void rj_pairs_kernel(RjArgs a, int64_t* __restrict__ cnt, const int64_t* __restrict__ off,
+                                                      int64_t* __restrict__ out_right, double* __restrict__ out_dist) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n_left) return;
+  const double px = a.lx[i], py = a.ly[i];
+  int64_t m = 0, q = WRITE ? off[i] : 0;
+  for (int64_t r = a.ring_off[i]; r < a.ring_off[i + 1]; r++) {
+    const uint64_t c = (uint64_t)a.ring[r];
+    uint64_t h = rj_hash(c) & a.mask;
+    while (a.slot_cell[h] != 0 && a.slot_cell[h] != c) h = (h + 1) & a.mask;
+    if (a.slot_cell[h] != c) continue;
+    for (int64_t k = a.slot_head[h]; k >= 0; k = a.next[k]) {
+      const double qx = a.rx[k], qy = a.ry[k];
+      if (same_bits(px, qx) && same_bits(py, qy)) continue;
+      const double d = mgpu::geom::jhypot(px - qx, py - qy);
+      if (a.max_dist >= 0.0 && !(d <= a.max_dist)) continue;
+      if (WRITE) {
+        out_right[q] = k;
+        out_dist[q] = d;
+        q++;
+      }
+      m++;
+    }
+  }
+  if (!WRITE) cnt[i] = m;
+}
+
+__device__ __forceinline__ bool rj_less(double da, int64_t ia, double db, int64_t ib) {
+  return da < db || (da == db && ia < ib);
+}
+
+// each landmark's segment in (distance, candidate) order -- the first `keep` of it by
+// selection when keep is small, else all of it by a Shell sort -- and its kept count
+__global__ __launch_bounds__(256) void rj_sort_kernel(const int64_t* __restrict__ off, int64_t n, int64_t keep,
+                                                      int64_t* __restrict__ right, double* __restrict__ dist,
+                                                      int64_t* __restrict__ kept) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t b = off[i], m = off[i + 1] - b;
+  int64_t* R = right + b;
+  double* D = dist + b;
+  const int64_t want = keep > 0 && keep < m ? keep : m;
+  if (keep > 0 && keep < m && keep <= 32) {
+    for (int64_t r = 0; r < want; r++) {
+      int64_t best = r;
+      for (int64_t j = r + 1; j < m; j++)
+        if (rj_less(D[j], R[j], D[best], R[best])) best = j;
+      const double td = D[r];
+      const int64_t tr = R[r];
+      D[r] = D[best], R[r] = R[best];
+      D[best] = td, R[best] = tr;
+    }
+  } else {
+    int64_t gap = 1;
+    while (gap < m / 3) gap = 3 * gap + 1;
+    for (; gap > 0; gap /= 3)
+      for (int64_t j = gap; j < m; j++) {
+        const double td = D[j];
+        const int64_t tr = R[j];
+        int64_t q = j;
+        while (q >= gap && rj_less(td, tr, D[q - gap], R[q - gap])) {
+          D[q] = D[q - gap];
+          R[q] = R[q - gap];
+          q -= gap;
+        }
+        D[q] = td;
+        R[q] = tr;
+      }
+  }
+  kept[i] = want;
+}
+
+// exclusive scan of v[0 .. n) into out[0 .. n] (out[n] = the total), three launches:
+// per-block scans with block sums, the block sums scanned by one workgroup, added back
+constexpr int kScanB = 1024;
+__global__ __launch_bounds__(kScanB) void rj_scan_block_kernel(const int64_t* __restrict__ v, int64_t n,
+                                                              int64_t* __restrict__ out, int64_t* __restrict__ bsum) {
+  __shared__ int64_t s[kScanB];
+  const int64_t i = (int64_t)blockIdx.x * kScanB + threadIdx.x;
+  const int64_t x = i < n ? v[i] : 0;
+  s[threadIdx.x] = x;
+  __syncthreads();
+  for (int d = 1; d < kScanB; d <<= 1) {
+    const int64_t t = threadIdx.x >= (unsigned)d ? s[threadIdx.x - d] : 0;
+    __syncthreads();
+    s[threadIdx.x] += t;
+    __syncthreads();
+  }
+  if (i < n) out[i] = s[threadIdx.x] - x;
+  if (threadIdx.x == kScanB - 1) bsum[blockIdx.x] = s[kScanB - 1];
+}
+__global__ __launch_bounds__(kScanB) void rj_scan_sums_kernel(int64_t* __restrict__ bsum, int64_t nb) {
+  __shared__ int64_t s[kScanB];
+  int64_t carry = 0;
+  for (int64_t b0 = 0; b0 < nb; b0 += kScanB) {
+    const int64_t i = b0 + threadIdx.x;
+    const int64_t x = i < nb ? bsum[i] : 0;
+    s[threadIdx.x] = x;
+    __syncthreads();
+    for (int d = 1; d < kScanB; d <<= 1) {
+      const int64_t t = threadIdx.x >= (unsigned)d ? s[threadIdx.x - d] : 0;
+      __syncthreads();
+      s[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (i < nb) bsum[i] = carry + s[threadIdx.x] - x;
+    const int64_t tot = s[kScanB - 1];
+    __syncthreads();
+    carry += tot;
+  }
+  if (threadIdx.x == 0) bsum[nb] = carry;
+}
+__global__ __launch_bounds__(kScanB) void rj_scan_add_kernel(int64_t* __restrict__ out, int64_t n,
+                                                            const int64_t* __restrict__ bsum, int64_t nb) {
+  const int64_t i = (int64_t)blockIdx.x * kScanB + threadIdx.x;
+  if (i < n) out[i] += bsum[blockIdx.x];
+  if (i == 0) out[n] = bsum[nb];
+}
+
+// the first kept[i] pairs of landmark i's sorted segment to its output range
+__global__ __launch_bounds__(256) void rj_copy_kernel(const int64_t* __restrict__ off, const int64_t* __restrict__ koff,
+                                                      int64_t n, const int64_t* __restrict__ right,
+                                                      const double* __restrict__ dist, int64_t left_base,
+                                                      int64_t capacity, int64_t* __restrict__ out_left,
+                                                      int64_t* __restrict__ out_right, double* __restrict__ out_dist) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t b = off[i], o = koff[i], e = koff[i + 1];
+  for (int64_t q = o; q < e && q < capacity; q++) {
+    out_left[q] = left_base + i;
+    out_right[q] = right[b + q - o];
+    out_dist[q] = dist[b + q - o];
+  }
+}
+
+unsigned grid_of(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + 255) / 256); }
+
+// device scratch freed on every return path
+struct Scratch {
+  std::vector<void*> ptrs;
+  ~Scratch() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  template <class T>
+  hipError_t get(T** p, size_t count) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T));
+    if (e == hipSuccess) ptrs.push_back(q);
+    *p = (T*)q;
+    return e;
+  }
+};
+
+}  // namespace
+
+extern "C" int32_t mgpu_ring_join(mgpu_ctx* ctx, int32_t index_system, int32_t res, int32_t k, int32_t loop_only,
+                                  const double* lx, const double* ly, int64_t n_left, const double* rx,
+                                  const double* ry, int64_t n_right, int64_t left_id_base, int32_t max_per_left,
+                                  double max_distance, int64_t capacity, int64_t* out_n, int64_t* out_left,
+                                  int64_t* out_right, double* out_dist, void* stream) {
+  if (!ctx || n_left < 0 || n_right < 0 || (n_left && (!lx || !ly)) || (n_right && (!rx || !ry)) || capacity < 0 ||
+      (capacity > 0 && (!out_left || !out_right || !out_dist)) || max_per_left < 0)
+    return mgpu::set_error(MGPU_E_INVALID_ARG, "ring_join: bad arguments");
+  if (k < 0 || k > 1024) return mgpu::set_error(MGPU_E_INVALID_ARG, "ring_join: k must be in [0, 1024]");
+  if (int32_t st = mgpu_check_resolution(index_system, res)) return st;
+  RJ_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (out_n) *out_n = 0;
+  if (n_left == 0) return MGPU_OK;
+  Scratch S;
+  int64_t *lc, *rc;
+  RJ_TRY(S.get(&lc, n_left));
+  RJ_TRY(S.get(&rc, n_right));
+  // both sides' cells, the reference's (near-ties by its libm): IndexSystem.pointToIndex
+  if (int32_t st = mgpu_points_to_cells(ctx, index_system, res, lx, ly, n_left, lc, stream, nullptr)) return st;
+  if (n_right)
+    if (int32_t st = mgpu_points_to_cells(ctx, index_system, res, rx, ry, n_right, rc, stream, nullptr)) return st;
+  // the candidates' cell hash (cell ids are never 0)
+  uint64_t slots = 16;
+  while (slots < 2 * (uint64_t)std::max<int64_t>(n_right, 1)) slots <<= 1;
+  uint64_t* slot_cell;
+  int64_t *slot_head, *next;
+  RJ_TRY(S.get(&slot_cell, slots));
+  RJ_TRY(S.get(&slot_head, slots));
+  RJ_TRY(S.get(&next, n_right));
+  RJ_TRY(hipMemsetAsync(slot_cell, 0, slots * 8, s));
+  RJ_TRY(hipMemsetAsync(slot_head, 0xFF, slots * 8, s));
+  if (n_right)
+    hipLaunchKernelGGL(rj_insert_kernel, dim3(grid_of(n_right)), dim3(256), 0, s, rc, n_right, slot_cell,
+                       (unsigned long long*)slot_head, next, slots - 1);
+  // the landmarks' ring cells (IndexSystem.kRing / kLoop through mgpu_grid_kring)
+  int64_t *ring_off, *ring;
+  RJ_TRY(S.get(&ring_off, n_left + 1));
+  const int64_t per = loop_only ? (k == 0 ? 1 : 6 * (int64_t)k) : 3 * (int64_t)k * (k + 1) + 1;
+  int64_t ring_cap = n_left * per + 1024, ring_total = 0;
+  RJ_TRY(S.get(&ring, ring_cap));
+  int32_t st = mgpu_grid_kring(ctx, index_system, lc, n_left, k, loop_only, ring, ring_cap, ring_off, &ring_total, stream);
+  if (st == MGPU_E_CAPACITY) {
+    ring_cap = ring_total;
+    RJ_TRY(S.get(&ring, ring_cap));
+    st = mgpu_grid_kring(ctx, index_system, lc, n_left, k, loop_only, ring, ring_cap, ring_off, &ring_total, stream);
+  }
+  if (st) return st;
+  const int64_t nb = (n_left + kScanB - 1) / kScanB;
+  int64_t* bsum;
+  RJ_TRY(S.get(&bsum, nb + 1));
+  auto scan = [&](const int64_t* v, int64_t* out) {
+    hipLaunchKernelGGL(rj_scan_block_kernel, dim3((unsigned)nb), dim3(kScanB), 0, s, v, n_left, out, bsum);
+    hipLaunchKernelGGL(rj_scan_sums_kernel, dim3(1), dim3(kScanB), 0, s, bsum, nb);
+    hipLaunchKernelGGL(rj_scan_add_kernel, dim3((unsigned)nb), dim3(kScanB), 0, s, out, n_left, bsum, nb);
+  };
+  // pairs: counts, offsets, the pairs; each landmark's segment ordered by (distance,
+  // candidate) and cut to max_per_left; kept counts, offsets, the output
+  RjArgs a{lx, ly, rx, ry, ring, ring_off, slot_cell, slot_head, next, slots - 1, n_left, max_distance};
+  int64_t *cnt, *off;
+  RJ_TRY(S.get(&cnt, n_left));
+  RJ_TRY(S.get(&off, n_left + 1));
+  hipLaunchKernelGGL(rj_pairs_kernel<false>, dim3(grid_of(n_left)), dim3(256), 0, s, a, cnt, nullptr, nullptr, nullptr);
+  scan(cnt, off);
+  int64_t total = 0;
+  RJ_TRY(hipMemcpyAsync(&total, off + n_left, 8, hipMemcpyDeviceToHost, s));
+  RJ_TRY(hipStreamSynchronize(s));
+  int64_t* pr;
+  double* pd;
+  RJ_TRY(S.get(&pr, total));
+  RJ_TRY(S.get(&pd, total));
+  hipLaunchKernelGGL(rj_pairs_kernel<true>, dim3(grid_of(n_left)), dim3(256), 0, s, a, nullptr, off, pr, pd);
+  int64_t *kept, *koff;
+  RJ_TRY(S.get(&kept, n_left));
+  RJ_TRY(S.get(&koff, n_left + 1));
+  hipLaunchKernelGGL(rj_sort_kernel, dim3(grid_of(n_left)), dim3(256), 0, s, off, n_left, (int64_t)max_per_left, pr, pd,
+                     kept);
+  scan(kept, koff);
+  int64_t n_out = 0;
+  RJ_TRY(hipMemcpyAsync(&n_out, koff + n_left, 8, hipMemcpyDeviceToHost, s));
+  if (capacity > 0)
+    hipLaunchKernelGGL(rj_copy_kernel, dim3(grid_of(n_left)), dim3(256), 0, s, off, koff, n_left, pr, pd, left_id_base,
+                       capacity, out_left, out_right, out_dist);
+  RJ_TRY(hipGetLastError());
+  RJ_TRY(hipStreamSynchronize(s));
+  if (out_n) *out_n = n_out;
+  if (n_out > capacity)
+    return mgpu::set_error(MGPU_E_CAPACITY, "ring_join: %lld pairs, capacity %lld", (long long)n_out, (long long)capacity);
+  return MGPU_OK;
+}

@@ -325,3 +325,40 @@ def pip_join_async(x, y, chips, resolution, index_system=None, point_id=None, po
                                         pid_ptr, int(point_id_base), n, cap, count.data_ptr(), op.data_ptr(),
                                         oq.data_ptr(), s))
     return AsyncJoin(chips.ctx, op, oq, count, (x, y, point_id, chips))
+
+
+def grid_ring_join(left_x, left_y, right_x, right_y, resolution, k=1, index_system=None, loop_only=False,
+                   max_per_left=0, max_distance=-1.0, left_id_base=0, stream=None):
+    """One iteration of SpatialKNN's grid-ring neighbour join for point landmarks (left) and
+    point candidates (right) -- GridRingNeighbours.transform (models/knn/
+    GridRingNeighbours.scala:121) with its resultTransform (mgpu_ring_join): the pairs whose
+    cells meet in kRing(cell(landmark), k) (``loop_only``: kLoop, iterations > 1), self
+    matches dropped, ``distance <= max_distance`` (< 0: none), per landmark by (distance,
+    candidate index), at most ``max_per_left`` (0: all).  Returns (left ids, right indices,
+    distances) on the points' device."""
+    import ctypes
+    import torch
+    from .context import default_context
+    isys = index_system or _H3
+    res = isys.get_resolution(resolution)
+    _check_points(left_x, left_y)
+    _check_points(right_x, right_y)
+    ctx = default_context(left_x.device)
+    s = stream if stream is not None else torch.cuda.current_stream(left_x.device).cuda_stream
+    n = ctypes.c_int64()
+    cap = max(16, left_x.numel() * (max_per_left if max_per_left > 0 else 8))
+    for _ in range(2):
+        ol = torch.empty(cap, dtype=torch.int64, device=left_x.device)
+        orr = torch.empty(cap, dtype=torch.int64, device=left_x.device)
+        od = torch.empty(cap, dtype=torch.float64, device=left_x.device)
+        st = N.lib().mgpu_ring_join(ctx.handle, isys.code, res, int(k), 1 if loop_only else 0, left_x.data_ptr(),
+                                    left_y.data_ptr(), left_x.numel(), right_x.data_ptr(), right_y.data_ptr(),
+                                    right_x.numel(), int(left_id_base), int(max_per_left), float(max_distance), cap,
+                                    ctypes.byref(n), ol.data_ptr(), orr.data_ptr(), od.data_ptr(), s)
+        if st == N.MGPU_E_CAPACITY:
+            cap = int(n.value)
+            continue
+        N.check(st)
+        m = int(n.value)
+        return ol[:m], orr[:m], od[:m]
+    N.check(st, required=n.value)

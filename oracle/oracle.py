@@ -311,3 +311,46 @@ def h3_k_loop(h, n):
         a = h3_k_ring(h, n)
         b = set(h3_k_ring(h, n - 1))
         return sorted(set(a) - b, key=scala_hashset_key)
+
+
+def ring_join(index_system, res, k, lx, ly, rx, ry, loop_only=False, max_per_left=0, max_distance=-1.0,
+              left_id_base=0):
+    """Test infrastructure: one iteration of GridRingNeighbours (models/knn/
+    GridRingNeighbours.scala:121 transform + resultTransform) for point landmarks and
+    point candidates, restated: the landmark's kRing(cell, k) (Mosaic.geometryKRing,
+    core/Mosaic.scala:123-128) or kLoop(cell, k) (geometryKLoop :142-156) cells joined with
+    the candidates' cells (Mosaic.pointChip :48-59), each (landmark, candidate) once,
+    self matches dropped, st_distance = JTS Coordinate.distance (Math.hypot: the fdlibm
+    port of jts_centroid.py), distance <= max_distance, ordered by (distance, candidate),
+    the first max_per_left.  Returns (left, right, distance) arrays."""
+    import jts_centroid as JC
+    lx, ly, rx, ry = (np.ascontiguousarray(v, dtype=np.float64) for v in (lx, ly, rx, ry))
+    if index_system == 0:
+        lc, rc = h3_points_to_cells(lx, ly, res), h3_points_to_cells(rx, ry, res)
+        ring = (lambda c: h3_k_loop(int(c), k)) if loop_only else (lambda c: h3_k_ring(int(c), k))
+    else:
+        lc, rc = bng_points_to_cells(lx, ly, res), bng_points_to_cells(rx, ry, res)
+        ring = (lambda c: bng_k_loop(int(c), k)) if loop_only else (lambda c: bng_k_ring(int(c), k))
+    by_cell = {}
+    for j, c in enumerate(rc.tolist()):
+        by_cell.setdefault(c, []).append(j)
+    L, R, D = [], [], []
+    bits = lambda v: np.float64(v).view(np.int64)  # noqa: E731
+    for i in range(len(lx)):
+        got = []
+        for c in set(ring(lc[i])):
+            for j in by_cell.get(c, ()):
+                if bits(lx[i]) == bits(rx[j]) and bits(ly[i]) == bits(ry[j]):
+                    continue
+                d = JC.hypot(float(lx[i] - rx[j]), float(ly[i] - ry[j]))
+                if max_distance >= 0 and not d <= max_distance:
+                    continue
+                got.append((d, j))
+        got.sort()
+        if max_per_left > 0:
+            got = got[:max_per_left]
+        for d, j in got:
+            L.append(left_id_base + i)
+            R.append(j)
+            D.append(d)
+    return np.array(L, np.int64), np.array(R, np.int64), np.array(D, np.float64)

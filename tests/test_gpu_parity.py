@@ -769,3 +769,43 @@ def test_broadcast_receiver_path(gpu, nyc_chips_r9):
     assert st == N.MGPU_E_INVALID_ARG and "no chip-table blob" in N.last_error()
     st = N.lib().mgpu_test_receive_blob(ctx.handle, blob.data_ptr(), 1, ctypes.byref(out))
     assert st == N.MGPU_E_DEVICE and "hipMalloc" in N.last_error()
+
+
+# ---------------------------------------------------------------- SpatialKNN's ring join
+
+@pytest.mark.parametrize("isys_name,res,k,loop_only,keep,maxd", [
+    ("H3", 9, 1, False, 0, -1.0), ("H3", 9, 2, True, 5, -1.0), ("H3", 8, 1, False, 3, 0.004),
+    ("BNG", 3, 1, False, 0, -1.0), ("BNG", 3, 2, True, 4, 2500.0), ("H3", 2, 1, False, 0, -1.0)])
+def test_ring_join_equals_oracle(gpu, isys_name, res, k, loop_only, keep, maxd):
+    """grid_ring_join (GridRingNeighbours.transform + resultTransform, one iteration, point
+    landmarks x point candidates) == the oracle's restatement, pairs and distances bit for
+    bit: kRing (iteration 1) and kLoop (iteration k) cells, self matches dropped (some
+    candidates are copies of landmarks), the distance threshold, the per-landmark cut; H3
+    res 2 around a pentagon (the kRing walks' pentagon fallback)."""
+    rng = np.random.default_rng(300 + res + 10 * k)
+    if isys_name == "BNG":
+        isys, code = M.BNGIndexSystem(), 1
+        lx, ly = rng.uniform(520_000, 540_000, 1000), rng.uniform(170_000, 190_000, 1000)
+        rx, ry = rng.uniform(518_000, 542_000, 8000), rng.uniform(168_000, 192_000, 8000)
+    elif res == 2:
+        isys, code = M.H3IndexSystem(), 0
+        import ctypes
+        from mosaic_amd import _native as N
+        xy, nv, ctr = np.zeros(20), np.zeros(1, np.int32), np.zeros(2)  # base cell 14's centre (a pentagon)
+        N.check(N.lib().mgpu_test_h3_boundary_host(np.array([(1 << 59) | (14 << 45) | 0x1FFFFFFFFFFF], np.int64).ctypes.data,
+                                                     1, xy.ctypes.data, nv.ctypes.data, ctr.ctypes.data))
+        lx, ly = rng.uniform(ctr[0] - 8, ctr[0] + 8, 600), rng.uniform(ctr[1] - 6, ctr[1] + 6, 600)
+        rx, ry = rng.uniform(ctr[0] - 12, ctr[0] + 12, 2500), rng.uniform(ctr[1] - 9, ctr[1] + 9, 2500)
+    else:
+        isys, code = M.H3IndexSystem(), 0
+        lx, ly = nyc_points(3000, 40 + k)
+        rx, ry = nyc_points(30000, 50 + k)
+    rx[:500], ry[:500] = lx[:500], ly[:500]  # self matches
+    got = M.grid_ring_join(T(lx, gpu), T(ly, gpu), T(rx, gpu), T(ry, gpu), res, k, index_system=isys,
+                           loop_only=loop_only, max_per_left=keep, max_distance=maxd, left_id_base=7)
+    gl, gr, gd = (v.cpu().numpy() for v in got)
+    ol, orr, od = O.ring_join(code, res, k, lx, ly, rx, ry, loop_only=loop_only, max_per_left=keep,
+                              max_distance=maxd, left_id_base=7)
+    assert len(ol) > len(lx) // 2
+    assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
+    assert np.array_equal(gd.view(np.int64), od.view(np.int64))
