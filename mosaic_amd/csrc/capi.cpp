@@ -62,8 +62,8 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // offsets, so a byte copy of the blob on another GPU (RCCL broadcast) is a
 // complete chip table there.
 constexpr uint64_t kBlobMagic = 0x4d4f534149434850ULL;  // "MOSAICHP"
-constexpr int kBlobArrays = 23;
-constexpr uint32_t kBlobVersion = 9;  // 9: 32-pixel rank words
+constexpr int kBlobArrays = 24;
+constexpr uint32_t kBlobVersion = 10;  // 10: class -> polygon table
 struct BlobHeader {
   uint64_t magic;
   uint32_t version, hash_mask, max_probe, n_chips, n_cells;
@@ -85,7 +85,7 @@ struct BlobHeader {
   uint32_t max_cell_chips, pad4;
   uint32_t raster_pc[4];
   uint32_t raster_sub_n, raster_sub_w;
-  uint32_t raster_bshift, raster_bnx, raster_bny, pad5;
+  uint32_t raster_bshift, raster_bnx, raster_bny, raster_ncls;
 };
 constexpr size_t kBlobHeaderBytes = 1024;
 static_assert(sizeof(BlobHeader) <= kBlobHeaderBytes, "header too large");
@@ -144,6 +144,8 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.raster_bnx = h.raster_bnx;
   v.raster_bny = h.raster_bny;
   v.raster_blk = h.raster_bshift ? (const uint16_t*)(base + h.off[22]) : nullptr;
+  v.raster_ncls = h.raster_ncls;
+  v.raster_cls_poly = (const int32_t*)(base + h.off[23]);
   return v;
 }
 
@@ -1848,6 +1850,15 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   }
 
   BLOB_MARK("hash");
+  // lonlat classes with one match -> their polygon (ChipTableView::raster_cls_poly)
+  std::vector<int32_t> cls_poly;
+  if (raster.mode == mgpu::kRasterLonLat) {
+    cls_poly.assign(raster.cls.size(), -1);
+    for (size_t c = 1; c < raster.cls.size(); c++) {
+      const uint32_t m = (uint32_t)(raster.cls[c] >> 32);
+      if (__builtin_popcount(m) == 1) cls_poly[c] = cpoly[(uint32_t)raster.cls[c] + __builtin_ctz(m)];
+    }
+  }
   // one blob
   struct Part {
     const void* src;
@@ -1878,6 +1889,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
       {raster.rank.data(), raster.rank.size() * sizeof(mgpu::RankWord), 0},
       {raster.sub.data(), raster.sub.size() * 2, 0},
       {raster.blk.data(), raster.blk.size() * 2, 0},
+      {cls_poly.data(), cls_poly.size() * 4, 0},
   };
   size_t total = kBlobHeaderBytes;
   BlobHeader hdr{};
@@ -1914,6 +1926,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   hdr.raster_bshift = raster.bshift;
   hdr.raster_bnx = raster.bnx;
   hdr.raster_bny = raster.bny;
+  hdr.raster_ncls = (uint32_t)cls_poly.size();
   for (size_t k = 0; k < parts.size(); k++) {
     parts[k].off = total;
     hdr.off[k] = total;

@@ -172,6 +172,11 @@ struct ChipTableView {
                                // matches for raster_pc[k - 1] <= c < raster_pc[k] (k < 4)
   const uint16_t* raster;      // [ny * nx] classes
   const uint64_t* raster_cls;  // [classes]
+  // raster_cls_poly[c] = the polygon of class c when it has one match (c < raster_pc[0]),
+  // else -1: the emit kernels copy it to LDS and answer a one-match pixel without the
+  // raster_cls / chip_poly gathers
+  const int32_t* raster_cls_poly;  // [raster_ncls]
+  uint32_t raster_ncls;
   // second level: every mixed pixel p is cut into sub_n x sub_n sub-pixels whose classes
   // are raster_sub[b * sub_n^2 + v * sub_n + u], b = the number of mixed pixels before p
   // (lonlat: u = the truncated sub_n * fractional pixel position, clamped; BNG: (metres

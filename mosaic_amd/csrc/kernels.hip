@@ -1090,6 +1090,11 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
 #elif MGPU_CFY_ABLATE == 3
         cl[k] = ri[k] < kRasterFull ? (bi[k] != kNoPixel && s_blk[bi[k]] != kPixMixed ? s_blk[bi[k]] : t.raster[ri[k]])
                                     : kPixEmpty;
+#elif MGPU_CFY_ABLATE == 4
+        cl[k] = ri[k] < kRasterFull ? t.raster[ri[k]] : kPixEmpty;  // every lane loads its pixel
+#elif MGPU_CFY_ABLATE == 5
+        cl[k] = ri[k] < kRasterFull ? (bi[k] != kNoPixel && s_blk[bi[k]] != kPixMixed ? s_blk[bi[k]] : kPixMixed)
+                                    : kPixEmpty;  // (LDS, then every non-uniform block point mixed: no global loads)
 #else
         cl[k] = ri[k] < kRasterFull ? raster_class_blk(t, s_blk, ri[k], bi[k], sb[k])
                                     : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
@@ -1172,11 +1177,25 @@ __global__ __launch_bounds__(kBlock) void pip_mixed_fix_kernel(JoinArgs a) {
 // too), a second scan of the pair counts each thread's first output slot.  The chunk's
 // pairs are one contiguous output range: staged in LDS (polygon id, point) a window of
 // kEmitWin pairs at a time, then written by consecutive lanes.
+// A workgroup barrier that orders LDS only: __syncthreads() also waits for the wave's
+// outstanding global loads and stores (its release fence), which would hold the emit
+// kernels' output stores and the next chunk's prefetched loads at every barrier.
+#ifndef MGPU_EMIT_LDSBAR
+#define MGPU_EMIT_LDSBAR 1
+#endif
+__device__ __forceinline__ void lds_barrier() {
+#if MGPU_EMIT_LDSBAR
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+  __syncthreads();
+#endif
+}
+
 __device__ __forceinline__ uint32_t chunk_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t incl = wave_incl_scan(v);
   if (lane == 63) s_w[wave] = incl;
-  __syncthreads();
+  lds_barrier();
   uint32_t before = 0, all = 0;
 #pragma unroll
   for (int w = 0; w < kClsBlock / 64; w++) {
@@ -1200,6 +1219,18 @@ constexpr int kEmitWin = 2048;  // pairs staged at a time
 #ifndef MGPU_EMIT_WAVES
 #define MGPU_EMIT_WAVES 5  // (8: 64 VGPRs, spills; 5: none, A/B equal or better)
 #endif
+// lonlat one-match classes answer from an LDS copy of raster_cls_poly, and the chunk's
+// mixed results (with the polygon of each one-chip match) are staged in LDS by one
+// cooperative load at the start: the per-item loops below then touch no global memory
+// for the common cases.  (A/B r4, profiles/r4_emit_ab.txt: the loops' per-item global
+// loads -- mixed_res, chip_poly -- serialised ~16 dependent L2 round trips per wave; with
+// staging skipped entirely the kernel took 0.19 ms instead of 0.34.  A resident-grid
+// variant prefetching the next chunk measured slower, 0.45 ms.)
+constexpr int kEmitCls = 2048;  // classes staged in LDS (8 KB)
+constexpr int kEmitMres = 512;  // mixed results of a chunk staged in LDS (the rest: global)
+#ifndef MGPU_EMIT_MR
+#define MGPU_EMIT_MR 1
+#endif
 template <int IS>
 __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_EMIT_WAVES))) void split_emit_kernel(SplitArgs sa) {
   using Code = typename CodeOf<IS>::T;
@@ -1209,6 +1240,9 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   __shared__ uint32_t s_w[2][kClsBlock / 64];
   __shared__ uint32_t s_poly[kEmitWin];  // staging: polygon id
   __shared__ uint16_t s_pt[kEmitWin];    // staging: point of the chunk
+  __shared__ int32_t s_cp[IS == MGPU_H3 ? kEmitCls : 1];
+  __shared__ uint64_t s_mr[MGPU_EMIT_MR ? kEmitMres : 1];  // mixed results: first chip | mask << 32
+  __shared__ int32_t s_mp[MGPU_EMIT_MR ? kEmitMres : 1];   // ... the polygon of a one-chip match, else -1
   const int64_t c0 = (int64_t)blockIdx.x * kChunk;
   const int64_t p0 = c0 + (int64_t)threadIdx.x * kClsItems;
   const Code kMixed = IS == MGPU_H3 ? (Code)kPixMixed : (Code)kCodeMixed32;
@@ -1233,6 +1267,24 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
           cw[k] = c;
       }
   }
+  // (the chunk scans below order these LDS stores before the reads)
+  uint32_t ncp = 0;
+  if (IS == MGPU_H3) {
+    ncp = min(min(t.raster_ncls, t.raster_pc[0]), (uint32_t)kEmitCls);
+    for (uint32_t i = threadIdx.x; i < ncp; i += kClsBlock) s_cp[i] = t.raster_cls_poly[i];
+  }
+  constexpr uint32_t kMr = MGPU_EMIT_MR ? (uint32_t)kEmitMres : 0u;
+#if MGPU_EMIT_MR
+  {
+    const uint32_t nm = sa.chunk_mixed[blockIdx.x], nms = nm < kMr ? nm : kMr;
+    for (uint32_t i = threadIdx.x; i < nms; i += kClsBlock) {
+      const uint64_t v = a.mixed_res[c0 + i];
+      const uint32_t m = (uint32_t)(v >> 32);
+      s_mr[i] = v;
+      s_mp[i] = __popc(m) == 1 ? t.chip_poly[(uint32_t)v + __builtin_ctz(m)] : -1;
+    }
+  }
+#endif
   auto code = [&](int k) -> Code {
     return sizeof(Code) == 2 ? (Code)(cw[k >> 1] >> ((k & 1) * 16)) : (Code)cw[k];
   };
@@ -1241,6 +1293,7 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
     if (IS == MGPU_H3) return t.raster_cls[(uint32_t)c];
     return (uint64_t)((uint32_t)c >> 8) | ((uint64_t)((uint32_t)c & 0xFFu) << 32);
   };
+  auto mres = [&](uint32_t r) -> uint64_t { return r < kMr ? s_mr[r] : a.mixed_res[c0 + r]; };
   uint32_t nmix = 0;
 #pragma unroll
   for (int k = 0; k < kClsItems; k++) nmix += code(k) == kMixed;
@@ -1251,9 +1304,17 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   for (int k = 0; k < kClsItems; k++) {
     const Code c = code(k);
     if (c == kMixed)
-      npair += __popc((uint32_t)(a.mixed_res[c0 + r++] >> 32));
-    else if (c != 0)
-      npair += IS == MGPU_H3 ? (uint32_t)__popc((uint32_t)(pure(c) >> 32)) : (uint32_t)__popc((uint32_t)c & 0xFFu);
+      npair += __popc((uint32_t)(mres(r++) >> 32));
+    else if (c != 0) {
+      if (IS == MGPU_H3)  // the match count from the class order (raster_pc)
+        npair += c < t.raster_pc[0]   ? 1u
+                 : c < t.raster_pc[1] ? 2u
+                 : c < t.raster_pc[2] ? 3u
+                 : c < t.raster_pc[3] ? 4u
+                                      : (uint32_t)__popc((uint32_t)(pure(c) >> 32));
+      else
+        npair += (uint32_t)__popc((uint32_t)c & 0xFFu);
+    }
   }
   uint32_t total;
   const uint32_t off0 = chunk_excl_scan(npair, s_w[1], &total);
@@ -1266,10 +1327,22 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
       for (int k = 0; k < kClsItems; k++) {
         const Code c = code(k);
         uint64_t v = 0;
-        if (c == kMixed)
-          v = a.mixed_res[c0 + r++];
+        int32_t one = -1;  // the one polygon, from LDS
+        if (c == kMixed) {
+          const uint32_t rr = r++;
+          if (rr < kMr) one = s_mp[rr];
+          if (one < 0) v = mres(rr);
+        } else if (IS == MGPU_H3 && c != 0 && (uint32_t)c < ncp)
+          one = s_cp[(uint32_t)c];
         else if (c != 0)
           v = pure(c);
+        if (one >= 0) {
+          if (q >= w0 && q < w0 + kEmitWin) {
+            s_poly[q - w0] = (uint32_t)one;
+            s_pt[q - w0] = (uint16_t)(threadIdx.x * kClsItems + k);
+          }
+          q++;
+        }
         const uint32_t first = (uint32_t)v;
         for (uint32_t m = (uint32_t)(v >> 32); m; m &= m - 1, q++)
           if (q >= w0 && q < w0 + kEmitWin) {
@@ -1278,7 +1351,7 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
           }
       }
     }
-    __syncthreads();
+    lds_barrier();
     const uint32_t cnt = total - w0 < (uint32_t)kEmitWin ? total - w0 : (uint32_t)kEmitWin;
     for (uint32_t i = threadIdx.x; i < cnt; i += kClsBlock) {
       const uint64_t q = base + w0 + i;
@@ -1292,7 +1365,7 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
       sa.out_poly[q] = (int32_t)s_poly[i];
 #endif
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -2294,6 +2367,11 @@ static int resident_blocks(const void* kernel, int block, size_t lds) {
 }
 
 template <int IS>
+static void launch_emit(const SplitArgs& a, int64_t nc, hipStream_t s) {
+  hipLaunchKernelGGL(split_emit_kernel<IS>, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
+}
+
+template <int IS>
 static void launch_split_t(const SplitArgs& a, hipStream_t s, hipEvent_t after_classify, hipEvent_t after_mixed) {
   const int64_t nc = split_chunks(a.j.n);
   const size_t lds = (IS == MGPU_H3 && a.j.chips.raster_blk) ? (size_t)a.j.chips.raster_bnx * a.j.chips.raster_bny * 2 : 0;
@@ -2311,7 +2389,7 @@ static void launch_split_t(const SplitArgs& a, hipStream_t s, hipEvent_t after_c
   if (after_mixed) hipEventRecord(after_mixed, s);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.chunk_pairs, a.j.group_cand, nc,
                      a.chunk_off, a.j.counters);
-  hipLaunchKernelGGL(split_emit_kernel<IS>, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
+  launch_emit<IS>(a, nc, s);
 }
 
 hipError_t launch_split(int is, const SplitArgs& a, hipStream_t s, hipEvent_t after_classify, hipEvent_t after_mixed) {
@@ -2328,9 +2406,9 @@ hipError_t launch_split_emit(int is, const SplitArgs& a, hipStream_t s) {
   if (a.j.n <= 0) return hipSuccess;
   const int64_t nc = split_chunks(a.j.n);
   if (is == MGPU_H3)
-    hipLaunchKernelGGL(split_emit_kernel<MGPU_H3>, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
+    launch_emit<MGPU_H3>(a, nc, s);
   else
-    hipLaunchKernelGGL(split_emit_kernel<MGPU_BNG>, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
+    launch_emit<MGPU_BNG>(a, nc, s);
   return hipGetLastError();
 }
 
