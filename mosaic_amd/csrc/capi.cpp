@@ -62,8 +62,8 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // offsets, so a byte copy of the blob on another GPU (RCCL broadcast) is a
 // complete chip table there.
 constexpr uint64_t kBlobMagic = 0x4d4f534149434850ULL;  // "MOSAICHP"
-constexpr int kBlobArrays = 24;
-constexpr uint32_t kBlobVersion = 10;  // 10: class -> polygon table
+constexpr int kBlobArrays = 25;
+constexpr uint32_t kBlobVersion = 11;  // 11: row-band second level
 struct BlobHeader {
   uint64_t magic;
   uint32_t version, hash_mask, max_probe, n_chips, n_cells;
@@ -86,6 +86,7 @@ struct BlobHeader {
   uint32_t raster_pc[4];
   uint32_t raster_sub_n, raster_sub_w;
   uint32_t raster_bshift, raster_bnx, raster_bny, raster_ncls;
+  uint32_t raster_band_shift, raster_nband;
 };
 constexpr size_t kBlobHeaderBytes = 1024;
 static_assert(sizeof(BlobHeader) <= kBlobHeaderBytes, "header too large");
@@ -138,7 +139,10 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.raster_cls = (const uint64_t*)(base + h.off[19]);
   v.raster_sub_n = h.raster_sub_n;
   v.raster_sub_w = h.raster_sub_w;
-  v.raster_rank = h.raster_sub_n ? (const mgpu::RankWord*)(base + h.off[20]) : nullptr;
+  v.raster_band_shift = h.raster_band_shift;
+  v.raster_nband = h.raster_nband;
+  v.raster_band = h.raster_nband ? (const uint32_t*)(base + h.off[24]) : nullptr;
+  v.raster_rank = h.raster_sub_n && !h.raster_nband ? (const mgpu::RankWord*)(base + h.off[20]) : nullptr;
   v.raster_sub = (const uint16_t*)(base + h.off[21]);
   v.raster_bshift = h.raster_bshift;
   v.raster_bnx = h.raster_bnx;
@@ -626,6 +630,9 @@ struct Raster {
   uint32_t sub_n = 0, sub_w = 0;
   std::vector<mgpu::RankWord> rank;
   std::vector<uint16_t> sub;
+  // lonlat: band[k] = the refined pixels before raster rows k << band_shift (rank unused)
+  uint32_t band_shift = 0;
+  std::vector<uint32_t> band;
   // blocks of 2^bshift x 2^bshift pixels: the class when all of them share it, else mixed
   uint32_t bshift = 0, bnx = 0, bny = 0;
   std::vector<uint16_t> blk;
@@ -815,6 +822,34 @@ void raster_classes(const mgpu::ChipTableView& hv, const std::vector<uint64_t>& 
   for (uint16_t v : R.cells) R.n_pure += v != mgpu::kPixMixed;
 }
 
+// The lonlat second level without the rank table: a refined mixed pixel holds 0x8000 |
+// its index among the refined pixels of its band of 2^band_shift raster rows, band[k] the
+// refined pixels before band k (a table small enough for LDS), so a mixed point's
+// sub-pixel block is band[row >> band_shift] + (class & 0x7FFF) -- one dependent load
+// fewer than the rank word (chip_table.h).  Needs fewer than 0x7FFF classes and
+// 2^band_shift * nx <= 0x7FFF; else the rank table stays.
+constexpr size_t kRasterBandBytes = 4096;
+#ifndef MGPU_RASTER_BANDS
+#define MGPU_RASTER_BANDS 1
+#endif
+void raster_bands(Raster& R) {
+  if (!MGPU_RASTER_BANDS || R.sub_n == 0 || R.rank.empty() || R.cls.size() >= 0x7FFF || R.nx > 0x7FFF) return;
+  uint32_t sh = 0;
+  while ((uint64_t)R.nx << (sh + 1) <= 0x7FFF && (1u << (sh + 1)) <= R.ny) sh++;
+  const uint32_t nb = (R.ny + (1u << sh) - 1) >> sh;
+  if ((size_t)nb * 4 > kRasterBandBytes) return;
+  R.band.assign(nb, 0);
+  uint32_t b = 0;
+  for (uint32_t k = 0; k < nb; k++) {
+    R.band[k] = b;
+    const size_t p0 = (size_t)(k << sh) * R.nx, p1 = std::min<size_t>((size_t)((k + 1) << sh) * R.nx, R.cells.size());
+    for (size_t p = p0; p < p1; p++)
+      if ((R.rank[p >> 5].bits >> (p & 31)) & 1) R.cells[p] = (uint16_t)(0x8000u | (b++ - R.band[k]));
+  }
+  R.band_shift = sh;
+  R.rank.clear();
+}
+
 // the block table over the level-1 classes: the smallest block edge 2^s (s >= 3) whose
 // table fits kRasterBlkBytes (the join kernels hold it in LDS)
 constexpr size_t kRasterBlkBytes = 40 * 1024;
@@ -973,6 +1008,7 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
   }
   raster_classes(hv, a1, a2, R);
   raster_blocks(R);
+  raster_bands(R);
   return true;
 }
 
@@ -1890,6 +1926,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
       {raster.sub.data(), raster.sub.size() * 2, 0},
       {raster.blk.data(), raster.blk.size() * 2, 0},
       {cls_poly.data(), cls_poly.size() * 4, 0},
+      {raster.band.data(), raster.band.size() * 4, 0},
   };
   size_t total = kBlobHeaderBytes;
   BlobHeader hdr{};
@@ -1927,6 +1964,8 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   hdr.raster_bnx = raster.bnx;
   hdr.raster_bny = raster.bny;
   hdr.raster_ncls = (uint32_t)cls_poly.size();
+  hdr.raster_band_shift = raster.band_shift;
+  hdr.raster_nband = (uint32_t)raster.band.size();
   for (size_t k = 0; k < parts.size(); k++) {
     parts[k].off = total;
     hdr.off[k] = total;

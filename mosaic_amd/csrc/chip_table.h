@@ -185,7 +185,12 @@ struct ChipTableView {
   // table 1/8 the size of the pixel classes -- it stays in L2 beside them -- that the
   // streaming kernel loads together with the pixel's class).
   uint32_t raster_sub_n, raster_sub_w;
-  const RankWord* raster_rank;  // [ceil(ny * nx / 32)], or null: no second level
+  const RankWord* raster_rank;  // [ceil(ny * nx / 32)], or null: no second level / bands
+  // lonlat, instead of raster_rank (capi.cpp raster_bands): a refined mixed pixel's class
+  // is 0x8000 | its index within its band of 2^raster_band_shift rows, b = raster_band[iy
+  // >> raster_band_shift] + (class & 0x7FFF); every other class is below 0x7FFF
+  uint32_t raster_band_shift, raster_nband;
+  const uint32_t* raster_band;  // [raster_nband], or null
   const uint16_t* raster_sub;
   // lonlat: blocks of 2^bshift x 2^bshift pixels, raster_blk[(iy >> bshift) * bnx + (ix >>
   // bshift)] = the class all of the block's pixels share, else kPixMixed (a table small

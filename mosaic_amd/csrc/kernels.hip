@@ -1029,13 +1029,15 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   constexpr int kItems = kChunk / 64;       // points per lane per chunk
   const JoinArgs& a = sa.j;
   const ChipTableView& t = a.chips;
-  extern __shared__ uint16_t s_blk[];       // [raster_bny * raster_bnx] (IS == H3)
+  extern __shared__ uint16_t s_blk[];       // [raster_bny * raster_bnx] (IS == H3), then the row bands
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool use_blk = IS == MGPU_H3 && t.raster_blk != nullptr;
-  if (use_blk) {
-    const uint32_t nb = t.raster_bnx * t.raster_bny;
-    for (uint32_t i = threadIdx.x; i < nb; i += kCfyBlock) s_blk[i] = t.raster_blk[i];
-  }
+  const uint32_t nblk = use_blk ? t.raster_bnx * t.raster_bny : 0u;
+  uint32_t* s_band = (uint32_t*)(s_blk + ((nblk + 1) & ~1u));
+  if (use_blk)
+    for (uint32_t i = threadIdx.x; i < nblk; i += kCfyBlock) s_blk[i] = t.raster_blk[i];
+  if (IS == MGPU_H3)
+    for (uint32_t i = threadIdx.x; i < t.raster_nband; i += kCfyBlock) s_band[i] = t.raster_band[i];
   __syncthreads();
   Code* codes = (Code*)sa.codes;
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -1096,7 +1098,7 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
         cl[k] = ri[k] < kRasterFull ? (bi[k] != kNoPixel && s_blk[bi[k]] != kPixMixed ? s_blk[bi[k]] : kPixMixed)
                                     : kPixEmpty;  // (LDS, then every non-uniform block point mixed: no global loads)
 #else
-        cl[k] = ri[k] < kRasterFull ? raster_class_blk(t, s_blk, ri[k], bi[k], sb[k])
+        cl[k] = ri[k] < kRasterFull ? raster_class_blk(t, s_blk, ri[k], bi[k], sb[k], s_band)
                                     : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
 #endif
         ge[k] = (IS == MGPU_BNG && ri[k] < kRasterFull) ? t.grid[gix[k]] : 0ull;
@@ -2374,7 +2376,9 @@ static void launch_emit(const SplitArgs& a, int64_t nc, hipStream_t s) {
 template <int IS>
 static void launch_split_t(const SplitArgs& a, hipStream_t s, hipEvent_t after_classify, hipEvent_t after_mixed) {
   const int64_t nc = split_chunks(a.j.n);
-  const size_t lds = (IS == MGPU_H3 && a.j.chips.raster_blk) ? (size_t)a.j.chips.raster_bnx * a.j.chips.raster_bny * 2 : 0;
+  const ChipTableView& ct = a.j.chips;
+  const size_t nblk = (IS == MGPU_H3 && ct.raster_blk) ? (size_t)ct.raster_bnx * ct.raster_bny : 0;
+  const size_t lds = IS == MGPU_H3 ? ((nblk + 1) & ~(size_t)1) * 2 + (size_t)ct.raster_nband * 4 : 0;
   const int64_t wg = (nc + kCfyBlock / 64 - 1) / (kCfyBlock / 64);
   const int64_t grid = std::min<int64_t>(wg, (int64_t)resident_blocks((const void*)classify_wave_kernel<IS>, kCfyBlock, lds));
   hipLaunchKernelGGL(classify_wave_kernel<IS>, dim3((unsigned)grid), dim3(kCfyBlock), lds, s, a, nc);

@@ -67,16 +67,25 @@ MGPU_HDI uint32_t raster_index(const ChipTableView& t, double px, double py, boo
     u = u < t.raster_sub_n ? u : t.raster_sub_n - 1;
     v = v < t.raster_sub_n ? v : t.raster_sub_n - 1;
     *sub = v * t.raster_sub_n + u;
+    if (t.raster_band) *sub |= (iy >> t.raster_band_shift) << 16;  // the row band (raster_class)
   }
   return iy * t.raster_nx + ix;
 }
 
 // The class of pixel ri (a raster_index result below kRasterFull), refined by its
-// second level when the pixel is mixed.
+// second level when the pixel is mixed (`band`: raster_band or its LDS copy).
 #ifndef MGPU_RANK_SPEC
 #define MGPU_RANK_SPEC 0
 #endif
-MGPU_HDI uint32_t raster_class(const ChipTableView& t, uint32_t ri, uint32_t sub) {
+MGPU_HDI uint32_t raster_class(const ChipTableView& t, uint32_t ri, uint32_t sub, const uint32_t* band = nullptr) {
+  if (t.raster_band) {
+    uint32_t cl = t.raster[ri];
+    if (cl >= 0x8000u && cl != kPixMixed) {
+      const uint64_t b = (uint64_t)(band ? band : t.raster_band)[sub >> 16] + (cl & 0x7FFFu);
+      cl = t.raster_sub[b * t.raster_sub_n * t.raster_sub_n + (sub & 0xFFFFu)];
+    }
+    return cl;
+  }
 #if MGPU_RANK_SPEC
   // the rank word loads beside the pixel's class (no second round trip for mixed pixels)
   const RankWord w = t.raster_rank ? t.raster_rank[ri >> 5] : RankWord{0u, 0u};
@@ -99,9 +108,9 @@ MGPU_HDI uint32_t raster_class(const ChipTableView& t, uint32_t ri, uint32_t sub
 // raster_class with the block table first (`blk_table`: raster_blk or its LDS copy; bi
 // from raster_index, kNoPixel: no block)
 MGPU_HDI uint32_t raster_class_blk(const ChipTableView& t, const uint16_t* blk_table, uint32_t ri, uint32_t bi,
-                                   uint32_t sub) {
+                                   uint32_t sub, const uint32_t* band = nullptr) {
   const uint32_t c = bi != kNoPixel ? blk_table[bi] : kPixMixed;
-  return c != kPixMixed ? c : raster_class(t, ri, sub);
+  return c != kPixMixed ? c : raster_class(t, ri, sub, band);
 }
 
 }  // namespace mgpu

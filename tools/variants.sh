@@ -10,9 +10,15 @@ pids=()
 names=()
 while [ $# -ge 2 ]; do
   d=../../build/variants/$1; mkdir -p $d
+  if [ "${2#host:}" != "$2" ]; then  # NAME "host:-D..." rebuilds capi.cpp (the chip-table builder) instead
+    (/opt/rocm/bin/hipcc $CXXFLAGS ${2#host:} -c capi.cpp -o $d/capi.o 2> $d/build.log &&
+     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $d/libmosaic_gpu.so kernels.o $d/capi.o comm.o tessellate.o \
+       bng_format.o h3_glibc.o ring_join.o geom_kernels.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib && rm -f $d/capi.o) &
+  else
   (/opt/rocm/bin/hipcc --offload-arch=gfx950 $CXXFLAGS $2 -c kernels.hip -o $d/kernels.o 2> $d/build.log &&
    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $d/libmosaic_gpu.so $d/kernels.o capi.o comm.o tessellate.o \
      bng_format.o h3_glibc.o ring_join.o geom_kernels.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib && rm -f $d/kernels.o) &
+  fi
   pids+=($!); names+=($1)
   shift 2
 done
