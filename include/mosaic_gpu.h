@@ -457,6 +457,15 @@ int32_t mgpu_test_raster_host(int32_t index_system, int32_t res, int64_t n_chips
                               const uint8_t* wkb, int64_t n, const double* x, const double* y, int8_t* out_kind,
                               uint32_t* out_first, uint32_t* out_mask, int32_t* out_chip_poly);
 
+/* TEST ONLY -- as mgpu_test_raster_host, for the BNG per-cell answer grids the fused
+ * join's phase 1 reads (chip_table.h cell_ans): out_kind 0 / 1 = answered, 2 = not
+ * answered (candidates' path), 3 = invalid coordinate, 4 = the table has none.
+ * MGPU_E_INVALID_ARG for H3.  Host pointers; no GPU. */
+int32_t mgpu_test_cell_answers_host(int32_t index_system, int32_t res, int64_t n_chips, const int64_t* cell,
+                                    const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
+                                    const uint8_t* wkb, int64_t n, const double* x, const double* y, int8_t* out_kind,
+                                    uint32_t* out_first, uint32_t* out_mask, int32_t* out_chip_poly);
+
 #ifdef __cplusplus
 }
 #endif

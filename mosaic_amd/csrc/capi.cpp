@@ -62,8 +62,8 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // offsets, so a byte copy of the blob on another GPU (RCCL broadcast) is a
 // complete chip table there.
 constexpr uint64_t kBlobMagic = 0x4d4f534149434850ULL;  // "MOSAICHP"
-constexpr int kBlobArrays = 25;
-constexpr uint32_t kBlobVersion = 11;  // 11: row-band second level
+constexpr int kBlobArrays = 27;
+constexpr uint32_t kBlobVersion = 12;  // 12: BNG cell answer grids
 struct BlobHeader {
   uint64_t magic;
   uint32_t version, hash_mask, max_probe, n_chips, n_cells;
@@ -87,6 +87,7 @@ struct BlobHeader {
   uint32_t raster_sub_n, raster_sub_w;
   uint32_t raster_bshift, raster_bnx, raster_bny, raster_ncls;
   uint32_t raster_band_shift, raster_nband;
+  uint32_t cell_ans_g, cell_ans_sw;
 };
 constexpr size_t kBlobHeaderBytes = 1024;
 static_assert(sizeof(BlobHeader) <= kBlobHeaderBytes, "header too large");
@@ -143,6 +144,11 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.raster_nband = h.raster_nband;
   v.raster_band = h.raster_nband ? (const uint32_t*)(base + h.off[24]) : nullptr;
   v.raster_rank = h.raster_sub_n && !h.raster_nband ? (const mgpu::RankWord*)(base + h.off[20]) : nullptr;
+  v.cell_ans_g = h.cell_ans_g;
+  v.cell_ans_sw = h.cell_ans_sw;
+  v.cell_ans_inv_sw = h.cell_ans_sw ? 1.0 / h.cell_ans_sw : 0.0;
+  v.cell_ans_row = h.cell_ans_g ? (const uint32_t*)(base + h.off[25]) : nullptr;
+  v.cell_ans = (const uint16_t*)(base + h.off[26]);
   v.raster_sub = (const uint16_t*)(base + h.off[21]);
   v.raster_bshift = h.raster_bshift;
   v.raster_bnx = h.raster_bnx;
@@ -645,7 +651,7 @@ constexpr int64_t kPixAnswerMixed = -1;
 // of grid entry `e` (first | count << 32 | core_mask << 48): a mask, or kPixAnswerMixed
 int64_t pixel_answer(const mgpu::ChipTableView& hv, uint64_t e, double x0, double y0, double x1, double y1) {
   using namespace mgpu;
-  const uint32_t first = (uint32_t)e, count = (uint32_t)(e >> 32) & 0xFFFF;
+  const uint32_t first = (uint32_t)e, count = mgpu::grid_count(e, false);  // (before the answer grids)
   if (count == 0) return 0;
   if (count > 32) return kPixAnswerMixed;
   uint64_t mask = 0;
@@ -1078,6 +1084,81 @@ bool build_raster_bng(const mgpu::ChipTableView& hv, const mgpu::DenseFace& D, u
   }
   R.n_pure = 0;
   for (uint16_t v : R.cells) R.n_pure += v != mgpu::kPixMixed;
+  return true;
+}
+
+// BNG per-cell answer grids (ChipTableView::cell_ans): every dense cell with border chips
+// (at most kCellAnsChips) is cut into g x g squares of whole metres (g = the largest
+// divisor of the edge <= kCellAnsSide, at least 4), each holding the match mask of the
+// cell's chips when it is certified like a pixel (pixel_answer: no chip edge meets the
+// widened square, the verdicts of its centre), else kCellAnsMixed.  The fused join's
+// phase 1 answers a point in a certified square with one load instead of one candidate
+// (envelope, classification grid) per border chip.
+struct CellAnswers {
+  uint32_t g = 0, sw = 0;
+  std::vector<uint32_t> row;  // answer cells before each dense row
+  std::vector<uint16_t> ans;
+};
+constexpr uint32_t kCellAnsSide = 32;
+constexpr size_t kCellAnsMaxBytes = (size_t)256 << 20;
+#ifndef MGPU_CELL_ANS
+#define MGPU_CELL_ANS 1
+#endif
+bool build_cell_answers(const mgpu::ChipTableView& hv, const mgpu::DenseFace& D, uint32_t edge,
+                        std::vector<uint64_t>& grid, CellAnswers& A) {
+  if (!MGPU_CELL_ANS || edge == 0 || grid.empty() || D.w > 4096) return false;
+  for (uint64_t e : grid)
+    if (((e >> 32) & 0xFFFF) >= 0x8000) return false;  // (bit 47 is the flag)
+  uint32_t g = 0;
+  for (uint32_t d = std::min(kCellAnsSide, edge); d >= 4; d--)
+    if (edge % d == 0) {
+      g = d;
+      break;
+    }
+  if (g == 0) return false;
+  std::vector<uint32_t> cells;
+  for (uint32_t k = 0; k < D.w * D.h; k++) {
+    const uint64_t e = grid[D.base + k];
+    const uint32_t count = (uint32_t)(e >> 32) & 0xFFFF, core = (uint32_t)(e >> 48);
+    if (count == 0 || count > mgpu::kCellAnsChips) continue;
+    if ((core & ((1u << count) - 1)) == (1u << count) - 1) continue;  // all core: nothing to test
+    cells.push_back(k);
+  }
+  // (only where border cells are common: at C4 res 3, 62% of the cells, the join's
+  // candidates fell 130M -> 25M per 1e8 points and its kernel 2.62 -> 1.85 ms; at res 4,
+  // 7.6%, candidates 13.9M -> 2.6M but the kernel 1.65 -> 1.68 ms, profiles/r4_cell_ans_ab.txt)
+  size_t nonempty = 0;
+  for (uint32_t k = 0; k < D.w * D.h; k++) nonempty += ((grid[D.base + k] >> 32) & 0xFFFF) != 0;
+  if (cells.empty() || cells.size() * 5 < nonempty || cells.size() * g * g * 2 > kCellAnsMaxBytes) return false;
+  A.g = g;
+  A.sw = edge / g;
+  A.ans.assign(cells.size() * g * g, mgpu::kCellAnsMixed);
+  const double mu0 = 64 * (std::nextafter(1e7, INFINITY) - 1e7), w = A.sw;
+  mgpu::parallel_for((int64_t)cells.size(), 4, [&](int64_t kb, int64_t ke, int) {
+    for (int64_t i = kb; i < ke; i++) {
+      const uint32_t k = cells[i];
+      const uint64_t e = grid[D.base + k];
+      const double x0 = (double)(D.a0 + (int64_t)(k % D.w)) * edge, y0 = (double)(D.b0 + (int64_t)(k / D.w)) * edge;
+      const double mu = 1e-6 * w + mu0;
+      for (uint32_t v = 0; v < g; v++)
+        for (uint32_t u = 0; u < g; u++) {
+          const int64_t m = pixel_answer(hv, e, x0 + u * w - mu, y0 + v * w - mu, x0 + (u + 1) * w + mu, y0 + (v + 1) * w + mu);
+          if (m != kPixAnswerMixed && m < (int64_t)mgpu::kCellAnsMixed) A.ans[(size_t)i * g * g + v * g + u] = (uint16_t)m;
+        }
+    }
+  });
+  // flag the cells (cells[] ascends: row-major), their index within the row in bits 36-47
+  A.row.assign(D.h, 0);
+  size_t i = 0;
+  for (uint32_t r = 0; r < D.h; r++) {
+    A.row[r] = (uint32_t)i;
+    for (; i < cells.size() && cells[i] / D.w == r; i++) {
+      uint64_t& e = grid[D.base + cells[i]];
+      const uint64_t count = (e >> 32) & 0xFFFF, k = i - A.row[r];
+      e = (e & ~(0xFFFFull << 32) & ~(1ull << 63)) | (count << 32) | ((k & 0x7FF) << 36) | ((k >> 11) << 63) |
+          mgpu::kCellAnsFlag;
+    }
+  }
   return true;
 }
 
@@ -1853,8 +1934,9 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   if (index_system == MGPU_BNG && build_bng_dense(distinct, &lres, &dense[0], &bng_edge, grid))
     probe_mode = mgpu::kProbeDense;
   BLOB_MARK("dense");
-  // pixel index over the dense grid (chip_table.h, build_raster_*)
+  // pixel index over the dense grid (chip_table.h, build_raster_*), BNG cell answer grids
   Raster raster;
+  CellAnswers cell_ans;
   if (probe_mode == mgpu::kProbeDense) {
     mgpu::ChipTableView hv{};
     hv.chip_poly = cpoly.data();
@@ -1869,6 +1951,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
                   ? build_raster_h3(hv, lres, mgpu::h3::k_of_res(lres), bbox, dense, grid, raster, bo)
                   : build_raster_bng(hv, dense[0], bng_edge, grid, raster, bo);
     if (!ok) raster = Raster{};
+    if (index_system == MGPU_BNG && !build_cell_answers(hv, dense[0], bng_edge, grid, cell_ans)) cell_ans = CellAnswers{};
   }
   BLOB_MARK("raster");
   uint32_t cap = 16;
@@ -1927,6 +2010,8 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
       {raster.blk.data(), raster.blk.size() * 2, 0},
       {cls_poly.data(), cls_poly.size() * 4, 0},
       {raster.band.data(), raster.band.size() * 4, 0},
+      {cell_ans.row.data(), cell_ans.row.size() * 4, 0},
+      {cell_ans.ans.data(), cell_ans.ans.size() * 2, 0},
   };
   size_t total = kBlobHeaderBytes;
   BlobHeader hdr{};
@@ -1966,6 +2051,8 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   hdr.raster_ncls = (uint32_t)cls_poly.size();
   hdr.raster_band_shift = raster.band_shift;
   hdr.raster_nband = (uint32_t)raster.band.size();
+  hdr.cell_ans_g = cell_ans.g;
+  hdr.cell_ans_sw = cell_ans.sw;
   for (size_t k = 0; k < parts.size(); k++) {
     parts[k].off = total;
     hdr.off[k] = total;
@@ -2765,6 +2852,54 @@ int32_t mgpu_test_chip_contains_host(int32_t index_system, int64_t n_chips, cons
     }
     out_join_path[i] = mgpu::pip::chip_contains_strips(v, c, x[i], y[i]) ? 1 : 0;
     out_point_locator[i] = mgpu::pip::chip_locate(v, c, x[i], y[i]) == mgpu::pip::kInterior ? 1 : 0;
+  }
+  return MGPU_OK;
+}
+
+// The BNG cell answer grids (ChipTableView::cell_ans), looked up as the fused kernel's
+// phase 1 does: out_kind 1 / 0 = answered (matches: chips out_first + j for the bits j of
+// out_mask), 2 = not answered (no grid for the cell, a mixed square, outside the dense
+// grid), 3 = invalid coordinate, 4 = the table has no answer grids.  Host pointers; no GPU.
+int32_t mgpu_test_cell_answers_host(int32_t index_system, int32_t res, int64_t n_chips, const int64_t* cell,
+                                    const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
+                                    const uint8_t* wkb, int64_t n, const double* x, const double* y, int8_t* out_kind,
+                                    uint32_t* out_first, uint32_t* out_mask, int32_t* out_chip_poly) {
+  if (index_system != MGPU_BNG) return fail(MGPU_E_INVALID_ARG, "cell answer grids are BNG only");
+  HostBlob host;
+  BlobHeader hdr;
+  mgpu_build_opts bo;
+  mgpu_build_opts_default(&bo);
+  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr, bo))
+    return st;
+  const mgpu::ChipTableView v = view_from_header(hdr, host.data());
+  for (int64_t c = 0; c < n_chips; c++) out_chip_poly[c] = v.chip_poly[c];
+  const bool usable = v.cell_ans_row != nullptr && v.res == res;
+  for (int64_t i = 0; i < n; i++) {
+    out_first[i] = out_mask[i] = 0;
+    out_kind[i] = usable ? 2 : 4;
+    if (!usable) continue;
+    if (!(x[i] == x[i] && y[i] == y[i])) {
+      out_kind[i] = 3;
+      continue;
+    }
+    const int32_t eI = mgpu::bng::d2i(x[i]), nI = mgpu::bng::d2i(y[i]);
+    if (!((uint32_t)eI < 10000000u && (uint32_t)nI < 10000000u)) continue;
+    const uint32_t ed = v.bng_edge;
+    const uint32_t col = mgpu::div_fix((uint32_t)eI, ed, v.bng_inv_edge), row = mgpu::div_fix((uint32_t)nI, ed, v.bng_inv_edge);
+    const mgpu::DenseFace& D = v.dense[0];
+    const uint32_t da = col - (uint32_t)D.a0, db = row - (uint32_t)D.b0;
+    if (da >= D.w || db >= D.h) continue;
+    const uint32_t gi = D.base + db * D.w + da;
+    const uint64_t e = v.grid[gi];
+    if (!(e & mgpu::kCellAnsFlag)) continue;
+    const uint32_t u = mgpu::div_fix((uint32_t)eI - col * ed, v.cell_ans_sw, v.cell_ans_inv_sw);
+    const uint32_t w = mgpu::div_fix((uint32_t)nI - row * ed, v.cell_ans_sw, v.cell_ans_inv_sw);
+    const uint64_t ai = (uint64_t)v.cell_ans_row[db] + mgpu::cell_ans_index(e);
+    const uint16_t m = v.cell_ans[(ai * v.cell_ans_g + w) * v.cell_ans_g + u];
+    if (m == mgpu::kCellAnsMixed) continue;
+    out_kind[i] = m ? 1 : 0;
+    out_first[i] = (uint32_t)v.grid[gi];
+    out_mask[i] = m;
   }
   return MGPU_OK;
 }

@@ -191,6 +191,18 @@ struct ChipTableView {
   // >> raster_band_shift] + (class & 0x7FFF); every other class is below 0x7FFF
   uint32_t raster_band_shift, raster_nband;
   const uint32_t* raster_band;  // [raster_nband], or null
+  // BNG dense grid: per-cell answer grids (capi.cpp build_cell_answers).  A cell with
+  // border chips (at most kCellAnsChips) is cut into cell_ans_g x cell_ans_g squares of
+  // cell_ans_sw whole metres; its grid entry carries kCellAnsFlag (bit 47: such tables
+  // have no cell of 2^15 chips) and its index k among the dense row's answer cells (bits
+  // 36-46 and 63 -- the count takes bits 32-35, the core mask no bit 15), and
+  // cell_ans[((cell_ans_row[row] + k) * g + v) * g + u] = the match mask of the cell's
+  // chips for every point of square (u, v) (certified like a pixel), or kCellAnsMixed:
+  // the candidates' path.  Only flagged cells cost a load.
+  uint32_t cell_ans_g, cell_ans_sw;
+  double cell_ans_inv_sw;
+  const uint32_t* cell_ans_row;  // [dense rows], or null: no answer grids
+  const uint16_t* cell_ans;
   const uint16_t* raster_sub;
   // lonlat: blocks of 2^bshift x 2^bshift pixels, raster_blk[(iy >> bshift) * bnx + (ix >>
   // bshift)] = the class all of the block's pixels share, else kPixMixed (a table small
@@ -201,6 +213,16 @@ struct ChipTableView {
 };
 
 enum RasterMode { kRasterNone = 0, kRasterLonLat = 1, kRasterBng = 2 };
+constexpr uint32_t kCellAnsChips = 15;      // chips of a cell with an answer grid, at most
+constexpr uint16_t kCellAnsMixed = 0xFFFF;
+constexpr uint32_t kNoCellAns = 0xFFFFFFFFu;
+constexpr uint64_t kCellAnsFlag = 1ull << 47;
+// the chip count of a dense grid entry (first | count << 32 | core mask << 48); `ans`: the
+// table has answer grids (ChipTableView::cell_ans_row)
+MGPU_HDI_FWD uint32_t grid_count(uint64_t e, bool ans) {
+  return (uint32_t)(e >> 32) & ((ans && (e & kCellAnsFlag)) ? 0xFu : 0xFFFFu);
+}
+MGPU_HDI_FWD uint32_t cell_ans_index(uint64_t e) { return (uint32_t)((e >> 36) & 0x7FF) | (uint32_t)(e >> 63) << 11; }
 constexpr uint16_t kPixEmpty = 0;
 constexpr uint16_t kPixMixed = 0xFFFF;
 

@@ -250,8 +250,8 @@ __device__ __forceinline__ Range probe_range(const ChipTableView& t, uint64_t ke
 // a lane's four points then fly together), else *gi = kNoEntry and the range is final.
 constexpr uint32_t kNoEntry = 0xFFFFFFFFu;
 
-__device__ __forceinline__ Range grid_range(uint64_t e) {
-  return Range{(uint32_t)e, (uint32_t)(e >> 32) & 0xFFFF, (uint32_t)(e >> 48)};
+__device__ __forceinline__ Range grid_range(uint64_t e, bool ans) {
+  return Range{(uint32_t)e, grid_count(e, ans), (uint32_t)(e >> 48)};
 }
 
 // The H3 route for a point the fast projection could not decide (fix kernels only).  A
@@ -378,10 +378,16 @@ template <bool SLOW, int CAND_CAP, int STASH, bool PT_STASH = false>
 __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, const Range& r, double px, double py,
                                             bool& any_tie, uint32_t* s_ncand, uint16_t* s_cand_pj,
                                             double2* s_cand_xy, uint32_t* s_first, uint16_t* s_cnt,
-                                            uint32_t* s_mask) {
+                                            uint32_t* s_mask, uint32_t answer = kNoCellAns) {
   // the streaming kernel keeps no sequential PIP path (its registers would cap
   // occupancy): a cell with more than 32 chips sends the tile to pip_fix_kernel
   if (!SLOW && r.count > (uint32_t)kMaskBits) any_tie = true;
+  if (answer != kNoCellAns) {  // the cell's answer grid decided every chip (BNG)
+    s_first[li] = r.first;
+    if (SLOW) s_cnt[li] = (uint16_t)r.count;
+    s_mask[li] = answer;
+    return;
+  }
   const uint32_t nj = r.count < (uint32_t)kMaskBits ? r.count : (uint32_t)kMaskBits;
   const uint32_t lowm = nj >= 32 ? 0xFFFFFFFFu : ((1u << nj) - 1);
   uint32_t border = ~r.core & lowm;
@@ -588,7 +594,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         bool ok, tie;
         uint32_t gi;
         Range r = chip_probe<IS, SLOW>(a, base + li, px, py, &ok, &tie, &gi);
-        if (gi != kNoEntry) r = grid_range(t.grid[gi]);
+        if (gi != kNoEntry) r = grid_range(t.grid[gi], t.cell_ans_row != nullptr);
         any_tie |= tie;
         phase1_item<SLOW, kCap, kStash, point_stash<G>()>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
       }
@@ -623,11 +629,27 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     uint64_t ge[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; k++) ge[k] = gi[k] != kNoEntry ? t.grid[gi[k]] : 0;
+    // a flagged cell's answer grid (chip_table.h cell_ans): its row base (a small table),
+    // then the square
+    uint32_t av[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
-      if (gi[k] != kNoEntry) r[k] = grid_range(ge[k]);
+      av[k] = kNoCellAns;
+      if (t.cell_ans_row && (ge[k] & kCellAnsFlag)) {
+        const uint32_t eI = (uint32_t)bng::d2i(bx[k]), nI = (uint32_t)bng::d2i(by[k]), ed = t.bng_edge;
+        const uint32_t col = div_fix(eI, ed, t.bng_inv_edge), row = div_fix(nI, ed, t.bng_inv_edge);
+        const uint32_t u = div_fix(eI - col * ed, t.cell_ans_sw, t.cell_ans_inv_sw);
+        const uint32_t v = div_fix(nI - row * ed, t.cell_ans_sw, t.cell_ans_inv_sw);
+        const uint32_t ai = t.cell_ans_row[row - (uint32_t)t.dense[0].b0] + cell_ans_index(ge[k]);
+        const uint16_t m = t.cell_ans[((size_t)ai * t.cell_ans_g + v) * t.cell_ans_g + u];
+        if (m != kCellAnsMixed) av[k] = m;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      if (gi[k] != kNoEntry) r[k] = grid_range(ge[k], t.cell_ans_row != nullptr);
       phase1_item<SLOW, kCap, kStash, point_stash<G>()>(t, k * kBlock + threadIdx.x, r[k], bx[k], by[k], any_tie, &s_ncand, s_cand_pj,
-                        s_cand_xy, s_first, s_cnt, s_mask);
+                        s_cand_xy, s_first, s_cnt, s_mask, av[k]);
     }
   } else {
     // one item ahead: item k + 1's coordinates load while item k projects
@@ -650,7 +672,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         bool ok, tie;
         uint32_t gi;
         r = chip_probe<IS, SLOW>(a, p, px, py, &ok, &tie, &gi);
-        if (gi != kNoEntry) r = grid_range(t.grid[gi]);
+        if (gi != kNoEntry) r = grid_range(t.grid[gi], t.cell_ans_row != nullptr);
         n_tie_pts += (SLOW && tie) ? 1u : 0u;
         any_bad |= !ok;
         any_tie |= tie;

@@ -30,7 +30,7 @@ import oracle as O  # noqa: E402  (test infrastructure: the checker)
 from test_pip_exact_host import adversarial, rings_of  # noqa: E402
 
 
-def raster_lookup(c, res, x, y):
+def raster_lookup(c, res, x, y, hook="mgpu_test_raster_host"):
     n = len(x)
     x = np.ascontiguousarray(x, dtype=np.float64)
     y = np.ascontiguousarray(y, dtype=np.float64)
@@ -39,9 +39,8 @@ def raster_lookup(c, res, x, y):
     mask = np.empty(n, np.uint32)
     cpoly = np.empty(len(c), np.int32)
     p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-    N.check(N.lib().mgpu_test_raster_host(c.index_system, res, len(c), p(c.cell), p(c.polygon_id), p(c.is_core),
-                                          p(c.wkb_offsets), p(c.wkb), n, p(x), p(y), p(kind), p(first), p(mask),
-                                          p(cpoly)))
+    N.check(getattr(N.lib(), hook)(c.index_system, res, len(c), p(c.cell), p(c.polygon_id), p(c.is_core),
+                                   p(c.wkb_offsets), p(c.wkb), n, p(x), p(y), p(kind), p(first), p(mask), p(cpoly)))
     return kind, first, mask, cpoly
 
 
@@ -55,8 +54,8 @@ def adversarial_points(c, rng, n_chips):
     return np.concatenate(pts)
 
 
-def check_raster(c, res, x, y, min_pure):
-    kind, first, mask, cpoly = raster_lookup(c, res, x, y)
+def check_raster(c, res, x, y, min_pure, hook="mgpu_test_raster_host"):
+    kind, first, mask, cpoly = raster_lookup(c, res, x, y, hook)
     assert not (kind == 4).any(), "no pixel index was built"
     assert not (kind == 3).any()
     pure = kind <= 1
@@ -141,3 +140,42 @@ def test_raster_skewed_fractal_polygons():
     c = M.tessellate(P, M.H3IndexSystem(), 9)
     x, y = W.boundary_points(P, 200_000, 16, 0.003)
     check_raster(c, 9, x, y, 0.2)
+
+
+def test_cell_answers_bng_london():
+    # the fused join's per-cell answer grids (BNG cells with border chips): every answered
+    # point's matches equal the oracle's, on random points, chip-edge adversaries and
+    # whole-metre points on square lines
+    import bench_workloads as W
+    res = 3
+    c = M.tessellate(W.london_districts(), M.BNGIndexSystem(), res)
+    rng = np.random.default_rng(20)
+    x, y = W.london_points(300_000, 21)
+    hook = "mgpu_test_cell_answers_host"
+    frac, pairs = check_raster(c, res, x, y, 0.3, hook)
+    print("res %d: %.3f of the points answered, %d pairs" % (res, frac, pairs))
+    assert pairs > 50_000
+    a = adversarial_points(c, rng, 3000)
+    e = rng.integers(503000, 561000, 20000).astype(np.float64)
+    nn = rng.integers(155000, 201000, 20000).astype(np.float64)
+    xs = np.concatenate([a[:, 0], e, np.nextafter(e, -np.inf), e + 0.999999])
+    ys = np.concatenate([a[:, 1], nn, nn, np.nextafter(nn, np.inf)])
+    check_raster(c, res, xs, ys, 0.02, hook)
+    # res 4: border cells are 7.6% of the cells -- the builder leaves the grids out
+    c4 = M.tessellate(W.london_districts(), M.BNGIndexSystem(), 4)
+    kind, _, _, _ = raster_lookup(c4, 4, np.array([530000.0]), np.array([180000.0]), hook)
+    assert kind[0] == 4
+
+
+def test_cell_answers_bng_crowded_cells():
+    # 40 nested squares: cells of 40 chips (no answer grid; their core masks use bit 15)
+    # beside cells of 7 / 15 chips that have one -- the entries' flag must not be misread
+    base, sc, res = (530000.0, 180000.0), 3000.0, 3
+    sq = [(0.0, 0.0), (1.0, 0.0), (1.0, 1.0), (0.0, 1.0), (0.0, 0.0)]
+    polys = [(pid, [[[(base[0] + sc * u * (1 + 0.01 * pid), base[1] + sc * v * (1 + 0.013 * pid))
+                      for u, v in sq]]]) for pid in range(40, 0, -1)]
+    c = M.tessellate(M.Polygons.from_lists(polys), M.BNGIndexSystem(), res)
+    rng = np.random.default_rng(33)
+    x = base[0] + sc * rng.uniform(-0.1, 1.6, 60_000)
+    y = base[1] + sc * rng.uniform(-0.1, 1.6, 60_000)
+    check_raster(c, res, x, y, 0.05, "mgpu_test_cell_answers_host")
