@@ -410,7 +410,9 @@ def main():
         "libm_overrides": r.stats["libm_overrides"],
         "candidates_per_point": float(r.stats["n_candidates"]) / n,
     }
-    name = "pmc_join_traffic.json" if a.config == "c2" else "pmc_join_traffic_%s.json" % a.config
+    default_res = {"c2": 9, "c3": 10, "c4": 4, "c5": 9}[a.config]
+    name = ("pmc_join_traffic" if a.config == "c2" else "pmc_join_traffic_%s" % a.config) + \
+        ("" if a.res == default_res else "_r%d" % a.res) + ".json"
     prof = os.path.join(ROOT, "profiles", name)
     if os.path.exists(prof):
         try:
@@ -423,6 +425,23 @@ def main():
                 out["roofline"]["traffic"] = p["hbm_bytes_per_launch"] * n / p["points"]
                 out["roofline"]["traffic_source"] = "profiles/%s (%s%s)" % (
                     name, p.get("round", "?"), "" if p["points"] == n else ", measured on %d points, scaled" % p["points"])
+        except (ValueError, KeyError):
+            pass
+    # VALU issue: the kernel's VALU wave-instructions per point (rocprofv3 SQ_INSTS_VALU of
+    # the same workload, profiles/pmc_valu.json) over this run's kernel time: each wave64
+    # VALU instruction occupies a SIMD-32 for 2 cycles (FP64 FMAs 4: a lower bound), 1024
+    # SIMDs at 2.4 GHz.  When it exceeds the HBM fraction the kernel is issue-bound.
+    vprof = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    if os.path.exists(vprof):
+        try:
+            v = json.load(open(vprof)).get("%s_r%d" % (a.config, a.res))
+            if v and v["kernel"].split("<")[0] == kernel.split("<")[0]:
+                valu = v["valu_insts_per_point"] * n * 2.0 / (1024 * 2.4e9 * stream_ms * 1e-3)
+                out["roofline"]["valu_issue_frac"] = valu
+                out["roofline"]["salu_insts_per_point"] = v["salu_insts_per_point"]
+                out["roofline"]["valu_source"] = "profiles/pmc_valu.json (%s)" % v["round"]
+                if valu > out["roofline"]["frac"]:
+                    out["roofline"]["bound"] = "valu"
         except (ValueError, KeyError):
             pass
     if rank == 0 and world == 1 and not a.no_pcie:

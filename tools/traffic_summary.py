@@ -19,6 +19,9 @@ DESC = {"c2": ("uniform NYC-bbox points, H3 res 9, 263 zones", 9),
         "c3": ("uniform points in the C3 extent, H3 res 10, 74k tract-like polygons (9.4M chips)", 10),
         "c4": ("UPRN-like London points, BNG res 4, 180 districts", 4),
         "c5": ("skewed points near 4 fractal polygons, H3 res 9", 9)}[CFG]
+RES = int(sys.argv[4]) if len(sys.argv) > 4 else DESC[1]   # the join_once --res, if not the default
+if RES != DESC[1]:
+    DESC = (DESC[0].replace("res %d" % DESC[1], "res %d" % RES), RES)
 
 
 def per_kernel(sub):
@@ -31,6 +34,13 @@ def per_kernel(sub):
         short = name.split("mgpu::", 1)[1].split("(", 1)[0]
         tot[short][r["Dispatch_Id"]] += float(r["Counter_Value"])
     return {k: (sum(v.values()) / len(v) * 1024.0, len(v)) for k, v in tot.items()}
+
+
+def traffic_name(cfg, res):
+    """(bench.py reads the same names)"""
+    default = {"c2": 9, "c3": 10, "c4": 4, "c5": 9}[cfg]
+    base = "pmc_join_traffic" if cfg == "c2" else "pmc_join_traffic_%s" % cfg
+    return base + ("" if res == default else "_r%d" % res) + ".json"
 
 
 jf_all, jw_all = per_kernel("join_fetch"), per_kernel("join_write")
@@ -58,6 +68,6 @@ out = {
             "(16 B read + 8 B written per point)",
 }
 json.dump(out, open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles",
-                                 "pmc_join_traffic.json" if CFG == "c2" else "pmc_join_traffic_%s.json" % CFG), "w"),
+                                 traffic_name(CFG, RES)), "w"),
           indent=1)
 print(json.dumps(out, indent=1))
