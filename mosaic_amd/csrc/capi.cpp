@@ -1369,6 +1369,7 @@ int32_t mgpu_ctx_destroy(mgpu_ctx* ctx) {
   if (ctx->split_ws) hipFree(ctx->split_ws);
   if (ctx->bin_ws) hipFree(ctx->bin_ws);
   if (ctx->scratch) hipFree(ctx->scratch);
+  if (ctx->redo) hipFree(ctx->redo);
   if (ctx->tq) hipFree(ctx->tq);
   if (ctx->ovr) hipFree(ctx->ovr);
   if (ctx->ws) hipFree(ctx->ws);
@@ -2517,6 +2518,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   L2.pts_valid = valid;
   L2.pts_valid_off = valid_off;
   L2.emit = e;
+  L2.jargs = a;
   L2.n_tiles = tiles;
   L2.n_ovr = n_ovr;
   L2.tie_host = a.tie_host;
@@ -2599,6 +2601,64 @@ static int32_t launch_call(mgpu_ctx* ctx, const JoinCall& c, bool timed, int64_t
   return MGPU_OK;
 }
 
+// The override pass of a join whose host libm pass moved a cell: only the units holding
+// the overridden points run again (the fused join's tiles; the split pipeline's chunks),
+// then -- if some unit's pair count changed -- the scan and the whole emit, else only
+// those units' output (kernels.hip launch_join_redo).  The binned pipeline -- its tiles
+// hold binned slots -- and a fused join whose first pass used the overflow pool (a rerun
+// would take more of it) run whole.
+static int32_t launch_override_pass(mgpu_ctx* ctx, const JoinCall& c, bool timed, int64_t n_ovr,
+                                    const std::vector<int64_t>& pos, uint64_t pool_used) {
+  auto& L = ctx->last;
+  if (!L.valid || L.binned || (!L.split && pool_used > 0)) return launch_call(ctx, c, timed, n_ovr, 0);
+  // the units, ascending (the positions ascend)
+  const int64_t unit = L.split ? mgpu::split_chunk() : mgpu::join_tile_points();
+  const int64_t n_units = L.split ? mgpu::split_chunks(L.n) : L.n_tiles;
+  std::vector<uint32_t> list;
+  for (int64_t p : pos)
+    if (list.empty() || list.back() != (uint32_t)(p / unit)) list.push_back((uint32_t)(p / unit));
+  if ((int64_t)list.size() * (L.split ? mgpu::split_chunk_tiles() : 1) > L.n_tiles)
+    return launch_call(ctx, c, timed, n_ovr, 0);
+  const size_t o_aff = 256, o_list = align_up(o_aff + (size_t)n_units, 256), o_old = o_list + list.size() * 4;
+  // [0] changed flag, [4] first changed unit (~0), [256] flags per unit, the list, the old counts
+  const size_t bytes = o_old + list.size() * 4;
+  if (bytes > ctx->redo_bytes) {
+    if (ctx->redo) HIP_TRY(hipFree(ctx->redo));
+    ctx->redo = nullptr;
+    ctx->redo_bytes = 0;
+    HIP_TRY(hipMalloc(&ctx->redo, bytes));
+    ctx->redo_bytes = bytes;
+  }
+  auto* rb = (uint8_t*)ctx->redo;
+  mgpu::RedoArgs R{(const uint32_t*)(rb + o_list), (uint32_t*)(rb + o_old), rb + o_aff, (uint32_t*)rb,
+                   (uint32_t*)(rb + 4)};
+  mgpu::JoinArgs a = L.split ? L.sargs.j : L.jargs;
+  a.ovr = ctx->ovr;
+  a.n_ovr = n_ovr;
+  a.tie_host = 0;
+  // (the first pass has finished: settle_join waited for its counters)
+  HIP_TRY(hipMemsetAsync(rb, 0, o_list, c.s));
+  HIP_TRY(hipMemsetAsync(rb + 4, 0xFF, 4, c.s));
+  HIP_TRY(hipMemcpyAsync(rb + o_list, list.data(), list.size() * 4, hipMemcpyHostToDevice, c.s));
+  const uint32_t nd = L.split ? 0u : (uint32_t)list.size();  // (split: the unpair kernel lists the tiles)
+  HIP_TRY(hipMemcpyAsync(a.n_dirty, &nd, 4, hipMemcpyHostToDevice, c.s));
+  HIP_TRY(hipStreamSynchronize(c.s));  // (the pageable sources above)
+  if (L.split) {
+    mgpu::SplitArgs sa = L.sargs;
+    sa.j = a;
+    HIP_TRY(mgpu::launch_split_redo(c.is, sa, R, (int64_t)list.size(), c.s));
+    L.sargs = sa;
+  } else {
+    HIP_TRY(mgpu::launch_join_redo(c.is, a, L.emit, R, (int64_t)list.size(), c.s));
+    L.jargs = a;
+  }
+  if (timed) HIP_TRY(hipEventRecord(ctx->ev1, c.s));
+  if (c.d_n_pairs) HIP_TRY(hipMemcpyAsync(c.d_n_pairs, ctx->ws, 8, hipMemcpyDeviceToDevice, c.s));
+  L.n_ovr = n_ovr;
+  L.tie_host = 0;
+  return MGPU_OK;
+}
+
 // After a join's first launch (near-ties queued for the host when reference_libm): read
 // its counters; grow an overflowed near-tie queue and launch again; recompute the queued
 // points with the reference's libm and, only if a cell moves, launch once more with the
@@ -2640,7 +2700,9 @@ static int32_t settle_join(mgpu_ctx* ctx, const JoinCall& c, bool timed, bool re
     if (int32_t e = ensure_ovr(ctx, (int64_t)hv.size())) return e;
     HIP_TRY(hipMemcpy(ctx->ovr, hv.data(), hv.size() * 8, hipMemcpyHostToDevice));
     n_ovr = (int64_t)ref.size();
-    if (int32_t e = launch_call(ctx, c, timed, n_ovr, 0)) return e;
+    std::vector<int64_t> pos(ref.size());
+    for (size_t k = 0; k < ref.size(); k++) pos[k] = (int64_t)ref[k].first;
+    if (int32_t e = launch_override_pass(ctx, c, timed, n_ovr, pos, h[5])) return e;
   }
   const int32_t is = c.is;
   const int64_t n = c.n, capacity = c.capacity;

@@ -46,6 +46,9 @@ struct mgpu_ctx {
   // scratch of the geometry / Arrow entries (decoded points, validity bitmaps), grown on demand
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  // the override pass's scratch (kernels.h RedoArgs), grown on demand
+  void* redo = nullptr;
+  size_t redo_bytes = 0;
   // the last mgpu_pip_join on this context, whose pair records stay in the workspace
   // until the next call (mgpu_pip_join_fetch)
   struct {
@@ -58,6 +61,7 @@ struct mgpu_ctx {
     const uint8_t* pts_valid = nullptr;
     int64_t pts_valid_off = 0;
     mgpu::EmitArgs emit{};
+    mgpu::JoinArgs jargs{};  // (the fused pipeline's, for a rerun of some tiles)
     int64_t n_tiles = 0;
     int64_t n_ovr = 0;  // libm overrides the join ran with
     int tie_host = 0;   // near-ties queued for the host (JoinArgs.tie_host)

@@ -60,6 +60,17 @@ struct JoinArgs {
   int poly_answers;                 // binned pipeline: a one-match answer is (polygon id | 1 << 32)
 };
 
+// The override pass's scratch (launch_join_redo / launch_split_redo): the units (fused
+// tiles / split chunks) to rerun, their counts before, a flag per unit, and whether any
+// count changed.
+struct RedoArgs {
+  const uint32_t* list;
+  uint32_t* old;
+  uint8_t* affected;  // [units], zeroed
+  uint32_t* changed;  // zeroed: 1 when some unit's count changed
+  uint32_t* first;    // ~0 before: the first unit whose count changed
+};
+
 // The split pipeline (a chip table with a pixel index and at most 32 chips per cell):
 //   classify_kernel   per point: pixel class -> code (pure answer or "mixed"); per chunk of
 //                     split_chunk() points the pure pairs and the ordered list of mixed points
@@ -80,11 +91,17 @@ struct SplitArgs {
   int64_t capacity;
   int64_t* out_point;
   int32_t* out_poly;
+  // an override rerun (launch_split_redo): as EmitArgs.redo_*, per chunk
+  const uint32_t* redo_first = nullptr;
+  const uint8_t* redo_affected = nullptr;
 };
 int64_t split_chunk();
+int64_t split_chunk_tiles();
 int64_t split_chunks(int64_t n);
 hipError_t launch_split(int is, const SplitArgs& a, hipStream_t s, hipEvent_t after_classify, hipEvent_t after_mixed);
 hipError_t launch_split_emit(int is, const SplitArgs& a, hipStream_t s);
+// the override passes (kernels.hip launch_join_redo): the split pipeline's over R.list's n chunks
+hipError_t launch_split_redo(int is, const SplitArgs& sa, const RedoArgs& R, int64_t n, hipStream_t s);
 
 // The binned pipeline (a chip table far larger than the caches): the points
 // are counting-sorted by a coarse spatial bin so that the join walks the chip table bin
@@ -135,7 +152,13 @@ struct EmitArgs {
   int64_t capacity;
   int64_t* out_point;
   int32_t* out_poly;
+  // an override rerun (launch_join_redo): a tile before *redo_first (the first whose count
+  // changed, ~0: none) and not flagged in redo_affected keeps its output (null: every tile
+  // is emitted)
+  const uint32_t* redo_first = nullptr;
+  const uint8_t* redo_affected = nullptr;
 };
+
 
 // ties: [0] count, [1 .. tie_cap] positions of the points the fast projection hands to the
 // H3 route (zero ties[0] before launch; on overflow the route pass redoes every point);
@@ -168,6 +191,8 @@ int64_t join_tile_points();
 int64_t join_slot_records();   // records reserved per tile (pairs beyond go to the overflow pool)
 // `after_stream` (optional) is recorded right after pip_join_kernel
 hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t s, hipEvent_t after_stream);
+// ... and the fused join's over R.list's n tiles
+hipError_t launch_join_redo(int is, const JoinArgs& a, const EmitArgs& e, const RedoArgs& R, int64_t n, hipStream_t s);
 // pair_emit_kernel alone, over the records a join left in the workspace
 hipError_t launch_emit(const EmitArgs& e, int64_t n_tiles, hipStream_t s);
 // StringType cell ids: offsets[n + 1] (device); chunk: scratch of format_chunks(n) int64;

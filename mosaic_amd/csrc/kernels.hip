@@ -493,6 +493,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #define MGPU_PT(li) (G == 2 ? gbase + (int64_t)s_gidx[li] : G == 1 ? lbase + (li) : (int64_t)tile * kTile + (li))
 #define MGPU_VALID(li) (G ? (uint32_t)(li) < gcount : (int64_t)tile * kTile + (li) < a.n)
 
+
 #ifdef MGPU_STAMPS
   uint64_t st_t = 0;
 #endif
@@ -1267,6 +1268,9 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   __shared__ int32_t s_cp[IS == MGPU_H3 ? kEmitCls : 1];
   __shared__ uint64_t s_mr[MGPU_EMIT_MR ? kEmitMres : 1];  // mixed results: first chip | mask << 32
   __shared__ int32_t s_mp[MGPU_EMIT_MR ? kEmitMres : 1];   // ... the polygon of a one-chip match, else -1
+  // (an override rerun: the chunks before the first whose count changed keep their
+  // output, but for the rerun ones)
+  if (sa.redo_affected && blockIdx.x < *sa.redo_first && !sa.redo_affected[blockIdx.x]) return;
   const int64_t c0 = (int64_t)blockIdx.x * kChunk;
   const int64_t p0 = c0 + (int64_t)threadIdx.x * kClsItems;
   const Code kMixed = IS == MGPU_H3 ? (Code)kPixMixed : (Code)kCodeMixed32;
@@ -1402,7 +1406,9 @@ constexpr int kScanLds = 24576;  // counts staged in LDS (96 KB): 1e8 points in 
 __global__ __launch_bounds__(kScanBlock) void tile_scan_kernel(const uint32_t* __restrict__ gsum,
                                                                const uint32_t* __restrict__ gcand, int64_t ng,
                                                                uint64_t* __restrict__ goff,
-                                                               unsigned long long* __restrict__ counters) {
+                                                               unsigned long long* __restrict__ counters,
+                                                               const uint32_t* only_if = nullptr) {
+  if (only_if && *only_if == 0) return;  // (a rerun that changed no count: the offsets stand)
   // thread i owns the contiguous run [i * per, (i + 1) * per): every load is issued
   // before the one workgroup scan of the run sums (a loop of block scans waits on each)
   __shared__ unsigned long long s_w[kScanBlock / 64];
@@ -1474,6 +1480,11 @@ __global__ __launch_bounds__(kEmitBlock) void pair_emit_kernel(EmitArgs a, int64
   __shared__ uint64_t s_where[kEmitTiles];
   __shared__ int64_t s_off;
   const int64_t t0 = (int64_t)blockIdx.x * kEmitTiles;
+  if (a.redo_affected && t0 + kEmitTiles <= (int64_t)*a.redo_first) {  // (an override rerun: as split_emit_kernel)
+    bool any = false;
+    for (int k = 0; k < kEmitTiles && t0 + k < n_tiles; k++) any |= a.redo_affected[t0 + k] != 0;
+    if (!any) return;
+  }
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     // this block's tiles: counts, slots, in-block prefix
@@ -2378,7 +2389,76 @@ hipError_t launch_join(int is, const JoinArgs& a, const EmitArgs& e, hipStream_t
   return hipGetLastError();
 }
 
+// The override pass (capi.cpp launch_override_pass): a rerun of only the units -- fused
+// tiles, split chunks -- holding points whose H3 cell the host's libm moved (R.list[0 ..
+// n)).  Each unit's pairs leave its count first (the old count kept in R.old), the fix
+// kernel redoes it with the overrides; when no unit's count changed (a point moved to a
+// cell of the same polygons) the offsets stand and only the rerun units are emitted
+// again, else the scan runs and the units from the first changed one on are emitted.
+__global__ __launch_bounds__(256) void tile_unpair_kernel(JoinArgs a, RedoArgs R, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t tile = R.list[i];
+  const uint32_t c = a.tile_count[tile];
+  R.old[i] = c;
+  if (c) atomicSub(&a.group_sum[tile / kScanGroup], c);
+  a.tile_count[tile] = 0;
+  a.tile_where[tile] = kNoDst;
+  R.affected[tile] = 1;
+  a.dirty[i] = tile;
+}
+
+__global__ __launch_bounds__(256) void chunk_unpair_kernel(JoinArgs a, RedoArgs R) {
+  __shared__ uint32_t s_w[4];
+  const uint32_t chunk = R.list[blockIdx.x];
+  const uint32_t nm = a.chunk_mixed[chunk];
+  uint32_t mine = 0;
+  for (uint32_t i = threadIdx.x; i < nm; i += 256) mine += __popc((uint32_t)(a.mixed_res[(int64_t)chunk * kChunk + i] >> 32));
+  mine = wave_sum_u32(mine);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = mine;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    R.old[blockIdx.x] = a.group_sum[chunk];
+    a.group_sum[chunk] -= tot;
+    a.group_cand[chunk] = 0;  // (recounted by the rerun)
+    R.affected[chunk] = 1;
+    const uint32_t nt = (nm + kGTile - 1) / kGTile;  // the chunk's mixed tiles
+    const uint32_t q = atomicAdd(a.n_dirty, nt);
+    for (uint32_t t = 0; t < nt; t++) a.dirty[q + t] = chunk * kChunkTiles + t;
+  }
+}
+
+__global__ __launch_bounds__(256) void redo_compare_kernel(const uint32_t* counts, RedoArgs R, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n && counts[R.list[i]] != R.old[i]) {
+    atomicOr(R.changed, 1u);
+    atomicMin(R.first, R.list[i]);
+  }
+}
+
+hipError_t launch_join_redo(int is, const JoinArgs& a, const EmitArgs& e, const RedoArgs& R, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const unsigned g = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(tile_unpair_kernel, dim3(g), dim3(256), 0, s, a, R, n);
+  const unsigned fix_blocks = (unsigned)(n < kFixGrid ? n : kFixGrid);
+  if (is == MGPU_H3)
+    hipLaunchKernelGGL(pip_fix_kernel<MGPU_H3>, dim3(fix_blocks), dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL(pip_fix_kernel<MGPU_BNG>, dim3(fix_blocks), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(redo_compare_kernel, dim3(g), dim3(256), 0, s, (const uint32_t*)a.tile_count, R, n);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.group_sum, a.group_cand,
+                     (a.n_tiles + kScanGroup - 1) / kScanGroup, e.group_off, a.counters, (const uint32_t*)R.changed);
+  EmitArgs er = e;
+  er.redo_first = R.first;
+  er.redo_affected = R.affected;
+  hipLaunchKernelGGL(pair_emit_kernel, dim3((unsigned)((a.n_tiles + kEmitTiles - 1) / kEmitTiles)),
+                     dim3(kEmitBlock), 0, s, er, a.n_tiles);
+  return hipGetLastError();
+}
+
 int64_t split_chunk() { return kChunk; }
+int64_t split_chunk_tiles() { return kChunkTiles; }
 int64_t split_chunks(int64_t n) { return (n + kChunk - 1) / kChunk; }
 
 // workgroups of `block` threads with `lds` dynamic LDS bytes resident on the whole GPU at once
@@ -2424,6 +2504,31 @@ hipError_t launch_split(int is, const SplitArgs& a, hipStream_t s, hipEvent_t af
     launch_split_t<MGPU_H3>(a, s, after_classify, after_mixed);
   else
     launch_split_t<MGPU_BNG>(a, s, after_classify, after_mixed);
+  return hipGetLastError();
+}
+
+// the split pipeline's override pass (launch_join_redo): R.list = the chunks, n of them
+hipError_t launch_split_redo(int is, const SplitArgs& sa, const RedoArgs& R, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t nc = split_chunks(sa.j.n);
+  hipLaunchKernelGGL(chunk_unpair_kernel, dim3((unsigned)n), dim3(256), 0, s, sa.j, R);
+  const int64_t most = n * kChunkTiles;
+  const unsigned fix = (unsigned)(most < kFixGrid ? most : kFixGrid);
+  if (is == MGPU_H3)
+    hipLaunchKernelGGL((pip_mixed_fix_kernel<MGPU_H3, 2>), dim3(fix), dim3(kBlock), 0, s, sa.j);
+  else
+    hipLaunchKernelGGL((pip_mixed_fix_kernel<MGPU_BNG, 2>), dim3(fix), dim3(kBlock), 0, s, sa.j);
+  hipLaunchKernelGGL(redo_compare_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     (const uint32_t*)sa.chunk_pairs, R, n);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, sa.chunk_pairs, sa.j.group_cand, nc,
+                     sa.chunk_off, sa.j.counters, (const uint32_t*)R.changed);
+  SplitArgs sr = sa;
+  sr.redo_first = R.first;
+  sr.redo_affected = R.affected;
+  if (is == MGPU_H3)
+    launch_emit<MGPU_H3>(sr, nc, s);
+  else
+    launch_emit<MGPU_BNG>(sr, nc, s);
   return hipGetLastError();
 }
 

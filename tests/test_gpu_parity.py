@@ -416,6 +416,30 @@ def test_pip_join_adversarial_points(gpu, nyc_chips_r9):
     assert np.array_equal(gp, op) and np.array_equal(gq, oq)
 
 
+@pytest.mark.parametrize("pipeline", [0, 1, 2])
+def test_pip_join_adversarial_override_pass(gpu, nyc_chips_r9, pipeline):
+    """The override pass after the host's libm moved some cells reruns only the tiles
+    (fused) / chunks (split) holding those points -- the binned pipeline whole -- and the
+    pairs still equal the reference (glibc) oracle's, with the adversarial points spread
+    through a larger batch of uniform points (so most tiles are clean)."""
+    c = nyc_chips_r9
+    ax, ay = adversarial_points(c)
+    rng = np.random.default_rng(91)
+    n = 600_000
+    x = rng.uniform(-74.25, -73.70, n)
+    y = rng.uniform(40.50, 40.91, n)
+    at = np.sort(rng.choice(n, len(ax), replace=False))
+    x[at], y[at] = ax, ay
+    op, oq = oracle_join(c, x, y)
+    ctx = M.default_context(gpu)
+    with ctx.options(pipeline=pipeline):
+        r = M.pip_join(T(x, gpu), T(y, gpu), c, 9)
+    assert r.stats["pipeline"] == pipeline
+    assert r.stats["libm_overrides"] > 0
+    gp, gq = r.numpy()
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+
+
 def test_pip_join_async_adversarial_points(gpu, nyc_chips_r9):
     """mgpu_pip_join_async + mgpu_pip_join_finish on the adversarial points: the pairs
     equal the reference (glibc) oracle's -- which differ from the correctly rounded
