@@ -1872,7 +1872,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   std::vector<std::pair<uint64_t, uint32_t>> keys;
   if (index_system == MGPU_H3 && build_lattice(distinct, keys, &lres, &face_mask, bbox)) {
     probe_mode = mgpu::kProbeLattice;
-    std::sort(keys.begin(), keys.end());
+    parallel_sort(keys, [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) { return a < b; });
     for (size_t k = 0; k < keys.size(); k++) {
       if (k && keys[k].first == keys[k - 1].first) {
         if (keys[k].second != keys[k - 1].second) return fail(MGPU_E_INTERNAL, "lattice key collision");

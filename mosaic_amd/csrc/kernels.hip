@@ -1232,6 +1232,15 @@ __device__ __forceinline__ uint32_t chunk_excl_scan(uint32_t v, uint32_t* s_w, u
 }
 
 constexpr int kEmitWin = 2048;  // pairs staged at a time
+// A thread stages its points' pairs at consecutive slots, so at one item the lanes write
+// slots a thread's pair count apart (~16 at one pair per point: the lanes fall on 4 of
+// the 64 LDS banks).  The slot index is swizzled within its 64-slot row -- the row's
+// index XORed into the low bits -- which spreads those writes over the banks and keeps
+// the reads (consecutive slots: one row per wave) conflict-free.
+#ifndef MGPU_EMIT_SWZ
+#define MGPU_EMIT_SWZ 1
+#endif
+__device__ __forceinline__ uint32_t emit_swz(uint32_t q) { return MGPU_EMIT_SWZ ? q ^ ((q >> 6) & 63u) : q; }
 // the split emit's ordered pairs with non-temporal stores (A/B r3, profiles/r3_emit_nt_ab.txt:
 // C2 emit 0.362 -> 0.328 ms, C5 0.397 -> 0.355); bin_emit_kernel / pair_emit_kernel with
 // plain stores (non-temporal: C3 emit +0.09 ms, C4 +0.06)
@@ -1366,16 +1375,16 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
           v = pure(c);
         if (one >= 0) {
           if (q >= w0 && q < w0 + kEmitWin) {
-            s_poly[q - w0] = (uint32_t)one;
-            s_pt[q - w0] = (uint16_t)(threadIdx.x * kClsItems + k);
+            s_poly[emit_swz(q - w0)] = (uint32_t)one;
+            s_pt[emit_swz(q - w0)] = (uint16_t)(threadIdx.x * kClsItems + k);
           }
           q++;
         }
         const uint32_t first = (uint32_t)v;
         for (uint32_t m = (uint32_t)(v >> 32); m; m &= m - 1, q++)
           if (q >= w0 && q < w0 + kEmitWin) {
-            s_poly[q - w0] = (uint32_t)t.chip_poly[first + __builtin_ctz(m)];
-            s_pt[q - w0] = (uint16_t)(threadIdx.x * kClsItems + k);
+            s_poly[emit_swz(q - w0)] = (uint32_t)t.chip_poly[first + __builtin_ctz(m)];
+            s_pt[emit_swz(q - w0)] = (uint16_t)(threadIdx.x * kClsItems + k);
           }
       }
     }
@@ -1384,13 +1393,13 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
     for (uint32_t i = threadIdx.x; i < cnt; i += kClsBlock) {
       const uint64_t q = base + w0 + i;
       if ((int64_t)q >= sa.capacity) break;
-      const int64_t p = c0 + s_pt[i];
+      const int64_t p = c0 + s_pt[emit_swz(i)];
 #if MGPU_EMIT_NT
       __builtin_nontemporal_store(sa.point_id ? sa.point_id[p] : sa.id_base + p, &sa.out_point[q]);
-      __builtin_nontemporal_store((int32_t)s_poly[i], &sa.out_poly[q]);
+      __builtin_nontemporal_store((int32_t)s_poly[emit_swz(i)], &sa.out_poly[q]);
 #else
       sa.out_point[q] = sa.point_id ? sa.point_id[p] : sa.id_base + p;
-      sa.out_poly[q] = (int32_t)s_poly[i];
+      sa.out_poly[q] = (int32_t)s_poly[emit_swz(i)];
 #endif
     }
     lds_barrier();
@@ -2257,16 +2266,16 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
         const uint32_t first = (uint32_t)v[k], msk = (uint32_t)(v[k] >> 32);
         if (msk == 1u) {  // one match: first is the polygon id (JoinArgs.poly_answers)
           if (q >= w0 && q < w0 + kEmitWin) {
-            s_poly[q - w0] = first;
-            s_pt[q - w0] = (uint16_t)(l0 + k);
+            s_poly[emit_swz(q - w0)] = first;
+            s_pt[emit_swz(q - w0)] = (uint16_t)(l0 + k);
           }
           q++;
           continue;
         }
         for (uint32_t m = msk; m; m &= m - 1, q++)
           if (q >= w0 && q < w0 + kEmitWin) {
-            s_poly[q - w0] = (uint32_t)t.chip_poly[first + __builtin_ctz(m)];
-            s_pt[q - w0] = (uint16_t)(l0 + k);
+            s_poly[emit_swz(q - w0)] = (uint32_t)t.chip_poly[first + __builtin_ctz(m)];
+            s_pt[emit_swz(q - w0)] = (uint16_t)(l0 + k);
           }
       }
     }
@@ -2275,13 +2284,13 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
     for (uint32_t i = threadIdx.x; i < cnt; i += kClsBlock) {
       const uint64_t q = base + w0 + i;
       if ((int64_t)q >= sa.capacity) break;
-      const int64_t p = c0 + s_pt[i];
+      const int64_t p = c0 + s_pt[emit_swz(i)];
 #if MGPU_EMIT_NT_OTHER
       __builtin_nontemporal_store(sa.point_id ? sa.point_id[p] : sa.id_base + p, &sa.out_point[q]);
-      __builtin_nontemporal_store((int32_t)s_poly[i], &sa.out_poly[q]);
+      __builtin_nontemporal_store((int32_t)s_poly[emit_swz(i)], &sa.out_poly[q]);
 #else
       sa.out_point[q] = sa.point_id ? sa.point_id[p] : sa.id_base + p;
-      sa.out_poly[q] = (int32_t)s_poly[i];
+      sa.out_poly[q] = (int32_t)s_poly[emit_swz(i)];
 #endif
     }
     __syncthreads();
