@@ -1099,8 +1099,14 @@ struct CellAnswers {
   std::vector<uint32_t> row;  // answer cells before each dense row
   std::vector<uint16_t> ans;
 };
-constexpr uint32_t kCellAnsSide = 32;
-constexpr size_t kCellAnsMaxBytes = (size_t)256 << 20;
+// (squares per cell side: 25 -> 100 at C4 res 3, 40 m -> 10 m squares, took the join's
+// candidates 25M -> 6.7M per 1e8 points and its kernel 1.85 -> 1.72 ms; 33 MB of grids,
+// built in 0.5 s on 8 host threads -- profiles/r4_cell_ans_ab.txt)
+#ifndef MGPU_CELL_ANS_SIDE
+#define MGPU_CELL_ANS_SIDE 100
+#endif
+constexpr uint32_t kCellAnsSide = MGPU_CELL_ANS_SIDE;
+constexpr size_t kCellAnsMaxBytes = (size_t)64 << 20;
 #ifndef MGPU_CELL_ANS
 #define MGPU_CELL_ANS 1
 #endif
@@ -1109,13 +1115,6 @@ bool build_cell_answers(const mgpu::ChipTableView& hv, const mgpu::DenseFace& D,
   if (!MGPU_CELL_ANS || edge == 0 || grid.empty() || D.w > 4096) return false;
   for (uint64_t e : grid)
     if (((e >> 32) & 0xFFFF) >= 0x8000) return false;  // (bit 47 is the flag)
-  uint32_t g = 0;
-  for (uint32_t d = std::min(kCellAnsSide, edge); d >= 4; d--)
-    if (edge % d == 0) {
-      g = d;
-      break;
-    }
-  if (g == 0) return false;
   std::vector<uint32_t> cells;
   for (uint32_t k = 0; k < D.w * D.h; k++) {
     const uint64_t e = grid[D.base + k];
@@ -1129,7 +1128,12 @@ bool build_cell_answers(const mgpu::ChipTableView& hv, const mgpu::DenseFace& D,
   // 7.6%, candidates 13.9M -> 2.6M but the kernel 1.65 -> 1.68 ms, profiles/r4_cell_ans_ab.txt)
   size_t nonempty = 0;
   for (uint32_t k = 0; k < D.w * D.h; k++) nonempty += ((grid[D.base + k] >> 32) & 0xFFFF) != 0;
-  if (cells.empty() || cells.size() * 5 < nonempty || cells.size() * g * g * 2 > kCellAnsMaxBytes) return false;
+  if (cells.empty() || cells.size() * 5 < nonempty) return false;
+  // the finest square side (a divisor of the edge, whole metres) within the memory bound
+  uint32_t g = 0;
+  for (uint32_t d = std::min(kCellAnsSide, edge); d >= 4 && !g; d--)
+    if (edge % d == 0 && cells.size() * d * d * 2 <= kCellAnsMaxBytes) g = d;
+  if (g == 0) return false;
   A.g = g;
   A.sw = edge / g;
   A.ans.assign(cells.size() * g * g, mgpu::kCellAnsMixed);
