@@ -280,24 +280,29 @@ bool build_lattice(const std::vector<mgpu::HashSlot>& cells, std::vector<std::pa
       H::ijk_to_hex2d(ijk, &hx, &hy);
       H::hex2d_to_geo(hx, hy, face, res, &lat, &lon);
       double v[3] = {cos(lat) * cos(lon), cos(lat) * sin(lon), sin(lat)};
-      double amin = 1e9, ang[20];
+      // faces within 3 rho of the nearest face centre, by dot products (angle <= amin + 3
+      // rho  <=>  dot >= cos(amin + 3 rho): one acos and one cos per cell instead of 20 acos)
+      double dot[20], dmax = -2.0;
       for (int f = 0; f < 20; f++) {
-        ang[f] = angle_between(v, H3T_FACE_CENTER_POINT[f]);
-        amin = std::min(amin, ang[f]);
+        const double* c = H3T_FACE_CENTER_POINT[f];
+        dot[f] = v[0] * c[0] + v[1] * c[1] + v[2] * c[2];
+        dmax = std::max(dmax, dot[f]);
       }
+      const double amin = acos(std::min(1.0, std::max(-1.0, dmax)));
+      const double cthr = cos(std::min(kPi, amin + 3 * rho));
       // a cell deep inside its home face (the only face within 3 rho, every lattice
       // position within hex distance 3 of its own strictly inside the face triangle --
       // normalized i + j + k below the face's maxDim, for Class III compared after the
       // aperture-7 step to the next Class II resolution, which at most quadruples the sum)
       // is reached at its own position only: positions inside one face are distinct cells
       int near = 0;
-      for (int f = 0; f < 20; f++) near += ang[f] <= amin + 3 * rho;
+      for (int f = 0; f < 20; f++) near += dot[f] >= cthr;
       const int64_t sum = (int64_t)ijk.i + ijk.j + ijk.k;
-      const bool interior = near == 1 && ang[face] <= amin + 3 * rho &&
+      const bool interior = near == 1 && dot[face] >= cthr &&
                             ((res & 1) ? 4 * (sum + 6) < kMaxDimCII[res + 1] : sum + 6 < kMaxDimCII[res]);
       if (interior) tk.push_back({H::lattice_key(face, ijk), (uint32_t)ci});
       for (int f = 0; f < 20 && !interior; f++) {
-        if (ang[f] > amin + 3 * rho) continue;
+        if (dot[f] < cthr) continue;
         const double(*F)[3] = H3T_FACE_FRAME[f][res & 1];
         double dc = v[0] * F[2][0] + v[1] * F[2][1] + v[2] * F[2][2];
         if (dc <= 0.5) continue;
@@ -407,7 +412,10 @@ void build_strips(int64_t n_chips, std::vector<uint8_t>& cflags, const std::vect
   const int64_t NC = (n_chips + G - 1) / G;
   std::vector<Strips> cs(NC);
   mgpu::parallel_for(NC, 1, [&](int64_t kb, int64_t ke, int) {
-    std::vector<std::vector<uint32_t>> bucket;
+    // (per chip: each edge's strip range, a count per strip, then the edges placed by a
+    // counting sort -- no per-strip vectors)
+    std::vector<uint32_t> cnt, pos;
+    std::vector<int> sa_of, sb_of;
     std::vector<double> rec;
     std::vector<uint8_t> rring;
     for (int64_t kc = kb; kc < ke; kc++) {
@@ -435,10 +443,11 @@ void build_strips(int64_t n_chips, std::vector<uint8_t>& cflags, const std::vect
         const double inv_h = (H > 0) ? (double)S / H : 0.0;
         st.chip_sy[2 * c] = y0;
         st.chip_sy[2 * c + 1] = inv_h;
-        bucket.assign(S, {});
+        cnt.assign(S + 1, 0);
         rec.clear();
         rring.clear();
-        uint32_t k = 0;
+        sa_of.clear();
+        sb_of.clear();
         for (uint32_t r = r0; r < r1; r++) {
           const uint32_t vb = geo.ring_vtx[r], ve = geo.ring_vtx[r + 1];
           for (uint32_t i = vb + 1; i < ve; i++) {
@@ -448,17 +457,24 @@ void build_strips(int64_t n_chips, std::vector<uint8_t>& cflags, const std::vect
             rring.push_back((uint8_t)(r - r0));
             const int sa = mgpu::strip_of(std::min(p1y, p2y), y0, inv_h, S);
             const int sb = mgpu::strip_of(std::max(p1y, p2y), y0, inv_h, S);
-            for (int q = sa; q <= sb; q++) bucket[q].push_back(k);
-            k++;
+            sa_of.push_back(sa);
+            sb_of.push_back(sb);
+            for (int q = sa; q <= sb; q++) cnt[q + 1]++;
           }
         }
-        for (int q = 0; q < S; q++) {
-          for (uint32_t e : bucket[q]) {
-            L.edges.insert(L.edges.end(), rec.begin() + 4 * e, rec.begin() + 4 * e + 4);
-            L.edge_ring.push_back(rring[e]);
+        for (int q = 0; q < S; q++) cnt[q + 1] += cnt[q];
+        const size_t e_base = L.edge_ring.size();
+        L.edges.resize(4 * (e_base + cnt[S]));
+        L.edge_ring.resize(e_base + cnt[S]);
+        pos.assign(cnt.begin(), cnt.end() - 1);
+        // (edges in ring order within each strip, as the per-strip lists had them)
+        for (size_t e = 0; e < rring.size(); e++)
+          for (int q = sa_of[e]; q <= sb_of[e]; q++) {
+            const size_t d = e_base + pos[q]++;
+            std::copy(rec.begin() + 4 * e, rec.begin() + 4 * e + 4, L.edges.begin() + 4 * d);
+            L.edge_ring[d] = rring[e];
           }
-          L.strip_edge.push_back((uint32_t)L.edge_ring.size());
-        }
+        for (int q = 0; q < S; q++) L.strip_edge.push_back((uint32_t)(e_base + cnt[q + 1]));
       }
     }
   });
@@ -541,8 +557,8 @@ void build_grid(const mgpu::ChipTableView& hv, uint32_t c, const mgpu::wkb::Flat
   // per row for the row's 16 centres at once instead of a ring walk per centre.  A part
   // is entered when its shell's parity is odd and no hole's is; the chip when some part
   // is (a point on no boundary: the Mod-2 rule does not arise).
-  std::vector<double> xs;
-  std::vector<uint32_t> ring_first;  // per ring of the chip: its first crossing in xs
+  static thread_local std::vector<double> xs;
+  static thread_local std::vector<uint32_t> ring_first;  // per ring of the chip: its first crossing in xs
   for (int gy = 0; gy < kGrid; gy++) {
     uint32_t row = 0;
     bool any = false;
