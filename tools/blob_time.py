@@ -17,9 +17,13 @@ def main():
     import bench_workloads as W
     from mosaic_amd import _native as N
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    if "--upload" in sys.argv:  # (the GPU first, as bench.py: torch sets the device up)
+        import torch
+        torch.cuda.set_device(0)
+        M.default_context(torch.device("cuda", 0))
     P, isys, res = {"c3": (W.tract_polygons, M.H3IndexSystem(), 10), "c2": (W.nyc_zones, M.H3IndexSystem(), 9)}[cfg]
     t = time.perf_counter()
-    c = M.tessellate(P(), isys, res)
+    c = M.tessellate(P(), isys, res, keep_core_geometries=("--keep-core" in sys.argv))
     t1 = time.perf_counter()
     out, nb = ctypes.c_void_p(), ctypes.c_int64()
     p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
@@ -29,6 +33,16 @@ def main():
     N.lib().mgpu_host_free(out)
     print("%s: tessellate %.2f s, blob %.2f s (%.2f GB), threads %s" % (cfg, t1 - t, t2 - t1, nb.value / 1e9,
                                                                           os.environ.get("OMP_NUM_THREADS")))
+    if "--upload" in sys.argv:  # (GPU) the whole upload: build + host-to-device copy
+        import torch
+        dev = torch.device("cuda", 0)
+        ctx = M.default_context(dev)
+        for _ in range(2):
+            t3 = time.perf_counter()
+            chips = c.upload(ctx)
+            torch.cuda.synchronize()
+            print("upload %.2f s" % (time.perf_counter() - t3))
+            del chips
 
 
 if __name__ == "__main__":
