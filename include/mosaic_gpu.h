@@ -118,7 +118,7 @@ int32_t mgpu_ctx_get_option(const mgpu_ctx* ctx, const char* key, int64_t* value
 /* Chip-table builder options (mgpu_chips_host_blob_ex; mgpu_chips_upload takes its
  * context's).  raster: 1 = build the pixel index where it pays (H3 res >= 5), 0 = never;
  * raster_bng: 1 = build it for BNG tables too (default 0: measured slower on C4);
- * raster_sub: sub-pixels per mixed pixel edge (2..16, 0 = no second level; default 8);
+ * raster_sub: sub-pixels per mixed pixel edge (2..16, 0 = no second level; default 16);
  * raster_milli: pixel edge / mean cell edge x 1000 (10..1000, default 250). */
 typedef struct mgpu_build_opts {
     int32_t raster, raster_bng, raster_sub, raster_milli;

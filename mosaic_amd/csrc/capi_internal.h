@@ -18,7 +18,7 @@ struct mgpu_options {
   int64_t bin_xcd = 1;                    // ... tiles dealt to the XCDs in contiguous runs
   int64_t spin_us = 2000;                 // synchronous calls: poll (yielding) this long, then block
   // the chip-table builder of mgpu_chips_upload on this context (mgpu_build_opts)
-  int64_t raster = 1, raster_bng = 0, raster_sub = 8, raster_milli = 250;
+  int64_t raster = 1, raster_bng = 0, raster_sub = 16, raster_milli = 250;
 };
 
 struct mgpu_ctx {
