@@ -585,6 +585,26 @@ def test_pip_join_c4_london_districts_bng(gpu):
         assert len(gp) > 0.95 * len(x)  # the districts tile the extent
 
 
+def test_pip_join_c4_answer_grid_edges(gpu):
+    """C4 res 3 joins through the cells' answer grids (10 m squares): chip vertices and
+    edge points (and their ulp neighbours), whole-metre points on square lines and just
+    below them -- every pair equals the oracle's."""
+    import bench_workloads as W
+    from test_raster_host import adversarial_points as chip_adversaries
+    P = W.london_districts()
+    c = M.tessellate(P, M.BNGIndexSystem(), 3)
+    rng = np.random.default_rng(58)
+    a = chip_adversaries(c, rng, 2500)
+    sq = rng.integers(50300, 56100, 60000).astype(np.float64) * 10.0  # square lines (10 m)
+    nn = rng.integers(155000, 201000, 60000).astype(np.float64)
+    x = np.concatenate([a[:, 0], sq, np.nextafter(sq, -np.inf), sq + 9.999999, nn * 0 + 530000.5])
+    y = np.concatenate([a[:, 1], nn, nn, np.nextafter(nn * 1.0, np.inf), nn])
+    r = M.pip_join(T(x, gpu), T(y, gpu), c, 3, index_system=M.BNGIndexSystem())
+    op, oq = oracle_join(c, x, y, res=3, isys=1)
+    gp, gq = r.numpy()
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+
+
 def test_pip_join_c5_skewed_fractal(gpu):
     """C5: points concentrated on the boundaries of 49k-vertex fractal polygons."""
     import bench_workloads as W
