@@ -35,6 +35,7 @@
 #include "capi_internal.h"
 #include "geom_decode.h"
 #include "h3_glibc.h"
+#include "h3_boundary.h"
 
 namespace {
 
@@ -247,7 +248,7 @@ double angle_between(const double* a, const double* b) {
 constexpr int64_t kMaxDimCII[17] = {2, -1, 14, -1, 98, -1, 686, -1, 4802, -1, 33614, -1, 235298, -1, 1647086, -1, 11529602};
 
 bool build_lattice(const std::vector<mgpu::HashSlot>& cells, std::vector<std::pair<uint64_t, uint32_t>>& keys,
-                   int* res_out, uint32_t* face_mask, double bbox[4]) {
+                   int* res_out, uint32_t* face_mask, double bbox[4], std::vector<uint8_t>* interior_out = nullptr) {
   namespace H = mgpu::h3;
   if (cells.empty()) return false;
   int res = (int)((cells[0].cell >> 52) & 15);
@@ -256,6 +257,7 @@ bool build_lattice(const std::vector<mgpu::HashSlot>& cells, std::vector<std::pa
   double k_res = H::k_of_res(res);
   // cells are independent: per-thread key lists and extents, merged afterwards (the
   // caller sorts the keys, so the merge order does not matter)
+  if (interior_out) interior_out->assign(cells.size(), 0);
   const int64_t grain = 4096;
   const int T = mgpu::parallel_slots((int64_t)cells.size(), grain);
   std::vector<std::vector<std::pair<uint64_t, uint32_t>>> tkeys(T);
@@ -301,6 +303,7 @@ bool build_lattice(const std::vector<mgpu::HashSlot>& cells, std::vector<std::pa
       const bool interior = near == 1 && dot[face] >= cthr &&
                             ((res & 1) ? 4 * (sum + 6) < kMaxDimCII[res + 1] : sum + 6 < kMaxDimCII[res]);
       if (interior) tk.push_back({H::lattice_key(face, ijk), (uint32_t)ci});
+      if (interior_out) (*interior_out)[ci] = interior ? 1 : 0;
       for (int f = 0; f < 20 && !interior; f++) {
         if (dot[f] < cthr) continue;
         const double(*F)[3] = H3T_FACE_FRAME[f][res & 1];
@@ -1758,6 +1761,48 @@ static void parallel_sort(std::vector<T>& v, Cmp cmp) {
   }
 }
 
+// Whole-cell chips (H3): a border chip that is its cell's own hexagon -- the reference's
+// demoted border-set cells (§5 of DESIGN.md) -- contains every point of its cell but
+// those next to the hexagon's edges, where H3's spherical cell and the planar lon/lat
+// hexagon part.  Such a cell (the only chip of its cell, res >= 6, a lattice-interior
+// cell: reached from its home face only, six boundary vertices, |lat| <= 75 deg) is
+// flagged by bit 15 of its core mask (unused with one chip); the streaming join answers
+// a point of it whose fast projection lies inside the hexagon scaled by 0.9 about the
+// cell centre (h3_core.h FastHex::deep: a margin of a tenth of the apothem, against the
+// planar lon/lat hexagon's deviation from the projected one -- second order in the cell's
+// angular size times tan(lat) and its distance from the face centre, < 1e-3 of the cell at
+// res >= 6 and |lat| <= 75) without a candidate (kernels.hip phase1_item).  C3: candidates
+// 68.5M -> 59.2M per 1e8 points with a circle of 0.4 (profiles/r4_whole_cell_ab.txt).
+void mark_whole_cells(std::vector<mgpu::HashSlot>& cells, const std::vector<uint8_t>& interior, int res,
+                      const double bbox[4], const std::vector<uint8_t>& cflags, const std::vector<uint32_t>& cpart,
+                      const mgpu::wkb::Flat& geo) {
+  if (res < 6 || interior.size() != cells.size() || !(bbox[1] >= -75.0 && bbox[3] <= 75.0)) return;
+  mgpu::parallel_for((int64_t)cells.size(), 4096, [&](int64_t b, int64_t e, int) {
+    for (int64_t ci = b; ci < e; ci++) {
+      mgpu::HashSlot& d = cells[ci];
+      if (!interior[ci] || d.count != 1 || (d.core_mask & 1)) continue;
+      const uint32_t c = d.first;
+      if (cflags[c] & (mgpu::kChipMulti | mgpu::kChipEmpty | mgpu::kChipNoGeom | mgpu::kChipRect)) continue;
+      if (cpart[c + 1] - cpart[c] != 1) continue;
+      const uint32_t r0 = geo.part_ring[cpart[c]];
+      if (geo.part_ring[cpart[c] + 1] - r0 != 1) continue;
+      const uint32_t v0 = geo.ring_vtx[r0], nv = geo.ring_vtx[r0 + 1] - v0;
+      if (nv != 7 || mgpu::h3b::is_pentagon(d.cell)) continue;
+      const auto bd = mgpu::h3b::cell_boundary(d.cell);
+      if (bd.size() != 6) continue;
+      bool same = true;
+      for (const auto& q : bd) {
+        const double qx = mgpu::h3b::to_degrees(q.lon), qy = mgpu::h3b::to_degrees(q.lat);
+        bool hit = false;
+        for (uint32_t k = 0; k < 6 && !hit; k++)
+          hit = std::fabs(geo.vtx[2 * (v0 + k)] - qx) <= 1e-9 && std::fabs(geo.vtx[2 * (v0 + k) + 1] - qy) <= 1e-9;
+        same = same && hit;
+      }
+      if (same) d.core_mask |= (uint16_t)mgpu::kCoreWhole;
+    }
+  });
+}
+
 // The whole chip table as one host blob (header + arrays, chip_table.h); uploaded as
 // is by mgpu_chips_upload, evaluated in place by mgpu_test_chip_contains_host.
 static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
@@ -1915,8 +1960,10 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   double bbox[4] = {-1e300, -1e300, 1e300, 1e300};
   std::vector<mgpu::HashSlot> entries;
   std::vector<std::pair<uint64_t, uint32_t>> keys;
-  if (index_system == MGPU_H3 && build_lattice(distinct, keys, &lres, &face_mask, bbox)) {
+  std::vector<uint8_t> interior;
+  if (index_system == MGPU_H3 && build_lattice(distinct, keys, &lres, &face_mask, bbox, &interior)) {
     probe_mode = mgpu::kProbeLattice;
+    mark_whole_cells(distinct, interior, lres, bbox, cflags, cpart, geo);
     parallel_sort(keys, [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) { return a < b; });
     for (size_t k = 0; k < keys.size(); k++) {
       if (k && keys[k].first == keys[k - 1].first) {

@@ -217,6 +217,9 @@ constexpr uint32_t kCellAnsChips = 15;      // chips of a cell with an answer gr
 constexpr uint16_t kCellAnsMixed = 0xFFFF;
 constexpr uint32_t kNoCellAns = 0xFFFFFFFFu;
 constexpr uint64_t kCellAnsFlag = 1ull << 47;
+// H3: core-mask bit 15 of a one-chip cell whose chip is the cell's own hexagon (capi.cpp
+// mark_whole_cells): a point deep inside the cell (FastHex::deep) matches it
+constexpr uint32_t kCoreWhole = 0x8000u;
 // the chip count of a dense grid entry (first | count << 32 | core mask << 48); `ans`: the
 // table has answer grids (ChipTableView::cell_ans_row)
 MGPU_HDI_FWD uint32_t grid_count(uint64_t e, bool ans) {

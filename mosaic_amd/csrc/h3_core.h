@@ -557,7 +557,8 @@ MGPU_HD IJK hex2d_to_ijk_fast(double vx, double vy, double* margin) {
 struct FastHex {
   int face;
   IJK ijk;
-  bool tie;  // a decision may differ from the H3 route: recompute with route_face_ijk
+  bool tie;   // a decision may differ from the H3 route: recompute with route_face_ijk
+  bool deep;  // not a tie, and inside the cell's hexagon scaled by 0.9 about its centre
 };
 
 // k_res = sqrt7^res / RES0_U_GNOMONIC; `faces` = the faces to consider (bit mask);
@@ -615,6 +616,14 @@ MGPU_HD FastHex fast_hex2d(double lat, double lon, int res, double k_res, uint32
   double x = da * q, y = db * q;
   double margin;
   o.ijk = hex2d_to_ijk_fast(x, y, &margin);
+  {
+    // inside the hexagon scaled by 0.9 about the centre: the offset's projections on the
+    // three edge normals (0, 60, 120 degrees) within 0.45 (the apothem is 0.5)
+    const double ci = (double)(o.ijk.i - o.ijk.k), cj = (double)(o.ijk.j - o.ijk.k);
+    const double ex = x - (ci - 0.5 * cj), ey = y - cj * 0.8660254037844386;
+    const double p60 = 0.5 * ex + 0.8660254037844386 * ey, p120 = -0.5 * ex + 0.8660254037844386 * ey;
+    o.deep = fabs(ex) < 0.45 && fabs(p60) < 0.45 && fabs(p120) < 0.45;
+  }
   // margin < tie_band(x, y, sin2r) without the division: with sin2r = 1 - dc^2 > 0,
   //   margin < kTieRel * (1 + 1/sin2r) * scale  <=>  margin * sin2r < kTieRel * (sin2r + 1) * scale
   double scale = fabs(x) > fabs(y) ? fabs(x) : fabs(y);
@@ -622,6 +631,7 @@ MGPU_HD FastHex fast_hex2d(double lat, double lon, int res, double k_res, uint32
   double sin2r = fma_(-dc, dc, 1.0);
   o.tie = !in_table || (second - best < 1e-12) || !(dc > 0.5) || !(sin2r > 1e-300) ||
           (margin * sin2r < kTieRel * (sin2r + 1.0) * scale);
+  o.deep = o.deep && !o.tie;
   return o;
 }
 

@@ -291,11 +291,12 @@ __device__ __forceinline__ void route_point(const JoinArgs& a, int64_t p, double
 
 template <int IS, bool SLOW>
 __device__ __forceinline__ Range chip_probe(const JoinArgs& a, int64_t p, double px, double py, bool* ok, bool* tie,
-                                            uint32_t* gi) {
+                                            uint32_t* gi, bool* deep = nullptr) {
   const ChipTableView& t = a.chips;
   const int res = a.res;
   *tie = false;
   *gi = kNoEntry;
+  if (deep) *deep = false;
   if (IS == MGPU_BNG) {
     *ok = px == px && py == py;  // pointToIndex rejects NaN only
     if (!*ok || !a.res_match) return Range{0, 0, 0};
@@ -325,6 +326,7 @@ __device__ __forceinline__ Range chip_probe(const JoinArgs& a, int64_t p, double
     // outside the chip cells' bounding box no cell can match
     if (!(px >= t.bbox[0] && px <= t.bbox[2] && py >= t.bbox[1] && py <= t.bbox[3])) return Range{0, 0, 0};
     h3::FastHex f = h3::fast_hex2d(lat, lon, res, t.k_res, t.face_mask);
+    if (deep) *deep = f.deep;
     if (f.tie) {
       if (a.tie_host) {
         // the host decides: queued with the fast cell, joined with it (a fix kernel
@@ -378,10 +380,11 @@ template <bool SLOW, int CAND_CAP, int STASH, bool PT_STASH = false>
 __device__ __forceinline__ void phase1_item(const ChipTableView& t, int li, const Range& r, double px, double py,
                                             bool& any_tie, uint32_t* s_ncand, uint16_t* s_cand_pj,
                                             double2* s_cand_xy, uint32_t* s_first, uint16_t* s_cnt,
-                                            uint32_t* s_mask, uint32_t answer = kNoCellAns) {
+                                            uint32_t* s_mask, uint32_t answer = kNoCellAns, bool deep = false) {
   // the streaming kernel keeps no sequential PIP path (its registers would cap
   // occupancy): a cell with more than 32 chips sends the tile to pip_fix_kernel
   if (!SLOW && r.count > (uint32_t)kMaskBits) any_tie = true;
+  if (deep && r.count == 1 && (r.core & kCoreWhole)) answer = 1u;  // (H3 whole-cell chip, capi.cpp mark_whole_cells)
   if (answer != kNoCellAns) {  // the cell's answer grid decided every chip (BNG)
     s_first[li] = r.first;
     if (SLOW) s_cnt[li] = (uint16_t)r.count;
@@ -669,16 +672,18 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
         nx = MGPU_LDPT(&a.x[MGPU_PT(li + kBlock)]);
         ny = MGPU_LDPT(&a.y[MGPU_PT(li + kBlock)]);
       }
+      bool deep = false;
       if (MGPU_VALID(li) && pt_valid(a.valid, a.valid_off, p)) {
         bool ok, tie;
         uint32_t gi;
-        r = chip_probe<IS, SLOW>(a, p, px, py, &ok, &tie, &gi);
+        r = chip_probe<IS, SLOW>(a, p, px, py, &ok, &tie, &gi, &deep);
         if (gi != kNoEntry) r = grid_range(t.grid[gi], t.cell_ans_row != nullptr);
         n_tie_pts += (SLOW && tie) ? 1u : 0u;
         any_bad |= !ok;
         any_tie |= tie;
       }
-      phase1_item<SLOW, kCap, kStash, point_stash<G>()>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask);
+      phase1_item<SLOW, kCap, kStash, point_stash<G>()>(t, li, r, px, py, any_tie, &s_ncand, s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask,
+                                                        kNoCellAns, deep);
     }
   }
   count_wave(&a.counters[2], any_bad);
