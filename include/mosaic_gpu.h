@@ -466,6 +466,15 @@ int32_t mgpu_test_cell_answers_host(int32_t index_system, int32_t res, int64_t n
                                     const uint8_t* wkb, int64_t n, const double* x, const double* y, int8_t* out_kind,
                                     uint32_t* out_first, uint32_t* out_mask, int32_t* out_chip_poly);
 
+/* TEST ONLY -- as mgpu_test_raster_host, for the H3 whole-cell shortcut of the streaming
+ * joins (a one-chip cell whose chip is its own hexagon, a point deep inside the cell):
+ * out_kind 1 = answered (chip out_first), 2 = not answered, 3 = invalid coordinate,
+ * 4 = no dense H3 probe.  MGPU_E_INVALID_ARG for BNG.  Host pointers; no GPU. */
+int32_t mgpu_test_whole_cells_host(int32_t index_system, int32_t res, int64_t n_chips, const int64_t* cell,
+                                   const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
+                                   const uint8_t* wkb, int64_t n, const double* x, const double* y, int8_t* out_kind,
+                                   uint32_t* out_first, uint32_t* out_mask, int32_t* out_chip_poly);
+
 #ifdef __cplusplus
 }
 #endif

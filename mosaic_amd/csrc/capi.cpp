@@ -1764,23 +1764,25 @@ static void parallel_sort(std::vector<T>& v, Cmp cmp) {
 // Whole-cell chips (H3): a border chip that is its cell's own hexagon -- the reference's
 // demoted border-set cells (§5 of DESIGN.md) -- contains every point of its cell but
 // those next to the hexagon's edges, where H3's spherical cell and the planar lon/lat
-// hexagon part.  Such a cell (the only chip of its cell, res >= 6, a lattice-interior
-// cell: reached from its home face only, six boundary vertices, |lat| <= 75 deg) is
-// flagged by bit 15 of its core mask (unused with one chip); the streaming join answers
+// hexagon part.  Such a cell (the only chip of its cell, res >= 6, six boundary vertices
+// -- no icosahedron edge crosses it --, not a pentagon, |lat| <= 75 deg) is
+// flagged by bit 15 of its core mask (unused with one chip) in its home face's lattice
+// entry only, so a point probing from another face's frame never sees the flag (its
+// offset would be measured in that frame); the streaming join answers
 // a point of it whose fast projection lies inside the hexagon scaled by 0.9 about the
 // cell centre (h3_core.h FastHex::deep: a margin of a tenth of the apothem, against the
 // planar lon/lat hexagon's deviation from the projected one -- second order in the cell's
 // angular size times tan(lat) and its distance from the face centre, < 1e-3 of the cell at
-// res >= 6 and |lat| <= 75) without a candidate (kernels.hip phase1_item).  C3: candidates
-// 68.5M -> 59.2M per 1e8 points with a circle of 0.4 (profiles/r4_whole_cell_ab.txt).
-void mark_whole_cells(std::vector<mgpu::HashSlot>& cells, const std::vector<uint8_t>& interior, int res,
+// res >= 6 and |lat| <= 75) without a candidate (kernels.hip phase1_item).
+// (profiles/r4_whole_cell_ab.txt: C3 candidates 68.5M -> 55.6M per 1e8 points.)
+void mark_whole_cells(std::vector<mgpu::HashSlot>& cells, int res,
                       const double bbox[4], const std::vector<uint8_t>& cflags, const std::vector<uint32_t>& cpart,
                       const mgpu::wkb::Flat& geo) {
-  if (res < 6 || interior.size() != cells.size() || !(bbox[1] >= -75.0 && bbox[3] <= 75.0)) return;
+  if (res < 6 || !(bbox[1] >= -75.0 && bbox[3] <= 75.0)) return;
   mgpu::parallel_for((int64_t)cells.size(), 4096, [&](int64_t b, int64_t e, int) {
     for (int64_t ci = b; ci < e; ci++) {
       mgpu::HashSlot& d = cells[ci];
-      if (!interior[ci] || d.count != 1 || (d.core_mask & 1)) continue;
+      if (d.count != 1 || (d.core_mask & 1)) continue;
       const uint32_t c = d.first;
       if (cflags[c] & (mgpu::kChipMulti | mgpu::kChipEmpty | mgpu::kChipNoGeom | mgpu::kChipRect)) continue;
       if (cpart[c + 1] - cpart[c] != 1) continue;
@@ -1960,10 +1962,9 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   double bbox[4] = {-1e300, -1e300, 1e300, 1e300};
   std::vector<mgpu::HashSlot> entries;
   std::vector<std::pair<uint64_t, uint32_t>> keys;
-  std::vector<uint8_t> interior;
-  if (index_system == MGPU_H3 && build_lattice(distinct, keys, &lres, &face_mask, bbox, &interior)) {
+  if (index_system == MGPU_H3 && build_lattice(distinct, keys, &lres, &face_mask, bbox)) {
     probe_mode = mgpu::kProbeLattice;
-    mark_whole_cells(distinct, interior, lres, bbox, cflags, cpart, geo);
+    mark_whole_cells(distinct, lres, bbox, cflags, cpart, geo);
     parallel_sort(keys, [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) { return a < b; });
     for (size_t k = 0; k < keys.size(); k++) {
       if (k && keys[k].first == keys[k - 1].first) {
@@ -1971,7 +1972,14 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
         continue;
       }
       const mgpu::HashSlot& d = distinct[keys[k].second];
-      entries.push_back(mgpu::HashSlot{keys[k].first, d.first, d.count, d.core_mask});
+      uint16_t core = d.core_mask;
+      if (core & mgpu::kCoreWhole) {  // (the whole-cell flag only where the key's face is the cell's home face)
+        int hf, r_;
+        mgpu::h3::IJK hijk;
+        if (!mgpu::h3::h3_home_face_ijk(d.cell, &hf, &hijk, &r_) || (int)(keys[k].first >> 56) != hf)
+          core = (uint16_t)(core & ~mgpu::kCoreWhole);
+      }
+      entries.push_back(mgpu::HashSlot{keys[k].first, d.first, d.count, core});
     }
   } else {
     entries = distinct;
@@ -3049,6 +3057,48 @@ int32_t mgpu_test_chip_contains_host(int32_t index_system, int64_t n_chips, cons
     }
     out_join_path[i] = mgpu::pip::chip_contains_strips(v, c, x[i], y[i]) ? 1 : 0;
     out_point_locator[i] = mgpu::pip::chip_locate(v, c, x[i], y[i]) == mgpu::pip::kInterior ? 1 : 0;
+  }
+  return MGPU_OK;
+}
+
+// The H3 whole-cell shortcut (mark_whole_cells + FastHex::deep), looked up as the
+// streaming kernels do (dense probe tables): out_kind 1 = answered, the point matches chip
+// out_first (out_mask 1); 2 = not answered (not deep, not a flagged cell); 3 = invalid
+// coordinate; 4 = the table has no dense H3 probe.  Host pointers; no GPU.
+int32_t mgpu_test_whole_cells_host(int32_t index_system, int32_t res, int64_t n_chips, const int64_t* cell,
+                                   const int32_t* polygon_id, const uint8_t* is_core, const int64_t* wkb_offsets,
+                                   const uint8_t* wkb, int64_t n, const double* x, const double* y, int8_t* out_kind,
+                                   uint32_t* out_first, uint32_t* out_mask, int32_t* out_chip_poly) {
+  if (index_system != MGPU_H3) return fail(MGPU_E_INVALID_ARG, "whole-cell chips are H3 only");
+  HostBlob host;
+  BlobHeader hdr;
+  mgpu_build_opts bo;
+  mgpu_build_opts_default(&bo);
+  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr, bo))
+    return st;
+  const mgpu::ChipTableView v = view_from_header(hdr, host.data());
+  for (int64_t c = 0; c < n_chips; c++) out_chip_poly[c] = v.chip_poly[c];
+  const bool usable = v.probe_mode == mgpu::kProbeDense && v.res == res;
+  for (int64_t i = 0; i < n; i++) {
+    out_first[i] = out_mask[i] = 0;
+    out_kind[i] = usable ? 2 : 4;
+    if (!usable) continue;
+    if (!std::isfinite(x[i]) || !std::isfinite(y[i])) {
+      out_kind[i] = 3;
+      continue;
+    }
+    if (!(x[i] >= v.bbox[0] && x[i] <= v.bbox[2] && y[i] >= v.bbox[1] && y[i] <= v.bbox[3])) continue;
+    const mgpu::h3::FastHex f =
+        mgpu::h3::fast_hex2d(mgpu::h3::to_radians_fast(y[i]), mgpu::h3::to_radians_fast(x[i]), res, v.k_res, v.face_mask);
+    if (!f.deep) continue;
+    const mgpu::DenseFace& D = v.dense[f.face];
+    const uint32_t da = (uint32_t)(f.ijk.i - f.ijk.k - D.a0), db = (uint32_t)(f.ijk.j - f.ijk.k - D.b0);
+    if (da >= D.w || db >= D.h) continue;
+    const uint64_t e = v.grid[D.base + db * D.w + da];
+    if (((e >> 32) & 0xFFFF) != 1 || !((e >> 48) & mgpu::kCoreWhole)) continue;
+    out_kind[i] = 1;
+    out_first[i] = (uint32_t)e;
+    out_mask[i] = 1;
   }
   return MGPU_OK;
 }

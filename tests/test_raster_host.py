@@ -179,3 +179,29 @@ def test_cell_answers_bng_crowded_cells():
     x = base[0] + sc * rng.uniform(-0.1, 1.6, 60_000)
     y = base[1] + sc * rng.uniform(-0.1, 1.6, 60_000)
     check_raster(c, res, x, y, 0.05, "mgpu_test_cell_answers_host")
+
+
+def test_whole_cell_shortcut_nyc_r9(nyc_chips_r9):
+    # H3 whole-cell chips (the reference's demoted border-set cells: one chip, the cell's
+    # own hexagon) answer a point deep inside the cell without a candidate; every such
+    # answer equals the oracle's JTS contains, on uniform points and chip-edge adversaries
+    rng = np.random.default_rng(23)
+    n = 400_000
+    x = rng.uniform(-74.25559136315209, -73.7000090639354, n)
+    y = rng.uniform(40.496115395170364, 40.91553277700258, n)
+    hook = "mgpu_test_whole_cells_host"
+    frac, pairs = check_raster(nyc_chips_r9, 9, x, y, 0.02, hook)
+    print("whole-cell answers: %.3f of the points" % frac)
+    a = adversarial_points(nyc_chips_r9, rng, 2500)
+    check_raster(nyc_chips_r9, 9, a[:, 0], a[:, 1], 0.0, hook)
+
+
+def test_whole_cell_shortcut_tracts_r10():
+    # 400 tract-like polygons (the C3 generator on a small extent) at res 10
+    import bench_workloads as W
+    ext = (-74.3, 40.5, -73.9, 40.8)
+    P = W.tract_polygons(n_cells=400, extent=ext)
+    c = M.tessellate(P, M.H3IndexSystem(), 10)
+    x, y = W.extent_points(ext, 300_000, 5)
+    frac, _ = check_raster(c, 10, np.asarray(x), np.asarray(y), 0.01, "mgpu_test_whole_cells_host")
+    print("whole-cell answers: %.3f of the points" % frac)
