@@ -106,6 +106,14 @@ def test_binned_adversarial_points_and_near_tie_positions(gpu, nyc_chips_r9):
     assert len(ties_b) == r.stats["n_near_ties"] > 0 and len(ties_f) == rf.stats["n_near_ties"] > 0
     assert np.array_equal(ties_b, np.unique(ties_b)) and np.array_equal(ties_f, np.unique(ties_f))
     assert set(ties_f.tolist()) <= set(ties_b.tolist())
+    # ... and every position the fused list lacks lies in a certified pixel (the host's
+    # replica of the pixel index, tests/test_raster_host.py), which the fused join answers
+    # without projecting
+    from test_raster_host import raster_lookup
+    only_b = np.array(sorted(set(ties_b.tolist()) - set(ties_f.tolist())), dtype=np.int64)
+    if len(only_b):
+        kind, _, _, _ = raster_lookup(nyc_chips_r9, 9, x[only_b], y[only_b])
+        assert (kind <= 1).all(), "%d of %d binned-only near-ties not in a certified pixel" % ((kind > 1).sum(), len(only_b))
     assert np.array_equal(rf.numpy()[0], op) and np.array_equal(rf.numpy()[1], oq)
 
 
