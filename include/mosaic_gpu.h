@@ -428,6 +428,10 @@ int32_t mgpu_test_h3_glibc_host(const double* lon, const double* lat, int64_t n,
  * out_lonlat[20 n] (up to 10 vertices per cell), out_nverts[n], out_center[2 n]. */
 int32_t mgpu_test_h3_boundary_host(const int64_t* cells, int64_t n, double* out_lonlat, int32_t* out_nverts,
                                    double* out_center);
+/* TEST ONLY: an H3 cell's geometry as a core chip of it carries it (indexToGeometry,
+ * H3IndexSystem.scala:103-112: the polar caps of makePoleGeometry, antimeridian cells
+ * cut) as WKB into out[cap]; *out_len = its size (MGPU_E_CAPACITY when it exceeds cap). */
+int32_t mgpu_test_h3_cell_wkb_host(int64_t cell, uint8_t* out, int64_t cap, int64_t* out_len);
 int32_t mgpu_test_decode_point(int32_t format, const uint8_t* data, int64_t len, double* x, double* y);
 /* TEST ONLY (profiling): the last join's 16 workspace counters (pairs, near-ties, invalid
  * points, candidates, ...; builds with -DMGPU_STAMPS add per-phase clock ticks of the

@@ -38,7 +38,7 @@ EXPORTS = (
     "mgpu_comm_unique_id", "mgpu_comm_init", "mgpu_comm_info", "mgpu_comm_destroy", "mgpu_chips_broadcast",
     "mgpu_pair_offsets", "mgpu_test_blob_contains_host", "mgpu_points_from_geometry", "mgpu_geometry_to_cells",
     "mgpu_geometry_to_cells_arrow", "mgpu_pip_join_arrow", "mgpu_test_parse_number", "mgpu_test_decode_point",
-    "mgpu_test_h3_elementary_host", "mgpu_test_h3_route_host", "mgpu_test_h3_boundary_host",
+    "mgpu_test_h3_elementary_host", "mgpu_test_h3_route_host", "mgpu_test_h3_boundary_host", "mgpu_test_h3_cell_wkb_host",
     "mgpu_ctx_set_option", "mgpu_ctx_get_option", "mgpu_build_opts_default", "mgpu_chips_host_blob_ex",
     "mgpu_test_h3_glibc_host", "mgpu_internal_geometry_to_cells", "mgpu_test_internal_centroid", "mgpu_test_join_counters",
     "mgpu_test_receive_blob", "mgpu_ring_join",
@@ -169,6 +169,7 @@ def lib():
         "mgpu_test_h3_elementary_host": (I32, [I32, P, P, I64, P]),
         "mgpu_test_h3_route_host": (I32, [P, P, I64, I32, P]),
         "mgpu_test_h3_boundary_host": (I32, [P, I64, P, P, P]),
+        "mgpu_test_h3_cell_wkb_host": (I32, [I64, P, I64, P]),
         "mgpu_ctx_set_option": (I32, [P, ctypes.c_char_p, I64]),
         "mgpu_ctx_get_option": (I32, [P, ctypes.c_char_p, ctypes.POINTER(I64)]),
         "mgpu_build_opts_default": (None, [ctypes.POINTER(BuildOpts)]),

@@ -230,29 +230,52 @@ void write_cell_wkb(const std::vector<std::vector<Pt>>& rings, std::vector<uint8
   mgpu::wkb::write_polygons(out, parts);
 }
 
-// the polar cap: the boundary's vertices by longitude, the edge that crosses the
-// antimeridian cut there, closed along the pole (ccw)
-std::vector<Pt> pole_cap(std::vector<Pt> v, bool north) {
-  std::sort(v.begin(), v.end(), [](const Pt& a, const Pt& b) { return a.x < b.x; });
-  const Pt a = v.back(), b{v.front().x + 360.0, v.front().y};
-  const double t = b.x > a.x ? (180.0 - a.x) / (b.x - a.x) : 0.5;
-  const double lat_x = a.y + t * (b.y - a.y);
-  std::vector<Pt> r;
+// JTS Intersection.intersection (JTS 1.20 algorithm/Intersection.java, what
+// RobustLineIntersector computes for a proper crossing): homogeneous coordinates about the
+// midpoint of the two segments' envelope overlap, every product rounded on its own
+Pt jts_intersection(Pt p1, Pt p2, Pt q1, Pt q2) {
+  const double minX0 = p1.x < p2.x ? p1.x : p2.x, minY0 = p1.y < p2.y ? p1.y : p2.y;
+  const double maxX0 = p1.x > p2.x ? p1.x : p2.x, maxY0 = p1.y > p2.y ? p1.y : p2.y;
+  const double minX1 = q1.x < q2.x ? q1.x : q2.x, minY1 = q1.y < q2.y ? q1.y : q2.y;
+  const double maxX1 = q1.x > q2.x ? q1.x : q2.x, maxY1 = q1.y > q2.y ? q1.y : q2.y;
+  const double midx = ((minX0 > minX1 ? minX0 : minX1) + (maxX0 < maxX1 ? maxX0 : maxX1)) / 2.0;
+  const double midy = ((minY0 > minY1 ? minY0 : minY1) + (maxY0 < maxY1 ? maxY0 : maxY1)) / 2.0;
+  const double p1x = p1.x - midx, p1y = p1.y - midy, p2x = p2.x - midx, p2y = p2.y - midy;
+  const double q1x = q1.x - midx, q1y = q1.y - midy, q2x = q2.x - midx, q2y = q2.y - midy;
+  const double px = p1y - p2y, py = p2x - p1x, pw = p1x * p2y - p2x * p1y;
+  const double qx = q1y - q2y, qy = q2x - q1x, qw = q1x * q2y - q2x * q1y;
+  const double x = py * qw - qy * pw, y = qx * pw - px * qw, w = px * qy - qx * py;
+  return {x / w + midx, y / w + midy};
+}
+
+// The polar cap as makePoleGeometry builds it (H3IndexSystem.scala:361-380): the
+// boundary's vertices shifted east (lng < 0: +360, shiftEast :277-280) and sorted by that
+// longitude form a line; its part in [0, 180] (westernLine), the pole edge (180, pole) ->
+// (-180, pole), its part in [180, 360] shifted back west (easternLine, lng - 360 in
+// floating point, as shiftWest), closed at the first vertex.  Both parts end / start at the
+// crossing JTS's overlay computes with the box edge x = 180.  That ring is ccw at the north
+// pole and clockwise at the south pole; it is returned ccw (the tessellation's convex
+// pieces and clipping need ccw) and write_cell_wkb writes the south cap reversed
+// (Grid::cw_ring), which restores the reference's vertex order from the same start.
+std::vector<Pt> pole_cap(const std::vector<Pt>& b, bool north) {
+  std::vector<Pt> v;
+  for (auto& q : b) v.push_back({q.x < 0 ? q.x + 360.0 : q.x, q.y});
+  std::stable_sort(v.begin(), v.end(), [](const Pt& a, const Pt& c) { return a.x < c.x; });
+  size_t k = 0;  // first vertex east of 180 (shifted)
+  while (k < v.size() && v[k].x <= 180.0) k++;
   const double pl = north ? 90.0 : -90.0;
-  if (north) {
-    r.push_back({-180.0, lat_x});
-    for (auto& q : v) r.push_back(q);
-    r.push_back({180.0, lat_x});
+  std::vector<Pt> r(v.begin(), v.begin() + k);
+  if (k > 0 && k < v.size()) {
+    Pt cut = jts_intersection(v[k - 1], v[k], {180.0, -90.0}, {180.0, 90.0});
+    if (r.back().x != cut.x || r.back().y != cut.y) r.push_back(cut);
     r.push_back({180.0, pl});
     r.push_back({-180.0, pl});
-  } else {
-    r.push_back({-180.0, pl});
-    r.push_back({180.0, pl});
-    r.push_back({180.0, lat_x});
-    for (auto it = v.rbegin(); it != v.rend(); ++it) r.push_back(*it);
-    r.push_back({-180.0, lat_x});
+    if (cut.x >= 180.0) cut.x -= 360.0;
+    r.push_back(cut);
   }
+  for (size_t t = k; t < v.size(); t++) r.push_back({v[t].x >= 180.0 ? v[t].x - 360.0 : v[t].x, v[t].y});
   r.push_back(r[0]);
+  if (!north) std::reverse(r.begin(), r.end());
   return r;
 }
 
@@ -273,6 +296,9 @@ std::vector<std::vector<Pt>> h3_cell_rings(uint64_t id, int res) {
   }
   b.push_back(b[0]);
   if (ring_area(b) < 0) std::reverse(b.begin(), b.end());
+  // (crossesAntiMeridian's `|| !geometry.isValid` arm never fires here: no H3 cell of res
+  // 0-3 -- every one enumerated, tests/test_tessellate_host.py -- with lo < 0 <= hi and a
+  // span <= 180 is self-intersecting, and finer cells are smaller)
   if (!(lo < 0 && hi >= 0 && hi - lo > 180.0)) return {b};
   // across the antimeridian: shift the western longitudes east, cut at 180
   for (auto& q : b)
@@ -309,6 +335,8 @@ struct Grid {
   // ring, or several (H3: a cell cut at the antimeridian); empty = no geometry
   virtual int64_t cell_id(long i, long j) const = 0;
   virtual std::vector<std::vector<Pt>> boundary(long i, long j) const = 0;
+  // a cell whose reference geometry is a clockwise ring (H3's south polar cap)
+  virtual bool cw_ring(int64_t) const { return false; }
   // the cell's centre in input coords (H3: h3ToGeo; BNG: the square's centre)
   virtual Pt center_input(long i, long j, int64_t id) const = 0;
   // lattice row/column iteration for the scanline: row index of a lattice y,
@@ -406,6 +434,7 @@ struct H3Grid : Grid {
     if (!id) return {};
     return h3_cell_rings((uint64_t)id, res);
   }
+  bool cw_ring(int64_t id) const override { return (uint64_t)id == pole_cell(false, res); }
   Pt center_input(long, long, int64_t id) const override {
     const auto c = mgpu::h3b::cell_center((uint64_t)id);
     return {mgpu::h3b::to_degrees(c.lon), mgpu::h3b::to_degrees(c.lat)};
@@ -659,7 +688,10 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
       return;
     }
     Chip ch{id, pid, 1, {}};
-    if (keep_core) write_cell_wkb(rings ? *rings : g.boundary(i, j), ch.wkb);
+    if (keep_core) {
+      const auto rs = rings ? *rings : g.boundary(i, j);
+      write_cell_wkb(g.cw_ring(id) ? reversed(rs) : rs, ch.wkb);
+    }
     out.push_back(std::move(ch));
   };
   // 2. border cells: walk every edge in lattice space; per cell the smallest distance
@@ -816,7 +848,7 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
       if (v == CoreRule::kCore) {
         rule->st.promoted++;
         Chip ch{cid, pid, 1, {}};
-        if (keep_core) write_cell_wkb(rings, ch.wkb);
+        if (keep_core) write_cell_wkb(g.cw_ring(cid) ? reversed(rings) : rings, ch.wkb);
         out.push_back(std::move(ch));
         continue;
       }
@@ -1134,6 +1166,21 @@ int32_t mgpu_test_h3_boundary_host(const int64_t* cells, int64_t n, double* out_
     out_center[2 * i] = mgpu::h3b::to_degrees(c.lon);
     out_center[2 * i + 1] = mgpu::h3b::to_degrees(c.lat);
   }
+  return MGPU_OK;
+}
+
+int32_t mgpu_test_h3_cell_wkb_host(int64_t cell, uint8_t* out, int64_t cap, int64_t* out_len) {
+  const uint64_t h = (uint64_t)cell;
+  const int res = (int)((h >> 52) & 15), bc = (int)((h >> 45) & 127);
+  if (((h >> 59) & 15) != 1 || bc >= H3T_NUM_BASE_CELLS || !out_len)
+    return mgpu::set_error(MGPU_E_INVALID_ARG, "h3 cell wkb: not a cell id");
+  auto rings = h3_cell_rings(h, res);
+  if (h == pole_cell(false, res)) rings = reversed(rings);  // as H3Grid::cw_ring
+  std::vector<uint8_t> w;
+  write_cell_wkb(rings, w);
+  *out_len = (int64_t)w.size();
+  if ((int64_t)w.size() > cap || !out) return mgpu::set_error(MGPU_E_CAPACITY, "h3 cell wkb: %zu bytes", w.size());
+  std::memcpy(out, w.data(), w.size());
   return MGPU_OK;
 }
 

@@ -454,3 +454,54 @@ def test_polar_cap_cells(res):
         got = set(zip(pts.tolist(), polys.tolist()))
         want = brute_force_pairs(P, x, y, O)
         assert got <= want and len(got) > {1: 0.8, 2: 0.95, 3: 0.98}[res] * len(want), (north, len(got), len(want))
+
+
+def _jts_intersection(p1, p2, q1, q2):
+    """JTS 1.20 Intersection.intersection (what RobustLineIntersector computes for a
+    proper crossing), in the same operation order (Python floats are IEEE doubles)."""
+    midx = (max(min(p1[0], p2[0]), min(q1[0], q2[0])) + min(max(p1[0], p2[0]), max(q1[0], q2[0]))) / 2.0
+    midy = (max(min(p1[1], p2[1]), min(q1[1], q2[1])) + min(max(p1[1], p2[1]), max(q1[1], q2[1]))) / 2.0
+    p1x, p1y, p2x, p2y = p1[0] - midx, p1[1] - midy, p2[0] - midx, p2[1] - midy
+    q1x, q1y, q2x, q2y = q1[0] - midx, q1[1] - midy, q2[0] - midx, q2[1] - midy
+    px, py, pw = p1y - p2y, p2x - p1x, p1x * p2y - p2x * p1y
+    qx, qy, qw = q1y - q2y, q2x - q1x, q1x * q2y - q2x * q1y
+    x, y, w = py * qw - qy * pw, qx * pw - px * qw, px * qy - qx * py
+    return (x / w + midx, y / w + midy)
+
+
+def _make_pole_geometry(boundary, north):
+    """makePoleGeometry (H3IndexSystem.scala:361-380) restated: shiftEast, sort by
+    longitude, the line's part in [0, 180] up to its crossing with x = 180, the pole edge
+    (180, pole) -> (-180, pole), the part beyond 180 shifted west, closed at the start."""
+    pl = 90.0 if north else -90.0
+    v = sorted(((x + 360.0 if x < 0 else x, y) for x, y in boundary), key=lambda p: p[0])
+    k = next(i for i, p in enumerate(v) if p[0] > 180.0)
+    cut = _jts_intersection(v[k - 1], v[k], (180.0, 90.0), (180.0, -90.0))
+    west = v[:k] + [cut]
+    east = [(cut[0] - 360.0, cut[1])] + [(x - 360.0, y) for x, y in v[k:]]
+    return west + [(180.0, pl), (-180.0, pl)] + east + [west[0]]
+
+
+@pytest.mark.parametrize("res", [0, 1, 2, 3, 5, 9])
+def test_pole_cell_geometry_matches_make_pole_geometry(res):
+    """an H3 pole cell's geometry (as a core chip of it carries it) is the
+    reference's ring byte for byte -- vertex order, start, orientation (the south cap
+    clockwise) and the JTS crossing with x = 180."""
+    import struct
+    for north in (True, False):
+        s = 1 if north else -1
+        pole = int(O.h3_points_to_cells(np.array([0.0]), np.array([90.0 * s]), res)[0])
+        buf = np.zeros(4096, np.uint8)
+        ln = ctypes.c_int64()
+        _native.check(_native.lib().mgpu_test_h3_cell_wkb_host(pole, _P(buf), len(buf), ctypes.byref(ln)))
+        w = bytes(buf[:ln.value])
+        xy, nv, _ = cell_geometry(np.array([pole]))
+        want = _make_pole_geometry([tuple(p) for p in xy[0, :nv[0]]], north)
+        bo = "<" if w[0] == 1 else ">"  # (JTS's WKBWriter default: big endian)
+        assert struct.unpack(bo + "I", w[1:5])[0] == 3 and struct.unpack(bo + "I", w[5:9])[0] == 1
+        npt = struct.unpack(bo + "I", w[9:13])[0]
+        got = np.frombuffer(w[13:13 + 16 * npt], dtype=bo + "f8").reshape(-1, 2)
+        assert np.array_equal(got, np.array(want)), (north, got.tolist(), want)
+        signed = 0.5 * sum(got[t, 0] * got[t + 1, 1] - got[t + 1, 0] * got[t, 1] for t in range(npt - 1))
+        assert (signed > 0) == north  # the south cap is clockwise, as the reference's
+        assert got[0, 0] >= 0 and got[0, 0] == min(p[0] for p in got if p[0] >= 0)
