@@ -1281,7 +1281,7 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   __shared__ uint16_t s_pt[kEmitWin];    // staging: point of the chunk
   __shared__ int32_t s_cp[IS == MGPU_H3 ? kEmitCls : 1];
   __shared__ uint64_t s_mr[MGPU_EMIT_MR ? kEmitMres : 1];  // mixed results: first chip | mask << 32
-  __shared__ int32_t s_mp[MGPU_EMIT_MR ? kEmitMres : 1];   // ... the polygon of a one-chip match, else -1
+  __shared__ int32_t s_mp[MGPU_EMIT_MR ? kEmitMres : 1];   // ... the polygon of a one-chip match
   // (an override rerun: the chunks before the first whose count changed keep their
   // output, but for the rerun ones)
   if (sa.redo_affected && blockIdx.x < *sa.redo_first && !sa.redo_affected[blockIdx.x]) return;
@@ -1323,7 +1323,7 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
       const uint64_t v = a.mixed_res[c0 + i];
       const uint32_t m = (uint32_t)(v >> 32);
       s_mr[i] = v;
-      s_mp[i] = __popc(m) == 1 ? t.chip_poly[(uint32_t)v + __builtin_ctz(m)] : -1;
+      s_mp[i] = __popc(m) == 1 ? t.chip_poly[(uint32_t)v + __builtin_ctz(m)] : 0;
     }
   }
 #endif
@@ -1369,16 +1369,19 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
       for (int k = 0; k < kClsItems; k++) {
         const Code c = code(k);
         uint64_t v = 0;
-        int32_t one = -1;  // the one polygon, from LDS
+        bool has_one = false;  // one match, its polygon from LDS (any int32 id, negative too)
+        int32_t one = 0;
         if (c == kMixed) {
           const uint32_t rr = r++;
-          if (rr < kMr) one = s_mp[rr];
-          if (one < 0) v = mres(rr);
+          if (rr < kMr && __popc((uint32_t)(s_mr[rr] >> 32)) == 1)
+            has_one = true, one = s_mp[rr];
+          else
+            v = mres(rr);
         } else if (IS == MGPU_H3 && c != 0 && (uint32_t)c < ncp)
-          one = s_cp[(uint32_t)c];
+          has_one = true, one = s_cp[(uint32_t)c];  // classes below raster_pc[0] match once
         else if (c != 0)
           v = pure(c);
-        if (one >= 0) {
+        if (has_one) {
           if (q >= w0 && q < w0 + kEmitWin) {
             s_poly[emit_swz(q - w0)] = (uint32_t)one;
             s_pt[emit_swz(q - w0)] = (uint16_t)(threadIdx.x * kClsItems + k);

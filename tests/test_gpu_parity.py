@@ -440,6 +440,26 @@ def test_pip_join_adversarial_override_pass(gpu, nyc_chips_r9, pipeline):
     assert np.array_equal(gp, op) and np.array_equal(gq, oq)
 
 
+@pytest.mark.parametrize("pipeline", [0, 1, 2])
+def test_pip_join_negative_polygon_ids(gpu, nyc_chips_r9, pipeline):
+    """Polygon ids are caller-supplied int32: negative ids (and INT32_MIN) must come out
+    as given in every pipeline -- the split emit's one-match LDS shortcut must not use the
+    id's sign as a flag (advisor finding, round 4)."""
+    c0 = nyc_chips_r9
+    pid = -c0.polygon_id.astype(np.int64) * 1000
+    pid[c0.polygon_id == c0.polygon_id.max()] = -2 ** 31
+    c = M.ChipTable(c0.cell, pid.astype(np.int32), c0.is_core, c0.wkb_offsets, c0.wkb)
+    x, y = nyc_points(400_000, 17)
+    op, oq = oracle_join(c, x, y)
+    assert (oq < 0).all() and (oq == -2 ** 31).any()
+    ctx = M.default_context(gpu)
+    with ctx.options(pipeline=pipeline):
+        r = M.pip_join(T(x, gpu), T(y, gpu), c, 9)
+    assert r.stats["pipeline"] == pipeline
+    gp, gq = r.numpy()
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+
+
 def test_pip_join_async_adversarial_points(gpu, nyc_chips_r9):
     """mgpu_pip_join_async + mgpu_pip_join_finish on the adversarial points: the pairs
     equal the reference (glibc) oracle's -- which differ from the correctly rounded
