@@ -387,16 +387,29 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
  *                         so a cell the polygon holds whole but outside the core set is a
  *                         border chip whose geometry is the whole cell; chip cells beyond
  *                         the border band are dropped (never visited by the reference);
- *   MGPU_CORE_CLIP        every cell the polygon holds whole is core.
+ *                         Near r the sets are decided as JTS 1.20's BufferOp builds them
+ *                         (8 quadrant segments: fillets of chords, input simplification,
+ *                         depth >= 1 of the raw offset curves -- mosaic_amd/csrc/jts_buffer.h);
+ *   MGPU_CORE_CLIP        every cell the polygon holds whole is core;
+ *   MGPU_CORE_DISTANCE    round 4's form of MOSAICFILL: the sets decided by the centre's
+ *                         exact distance to the boundary (arcs, no simplification).
  * mgpu_tess_result_stats: out6 = {rows, core rows, whole cells flagged border (demoted),
- * partly covered cells flagged core (promoted), dropped, rows within the JTS buffer /
- * simplification tolerance bands (ambiguous)}. */
+ * partly covered cells flagged core (promoted), dropped, rows the restatement leaves
+ * undecided (ambiguous: a centre within 1e-9 r of a buffer curve, or band membership
+ * within the band simplification's 0.01 r; MGPU_CORE_DISTANCE: rows within the JTS
+ * tolerance bands)}. */
 #define MGPU_CORE_MOSAICFILL 0
 #define MGPU_CORE_CLIP 1
+#define MGPU_CORE_DISTANCE 2
 int32_t mgpu_tessellate_ex(int32_t index_system, int32_t res, int64_t n_polys, const int32_t* polygon_id,
                            const int64_t* poly_part_off, const int64_t* part_ring_off, const int64_t* ring_off,
                            const double* xy, int32_t keep_core_geometries, int32_t core_rule, mgpu_tess** out);
 int32_t mgpu_tess_result_stats(const mgpu_tess* t, int64_t* out6);
+/* mgpu_tess_result_core_stats: the first n of {rows, core rows, demoted, promoted,
+ * dropped, ambiguous, carved tests, band tests, core rows whose centre is < r deep,
+ * border rows whose centre is >= r deep, chip cells outside the band (dropped),
+ * DP-sensitive rows, unresolved rows, polygons with an empty buffer(-r)}. */
+int32_t mgpu_tess_result_core_stats(const mgpu_tess* t, int64_t* out, int32_t n);
 int32_t mgpu_tess_result_sizes(const mgpu_tess* t, int64_t* n_chips, int64_t* wkb_bytes);
 int32_t mgpu_tess_result_copy(const mgpu_tess* t, int64_t* cell, int32_t* polygon_id, uint8_t* is_core,
                               int64_t* wkb_offsets, uint8_t* wkb);

@@ -152,7 +152,9 @@ class Polygons:
         return self.xy[:, 0].min(), self.xy[:, 1].min(), self.xy[:, 0].max(), self.xy[:, 1].max()
 
 
-CORE_RULES = {"mosaicfill": 0, "clip": 1}
+CORE_RULES = {"mosaicfill": 0, "clip": 1, "distance": 2}
+CORE_STATS = ("rows", "core", "demoted", "promoted", "dropped", "ambiguous", "carved_tests", "band_tests",
+              "core_below_r", "border_above_r", "band_dropped", "dp_sensitive", "unresolved", "carved_empty")
 
 
 def tessellate(polygons, index_system, resolution, keep_core_geometries=True, core_rule="mosaicfill"):
@@ -160,9 +162,10 @@ def tessellate(polygons, index_system, resolution, keep_core_geometries=True, co
 
     ``core_rule``: "mosaicfill" (default, the reference's: core iff the cell is in
     polyfill(buffer(-r)); a border-set cell the polygon holds whole is a border chip of the
-    whole cell) or "clip" (every wholly covered cell is core) -- include/mosaic_gpu.h
-    MGPU_CORE_*.  The table's ``core_stats`` = rows, core rows, demoted, promoted, dropped,
-    ambiguous (mgpu_tess_result_stats)."""
+    whole cell; near r the sets follow JTS's chorded buffers), "clip" (every wholly covered
+    cell is core) or "distance" (round 4's form of the reference's rule: exact distances) --
+    include/mosaic_gpu.h MGPU_CORE_*.  The table's ``core_stats``: CORE_STATS
+    (mgpu_tess_result_core_stats)."""
     res = index_system.get_resolution(resolution)
     L = N.lib()
     h = ctypes.c_void_p()
@@ -172,8 +175,8 @@ def tessellate(polygons, index_system, resolution, keep_core_geometries=True, co
                               1 if keep_core_geometries else 0, CORE_RULES[core_rule], ctypes.byref(h))
     N.check(st, "tessellation failed")
     try:
-        stats = np.zeros(6, np.int64)
-        N.check(L.mgpu_tess_result_stats(h, stats.ctypes.data))
+        stats = np.zeros(len(CORE_STATS), np.int64)
+        N.check(L.mgpu_tess_result_core_stats(h, stats.ctypes.data, len(CORE_STATS)))
         n, b = ctypes.c_int64(), ctypes.c_int64()
         N.check(L.mgpu_tess_result_sizes(h, ctypes.byref(n), ctypes.byref(b)))
         cell = np.zeros(n.value, np.int64)
@@ -186,5 +189,5 @@ def tessellate(polygons, index_system, resolution, keep_core_geometries=True, co
     finally:
         L.mgpu_tess_destroy(h)
     t = ChipTable(cell, pid, core, off, wkb[:b.value], index_system.code)
-    t.core_stats = dict(zip(("rows", "core", "demoted", "promoted", "dropped", "ambiguous"), stats.tolist()))
+    t.core_stats = dict(zip(CORE_STATS, stats.tolist()))
     return t

@@ -52,6 +52,7 @@
 #include "bng_core.h"
 #include "h3_core.h"
 #include "h3_boundary.h"
+#include "jts_buffer.h"
 #include "parallel.h"
 #include "wkb.h"
 
@@ -608,24 +609,100 @@ struct SegIndex {
 
 struct CoreStats {
   int64_t demoted = 0, promoted = 0, dropped = 0, ambiguous = 0;
+  // the JTS restatement's verdicts near the thresholds (jts_buffer.h)
+  int64_t carved_tests = 0, band_tests = 0;
+  int64_t core_below_r = 0;   // core, centre < r deep: inside a fillet's chords
+  int64_t border_above_r = 0; // not core, centre >= r deep: the input simplification
+  int64_t band_dropped = 0;   // a chip cell outside the (unsimplified) band: never visited
+  int64_t dp_sensitive = 0;   // band membership within the band simplification's 0.01 r
+  int64_t unresolved = 0;     // a centre within 1e-9 r of a buffer curve
+  int64_t carved_empty = 0;   // polygons whose buffer(-r) is empty
 };
 
 struct CoreRule {
   double r = 0;
   SegIndex seg;
   CoreStats st;
+  // the exact-distance decision of round 4 (MGPU_CORE_DISTANCE) instead of the JTS
+  // restatement
+  bool distance_only = false;
+  const Polygon* poly = nullptr;
+  int carved_state = 0;  // 0 not built, 1 non-empty, 2 empty
+  mgpu::jtsbuf::DepthField carved, band;
+  bool band_built = false;
   enum Verdict { kCore, kBorder, kDrop };
+
+  std::vector<mgpu::jtsbuf::Rings> parts() const {
+    std::vector<mgpu::jtsbuf::Rings> o;
+    for (auto& part : poly->parts) {
+      mgpu::jtsbuf::Rings rs;
+      for (auto& ring : part) {
+        std::vector<mgpu::jtsbuf::XY> v;
+        v.reserve(ring.size());
+        for (auto& q : ring) v.push_back({q.x, q.y});
+        rs.push_back(std::move(v));
+      }
+      o.push_back(std::move(rs));
+    }
+    return o;
+  }
+  void ensure_carved() {
+    if (carved_state) return;
+    mgpu::jtsbuf::carved_field(parts(), r, carved);
+    carved.build_index(r);
+    carved_state = carved.any_positive(1e-7 * r) ? 1 : 2;
+    if (carved_state == 2) st.carved_empty++;
+  }
+  void ensure_band() {
+    if (band_built) return;
+    ensure_carved();
+    mgpu::jtsbuf::band_field(parts(), 1.01 * r, carved_state == 2, band);
+    band.build_index(r);
+    band_built = true;
+  }
   // the reference's flag of a chip cell with centre c; inside: the clip's knowledge (1 in,
-  // 0 out, -1 unknown)
+  // 0 out, -1 unknown).  Every caller holds a cell with a non-empty chip.
   Verdict decide(Pt c, int inside) {
     const double q = 1.1 * r;
     double d = seg.min_dist(c, q);
     const bool in = inside >= 0 ? inside == 1 : seg.inside(c);
     if (!in) d = -d;
-    if (std::fabs(d - r) <= 0.02 * r || std::fabs(-d - 1.01 * r) <= 0.03 * r) st.ambiguous++;
-    if (d >= r) return kCore;
-    if (-d > 1.04 * r) return kDrop;
-    return kBorder;
+    if (distance_only) {
+      if (std::fabs(d - r) <= 0.02 * r || std::fabs(-d - 1.01 * r) <= 0.03 * r) st.ambiguous++;
+      if (d >= r) return kCore;
+      if (-d > 1.04 * r) return kDrop;
+      return kBorder;
+    }
+    // polyfill(carved): the centre in buffer(-r).  Its chords reach no deeper than
+    // r cos(3 pi / 64) = 0.989 r and the input simplification removes < 0.0101 r: outside
+    // [0.97 r, 1.05 r) the exact distance decides
+    const mgpu::jtsbuf::XY p{c.x, c.y};
+    bool core;
+    if (d >= 1.05 * r) {
+      core = true;
+    } else if (d < 0.97 * r) {
+      core = false;
+    } else {
+      ensure_carved();
+      st.carved_tests++;
+      core = carved_state == 1 && carved.depth(p) >= 1;
+      if (carved_state == 1 && carved.outline_dist(p, 1e-9 * r, 1e-7 * r) < INFINITY) st.unresolved++, st.ambiguous++;
+      if (core && d < r) st.core_below_r++;
+      if (!core && d >= r) st.border_above_r++;
+    }
+    if (core) return kCore;
+    // polyfill(band) diff core: the band's outline lies 1.01 r out, its chords and the
+    // simplifications move it by < 0.03 r
+    if (std::fabs(d) < 0.95 * r) return kBorder;
+    if (-d > 1.1 * r) return kDrop;
+    ensure_band();
+    st.band_tests++;
+    const bool in_band = band.depth(p) >= 1;
+    const double near = band.outline_dist(p, 0.01 * r * (1 + 1e-6), 1e-7 * r);  // simplify(0.01 r)
+    if (near < 1e-9 * r) st.unresolved++, st.ambiguous++;
+    else if (near < INFINITY) st.dp_sensitive++, st.ambiguous++;
+    if (!in_band) st.band_dropped++;
+    return in_band ? kBorder : kDrop;
   }
 };
 
@@ -680,7 +757,12 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
   // a cell the polygon holds whole: core -- unless mosaicFill's rule (rule != null) puts
   // it in the border set (then its chip is the whole cell, not core)
   auto whole = [&](int64_t id, long i, long j, const std::vector<std::vector<Pt>>* rings) {
-    if (rule && rule->decide(g.center_input(i, j, id), 1) != CoreRule::kCore) {
+    const auto v = rule ? rule->decide(g.center_input(i, j, id), 1) : CoreRule::kCore;
+    if (v == CoreRule::kDrop) {
+      rule->st.dropped++;
+      return;
+    }
+    if (v != CoreRule::kCore) {
       rule->st.demoted++;
       Chip ch{id, pid, 0, {}};
       write_cell_wkb(reversed(rings ? *rings : g.boundary(i, j)), ch.wkb);
@@ -991,7 +1073,7 @@ int32_t mgpu_tessellate_ex(int32_t index_system, int32_t res, int64_t n_polys, c
                            const int64_t* poly_part_off, const int64_t* part_ring_off, const int64_t* ring_off,
                            const double* xy, int32_t keep_core_geometries, int32_t core_rule, mgpu_tess** out) {
   if (!out || n_polys < 0) return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellate: bad arguments");
-  if (core_rule != MGPU_CORE_MOSAICFILL && core_rule != MGPU_CORE_CLIP)
+  if (core_rule != MGPU_CORE_MOSAICFILL && core_rule != MGPU_CORE_CLIP && core_rule != MGPU_CORE_DISTANCE)
     return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellate: unknown core rule %d", core_rule);
   if (int32_t st = mgpu_check_resolution(index_system, res)) return st;
   if (index_system == MGPU_BNG && res == -1)
@@ -1021,10 +1103,12 @@ int32_t mgpu_tessellate_ex(int32_t index_system, int32_t res, int64_t n_polys, c
       // mosaicFill's core set (CoreRule) unless the clip rule was asked for
       CoreRule rule_storage;
       CoreRule* rule = nullptr;
-      if (core_rule == MGPU_CORE_MOSAICFILL) {
+      if (core_rule == MGPU_CORE_MOSAICFILL || core_rule == MGPU_CORE_DISTANCE) {
         rule_storage.r = index_system == MGPU_H3 ? h3_buffer_radius(poly, res)
                                                  : BngGrid(res).edge * std::sqrt(2.0) / 2.0;
         if (rule_storage.r > 0) {
+          rule_storage.poly = &poly;
+          rule_storage.distance_only = core_rule == MGPU_CORE_DISTANCE;
           rule_storage.seg.build(poly, rule_storage.r);
           rule = &rule_storage;
         }
@@ -1093,6 +1177,14 @@ int32_t mgpu_tessellate_ex(int32_t index_system, int32_t res, int64_t n_polys, c
     t->core_stats.promoted += q.promoted;
     t->core_stats.dropped += q.dropped;
     t->core_stats.ambiguous += q.ambiguous;
+    t->core_stats.carved_tests += q.carved_tests;
+    t->core_stats.band_tests += q.band_tests;
+    t->core_stats.core_below_r += q.core_below_r;
+    t->core_stats.border_above_r += q.border_above_r;
+    t->core_stats.band_dropped += q.band_dropped;
+    t->core_stats.dp_sensitive += q.dp_sensitive;
+    t->core_stats.unresolved += q.unresolved;
+    t->core_stats.carved_empty += q.carved_empty;
   }
   size_t total = 0;
   for (auto& v : per) total += v.size();
@@ -1141,6 +1233,18 @@ int32_t mgpu_tess_result_stats(const mgpu_tess* t, int64_t* out6) {
   out6[3] = t->core_stats.promoted;
   out6[4] = t->core_stats.dropped;
   out6[5] = t->core_stats.ambiguous;
+  return MGPU_OK;
+}
+
+int32_t mgpu_tess_result_core_stats(const mgpu_tess* t, int64_t* out, int32_t n) {
+  if (!t || !out || n < 0) return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellation result is NULL");
+  int64_t core = 0;
+  for (auto& c : t->chips) core += c.core;
+  const CoreStats& s = t->core_stats;
+  const int64_t v[] = {(int64_t)t->chips.size(), core, s.demoted, s.promoted, s.dropped, s.ambiguous,
+                       s.carved_tests, s.band_tests, s.core_below_r, s.border_above_r, s.band_dropped,
+                       s.dp_sensitive, s.unresolved, s.carved_empty};
+  for (int32_t i = 0; i < n; i++) out[i] = i < (int32_t)(sizeof(v) / sizeof(v[0])) ? v[i] : 0;
   return MGPU_OK;
 }
 
