@@ -236,6 +236,17 @@ def spawn_ranks(a):
     return rc
 
 
+def traffic_key(options, info):
+    """What a PMC traffic profile (profiles/pmc_join_traffic*.json, tools/traffic_summary.py)
+    must share with a bench line to be attached to it: the context options, the uploaded
+    table (chips, blob bytes) and the kernels' source."""
+    import hashlib
+    src = os.path.join(ROOT, "mosaic_amd", "csrc", "kernels.hip")
+    return {"options": dict(sorted(kv.split("=", 1) for kv in options)), "chips": int(info["chips"]),
+            "blob_bytes": int(info.get("bytes") or 0),
+            "kernels_sha16": hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "0"))
@@ -419,7 +430,10 @@ def main():
             p = json.load(open(prof))
             # (only a profile of the kernel this run's pipeline made dominant)
             same_kernel = p.get("kernel", "pip_join_kernel").split("<")[0] == kernel.split("<")[0]
-            if p.get("res") == a.res and p.get("config", "c2") == a.config and p.get("points") and same_kernel:
+            # (and only one measured on this build of the kernels, this table and these options:
+            # a stale profile attaches nothing)
+            if (p.get("res") == a.res and p.get("config", "c2") == a.config and p.get("points") and same_kernel
+                    and p.get("key") == traffic_key(a.option, info)):
                 # measured per launch on p["points"] points of this workload (rocprofv3 PMC
                 # passes, tools/gpu_traffic.sh); scaled to this launch's size if it differs
                 out["roofline"]["traffic"] = p["hbm_bytes_per_launch"] * n / p["points"]

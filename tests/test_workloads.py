@@ -48,3 +48,17 @@ def test_tract_polygons_partition_the_extent():
     pts, polys = O.pip_join(0, 9, x, y, c.cell, c.polygon_id, c.is_core, c.wkb_offsets, c.wkb)
     assert len(np.unique(pts)) == len(pts)
     assert len(pts) > 0.99 * len(x)
+
+
+def test_traffic_key_tracks_options_table_and_source():
+    """bench.py attaches a PMC traffic profile only when its key -- context options, the
+    uploaded table's size, the kernels' source hash -- equals the run's: a line run with
+    --option raster_sub=8 cannot carry counters measured on the default build."""
+    import bench as B
+    info = {"chips": 11890, "bytes": 86787072}
+    k = B.traffic_key([], info)
+    assert k == B.traffic_key([], dict(info))
+    assert k != B.traffic_key(["raster_sub=8"], info)
+    assert k != B.traffic_key([], {"chips": 11890, "bytes": 60000000})
+    assert B.traffic_key(["a=1", "b=2"], info) == B.traffic_key(["b=2", "a=1"], info)
+    assert len(k["kernels_sha16"]) == 16

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0x20250314)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--pipeline", type=int, default=-1)
+    ap.add_argument("--option", action="append", default=[], help="context option key=value (as bench.py)")
     ap.add_argument("--cells", action="store_true")
     ap.add_argument("--cache", default=None, help="npz of the tessellated chip table (written when absent): "
                     "PMC passes of a large config tessellate once")
@@ -31,6 +32,9 @@ def main():
     torch.cuda.set_device(dev)
     ctx = M.default_context(dev)
     ctx.set_option("pipeline", a.pipeline)
+    for kv in a.option:
+        k, v = kv.split("=", 1)
+        ctx.set_option(k, int(v))
     import bench_workloads as W
     wl = B.workload(a, W, M)
     isys = wl["isys"]
@@ -44,6 +48,10 @@ def main():
             np.savez(a.cache, cell=table.cell, polygon_id=table.polygon_id, is_core=table.is_core,
                      wkb_offsets=table.wkb_offsets, wkb=table.wkb)
     chips = table.upload(ctx)
+    if not a.cells:
+        import json
+        # what a bench line must match to carry this run's counters (bench.py traffic_key)
+        print("KEY " + json.dumps(B.traffic_key(a.option, chips.info())), flush=True)
     x, y = wl["points"](a.points, 0, dev)
     cap = int(a.points * wl["pairs_per_point"]) + 1024
     op = torch.empty(cap, dtype=torch.int64, device=dev)

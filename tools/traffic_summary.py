@@ -43,6 +43,15 @@ def traffic_name(cfg, res):
     return base + ("" if res == default else "_r%d" % res) + ".json"
 
 
+def run_key(sub):
+    for line in open(os.path.join(d, sub + ".log")):
+        if line.startswith("KEY "):
+            return json.loads(line[4:])
+    raise SystemExit("no KEY line in %s.log (tools/join_once.py)" % sub)
+
+
+key = run_key("join_fetch")
+assert key == run_key("join_write"), "the two passes ran different builds / tables"
 jf_all, jw_all = per_kernel("join_fetch"), per_kernel("join_write")
 bf, nb = per_kernel("bng_fetch")["cells_kernel<1>"]
 bw, _ = per_kernel("bng_write")["cells_kernel<1>"]
@@ -55,7 +64,7 @@ dom = next(k for k in jf_all if k.split("<")[0] in ("classify_kernel", "classify
 jf, nj = jf_all[dom]
 jw, _ = jw_all[dom]
 out = {
-    "round": tag, "config": CFG, "points": N, "res": DESC[1], "kernel": dom,
+    "round": tag, "config": CFG, "points": N, "res": DESC[1], "kernel": dom, "key": key,
     "join_fetch_bytes_raw": jf, "join_write_bytes_raw": jw, "dispatches": nj,
     "calib_bng_fetch_bytes_raw": bf, "calib_bng_write_bytes_raw": bw,
     "calib_read_factor": f_read, "calib_write_factor": f_write,
