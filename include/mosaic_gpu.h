@@ -105,6 +105,9 @@ int32_t mgpu_ctx_destroy(mgpu_ctx* ctx);
  *   "bin_min_mb"      the planner bins for chip tables of at least this size (256)
  *   "bin_min_points"  ... and batches of at least this many points (2^21)
  *   "bin_xcd"         1 (default): binned tiles dealt to the 8 XCDs in contiguous runs
+ *   "bin_keys"        1: H3 binned joins over a dense grid take each point's grid entry from
+ *                     the binning pass (which projects the point); 0 (default): the join
+ *                     projects (C3: binning +1.4 ms, join -0.16 ms per 1.25e8 points)
  *   "spin_us"         synchronous calls poll their stream (yielding the core between polls)
  *                     at most this long, then block in hipStreamSynchronize (default 2000;
  *                     0 = block at once)
@@ -292,6 +295,32 @@ int32_t mgpu_ring_join(mgpu_ctx* ctx, int32_t index_system, int32_t res, int32_t
                        const double* right_y, int64_t n_right, int64_t left_id_base, int32_t max_per_left,
                        double max_distance, int64_t capacity, int64_t* out_n, int64_t* out_left, int64_t* out_right,
                        double* out_dist, void* stream);
+/* mgpu_ring_join with flags.  MGPU_RING_LEFT_OUTER: the join is left_outer
+ * (GridRingNeighbours.scala:128) and resultTransform keeps the null group
+ * (coalesce(intersects, true), :151): a landmark with a ring cell that holds no candidate
+ * gets one row (left, -1, NaN) before its pairs -- Spark orders the null distance first in
+ * the ascending window -- not counted by max_per_left nor filtered by max_distance.
+ * Self matches: dropped when the coordinates are bit-identical; the reference compares
+ * hash() of the geometry column (:154), so two rows holding the same point in different
+ * text or WKB (or -0.0 vs 0.0) are distinct there but one here. */
+#define MGPU_RING_LEFT_OUTER 1
+int32_t mgpu_ring_join_ex(mgpu_ctx* ctx, int32_t index_system, int32_t res, int32_t k, int32_t loop_only,
+                          const double* left_x, const double* left_y, int64_t n_left, const double* right_x,
+                          const double* right_y, int64_t n_right, int64_t left_id_base, int32_t max_per_left,
+                          double max_distance, int32_t flags, int64_t capacity, int64_t* out_n, int64_t* out_left,
+                          int64_t* out_right, double* out_dist, void* stream);
+/* SpatialKNN's exactness iteration (GridRingNeighbours.leftTransform, iterationID = -1,
+ * GridRingNeighbours.scala:82-90; SpatialKNN.resultTransform): per landmark i, the cells of
+ * grid_tessellate(st_buffer(landmark, radius[i]), res) -- JTS's 32-gon circle, mosaicFill's
+ * cells (mgpu_tessellate) -- minus grid_geometrykring(landmark, res, k_iterated[i])
+ * (array_except), joined with the candidates as mgpu_ring_join_ex does.  radius[i] (the
+ * landmark's k-th match distance) NaN or <= 0 gives the landmark no cells.  radius and
+ * k_iterated are HOST arrays; the points are device pointers.  Synchronises `stream`. */
+int32_t mgpu_ring_join_final(mgpu_ctx* ctx, int32_t index_system, int32_t res, const double* left_x,
+                             const double* left_y, const double* radius, const int32_t* k_iterated, int64_t n_left,
+                             const double* right_x, const double* right_y, int64_t n_right, int64_t left_id_base,
+                             int32_t max_per_left, double max_distance, int32_t flags, int64_t capacity,
+                             int64_t* out_n, int64_t* out_left, int64_t* out_right, double* out_dist, void* stream);
 
 /* st_contains(chip.wkb, point) for explicit (chip row, point) pairs
  * (ST_Contains.scala:21-44 -> MosaicGeometryJTS.contains, MosaicGeometryJTS.scala:197).

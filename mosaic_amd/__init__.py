@@ -12,7 +12,7 @@ from ._native import (CapacityError, IllegalArgumentException, IllegalStateExcep
 from .chips import ChipTable, DeviceChips, Polygons, tessellate
 from .context import GpuContext, MosaicContext, default_context
 from .functions import (AsyncJoin, GeometryColumn, InternalGeometryColumn, JoinResult, grid_cellkloop, grid_cellkring, grid_longlatascellid, grid_pointascellid,
-                        grid_ring_join, grid_tessellateexplode, pip_join, pip_join_async, st_contains)
+                        grid_ring_join, grid_ring_join_final, grid_tessellateexplode, pip_join, pip_join_async, st_contains)
 from .index_system import BNGIndexSystem, H3IndexSystem, IndexSystem, get_index_system
 
 __version__ = "0.1.0"
@@ -22,5 +22,5 @@ __all__ = [
     "IllegalArgumentException", "IllegalStateException", "IndexSystem", "JoinResult", "LIB_PATH",
     "MosaicContext", "MosaicGpuError", "Polygons", "default_context", "get_index_system", "grid_cellkloop",
     "grid_cellkring", "grid_longlatascellid",
-    "grid_pointascellid", "grid_ring_join", "grid_tessellateexplode", "pip_join", "pip_join_async", "st_contains", "tessellate",
+    "grid_pointascellid", "grid_ring_join", "grid_ring_join_final", "grid_tessellateexplode", "pip_join", "pip_join_async", "st_contains", "tessellate",
 ]

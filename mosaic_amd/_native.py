@@ -17,6 +17,7 @@ MGPU_E_RESOLUTION = -2
 MGPU_E_NAN = -3
 MGPU_E_WKB = -4
 MGPU_E_CAPACITY = -5
+MGPU_RING_LEFT_OUTER = 1
 MGPU_E_DEVICE = -6
 MGPU_E_INTERNAL = -7
 MGPU_E_UNSUPPORTED = -8
@@ -41,7 +42,7 @@ EXPORTS = (
     "mgpu_test_h3_elementary_host", "mgpu_test_h3_route_host", "mgpu_test_h3_boundary_host", "mgpu_test_h3_cell_wkb_host",
     "mgpu_ctx_set_option", "mgpu_ctx_get_option", "mgpu_build_opts_default", "mgpu_chips_host_blob_ex",
     "mgpu_test_h3_glibc_host", "mgpu_internal_geometry_to_cells", "mgpu_test_internal_centroid", "mgpu_test_join_counters",
-    "mgpu_test_receive_blob", "mgpu_ring_join",
+    "mgpu_test_receive_blob", "mgpu_ring_join", "mgpu_ring_join_ex", "mgpu_ring_join_final",
 )
 MGPU_GEOM_WKB = 0
 MGPU_GEOM_WKT = 1
@@ -184,6 +185,10 @@ def lib():
         "mgpu_test_receive_blob": (I32, [P, P, I32, ctypes.POINTER(P)]),
         "mgpu_ring_join": (I32, [P, I32, I32, I32, I32, P, P, I64, P, P, I64, I64, I32, ctypes.c_double, I64,
                                  ctypes.POINTER(I64), P, P, P, P]),
+        "mgpu_ring_join_ex": (I32, [P, I32, I32, I32, I32, P, P, I64, P, P, I64, I64, I32, ctypes.c_double, I32,
+                                    I64, ctypes.POINTER(I64), P, P, P, P]),
+        "mgpu_ring_join_final": (I32, [P, I32, I32, P, P, P, P, I64, P, P, I64, I64, I32, ctypes.c_double, I32, I64,
+                                       ctypes.POINTER(I64), P, P, P, P]),
     }
     for name, (rt, args) in sig.items():
         f = getattr(L, name)

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <unordered_map>
 #include <chrono>
 #include <sched.h>
 #include <array>
@@ -689,7 +690,33 @@ constexpr int64_t kPixAnswerMixed = -1;
 
 // the matches of every point in the widened pixel [x0, x1] x [y0, y1] among the chips
 // of grid entry `e` (first | count << 32 | core_mask << 48): a mask, or kPixAnswerMixed
-int64_t pixel_answer(const mgpu::ChipTableView& hv, uint64_t e, double x0, double y0, double x1, double y1) {
+// (edges: when given, the chips' edges whose bounding boxes meet a box holding this one --
+// the widened pixel of a sub-pixel -- per chip, filled on first use; an edge outside it
+// cannot meet this box, so the answer is the same)
+struct PixelEdges {
+  std::vector<uint32_t> chip, start, items;  // chip k's edges (end vertex index) items[start[k] .. start[k + 1])
+  // chip k's PointLocator verdict when no edge of it meets the box (-1: not yet computed):
+  // the whole box then lies in one component of the plane minus the chip's boundary, where
+  // the (exact) predicate gives every point the same answer
+  std::vector<int> locate;
+  // chip k with edges in the box, a sub-box none of them meets: the PointLocator verdict at
+  // its centre from the rings' crossings of the centre's row (as build_grid: the centre
+  // lies off every edge by far more than the rounding of a crossing), kept per row
+  std::vector<double> row_y;
+  std::vector<std::vector<double>> xs;
+  std::vector<std::vector<uint32_t>> ring_first;
+  double x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+  void reset(double a0, double b0, double a1, double b1) {
+    chip.clear();
+    start.assign(1, 0);
+    items.clear();
+    locate.clear();
+    row_y.clear();
+    x0 = a0, y0 = b0, x1 = a1, y1 = b1;
+  }
+};
+int64_t pixel_answer(const mgpu::ChipTableView& hv, uint64_t e, double x0, double y0, double x1, double y1,
+                     PixelEdges* pe = nullptr) {
   using namespace mgpu;
   const uint32_t first = (uint32_t)e, count = mgpu::grid_count(e, false);  // (before the answer grids)
   if (count == 0) return 0;
@@ -705,11 +732,85 @@ int64_t pixel_answer(const mgpu::ChipTableView& hv, uint64_t e, double x0, doubl
     if (fl & (kChipEmpty | kChipNoGeom)) continue;
     const double* env = hv.chip_env + 4 * c;
     if (x1 < env[0] || x0 > env[2] || y1 < env[1] || y0 > env[3]) continue;  // outside the envelope
-    for (uint32_t p = hv.chip_part[c]; p < hv.chip_part[c + 1]; p++)
-      for (uint32_t r = hv.part_ring[p]; r < hv.part_ring[p + 1]; r++)
-        for (uint32_t i = hv.ring_vtx[r] + 1; i < hv.ring_vtx[r + 1]; i++)
-          if (seg_hits_box(hv.vtx[2 * i - 2], hv.vtx[2 * i - 1], hv.vtx[2 * i], hv.vtx[2 * i + 1], x0, y0, x1, y1))
-            return kPixAnswerMixed;
+    if (pe) {
+      size_t k = 0;
+      while (k < pe->chip.size() && pe->chip[k] != c) k++;
+      if (k == pe->chip.size()) {
+        for (uint32_t p = hv.chip_part[c]; p < hv.chip_part[c + 1]; p++)
+          for (uint32_t r = hv.part_ring[p]; r < hv.part_ring[p + 1]; r++)
+            for (uint32_t i = hv.ring_vtx[r] + 1; i < hv.ring_vtx[r + 1]; i++) {
+              const double ax = hv.vtx[2 * i - 2], ay = hv.vtx[2 * i - 1], bx = hv.vtx[2 * i], by = hv.vtx[2 * i + 1];
+              if (!(std::max(ax, bx) < pe->x0 || std::min(ax, bx) > pe->x1 || std::max(ay, by) < pe->y0 ||
+                    std::min(ay, by) > pe->y1))
+                pe->items.push_back(i);
+            }
+        pe->chip.push_back(c);
+        pe->start.push_back((uint32_t)pe->items.size());
+        pe->locate.push_back(-1);
+        pe->row_y.push_back(NAN);
+        if (pe->xs.size() < pe->chip.size()) {
+          pe->xs.resize(pe->chip.size());
+          pe->ring_first.resize(pe->chip.size());
+        }
+      }
+      for (uint32_t q = pe->start[k]; q < pe->start[k + 1]; q++) {
+        const uint32_t i = pe->items[q];
+        if (seg_hits_box(hv.vtx[2 * i - 2], hv.vtx[2 * i - 1], hv.vtx[2 * i], hv.vtx[2 * i + 1], x0, y0, x1, y1))
+          return kPixAnswerMixed;
+      }
+      if (pe->start[k] == pe->start[k + 1]) {
+        if (pe->locate[k] < 0) pe->locate[k] = pip::chip_locate(hv, c, 0.5 * (x0 + x1), 0.5 * (y0 + y1));
+        const int loc = pe->locate[k];
+        if (loc == pip::kBoundary) return kPixAnswerMixed;
+        if (loc == pip::kInterior) mask |= 1ull << j;
+        continue;
+      }
+      const double cxp = 0.5 * (x0 + x1), cyp = 0.5 * (y0 + y1);
+      const uint32_t r0 = hv.part_ring[hv.chip_part[c]], r1 = hv.part_ring[hv.chip_part[c + 1]];
+      std::vector<double>& xs = pe->xs[k];
+      std::vector<uint32_t>& rf = pe->ring_first[k];
+      if (!(pe->row_y[k] == cyp)) {
+        pe->row_y[k] = cyp;
+        xs.clear();
+        rf.clear();
+        for (uint32_t r = r0; r < r1; r++) {
+          rf.push_back((uint32_t)xs.size());
+          for (uint32_t i = hv.ring_vtx[r] + 1; i < hv.ring_vtx[r + 1]; i++) {
+            const double p1x = hv.vtx[2 * i], p1y = hv.vtx[2 * i + 1], p2x = hv.vtx[2 * i - 2], p2y = hv.vtx[2 * i - 1];
+            if (((p1y > cyp) && (p2y <= cyp)) || ((p2y > cyp) && (p1y <= cyp)))
+              xs.push_back(p1x + (cyp - p1y) * (p2x - p1x) / (p2y - p1y));
+          }
+          std::sort(xs.begin() + rf.back(), xs.end());
+        }
+        rf.push_back((uint32_t)xs.size());
+      }
+      auto odd = [&](uint32_t r) {  // ring r (index within the chip): crossings right of cxp
+        const auto b = xs.begin() + rf[r], e = xs.begin() + rf[r + 1];
+        return ((e - std::upper_bound(b, e, cxp)) & 1) != 0;
+      };
+      bool in = false;
+      for (uint32_t p = hv.chip_part[c]; p < hv.chip_part[c + 1] && !in; p++) {
+        const uint32_t rb = hv.part_ring[p], re = hv.part_ring[p + 1];
+        if (re == rb || hv.ring_vtx[rb + 1] == hv.ring_vtx[rb] || !odd(rb - r0)) continue;
+        bool hole = false;
+        for (uint32_t q = rb + 1; q < re && !hole; q++) hole = odd(q - r0);
+        in = !hole;
+      }
+#ifdef MGPU_GRID_VERIFY
+      if (pip::chip_locate(hv, c, cxp, cyp) != (in ? pip::kInterior : pip::kExterior)) {
+        fprintf(stderr, "pixel verify: chip %u row parity %d differs from PointLocator\n", c, (int)in);
+        abort();
+      }
+#endif
+      if (in) mask |= 1ull << j;
+      continue;
+    } else {
+      for (uint32_t p = hv.chip_part[c]; p < hv.chip_part[c + 1]; p++)
+        for (uint32_t r = hv.part_ring[p]; r < hv.part_ring[p + 1]; r++)
+          for (uint32_t i = hv.ring_vtx[r] + 1; i < hv.ring_vtx[r + 1]; i++)
+            if (seg_hits_box(hv.vtx[2 * i - 2], hv.vtx[2 * i - 1], hv.vtx[2 * i], hv.vtx[2 * i + 1], x0, y0, x1, y1))
+              return kPixAnswerMixed;
+    }
     const int loc = pip::chip_locate(hv, c, 0.5 * (x0 + x1), 0.5 * (y0 + y1));
     if (loc == pip::kBoundary) return kPixAnswerMixed;
     if (loc == pip::kInterior) mask |= 1ull << j;
@@ -725,13 +826,19 @@ struct Corner {
   bool ok = false;
 };
 
-Corner h3_corner(double lond, double latd, int res, double k_res) {
-  namespace H = mgpu::h3;
+struct SinCos {
+  double s = 0, c = 0;
+};
+SinCos deg_sincos(double deg) {
+  SinCos o;
+  mgpu::h3::sincos_fast(mgpu::h3::to_radians_fast(deg), &o.s, &o.c);
+  return o;
+}
+// (from the sines and cosines of the corner's longitude and latitude: a grid of corners
+// shares them per column and per row)
+Corner h3_corner_sc(const SinCos& lon, const SinCos& lat, int res, double k_res) {
   Corner o;
-  const double lat = H::to_radians_fast(latd), lon = H::to_radians_fast(lond);
-  double slat, clat, slon, clon;
-  H::sincos_fast(lat, &slat, &clat);
-  H::sincos_fast(lon, &slon, &clon);
+  const double slat = lat.s, clat = lat.c, slon = lon.s, clon = lon.c;
   const double vx = clon * clat, vy = slon * clat, vz = slat;
   double best = 5.0, second = 5.0;
   for (int f = 0; f < 20; f++) {
@@ -755,40 +862,72 @@ Corner h3_corner(double lond, double latd, int res, double k_res) {
   o.ok = std::fabs(o.x) < 1e8 && std::fabs(o.y) < 1e8;
   return o;
 }
+Corner h3_corner(double lond, double latd, int res, double k_res) {
+  return h3_corner_sc(deg_sincos(lond), deg_sincos(latd), res, k_res);
+}
 
 // Does the hexagon of axial lattice position (a, b) -- H3's _hex2dToCoordIJK rounds to
 // the nearest lattice centre (checked by tests/cpp), so a cell is the hexagon of
 // apothem 1/2 around (a - b/2, b sin60) -- come within `d` of the convex quad q?
 // (separating axes: the hexagon's three edge normals and the quad's four)
-bool hex_meets_quad(int64_t a, int64_t b, const double q[4][2], double d) {
+struct HexFrame {  // the hexagon's vertex offsets (circumradius R at 30 + 60 k degrees), edge normals
+  double off[6][2], nrm[3][2];
+  HexFrame() {
+    const double R = 0.57735026918962576451;  // circumradius
+    for (int k = 0; k < 6; k++) {
+      const double t = (30.0 + 60.0 * k) * kPi / 180.0;
+      off[k][0] = R * std::cos(t);
+      off[k][1] = R * std::sin(t);
+    }
+    for (int k = 0; k < 3; k++) {
+      const double t = 60.0 * k * kPi / 180.0;
+      nrm[k][0] = std::cos(t);
+      nrm[k][1] = std::sin(t);
+    }
+  }
+};
+// the quad's side of the separating-axis test, shared by the seven hexagons tested
+// against it: the hexagon's three edge normals and the quad's four (valid[k]: a non-zero
+// edge), and the quad's extent along each
+struct QuadAxes {
+  double n[7][2], lo[7], hi[7];
+  bool valid[7];
+  QuadAxes(const double q[4][2], const HexFrame& F) {
+    for (int k = 0; k < 7; k++) {
+      valid[k] = true;
+      if (k < 3) {
+        n[k][0] = F.nrm[k][0], n[k][1] = F.nrm[k][1];
+      } else {
+        const int e = k - 3;
+        const double ex = q[(e + 1) % 4][0] - q[e][0], ey = q[(e + 1) % 4][1] - q[e][1];
+        const double l = std::hypot(ex, ey);
+        valid[k] = l > 0;
+        n[k][0] = valid[k] ? -ey / l : 0.0, n[k][1] = valid[k] ? ex / l : 0.0;
+      }
+      double q0 = 1e300, q1 = -1e300;
+      for (int p = 0; p < 4; p++) {
+        const double v = q[p][0] * n[k][0] + q[p][1] * n[k][1];
+        q0 = std::min(q0, v), q1 = std::max(q1, v);
+      }
+      lo[k] = q0, hi[k] = q1;
+    }
+  }
+};
+bool hex_meets_quad(int64_t a, int64_t b, const QuadAxes& Q, const HexFrame& F, double d) {
   const double cx = (double)a - 0.5 * (double)b, cy = (double)b * mgpu::h3::kSin60;
-  const double R = 0.57735026918962576451;  // circumradius
   double hv[6][2];
   for (int k = 0; k < 6; k++) {
-    const double t = (30.0 + 60.0 * k) * kPi / 180.0;
-    hv[k][0] = cx + R * std::cos(t);
-    hv[k][1] = cy + R * std::sin(t);
+    hv[k][0] = cx + F.off[k][0];
+    hv[k][1] = cy + F.off[k][1];
   }
-  auto separated = [&](double nx, double ny) {
-    double h0 = 1e300, h1 = -1e300, q0 = 1e300, q1 = -1e300;
-    for (int k = 0; k < 6; k++) {
-      const double v = hv[k][0] * nx + hv[k][1] * ny;
+  for (int k = 0; k < 7; k++) {
+    if (!Q.valid[k]) continue;
+    double h0 = 1e300, h1 = -1e300;
+    for (int p = 0; p < 6; p++) {
+      const double v = hv[p][0] * Q.n[k][0] + hv[p][1] * Q.n[k][1];
       h0 = std::min(h0, v), h1 = std::max(h1, v);
     }
-    for (int k = 0; k < 4; k++) {
-      const double v = q[k][0] * nx + q[k][1] * ny;
-      q0 = std::min(q0, v), q1 = std::max(q1, v);
-    }
-    return h1 + d < q0 || q1 + d < h0;
-  };
-  for (int k = 0; k < 3; k++) {
-    const double t = 60.0 * k * kPi / 180.0;
-    if (separated(std::cos(t), std::sin(t))) return false;
-  }
-  for (int k = 0; k < 4; k++) {
-    const double ex = q[(k + 1) % 4][0] - q[k][0], ey = q[(k + 1) % 4][1] - q[k][1];
-    const double l = std::hypot(ex, ey);
-    if (l > 0 && separated(-ey / l, ex / l)) return false;
+    if (h1 + d < Q.lo[k] || Q.hi[k] + d < h0) return false;
   }
   return true;
 }
@@ -821,12 +960,17 @@ void raster_classes(const mgpu::ChipTableView& hv, const std::vector<uint64_t>& 
     return ps;
   };
   // distinct answers -> their polygon lists -> classes
-  std::map<uint64_t, int32_t> answer_key;
+  // (a hash of the distinct answers; neighbouring pixels mostly repeat the previous one)
+  std::unordered_map<uint64_t, int32_t> answer_key;
+  answer_key.reserve(1 << 16);
   std::map<std::vector<int32_t>, int32_t> list_key;
   std::vector<uint64_t> rep;  // per list: the representative answer
   std::vector<std::vector<int32_t>> lists;
+  uint64_t last = kAnsMixed;
   for (size_t i = 0; i < a1.size() + a2.size(); i++) {
     const uint64_t v = i < a1.size() ? a1[i] : a2[i - a1.size()];
+    if (v == last) continue;
+    last = v;
     if (v == kAnsMixed || (v >> 32) == 0 || answer_key.count(v)) continue;
     auto ps = polys_of(v);
     auto it = list_key.find(ps);
@@ -848,16 +992,24 @@ void raster_classes(const mgpu::ChipTableView& hv, const std::vector<uint64_t>& 
     cls_of[k] = (int32_t)R.cls.size();
     R.cls.push_back(rep[k]);
   }
-  for (size_t i = 0; i < a1.size() + a2.size(); i++) {
-    const uint64_t v = i < a1.size() ? a1[i] : a2[i - a1.size()];
-    if (v == kAnsMixed) continue;
-    if ((v >> 32) == 0) {
-      slot(i) = mgpu::kPixEmpty;
-      continue;
+  const size_t n_all = a1.size() + a2.size();
+  mgpu::parallel_for((int64_t)n_all, 1 << 16, [&](int64_t b, int64_t e, int) {
+    uint64_t lv = kAnsMixed;
+    int32_t lc = -1;
+    for (int64_t i = b; i < e; i++) {
+      const uint64_t v = (size_t)i < a1.size() ? a1[i] : a2[i - a1.size()];
+      if (v == kAnsMixed) continue;
+      if ((v >> 32) == 0) {
+        slot((size_t)i) = mgpu::kPixEmpty;
+        continue;
+      }
+      if (v != lv) {
+        lv = v;
+        lc = cls_of[answer_key.find(v)->second];
+      }
+      if (lc >= 0) slot((size_t)i) = (uint16_t)lc;
     }
-    const int32_t c = cls_of[answer_key[v]];
-    if (c >= 0) slot(i) = (uint16_t)c;
-  }
+  });
   auto pc = [](uint64_t v) { return __builtin_popcountll(v >> 32); };
   for (int k = 0; k < 4; k++) {
     uint32_t c = 1;
@@ -932,7 +1084,8 @@ struct H3RasterCtx {
   const std::vector<uint64_t>& grid;
 };
 uint64_t h3_rect_answer(const H3RasterCtx& X, double xa, double ya, double xb, double yb, const Corner* c[4],
-                        double mux, double muy, std::vector<int32_t>& polys, std::vector<int32_t>& ref) {
+                        double mux, double muy, std::vector<int32_t>& polys, std::vector<int32_t>& ref,
+                        PixelEdges* pe = nullptr) {
   double q[4][2], L = 0;
   for (int p = 0; p < 4; p++) q[p][0] = c[p]->x, q[p][1] = c[p]->y;
   for (int p = 0; p < 4; p++)
@@ -949,15 +1102,17 @@ uint64_t h3_rect_answer(const H3RasterCtx& X, double xa, double ya, double xb, d
   // every cell a point of the rectangle can take is h0 or a neighbour (L < 1/2) whose
   // hexagon meets the quad; all must give the same polygon list
   static const int da[7] = {0, 1, -1, 0, 0, 1, -1}, db[7] = {0, 0, 0, 1, -1, 1, -1};
+  static const HexFrame HF;
+  const QuadAxes QA(q, HF);
   const mgpu::DenseFace& D = X.dense[c[0]->face];
   bool first = true;
   uint64_t cls = 0;
   for (int k = 0; k < 7; k++) {
     const int64_t a = a0 + da[k], b = b0 + db[k];
-    if (!hex_meets_quad(a, b, q, d_hex)) continue;
+    if (!hex_meets_quad(a, b, QA, HF, d_hex)) continue;
     const uint64_t ua = (uint64_t)(a - D.a0), ub = (uint64_t)(b - D.b0);
     const uint64_t e = (ua < D.w && ub < D.h) ? X.grid[D.base + ub * D.w + ua] : 0;
-    const int64_t m = pixel_answer(X.hv, e, xa - mux, ya - muy, xb + mux, yb + muy);
+    const int64_t m = pixel_answer(X.hv, e, xa - mux, ya - muy, xb + mux, yb + muy, pe);
     if (m == kPixAnswerMixed) return kAnsMixed;
     polys.clear();
     for (uint64_t bits = (uint64_t)m; bits; bits &= bits - 1) polys.push_back(X.hv.chip_poly[(uint32_t)e + __builtin_ctzll(bits)]);
@@ -1011,9 +1166,13 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
     mgpu::parallel_for((int64_t)R.ny, 8, [&](int64_t yb, int64_t ye_, int) {
       std::vector<int32_t> polys, ref;
       std::vector<Corner> lo(R.nx + 1), hi(R.nx + 1);
-      for (uint32_t ix = 0; ix <= R.nx; ix++) lo[ix] = h3_corner(xe(ix, 0), ye((uint32_t)yb, 0), res, k_res);
+      std::vector<SinCos> scx(R.nx + 1);
+      for (uint32_t ix = 0; ix <= R.nx; ix++) scx[ix] = deg_sincos(xe(ix, 0));
+      const SinCos s0 = deg_sincos(ye((uint32_t)yb, 0));
+      for (uint32_t ix = 0; ix <= R.nx; ix++) lo[ix] = h3_corner_sc(scx[ix], s0, res, k_res);
       for (int64_t iy = yb; iy < ye_; iy++) {
-        for (uint32_t ix = 0; ix <= R.nx; ix++) hi[ix] = h3_corner(xe(ix, 0), ye((uint32_t)iy, 1), res, k_res);
+        const SinCos s1 = deg_sincos(ye((uint32_t)iy, 1));
+        for (uint32_t ix = 0; ix <= R.nx; ix++) hi[ix] = h3_corner_sc(scx[ix], s1, res, k_res);
         for (uint32_t ix = 0; ix < R.nx; ix++) {
           const Corner* c[4] = {&lo[ix], &lo[ix + 1], &hi[ix + 1], &hi[ix]};
           a1[(size_t)iy * R.nx + ix] =
@@ -1023,8 +1182,15 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
       }
     });
   }
+#ifdef MGPU_BLOB_TIMING
+  auto rt0 = std::chrono::steady_clock::now();
+  fprintf(stderr, "[raster] level 1 done: %u x %u pixels\n", R.nx, R.ny);
+#endif
   // level 2: the mixed pixels cut into S x S sub-pixels
   std::vector<uint64_t> a2;
+#ifdef MGPU_BLOB_TIMING
+  int64_t t_corner_ns_total = 0;
+#endif
   // (S = 16 by default: on C2, 8 -> 16 took the mixed points 2.5% -> 1.3% of all and the
   // join 1.23 -> 1.11 ms per 1e8 points, its sub-pixel table 17 -> 68 MB; the largest S
   // within kRasterMaxSub entries when the mixed pixels are many)
@@ -1038,27 +1204,56 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
     mixed_rank(mixed, a1.size(), R.rank);
     a2.assign(mixed.size() * S * S, kAnsMixed);
     const double mux = 1e-6 * sx / S + 64 * ulp, muy = 1e-6 * sy / S + 64 * ulp;
+    const double pmux = 1e-6 * sx + 64 * ulp, pmuy = 1e-6 * sy + 64 * ulp;  // (level 1's widening: holds every sub-pixel's)
+#ifdef MGPU_BLOB_TIMING
+    std::atomic<int64_t> t_corner_ns{0};
+    struct Flush {
+      std::atomic<int64_t>& a;
+      int64_t& t;
+      ~Flush() { t = a.load(); }
+    } flush{t_corner_ns, t_corner_ns_total};
+#endif
     mgpu::parallel_for((int64_t)mixed.size(), 64, [&](int64_t kb, int64_t ke, int) {
       std::vector<int32_t> polys, ref;
       std::vector<Corner> cg((size_t)(S + 1) * (S + 1));
+      std::vector<SinCos> scx(S + 1);
+      PixelEdges pe;
       for (int64_t k = kb; k < ke; k++) {
         const uint32_t ix = mixed[k] % R.nx, iy = mixed[k] / R.nx;
-        for (int v = 0; v <= S; v++)
-          for (int u = 0; u <= S; u++) cg[v * (S + 1) + u] = h3_corner(xe(ix, (double)u / S), ye(iy, (double)v / S), res, k_res);
+        pe.reset(xe(ix, 0) - pmux, ye(iy, 0) - pmuy, xe(ix, 1) + pmux, ye(iy, 1) + pmuy);
+#ifdef MGPU_BLOB_TIMING
+        const auto tc0 = std::chrono::steady_clock::now();
+#endif
+        for (int u = 0; u <= S; u++) scx[u] = deg_sincos(xe(ix, (double)u / S));
+        for (int v = 0; v <= S; v++) {
+          const SinCos sy_ = deg_sincos(ye(iy, (double)v / S));
+          for (int u = 0; u <= S; u++) cg[v * (S + 1) + u] = h3_corner_sc(scx[u], sy_, res, k_res);
+        }
+#ifdef MGPU_BLOB_TIMING
+        t_corner_ns += (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tc0).count();
+#endif
         for (int v = 0; v < S; v++)
           for (int u = 0; u < S; u++) {
             const Corner* c[4] = {&cg[v * (S + 1) + u], &cg[v * (S + 1) + u + 1], &cg[(v + 1) * (S + 1) + u + 1],
                                   &cg[(v + 1) * (S + 1) + u]};
             a2[(size_t)k * S * S + v * S + u] = h3_rect_answer(X, xe(ix, (double)u / S), ye(iy, (double)v / S),
                                                                xe(ix, (double)(u + 1) / S), ye(iy, (double)(v + 1) / S), c,
-                                                               mux, muy, polys, ref);
+                                                               mux, muy, polys, ref, &pe);
           }
       }
     });
   }
+#ifdef MGPU_BLOB_TIMING
+  fprintf(stderr, "[raster] level 2: %zu mixed pixels, S %d, %.3f s (corners: %.3f thread-s)\n", mixed.size(), S,
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - rt0).count(), 1e-9 * (double)t_corner_ns_total);
+  rt0 = std::chrono::steady_clock::now();
+#endif
   raster_classes(hv, a1, a2, R);
   raster_blocks(R);
   raster_bands(R);
+#ifdef MGPU_BLOB_TIMING
+  fprintf(stderr, "[raster] classes, blocks, bands %.3f s\n", std::chrono::duration<double>(std::chrono::steady_clock::now() - rt0).count());
+#endif
   return true;
 }
 
@@ -1453,6 +1648,9 @@ int32_t mgpu_ctx_set_option(mgpu_ctx* ctx, const char* key, int64_t v) {
   } else if (k == "bin_xcd") {
     if (v != 0 && v != 1) return bad();
     o.bin_xcd = v;
+  } else if (k == "bin_keys") {
+    if (v != 0 && v != 1) return bad();
+    o.bin_keys = v;
   } else if (k == "spin_us") {
     if (v < 0 || v > 10000000) return bad();
     o.spin_us = v;
@@ -1477,7 +1675,7 @@ int32_t mgpu_ctx_get_option(const mgpu_ctx* ctx, const char* key, int64_t* v) {
   const std::pair<const char*, int64_t> all[] = {
       {"h3_libm", o.h3_libm},       {"pipeline", o.pipeline}, {"bin_count", o.bin_count},
       {"bin_min_mb", o.bin_min_mb}, {"bin_min_points", o.bin_min_points}, {"bin_xcd", o.bin_xcd},
-      {"spin_us", o.spin_us},       {"raster", o.raster},     {"raster_bng", o.raster_bng},
+      {"bin_keys", o.bin_keys},     {"spin_us", o.spin_us},       {"raster", o.raster},     {"raster_bng", o.raster_bng},
       {"raster_sub", o.raster_sub}, {"raster_milli", o.raster_milli}};
   for (const auto& kv : all)
     if (strcmp(kv.first, key) == 0) {
@@ -2598,6 +2796,12 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
                  o_pre = carve((size_t)K * nb * 4), o_res = carve((size_t)nc * C * 8), o_cnt = carve((size_t)K * nb * 4),
                  o_gs = carve((size_t)G * nb * 4), o_pairs = carve(nc * 4), o_off = carve(nc * 8),
                  o_gperm = carve(nc * 4), o_gcand = carve(nc * 4);
+    // H3 over a dense grid: the scatter kernel's per-slot grid keys (kernels.hip bin_key_of)
+    const mgpu::ChipTableView& cv = chips->view;
+    uint64_t grid_entries = 0;
+    for (int f = 0; f < 20; f++) grid_entries = std::max<uint64_t>(grid_entries, (uint64_t)cv.dense[f].base + (uint64_t)cv.dense[f].w * cv.dense[f].h);
+    const bool keyed = is == MGPU_H3 && cv.probe_mode == mgpu::kProbeDense && o.bin_keys && grid_entries < (1ull << 30);
+    const size_t o_key = keyed ? carve((size_t)n * 4) : 0;
     if (off > ctx->bin_bytes) {
       if (ctx->bin_ws) HIP_TRY(hipFree(ctx->bin_ws));
       ctx->bin_ws = nullptr;
@@ -2615,7 +2819,9 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     ba.res = (uint64_t*)(bb + o_rorig);
     ba.cnt = (uint32_t*)(bb + o_cnt);
     ba.gsum = (uint32_t*)(bb + o_gs);
+    ba.key = keyed ? (uint32_t*)(bb + o_key) : nullptr;
     mgpu::JoinArgs j = a;
+    j.bin_key = ba.key;
     j.x = ba.bx;
     j.y = ba.by;
     j.mixed_idx = nullptr;

@@ -58,6 +58,9 @@ struct JoinArgs {
   const uint8_t* valid;             // null points (Arrow validity bitmap at bit offset valid_off), or null
   int64_t valid_off;
   int poly_answers;                 // binned pipeline: a one-match answer is (polygon id | 1 << 32)
+  // binned H3 pipeline over a dense lattice grid: per binned slot, the point's grid entry
+  // index (| kKeyDeep) or a kKey* code, written by bin_scatter_kernel (else null)
+  const uint32_t* bin_key = nullptr;
 };
 
 // The override pass's scratch (launch_join_redo / launch_split_redo): the units (fused
@@ -133,6 +136,7 @@ struct BinArgs {
   double x0, y0, inv_bx, inv_by;    // the bin grid over the chip table's extent
   int32_t nbx, nby;                 // nbx * nby <= bin_max()
   int32_t xcd_runs;                 // deal each XCD a contiguous run of binned tiles (option bin_xcd)
+  uint32_t* key;                    // [n] H3, dense grid: the binned slot's grid key (JoinArgs.bin_key), or null
 };
 int64_t bin_chunk();
 int64_t bin_chunks(int64_t n);

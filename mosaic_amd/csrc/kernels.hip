@@ -249,6 +249,9 @@ __device__ __forceinline__ Range probe_range(const ChipTableView& t, uint64_t ke
 // A dense-grid probe is left to the caller: *gi = the grid entry to load (the loads of
 // a lane's four points then fly together), else *gi = kNoEntry and the range is final.
 constexpr uint32_t kNoEntry = 0xFFFFFFFFu;
+// binned H3 slot keys (bin_key_of): a grid entry index | kKeyDeep, or one of the codes
+constexpr uint32_t kKeyNone = 0xFFFFFFFFu, kKeyBad = 0xFFFFFFFEu, kKeyTie = 0xFFFFFFFDu;
+constexpr uint32_t kKeyDeep = 0x80000000u, kKeyIndex = 0x3FFFFFFFu;
 
 __device__ __forceinline__ Range grid_range(uint64_t e, bool ans) {
   return Range{(uint32_t)e, grid_count(e, ans), (uint32_t)(e >> 48)};
@@ -654,6 +657,36 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
       if (gi[k] != kNoEntry) r[k] = grid_range(ge[k], t.cell_ans_row != nullptr);
       phase1_item<SLOW, kCap, kStash, point_stash<G>()>(t, k * kBlock + threadIdx.x, r[k], bx[k], by[k], any_tie, &s_ncand, s_cand_pj,
                         s_cand_xy, s_first, s_cnt, s_mask, av[k]);
+    }
+  } else if (!SLOW && G == 1 && IS == MGPU_H3 && a.bin_key != nullptr) {
+    // binned slots with their grid keys (bin_scatter_kernel): every grid load in flight at
+    // once, no projection here
+    uint32_t kv[kItems];
+    double bx[kItems], by[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      const int li = k * kBlock + threadIdx.x;
+      kv[k] = kKeyNone;
+      bx[k] = by[k] = 0.0;
+      if (MGPU_VALID(li)) {
+        const int64_t p = MGPU_PT(li);
+        kv[k] = MGPU_LDPT(&a.bin_key[p]);
+        bx[k] = MGPU_LDPT(&a.x[p]);
+        by[k] = MGPU_LDPT(&a.y[p]);
+      }
+    }
+    uint64_t ge[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; k++) ge[k] = kv[k] < kKeyTie ? t.grid[kv[k] & kKeyIndex] : 0ull;
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      const bool hit = kv[k] < kKeyTie;
+      any_bad |= kv[k] == kKeyBad;
+      any_tie |= kv[k] == kKeyTie;
+      const Range r = hit ? grid_range(ge[k], t.cell_ans_row != nullptr) : Range{0, 0, 0};
+      phase1_item<SLOW, kCap, kStash, point_stash<G>()>(t, k * kBlock + threadIdx.x, r, bx[k], by[k], any_tie, &s_ncand,
+                                                        s_cand_pj, s_cand_xy, s_first, s_cnt, s_mask, kNoCellAns,
+                                                        hit && (kv[k] & kKeyDeep) != 0u);
     }
   } else {
     // one item ahead: item k + 1's coordinates load while item k projects
@@ -1166,6 +1199,136 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   count_wave(&a.counters[2], any_bad);
 }
 
+
+// classify_wave_kernel with two consecutive points per lane: each coordinate array is
+// read 16 bytes per lane (one global_load_dwordx4 for a lane's two x, one for its two y)
+// and the two codes are stored together.  A wave's item covers 128 points; a mixed
+// point's rank in the chunk is the wave's running count plus the mixed points of the
+// lower lanes (both halves) plus, for the second point, the first's.  Launched when x and
+// y are 16-byte aligned (else classify_wave_kernel).
+#ifndef MGPU_CFY_PAIR
+#define MGPU_CFY_PAIR 1
+#endif
+typedef double dbl2_t __attribute__((ext_vector_type(2)));
+template <int IS>
+__global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_CFY_WAVES))) void classify_pair_kernel(SplitArgs sa, int64_t n_chunks) {
+  using Code = typename CodeOf<IS>::T;
+  constexpr int kW = kCfyBlock / 64;
+  constexpr int kPairItems = kChunk / 128;                       // pair items per lane per chunk
+  constexpr int kPB = kCfyBatch / 2 > 0 ? kCfyBatch / 2 : 1;      // pair items in flight
+  constexpr int kPts = 2 * kPB;
+  const JoinArgs& a = sa.j;
+  const ChipTableView& t = a.chips;
+  extern __shared__ uint16_t s_blk[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool use_blk = IS == MGPU_H3 && t.raster_blk != nullptr;
+  const uint32_t nblk = use_blk ? t.raster_bnx * t.raster_bny : 0u;
+  uint32_t* s_band = (uint32_t*)(s_blk + ((nblk + 1) & ~1u));
+  if (use_blk)
+    for (uint32_t i = threadIdx.x; i < nblk; i += kCfyBlock) s_blk[i] = t.raster_blk[i];
+  if (IS == MGPU_H3)
+    for (uint32_t i = threadIdx.x; i < t.raster_nband; i += kCfyBlock) s_band[i] = t.raster_band[i];
+  __syncthreads();
+  Code* codes = (Code*)sa.codes;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  bool any_bad = false;
+  const int64_t ch_step = (int64_t)gridDim.x * kW;
+  for (int64_t ch = (int64_t)blockIdx.x * kW + wave; ch < n_chunks; ch += ch_step) {
+    const int64_t c0 = ch * kChunk;
+    uint32_t pairs = 0, nmixed = 0;
+    for (int b = 0; b < kPairItems; b += kPB) {
+      double X[kPts], Y[kPts];
+#pragma unroll
+      for (int k = 0; k < kPB; k++) {
+        const int64_t p = c0 + (int64_t)(b + k) * 128 + 2 * lane;
+        if (p + 1 < a.n) {
+          const dbl2_t vx = __builtin_nontemporal_load((const dbl2_t*)(a.x + p));
+          const dbl2_t vy = __builtin_nontemporal_load((const dbl2_t*)(a.y + p));
+          X[2 * k] = vx.x, X[2 * k + 1] = vx.y, Y[2 * k] = vy.x, Y[2 * k + 1] = vy.y;
+        } else {
+          X[2 * k] = Y[2 * k] = X[2 * k + 1] = Y[2 * k + 1] = 0.0;
+          if (p < a.n) X[2 * k] = a.x[p], Y[2 * k] = a.y[p];
+        }
+      }
+      uint32_t ri[kPts], gix[kPts], sb[kPts], bi[kPts];
+#pragma unroll
+      for (int j = 0; j < kPts; j++) {
+        ri[j] = kNoPixel;
+        gix[j] = 0;
+        sb[j] = 0;
+        bi[j] = kNoPixel;
+        const int64_t pj = c0 + (int64_t)(b + j / 2) * 128 + 2 * lane + (j & 1);
+        if (pj < a.n && pt_valid(a.valid, a.valid_off, pj)) {
+          bool ok = true;
+          uint32_t g_ = 0, s_ = 0, b_ = kNoPixel;
+          ri[j] = raster_index<IS>(t, X[j], Y[j], &ok, &g_, &s_, use_blk ? &b_ : nullptr);
+          gix[j] = g_;
+          sb[j] = s_;
+          bi[j] = b_;
+          any_bad |= !ok;
+        }
+      }
+      uint32_t cl[kPts];
+      uint64_t ge[kPts];
+#pragma unroll
+      for (int j = 0; j < kPts; j++) {
+        cl[j] = ri[j] < kRasterFull ? raster_class_blk(t, s_blk, ri[j], bi[j], sb[j], s_band)
+                                    : (ri[j] == kRasterFull ? kPixMixed : kPixEmpty);
+        ge[j] = (IS == MGPU_BNG && ri[j] < kRasterFull) ? t.grid[gix[j]] : 0ull;
+      }
+      Code code[kPts];
+      bool mixed[kPts];
+#pragma unroll
+      for (int j = 0; j < kPts; j++) {
+        const int64_t pj = c0 + (int64_t)(b + j / 2) * 128 + 2 * lane + (j & 1);
+        bool m = cl[j] == kPixMixed;
+        if (IS == MGPU_H3) {
+          code[j] = (Code)cl[j];
+          if (!m && cl[j] != kPixEmpty) {
+            const uint32_t c = cl[j];
+            pairs += c < t.raster_pc[0] ? 1u : c < t.raster_pc[1] ? 2u : c < t.raster_pc[2] ? 3u : c < t.raster_pc[3] ? 4u
+                     : (uint32_t)__popc((uint32_t)(t.raster_cls[c] >> 32));
+          }
+        } else {
+          const uint32_t first = (uint32_t)ge[j], mm = cl[j];
+          if (!m && mm && !(mm < 256u && first < (1u << 24))) m = true;
+          code[j] = (Code)(m ? kCodeMixed32 : (mm ? (first << 8) | mm : 0u));
+          if (!m) pairs += __popc(mm);
+        }
+        mixed[j] = m && pj < a.n;
+      }
+#pragma unroll
+      for (int k = 0; k < kPB; k++) {
+        const int64_t p = c0 + (int64_t)(b + k) * 128 + 2 * lane;
+        if (p + 1 < a.n) {
+          if (sizeof(Code) == 2) {
+            MGPU_ST_INTER((uint32_t)code[2 * k] | ((uint32_t)code[2 * k + 1] << 16), (uint32_t*)(codes + p));
+          } else {
+            typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+            u32x2_t v;
+            v.x = (uint32_t)code[2 * k];
+            v.y = (uint32_t)code[2 * k + 1];
+            MGPU_ST_INTER(v, (u32x2_t*)(codes + p));
+          }
+        } else if (p < a.n) {
+          MGPU_ST_INTER(code[2 * k], &codes[p]);
+        }
+        const unsigned long long b0 = __ballot(mixed[2 * k]), b1 = __ballot(mixed[2 * k + 1]);
+        const uint32_t r0 = nmixed + (uint32_t)__popcll(b0 & below) + (uint32_t)__popcll(b1 & below);
+        const uint16_t li = (uint16_t)((b + k) * 128 + 2 * lane);
+        if (mixed[2 * k]) sa.mixed_idx[c0 + r0] = li;
+        if (mixed[2 * k + 1]) sa.mixed_idx[c0 + r0 + (mixed[2 * k] ? 1u : 0u)] = (uint16_t)(li + 1);
+        nmixed += (uint32_t)(__popcll(b0) + __popcll(b1));
+      }
+    }
+    pairs = wave_sum_u32(pairs);
+    if (lane == 0) {
+      sa.chunk_pairs[ch] = pairs;
+      sa.chunk_mixed[ch] = nmixed;
+    }
+  }
+  count_wave(&a.counters[2], any_bad);
+}
 
 // The mixed points of one chunk per workgroup: its first tile of kTile; a chunk with
 // more queues its further tiles for pip_mixed_more_kernel (a loop over tiles here pinned
@@ -2001,9 +2164,21 @@ __global__ __launch_bounds__(kBinBlock) void bin_hist_kernel(BinArgs b) {
       py[k] = __builtin_nontemporal_load(&b.y[p]);
     }
   }
+  // one LDS atomic per distinct bin of the wave (as bin_scatter_kernel's ranks)
+  const int nbits = nb > 1 ? 32 - __clz(nb - 1) : 0;
+  const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int k = 0; k < kBinItems; k++)
-    if (c0 + (int64_t)k * kBinBlock + threadIdx.x < n) atomicAdd(&s_h[bin_of(b, px[k], py[k])], 1u);
+  for (int k = 0; k < kBinItems; k++) {
+    const bool act = c0 + (int64_t)k * kBinBlock + threadIdx.x < n;
+    const uint32_t bi = act ? bin_of(b, px[k], py[k]) : 0u;
+    unsigned long long peers = __ballot(act);
+    for (int bit = 0; bit < nbits; bit++) {
+      const bool on = (bi >> bit) & 1u;
+      const unsigned long long m = __ballot(on);
+      peers &= on ? m : ~m;
+    }
+    if (act && lane == __ffsll((unsigned long long)peers) - 1) atomicAdd(&s_h[bi], (uint32_t)__popcll(peers));
+  }
   __syncthreads();
   if ((int)threadIdx.x < nb) b.cnt[(int64_t)blockIdx.x * nb + threadIdx.x] = s_h[threadIdx.x];
 }
@@ -2108,10 +2283,32 @@ __device__ __forceinline__ uint32_t bin_at(const uint32_t* s_loc, int nb, uint32
   return lo;
 }
 
+// Binned H3 joins over a dense lattice grid: the scatter kernel, which holds every point
+// anyway, projects it (the streaming fast path, h3::fast_hex2d, as chip_probe) and writes
+// the point's grid entry index per binned slot; the join's phase 1 then issues all of a
+// lane's grid loads at once instead of one projection -> grid load chain per item.  A
+// near-tie is queued here (tie_host) or sends the join's tile to the fix kernel (kKeyTie).
+__device__ __forceinline__ uint32_t bin_key_of(const JoinArgs& a, int64_t pos, double px, double py) {
+  const ChipTableView& t = a.chips;
+  if (!(isfinite(px) && isfinite(py))) return kKeyBad;
+  if (!a.res_match || !(px >= t.bbox[0] && px <= t.bbox[2] && py >= t.bbox[1] && py <= t.bbox[3])) return kKeyNone;
+  const h3::FastHex f = h3::fast_hex2d(h3::to_radians_fast(py), h3::to_radians_fast(px), a.res, t.k_res, t.face_mask);
+  if (f.tie) {
+    if (!a.tie_host) return kKeyTie;
+    tie_record(a.tie_queue, a.tie_cap, pos, px, py, h3::lattice_key(f.face, f.ijk));
+  }
+  const int32_t ga = f.ijk.i - f.ijk.k, gb = f.ijk.j - f.ijk.k;
+  const DenseFace& D = t.dense[f.face];
+  const uint32_t da = (uint32_t)(ga - D.a0), db = (uint32_t)(gb - D.b0);
+  if (da >= D.w || db >= D.h) return kKeyNone;
+  return (D.base + db * D.w + da) | (f.deep ? kKeyDeep : 0u);
+}
+
 // Per chunk: each point's rank among the chunk's points of its bin (LDS atomics -- any
 // order inside a bin will do: perm[slot] records where each point came from), the
 // chunk's points sorted by bin in LDS, then written as contiguous runs (one per bin) by
 // consecutive lanes: whole cache lines, not one scattered 8-byte store per point.
+template <bool KEY>
 __global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
   __shared__ double s_val[kBinChunk];   // x, then y, in the chunk's bin-sorted order
   __shared__ uint16_t s_li[kBinChunk];  // the point's index in the chunk
@@ -2135,15 +2332,31 @@ __global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
   }
   if ((int)threadIdx.x < nb) s_rank[threadIdx.x] = 0;
   bin_runs(b, k, s_off, s_loc, s_w);
+  // ranks: the wave's lanes with the same bin found by one ballot per bin bit; one LDS
+  // atomic per distinct bin (its lowest lane adds the group's size) -- not one per point,
+  // whose same-address collisions serialised (r4: 45M LDS conflict cycles per 1e8 points)
+  const int nbits = nb > 1 ? 32 - __clz(nb - 1) : 0;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
   uint32_t lps[kBinItems];
 #pragma unroll
   for (int q = 0; q < kBinItems; q++) {
     const int64_t p = c0 + (int64_t)q * kBinBlock + threadIdx.x;
+    const bool act = p < n;
+    const uint32_t bi = act ? bin_of(b, px[q], py[q]) : 0u;
+    unsigned long long peers = __ballot(act);
+    for (int bit = 0; bit < nbits; bit++) {
+      const bool on = (bi >> bit) & 1u;
+      const unsigned long long m = __ballot(on);
+      peers &= on ? m : ~m;
+    }
+    const int leader = act ? __ffsll((unsigned long long)peers) - 1 : lane;
+    uint32_t base = 0;
+    if (act && lane == leader) base = atomicAdd(&s_rank[bi], (uint32_t)__popcll(peers));
+    base = __shfl(base, leader, 64);
     lps[q] = 0xFFFFFFFFu;
-    if (p < n) {
-      const uint32_t bi = bin_of(b, px[q], py[q]);
-      const uint32_t r = atomicAdd(&s_rank[bi], 1u);
-      lps[q] = s_loc[bi] + r;
+    if (act) {
+      lps[q] = s_loc[bi] + base + (uint32_t)__popcll(peers & below);
       s_val[lps[q]] = px[q];
       s_li[lps[q]] = (uint16_t)(q * kBinBlock + threadIdx.x);
     }
@@ -2171,6 +2384,22 @@ __global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
 #pragma unroll
   for (int q = 0; q < kBinItems; q++)
     if (sls[q] != 0xFFFFFFFFu) MGPU_ST_INTER(s_val[q * kBinBlock + threadIdx.x], &b.by[sls[q]]);
+  if (KEY) {
+    // the grid keys, through the same LDS order (the first half of s_val as u32)
+    uint32_t* s_key = (uint32_t*)s_val;
+    uint32_t kv[kBinItems];
+#pragma unroll
+    for (int q = 0; q < kBinItems; q++)
+      kv[q] = lps[q] != 0xFFFFFFFFu ? bin_key_of(b.s.j, c0 + (int64_t)q * kBinBlock + threadIdx.x, px[q], py[q]) : kKeyNone;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kBinItems; q++)
+      if (lps[q] != 0xFFFFFFFFu) s_key[lps[q]] = kv[q];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kBinItems; q++)
+      if (sls[q] != 0xFFFFFFFFu) MGPU_ST_INTER(s_key[q * kBinBlock + threadIdx.x], &b.key[sls[q]]);
+  }
 }
 
 // the join over the binned points: join_tile's phases (G mode, no mixed list: every
@@ -2489,6 +2718,9 @@ static int resident_blocks(const void* kernel, int block, size_t lds) {
 
 template <int IS>
 static void launch_emit(const SplitArgs& a, int64_t nc, hipStream_t s) {
+  // (A/B r5, profiles/r5/ab_classify_pair_emit_wave.txt: one wave per chunk -- wave scans,
+  // no workgroup barrier, the class table loaded once per workgroup -- took the C2 emit
+  // 0.255 -> 0.467 ms: rejected)
   hipLaunchKernelGGL(split_emit_kernel<IS>, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
 }
 
@@ -2499,8 +2731,13 @@ static void launch_split_t(const SplitArgs& a, hipStream_t s, hipEvent_t after_c
   const size_t nblk = (IS == MGPU_H3 && ct.raster_blk) ? (size_t)ct.raster_bnx * ct.raster_bny : 0;
   const size_t lds = IS == MGPU_H3 ? ((nblk + 1) & ~(size_t)1) * 2 + (size_t)ct.raster_nband * 4 : 0;
   const int64_t wg = (nc + kCfyBlock / 64 - 1) / (kCfyBlock / 64);
-  const int64_t grid = std::min<int64_t>(wg, (int64_t)resident_blocks((const void*)classify_wave_kernel<IS>, kCfyBlock, lds));
-  hipLaunchKernelGGL(classify_wave_kernel<IS>, dim3((unsigned)grid), dim3(kCfyBlock), lds, s, a, nc);
+  if (MGPU_CFY_PAIR && ((((uintptr_t)a.j.x) | ((uintptr_t)a.j.y)) & 15) == 0) {
+    const int64_t grid = std::min<int64_t>(wg, (int64_t)resident_blocks((const void*)classify_pair_kernel<IS>, kCfyBlock, lds));
+    hipLaunchKernelGGL(classify_pair_kernel<IS>, dim3((unsigned)grid), dim3(kCfyBlock), lds, s, a, nc);
+  } else {
+    const int64_t grid = std::min<int64_t>(wg, (int64_t)resident_blocks((const void*)classify_wave_kernel<IS>, kCfyBlock, lds));
+    hipLaunchKernelGGL(classify_wave_kernel<IS>, dim3((unsigned)grid), dim3(kCfyBlock), lds, s, a, nc);
+  }
   if (after_classify) hipEventRecord(after_classify, s);
   // (one workgroup per chunk walking its mixed tiles; one workgroup per tile measured 8x
   // slower on C2: ~6 ns per dispatched workgroup, most of them empty)
@@ -2571,7 +2808,10 @@ static void launch_binned_t(const BinArgs& a, hipStream_t s, hipEvent_t after_bi
   hipLaunchKernelGGL(bin_hist_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
   hipLaunchKernelGGL(bin_colscan_kernel, dim3((unsigned)((nb + 255) / 256), (unsigned)G), dim3(256), 0, s, a, K);
   hipLaunchKernelGGL(bin_base_kernel, dim3(1), dim3(kBaseBlock), 0, s, a, G);
-  hipLaunchKernelGGL(bin_scatter_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
+  if (IS == MGPU_H3 && a.key)
+    hipLaunchKernelGGL(bin_scatter_kernel<true>, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL(bin_scatter_kernel<false>, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
   if (after_bin) hipEventRecord(after_bin, s);
   const int64_t nc = split_chunks(n), tiles = nc * kChunkTiles;
   const uint32_t per = a.xcd_runs ? (uint32_t)((tiles + 7) / 8) : 0u;

@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "capi_internal.h"
@@ -81,18 +82,25 @@ __device__ __forceinline__ bool same_bits(double a, double b) {
 // per landmark: the candidates sharing one of its ring cells, minus itself (the same
 // coordinates: the reference's hash of the same geometry), within the threshold --
 // counted (WRITE = false) or written from off[i] (WRITE = true)
+// (WRITE = false also flags, in nul[i], a landmark with a ring cell holding no candidate:
+// the left_outer join's null row, GridRingNeighbours.scala:128,151)
 template <bool WRITE>
 __global__ __launch_bounds__(256) void rj_pairs_kernel(RjArgs a, int64_t* __restrict__ cnt, const int64_t* __restrict__ off,
-                                                      int64_t* __restrict__ out_right, double* __restrict__ out_dist) {
+                                                      int64_t* __restrict__ out_right, double* __restrict__ out_dist,
+                                                      int8_t* __restrict__ nul) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n_left) return;
   const double px = a.lx[i], py = a.ly[i];
   int64_t m = 0, q = WRITE ? off[i] : 0;
+  bool empty_cell = false;
   for (int64_t r = a.ring_off[i]; r < a.ring_off[i + 1]; r++) {
     const uint64_t c = (uint64_t)a.ring[r];
     uint64_t h = rj_hash(c) & a.mask;
     while (a.slot_cell[h] != 0 && a.slot_cell[h] != c) h = (h + 1) & a.mask;
-    if (a.slot_cell[h] != c) continue;
+    if (a.slot_cell[h] != c) {
+      empty_cell = true;
+      continue;
+    }
     for (int64_t k = a.slot_head[h]; k >= 0; k = a.next[k]) {
       const double qx = a.rx[k], qy = a.ry[k];
       if (same_bits(px, qx) && same_bits(py, qy)) continue;
@@ -106,7 +114,10 @@ __global__ __launch_bounds__(256) void rj_pairs_kernel(RjArgs a, int64_t* __rest
       m++;
     }
   }
-  if (!WRITE) cnt[i] = m;
+  if (!WRITE) {
+    cnt[i] = m;
+    nul[i] = empty_cell ? 1 : 0;
+  }
 }
 
 __device__ __forceinline__ bool rj_less(double da, int64_t ia, double db, int64_t ib) {
@@ -117,7 +128,7 @@ __device__ __forceinline__ bool rj_less(double da, int64_t ia, double db, int64_
 // selection when keep is small, else all of it by a Shell sort -- and its kept count
 __global__ __launch_bounds__(256) void rj_sort_kernel(const int64_t* __restrict__ off, int64_t n, int64_t keep,
                                                       int64_t* __restrict__ right, double* __restrict__ dist,
-                                                      int64_t* __restrict__ kept) {
+                                                      int64_t* __restrict__ kept, const int8_t* __restrict__ nul) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t b = off[i], m = off[i + 1] - b;
@@ -151,7 +162,7 @@ __global__ __launch_bounds__(256) void rj_sort_kernel(const int64_t* __restrict_
         R[q] = tr;
       }
   }
-  kept[i] = want;
+  kept[i] = want + (nul ? nul[i] : 0);
 }
 
 // exclusive scan of v[0 .. n) into out[0 .. n] (out[n] = the total), three launches:
@@ -206,10 +217,20 @@ __global__ __launch_bounds__(256) void rj_copy_kernel(const int64_t* __restrict_
                                                       int64_t n, const int64_t* __restrict__ right,
                                                       const double* __restrict__ dist, int64_t left_base,
                                                       int64_t capacity, int64_t* __restrict__ out_left,
-                                                      int64_t* __restrict__ out_right, double* __restrict__ out_dist) {
+                                                      int64_t* __restrict__ out_right, double* __restrict__ out_dist,
+                                                      const int8_t* __restrict__ nul) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int64_t b = off[i], o = koff[i], e = koff[i + 1];
+  const int64_t b = off[i], e = koff[i + 1];
+  int64_t o = koff[i];
+  if (nul && nul[i]) {  // the null row first (Spark orders nulls first in an ascending window)
+    if (o < capacity) {
+      out_left[o] = left_base + i;
+      out_right[o] = -1;
+      out_dist[o] = __longlong_as_double(0x7FF8000000000000LL);
+    }
+    o++;
+  }
   for (int64_t q = o; q < e && q < capacity; q++) {
     out_left[q] = left_base + i;
     out_right[q] = right[b + q - o];
@@ -237,26 +258,17 @@ struct Scratch {
 
 }  // namespace
 
-extern "C" int32_t mgpu_ring_join(mgpu_ctx* ctx, int32_t index_system, int32_t res, int32_t k, int32_t loop_only,
-                                  const double* lx, const double* ly, int64_t n_left, const double* rx,
-                                  const double* ry, int64_t n_right, int64_t left_id_base, int32_t max_per_left,
-                                  double max_distance, int64_t capacity, int64_t* out_n, int64_t* out_left,
-                                  int64_t* out_right, double* out_dist, void* stream) {
-  if (!ctx || n_left < 0 || n_right < 0 || (n_left && (!lx || !ly)) || (n_right && (!rx || !ry)) || capacity < 0 ||
-      (capacity > 0 && (!out_left || !out_right || !out_dist)) || max_per_left < 0)
-    return mgpu::set_error(MGPU_E_INVALID_ARG, "ring_join: bad arguments");
-  if (k < 0 || k > 1024) return mgpu::set_error(MGPU_E_INVALID_ARG, "ring_join: k must be in [0, 1024]");
-  if (int32_t st = mgpu_check_resolution(index_system, res)) return st;
-  RJ_TRY(hipSetDevice(ctx->device));
-  hipStream_t s = (hipStream_t)stream;
-  if (out_n) *out_n = 0;
-  if (n_left == 0) return MGPU_OK;
-  Scratch S;
-  int64_t *lc, *rc;
-  RJ_TRY(S.get(&lc, n_left));
+// The join proper over given landmark cell lists (device CSR ring / ring_off): the
+// candidates' cells and hash, pairs, per-landmark order and cut, output.  flags:
+// MGPU_RING_LEFT_OUTER adds the null row of a landmark with a cell that holds no candidate.
+static int32_t cells_join(mgpu_ctx* ctx, hipStream_t s, Scratch& S, int32_t index_system, int32_t res, const double* lx,
+                          const double* ly, int64_t n_left, const int64_t* ring, const int64_t* ring_off,
+                          const double* rx, const double* ry, int64_t n_right, int64_t left_id_base,
+                          int32_t max_per_left, double max_distance, int32_t flags, int64_t capacity, int64_t* out_n,
+                          int64_t* out_left, int64_t* out_right, double* out_dist) {
+  void* stream = (void*)s;
+  int64_t* rc;
   RJ_TRY(S.get(&rc, n_right));
-  // both sides' cells, the reference's (near-ties by its libm): IndexSystem.pointToIndex
-  if (int32_t st = mgpu_points_to_cells(ctx, index_system, res, lx, ly, n_left, lc, stream, nullptr)) return st;
   if (n_right)
     if (int32_t st = mgpu_points_to_cells(ctx, index_system, res, rx, ry, n_right, rc, stream, nullptr)) return st;
   // the candidates' cell hash (cell ids are never 0)
@@ -272,19 +284,6 @@ extern "C" int32_t mgpu_ring_join(mgpu_ctx* ctx, int32_t index_system, int32_t r
   if (n_right)
     hipLaunchKernelGGL(rj_insert_kernel, dim3(grid_of(n_right)), dim3(256), 0, s, rc, n_right, slot_cell,
                        (unsigned long long*)slot_head, next, slots - 1);
-  // the landmarks' ring cells (IndexSystem.kRing / kLoop through mgpu_grid_kring)
-  int64_t *ring_off, *ring;
-  RJ_TRY(S.get(&ring_off, n_left + 1));
-  const int64_t per = loop_only ? (k == 0 ? 1 : 6 * (int64_t)k) : 3 * (int64_t)k * (k + 1) + 1;
-  int64_t ring_cap = n_left * per + 1024, ring_total = 0;
-  RJ_TRY(S.get(&ring, ring_cap));
-  int32_t st = mgpu_grid_kring(ctx, index_system, lc, n_left, k, loop_only, ring, ring_cap, ring_off, &ring_total, stream);
-  if (st == MGPU_E_CAPACITY) {
-    ring_cap = ring_total;
-    RJ_TRY(S.get(&ring, ring_cap));
-    st = mgpu_grid_kring(ctx, index_system, lc, n_left, k, loop_only, ring, ring_cap, ring_off, &ring_total, stream);
-  }
-  if (st) return st;
   const int64_t nb = (n_left + kScanB - 1) / kScanB;
   int64_t* bsum;
   RJ_TRY(S.get(&bsum, nb + 1));
@@ -297,9 +296,12 @@ extern "C" int32_t mgpu_ring_join(mgpu_ctx* ctx, int32_t index_system, int32_t r
   // candidate) and cut to max_per_left; kept counts, offsets, the output
   RjArgs a{lx, ly, rx, ry, ring, ring_off, slot_cell, slot_head, next, slots - 1, n_left, max_distance};
   int64_t *cnt, *off;
+  int8_t* nul;
   RJ_TRY(S.get(&cnt, n_left));
   RJ_TRY(S.get(&off, n_left + 1));
-  hipLaunchKernelGGL(rj_pairs_kernel<false>, dim3(grid_of(n_left)), dim3(256), 0, s, a, cnt, nullptr, nullptr, nullptr);
+  RJ_TRY(S.get(&nul, n_left));
+  hipLaunchKernelGGL(rj_pairs_kernel<false>, dim3(grid_of(n_left)), dim3(256), 0, s, a, cnt, nullptr, nullptr, nullptr,
+                     nul);
   scan(cnt, off);
   int64_t total = 0;
   RJ_TRY(hipMemcpyAsync(&total, off + n_left, 8, hipMemcpyDeviceToHost, s));
@@ -308,22 +310,208 @@ extern "C" int32_t mgpu_ring_join(mgpu_ctx* ctx, int32_t index_system, int32_t r
   double* pd;
   RJ_TRY(S.get(&pr, total));
   RJ_TRY(S.get(&pd, total));
-  hipLaunchKernelGGL(rj_pairs_kernel<true>, dim3(grid_of(n_left)), dim3(256), 0, s, a, nullptr, off, pr, pd);
+  hipLaunchKernelGGL(rj_pairs_kernel<true>, dim3(grid_of(n_left)), dim3(256), 0, s, a, nullptr, off, pr, pd, nullptr);
   int64_t *kept, *koff;
   RJ_TRY(S.get(&kept, n_left));
   RJ_TRY(S.get(&koff, n_left + 1));
+  const int8_t* nul_out = (flags & MGPU_RING_LEFT_OUTER) ? nul : nullptr;
   hipLaunchKernelGGL(rj_sort_kernel, dim3(grid_of(n_left)), dim3(256), 0, s, off, n_left, (int64_t)max_per_left, pr, pd,
-                     kept);
+                     kept, nul_out);
   scan(kept, koff);
   int64_t n_out = 0;
   RJ_TRY(hipMemcpyAsync(&n_out, koff + n_left, 8, hipMemcpyDeviceToHost, s));
   if (capacity > 0)
     hipLaunchKernelGGL(rj_copy_kernel, dim3(grid_of(n_left)), dim3(256), 0, s, off, koff, n_left, pr, pd, left_id_base,
-                       capacity, out_left, out_right, out_dist);
+                       capacity, out_left, out_right, out_dist, nul_out);
   RJ_TRY(hipGetLastError());
   RJ_TRY(hipStreamSynchronize(s));
   if (out_n) *out_n = n_out;
   if (n_out > capacity)
     return mgpu::set_error(MGPU_E_CAPACITY, "ring_join: %lld pairs, capacity %lld", (long long)n_out, (long long)capacity);
   return MGPU_OK;
+}
+
+static int32_t check_join_args(mgpu_ctx* ctx, int32_t index_system, int32_t res, const double* lx, const double* ly,
+                               int64_t n_left, const double* rx, const double* ry, int64_t n_right,
+                               int32_t max_per_left, int32_t flags, int64_t capacity, int64_t* out_left,
+                               int64_t* out_right, double* out_dist) {
+  if (!ctx || n_left < 0 || n_right < 0 || (n_left && (!lx || !ly)) || (n_right && (!rx || !ry)) || capacity < 0 ||
+      (capacity > 0 && (!out_left || !out_right || !out_dist)) || max_per_left < 0 || (flags & ~MGPU_RING_LEFT_OUTER))
+    return mgpu::set_error(MGPU_E_INVALID_ARG, "ring_join: bad arguments");
+  return mgpu_check_resolution(index_system, res);
+}
+
+extern "C" int32_t mgpu_ring_join_ex(mgpu_ctx* ctx, int32_t index_system, int32_t res, int32_t k, int32_t loop_only,
+                                     const double* lx, const double* ly, int64_t n_left, const double* rx,
+                                     const double* ry, int64_t n_right, int64_t left_id_base, int32_t max_per_left,
+                                     double max_distance, int32_t flags, int64_t capacity, int64_t* out_n,
+                                     int64_t* out_left, int64_t* out_right, double* out_dist, void* stream) {
+  if (int32_t st = check_join_args(ctx, index_system, res, lx, ly, n_left, rx, ry, n_right, max_per_left, flags,
+                                   capacity, out_left, out_right, out_dist))
+    return st;
+  if (k < 0 || k > 1024) return mgpu::set_error(MGPU_E_INVALID_ARG, "ring_join: k must be in [0, 1024]");
+  RJ_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (out_n) *out_n = 0;
+  if (n_left == 0) return MGPU_OK;
+  Scratch S;
+  int64_t* lc;
+  RJ_TRY(S.get(&lc, n_left));
+  // the landmarks' cells, the reference's (near-ties by its libm): IndexSystem.pointToIndex
+  if (int32_t st = mgpu_points_to_cells(ctx, index_system, res, lx, ly, n_left, lc, stream, nullptr)) return st;
+  // their ring cells (IndexSystem.kRing / kLoop through mgpu_grid_kring)
+  int64_t *ring_off, *ring;
+  RJ_TRY(S.get(&ring_off, n_left + 1));
+  const int64_t per = loop_only ? (k == 0 ? 1 : 6 * (int64_t)k) : 3 * (int64_t)k * (k + 1) + 1;
+  int64_t ring_cap = n_left * per + 1024, ring_total = 0;
+  RJ_TRY(S.get(&ring, ring_cap));
+  int32_t st = mgpu_grid_kring(ctx, index_system, lc, n_left, k, loop_only, ring, ring_cap, ring_off, &ring_total, stream);
+  if (st == MGPU_E_CAPACITY) {
+    ring_cap = ring_total;
+    RJ_TRY(S.get(&ring, ring_cap));
+    st = mgpu_grid_kring(ctx, index_system, lc, n_left, k, loop_only, ring, ring_cap, ring_off, &ring_total, stream);
+  }
+  if (st) return st;
+  return cells_join(ctx, s, S, index_system, res, lx, ly, n_left, ring, ring_off, rx, ry, n_right, left_id_base,
+                    max_per_left, max_distance, flags, capacity, out_n, out_left, out_right, out_dist);
+}
+
+extern "C" int32_t mgpu_ring_join(mgpu_ctx* ctx, int32_t index_system, int32_t res, int32_t k, int32_t loop_only,
+                                  const double* lx, const double* ly, int64_t n_left, const double* rx,
+                                  const double* ry, int64_t n_right, int64_t left_id_base, int32_t max_per_left,
+                                  double max_distance, int64_t capacity, int64_t* out_n, int64_t* out_left,
+                                  int64_t* out_right, double* out_dist, void* stream) {
+  return mgpu_ring_join_ex(ctx, index_system, res, k, loop_only, lx, ly, n_left, rx, ry, n_right, left_id_base,
+                           max_per_left, max_distance, 0, capacity, out_n, out_left, out_right, out_dist, stream);
+}
+
+// JTS OffsetSegmentGenerator.createCircle (the buffer of a point, 8 quadrant segments):
+// the start (x + r, y), then the fillet from angle 0 clockwise through 2 pi in 32 equal
+// steps (its first point repeats the start and is dropped), closed
+static void jts_circle(double x, double y, double r, std::vector<double>& xy) {
+  const double inc = 2.0 * M_PI / 32;
+  xy.push_back(x + r);
+  xy.push_back(y);
+  for (int i = 1; i < 32; i++) {
+    const double a = -(double)i * inc;
+    xy.push_back(x + r * std::cos(a));
+    xy.push_back(y + r * std::sin(a));
+  }
+  xy.push_back(x + r);
+  xy.push_back(y);
+}
+
+// SpatialKNN's last iteration (GridRingNeighbours.leftTransform with iterationID = -1,
+// models/knn/GridRingNeighbours.scala:82-90): per landmark, the cells of
+// grid_tessellate(st_buffer(landmark, radius[i]), res) not in grid_geometrykring(landmark,
+// res, k[i]) (array_except), joined with the candidates as every iteration is.  The
+// buffers are tessellated on the host by mgpu_tessellate (mosaicFill's sets, chips of
+// every cell meeting the circle); radius[i] NaN or <= 0 gives the landmark no cells.
+extern "C" int32_t mgpu_ring_join_final(mgpu_ctx* ctx, int32_t index_system, int32_t res, const double* lx,
+                                        const double* ly, const double* radius, const int32_t* k_iterated,
+                                        int64_t n_left, const double* rx, const double* ry, int64_t n_right,
+                                        int64_t left_id_base, int32_t max_per_left, double max_distance,
+                                        int32_t flags, int64_t capacity, int64_t* out_n, int64_t* out_left,
+                                        int64_t* out_right, double* out_dist, void* stream) {
+  if (int32_t st = check_join_args(ctx, index_system, res, lx, ly, n_left, rx, ry, n_right, max_per_left, flags,
+                                   capacity, out_left, out_right, out_dist))
+    return st;
+  if (n_left && (!radius || !k_iterated)) return mgpu::set_error(MGPU_E_INVALID_ARG, "ring_join_final: bad arguments");
+  if (n_left >= ((int64_t)1 << 31)) return mgpu::set_error(MGPU_E_INVALID_ARG, "ring_join_final: too many landmarks");
+  for (int64_t i = 0; i < n_left; i++)
+    if (k_iterated[i] < 0 || k_iterated[i] > 1024)
+      return mgpu::set_error(MGPU_E_INVALID_ARG, "ring_join_final: k must be in [0, 1024]");
+  RJ_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (out_n) *out_n = 0;
+  if (n_left == 0) return MGPU_OK;
+  Scratch S;
+  // the landmarks on the host (their circles), and their cells
+  std::vector<double> hx(n_left), hy(n_left);
+  RJ_TRY(hipMemcpyAsync(hx.data(), lx, n_left * 8, hipMemcpyDeviceToHost, s));
+  RJ_TRY(hipMemcpyAsync(hy.data(), ly, n_left * 8, hipMemcpyDeviceToHost, s));
+  int64_t* lc;
+  RJ_TRY(S.get(&lc, n_left));
+  if (int32_t st = mgpu_points_to_cells(ctx, index_system, res, lx, ly, n_left, lc, stream, nullptr)) return st;
+  RJ_TRY(hipStreamSynchronize(s));
+  // st_buffer(landmark, radius) -> grid_tessellate (mosaicFill's cells)
+  std::vector<int32_t> pid;
+  std::vector<int64_t> poff{0}, roff{0}, voff{0};
+  std::vector<double> xy;
+  for (int64_t i = 0; i < n_left; i++) {
+    if (!(radius[i] > 0) || !std::isfinite(radius[i]) || !std::isfinite(hx[i]) || !std::isfinite(hy[i])) continue;
+    pid.push_back((int32_t)i);
+    jts_circle(hx[i], hy[i], radius[i], xy);
+    voff.push_back((int64_t)xy.size() / 2);
+    roff.push_back((int64_t)voff.size() - 1);
+    poff.push_back((int64_t)roff.size() - 1);
+  }
+  std::vector<std::vector<int64_t>> cells(n_left);
+  if (!pid.empty()) {
+    mgpu_tess* t = nullptr;
+    if (int32_t st = mgpu_tessellate_ex(index_system, res, (int64_t)pid.size(), pid.data(), poff.data(), roff.data(),
+                                        voff.data(), xy.data(), 0, MGPU_CORE_MOSAICFILL, &t))
+      return st;
+    int64_t nc = 0, wb = 0;
+    mgpu_tess_result_sizes(t, &nc, &wb);
+    std::vector<int64_t> cell(nc), woff(nc + 1);
+    std::vector<int32_t> cpoly(nc);
+    std::vector<uint8_t> core(nc), wkb(std::max<int64_t>(wb, 1));
+    mgpu_tess_result_copy(t, cell.data(), cpoly.data(), core.data(), woff.data(), wkb.data());
+    mgpu_tess_destroy(t);
+    for (int64_t c = 0; c < nc; c++) cells[cpoly[c]].push_back(cell[c]);
+  }
+  // minus kRing(landmark cell, k[i]), per distinct k
+  std::vector<int64_t> hlc(n_left);
+  RJ_TRY(hipMemcpy(hlc.data(), lc, n_left * 8, hipMemcpyDeviceToHost));
+  std::vector<int32_t> ks(k_iterated, k_iterated + n_left);
+  std::sort(ks.begin(), ks.end());
+  ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
+  std::vector<std::vector<int64_t>> iterated(n_left);
+  for (int32_t k : ks) {
+    std::vector<int64_t> who;
+    for (int64_t i = 0; i < n_left; i++)
+      if (k_iterated[i] == k && !cells[i].empty()) who.push_back(i);
+    if (who.empty()) continue;
+    std::vector<int64_t> sub(who.size());
+    for (size_t q = 0; q < who.size(); q++) sub[q] = hlc[who[q]];
+    int64_t *dsub, *doff, *dring;
+    RJ_TRY(S.get(&dsub, sub.size()));
+    RJ_TRY(S.get(&doff, sub.size() + 1));
+    RJ_TRY(hipMemcpy(dsub, sub.data(), sub.size() * 8, hipMemcpyHostToDevice));
+    int64_t cap = (int64_t)sub.size() * (3 * (int64_t)k * (k + 1) + 1) + 1024, total = 0;
+    RJ_TRY(S.get(&dring, cap));
+    int32_t st = mgpu_grid_kring(ctx, index_system, dsub, (int64_t)sub.size(), k, 0, dring, cap, doff, &total, stream);
+    if (st == MGPU_E_CAPACITY) {
+      cap = total;
+      RJ_TRY(S.get(&dring, cap));
+      st = mgpu_grid_kring(ctx, index_system, dsub, (int64_t)sub.size(), k, 0, dring, cap, doff, &total, stream);
+    }
+    if (st) return st;
+    std::vector<int64_t> hr(total), ho(sub.size() + 1);
+    RJ_TRY(hipMemcpy(hr.data(), dring, total * 8, hipMemcpyDeviceToHost));
+    RJ_TRY(hipMemcpy(ho.data(), doff, ho.size() * 8, hipMemcpyDeviceToHost));
+    for (size_t q = 0; q < who.size(); q++) iterated[who[q]].assign(hr.begin() + ho[q], hr.begin() + ho[q + 1]);
+  }
+  // array_except: the distinct tessellation cells outside the iterated ring
+  std::vector<int64_t> ring, ring_off{0};
+  for (int64_t i = 0; i < n_left; i++) {
+    std::vector<int64_t> it = iterated[i];
+    std::sort(it.begin(), it.end());
+    std::vector<int64_t> seen;
+    for (int64_t c : cells[i]) {
+      if (std::binary_search(it.begin(), it.end(), c)) continue;
+      if (std::find(seen.begin(), seen.end(), c) != seen.end()) continue;
+      seen.push_back(c);
+      ring.push_back(c);
+    }
+    ring_off.push_back((int64_t)ring.size());
+  }
+  int64_t *dring, *droff;
+  RJ_TRY(S.get(&dring, ring.size()));
+  RJ_TRY(S.get(&droff, ring_off.size()));
+  if (!ring.empty()) RJ_TRY(hipMemcpy(dring, ring.data(), ring.size() * 8, hipMemcpyHostToDevice));
+  RJ_TRY(hipMemcpy(droff, ring_off.data(), ring_off.size() * 8, hipMemcpyHostToDevice));
+  return cells_join(ctx, s, S, index_system, res, lx, ly, n_left, dring, droff, rx, ry, n_right, left_id_base,
+                    max_per_left, max_distance, flags, capacity, out_n, out_left, out_right, out_dist);
 }

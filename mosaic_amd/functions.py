@@ -327,16 +327,36 @@ def pip_join_async(x, y, chips, resolution, index_system=None, point_id=None, po
     return AsyncJoin(chips.ctx, op, oq, count, (x, y, point_id, chips))
 
 
+def _ring_call(call, left_x, max_per_left):
+    """Run a ring-join entry with an output sized up front, once more at the reported size."""
+    import ctypes
+    import torch
+    n = ctypes.c_int64()
+    cap = max(16, left_x.numel() * (max_per_left + 1 if max_per_left > 0 else 8))
+    for _ in range(2):
+        ol = torch.empty(cap, dtype=torch.int64, device=left_x.device)
+        orr = torch.empty(cap, dtype=torch.int64, device=left_x.device)
+        od = torch.empty(cap, dtype=torch.float64, device=left_x.device)
+        st = call(cap, ctypes.byref(n), ol.data_ptr(), orr.data_ptr(), od.data_ptr())
+        if st == N.MGPU_E_CAPACITY:
+            cap = int(n.value)
+            continue
+        N.check(st)
+        m = int(n.value)
+        return ol[:m], orr[:m], od[:m]
+    N.check(st, required=n.value)
+
+
 def grid_ring_join(left_x, left_y, right_x, right_y, resolution, k=1, index_system=None, loop_only=False,
-                   max_per_left=0, max_distance=-1.0, left_id_base=0, stream=None):
+                   max_per_left=0, max_distance=-1.0, left_id_base=0, left_outer=False, stream=None):
     """One iteration of SpatialKNN's grid-ring neighbour join for point landmarks (left) and
     point candidates (right) -- GridRingNeighbours.transform (models/knn/
-    GridRingNeighbours.scala:121) with its resultTransform (mgpu_ring_join): the pairs whose
+    GridRingNeighbours.scala:121) with its resultTransform (mgpu_ring_join_ex): the pairs whose
     cells meet in kRing(cell(landmark), k) (``loop_only``: kLoop, iterations > 1), self
     matches dropped, ``distance <= max_distance`` (< 0: none), per landmark by (distance,
-    candidate index), at most ``max_per_left`` (0: all).  Returns (left ids, right indices,
-    distances) on the points' device."""
-    import ctypes
+    candidate index), at most ``max_per_left`` (0: all).  ``left_outer``: the left_outer
+    join's null row (right -1, distance NaN) first for a landmark with a cell holding no
+    candidate.  Returns (left ids, right indices, distances) on the points' device."""
     import torch
     from .context import default_context
     isys = index_system or _H3
@@ -345,20 +365,34 @@ def grid_ring_join(left_x, left_y, right_x, right_y, resolution, k=1, index_syst
     _check_points(right_x, right_y)
     ctx = default_context(left_x.device)
     s = stream if stream is not None else torch.cuda.current_stream(left_x.device).cuda_stream
-    n = ctypes.c_int64()
-    cap = max(16, left_x.numel() * (max_per_left if max_per_left > 0 else 8))
-    for _ in range(2):
-        ol = torch.empty(cap, dtype=torch.int64, device=left_x.device)
-        orr = torch.empty(cap, dtype=torch.int64, device=left_x.device)
-        od = torch.empty(cap, dtype=torch.float64, device=left_x.device)
-        st = N.lib().mgpu_ring_join(ctx.handle, isys.code, res, int(k), 1 if loop_only else 0, left_x.data_ptr(),
-                                    left_y.data_ptr(), left_x.numel(), right_x.data_ptr(), right_y.data_ptr(),
-                                    right_x.numel(), int(left_id_base), int(max_per_left), float(max_distance), cap,
-                                    ctypes.byref(n), ol.data_ptr(), orr.data_ptr(), od.data_ptr(), s)
-        if st == N.MGPU_E_CAPACITY:
-            cap = int(n.value)
-            continue
-        N.check(st)
-        m = int(n.value)
-        return ol[:m], orr[:m], od[:m]
-    N.check(st, required=n.value)
+    flags = N.MGPU_RING_LEFT_OUTER if left_outer else 0
+    return _ring_call(lambda cap, n, ol, orr, od: N.lib().mgpu_ring_join_ex(
+        ctx.handle, isys.code, res, int(k), 1 if loop_only else 0, left_x.data_ptr(), left_y.data_ptr(),
+        left_x.numel(), right_x.data_ptr(), right_y.data_ptr(), right_x.numel(), int(left_id_base),
+        int(max_per_left), float(max_distance), flags, cap, n, ol, orr, od, s), left_x, max_per_left)
+
+
+def grid_ring_join_final(left_x, left_y, radius, k_iterated, right_x, right_y, resolution, index_system=None,
+                         max_per_left=0, max_distance=-1.0, left_id_base=0, left_outer=False, stream=None):
+    """SpatialKNN's exactness iteration (GridRingNeighbours.leftTransform with iterationID
+    -1, GridRingNeighbours.scala:82-90; mgpu_ring_join_final): per landmark, the cells of
+    grid_tessellate(st_buffer(landmark, radius[i])) not in kRing(cell, k_iterated[i]),
+    joined with the candidates as grid_ring_join does.  ``radius`` / ``k_iterated``: host
+    arrays (the landmarks' k-th match distance and their last iteration)."""
+    import numpy as np
+    import torch
+    from .context import default_context
+    isys = index_system or _H3
+    res = isys.get_resolution(resolution)
+    _check_points(left_x, left_y)
+    _check_points(right_x, right_y)
+    rad = np.ascontiguousarray(radius, dtype=np.float64)
+    kit = np.ascontiguousarray(k_iterated, dtype=np.int32)
+    assert rad.shape == kit.shape == (left_x.numel(),)
+    ctx = default_context(left_x.device)
+    s = stream if stream is not None else torch.cuda.current_stream(left_x.device).cuda_stream
+    flags = N.MGPU_RING_LEFT_OUTER if left_outer else 0
+    return _ring_call(lambda cap, n, ol, orr, od: N.lib().mgpu_ring_join_final(
+        ctx.handle, isys.code, res, left_x.data_ptr(), left_y.data_ptr(), rad.ctypes.data, kit.ctypes.data,
+        left_x.numel(), right_x.data_ptr(), right_y.data_ptr(), right_x.numel(), int(left_id_base),
+        int(max_per_left), float(max_distance), flags, cap, n, ol, orr, od, s), left_x, max_per_left)

@@ -314,7 +314,7 @@ def h3_k_loop(h, n):
 
 
 def ring_join(index_system, res, k, lx, ly, rx, ry, loop_only=False, max_per_left=0, max_distance=-1.0,
-              left_id_base=0):
+              left_id_base=0, left_outer=False, cells=None):
     """Test infrastructure: one iteration of GridRingNeighbours (models/knn/
     GridRingNeighbours.scala:121 transform + resultTransform) for point landmarks and
     point candidates, restated: the landmark's kRing(cell, k) (Mosaic.geometryKRing,
@@ -322,7 +322,11 @@ def ring_join(index_system, res, k, lx, ly, rx, ry, loop_only=False, max_per_lef
     the candidates' cells (Mosaic.pointChip :48-59), each (landmark, candidate) once,
     self matches dropped, st_distance = JTS Coordinate.distance (Math.hypot: the fdlibm
     port of jts_centroid.py), distance <= max_distance, ordered by (distance, candidate),
-    the first max_per_left.  Returns (left, right, distance) arrays."""
+    the first max_per_left.  left_outer: the join is left_outer (GridRingNeighbours.scala:128)
+    and resultTransform keeps the null group (:151): a landmark with a cell that holds no
+    candidate gets a (left, -1, NaN) row first (Spark: nulls first in an ascending window).
+    cells: explicit per-landmark cell lists instead of the kRing / kLoop (the exactness
+    iteration, ring_join_final_cells).  Returns (left, right, distance) arrays."""
     import jts_centroid as JC
     lx, ly, rx, ry = (np.ascontiguousarray(v, dtype=np.float64) for v in (lx, ly, rx, ry))
     if index_system == 0:
@@ -338,7 +342,10 @@ def ring_join(index_system, res, k, lx, ly, rx, ry, loop_only=False, max_per_lef
     bits = lambda v: np.float64(v).view(np.int64)  # noqa: E731
     for i in range(len(lx)):
         got = []
-        for c in set(ring(lc[i])):
+        null_row = False
+        for c in set(ring(lc[i]) if cells is None else cells[i]):
+            if not by_cell.get(c):
+                null_row = True
             for j in by_cell.get(c, ()):
                 if bits(lx[i]) == bits(rx[j]) and bits(ly[i]) == bits(ry[j]):
                     continue
@@ -349,8 +356,42 @@ def ring_join(index_system, res, k, lx, ly, rx, ry, loop_only=False, max_per_lef
         got.sort()
         if max_per_left > 0:
             got = got[:max_per_left]
+        if left_outer and null_row:
+            got = [(float("nan"), -1)] + got
         for d, j in got:
             L.append(left_id_base + i)
             R.append(j)
             D.append(d)
     return np.array(L, np.int64), np.array(R, np.int64), np.array(D, np.float64)
+
+
+def jts_circle(x, y, r):
+    """JTS OffsetSegmentGenerator.createCircle (st_buffer of a point, 8 quadrant segments):
+    (x + r, y), then 31 more vertices clockwise at 2 pi / 32 steps, closed."""
+    import math
+    pts = [(x + r, y)] + [(x + r * math.cos(-i * 2 * math.pi / 32), y + r * math.sin(-i * 2 * math.pi / 32))
+                          for i in range(1, 32)]
+    return pts + [pts[0]]
+
+
+def ring_join_final_cells(index_system, res, lx, ly, radius, k_iterated, buffer_cells):
+    """The exactness iteration's landmark cells (GridRingNeighbours.leftTransform with
+    iterationID -1, GridRingNeighbours.scala:82-90): array_except(the cells of
+    grid_tessellate(st_buffer(landmark, radius)) -- `buffer_cells[i]`, the chip table of the
+    landmark's circle, an input as every chip table is -- , kRing(cell(landmark), k)),
+    distinct, in the tessellation's order."""
+    lx, ly = (np.ascontiguousarray(v, dtype=np.float64) for v in (lx, ly))
+    lc = h3_points_to_cells(lx, ly, res) if index_system == 0 else bng_points_to_cells(lx, ly, res)
+    out = []
+    for i in range(len(lx)):
+        if not (radius[i] > 0) or not np.isfinite(radius[i]):
+            out.append([])
+            continue
+        it = set(h3_k_ring(int(lc[i]), int(k_iterated[i])) if index_system == 0
+                 else bng_k_ring(int(lc[i]), int(k_iterated[i])))
+        seen = []
+        for c in buffer_cells[i]:
+            if c not in it and c not in seen:
+                seen.append(c)
+        out.append(seen)
+    return out

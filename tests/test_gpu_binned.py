@@ -117,6 +117,30 @@ def test_binned_adversarial_points_and_near_tie_positions(gpu, nyc_chips_r9):
     assert np.array_equal(rf.numpy()[0], op) and np.array_equal(rf.numpy()[1], oq)
 
 
+@pytest.mark.parametrize("keys,libm", [(0, 0), (1, 0), (0, 1), (1, 1)])
+def test_binned_grid_keys_adversarial(gpu, nyc_chips_r9, keys, libm):
+    """The binning pass's per-slot grid keys (option bin_keys, kernels.hip bin_key_of) and
+    the join's own projection give the same pairs on points at H3 cell corners, with the
+    reference's libm (near-ties queued by the scatter kernel, settled on the host) and with
+    the correctly rounded one (near-tie tiles sent to the fix kernel)."""
+    d = nyc_chips_r9.upload()
+    ax, ay = adversarial_points(nyc_chips_r9)
+    rng = np.random.default_rng(5)
+    x, y = nyc_points(300_000, 6)
+    at = np.sort(rng.choice(len(x), len(ax), replace=False))
+    x[at], y[at] = ax, ay
+    if libm:
+        with O.h3_libm("cr"):
+            op, oq = oracle_join(nyc_chips_r9, x, y)
+    else:
+        op, oq = oracle_join(nyc_chips_r9, x, y)
+    with opts(gpu, bin_keys=keys, h3_libm=libm):
+        r = binned_join(x, y, d, 9, gpu, nb=64)
+    gp, gq = r.numpy()
+    assert np.array_equal(gp, op) and np.array_equal(gq, oq)
+    assert r.stats["n_near_ties"] > 0
+
+
 def test_binned_bng_london(gpu):
     """BNG (C4's districts, res 3 and 4): bins over the dense grid's box."""
     import bench_workloads as W

@@ -873,3 +873,70 @@ def test_ring_join_equals_oracle(gpu, isys_name, res, k, loop_only, keep, maxd):
     assert len(ol) > len(lx) // 2
     assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
     assert np.array_equal(gd.view(np.int64), od.view(np.int64))
+
+
+@pytest.mark.parametrize("isys_name,res,keep", [("H3", 9, 0), ("H3", 9, 3), ("BNG", 3, 0)])
+def test_ring_join_left_outer_equals_oracle(gpu, isys_name, res, keep):
+    """left_outer = True: the left_outer join's null row (right -1, distance NaN) first for
+    every landmark with a ring cell that holds no candidate (GridRingNeighbours.scala:128,
+    151), sparse candidates so many cells are empty; otherwise the pairs of left_outer =
+    False."""
+    rng = np.random.default_rng(77 + res)
+    if isys_name == "BNG":
+        isys, code = M.BNGIndexSystem(), 1
+        lx, ly = rng.uniform(520_000, 540_000, 700), rng.uniform(170_000, 190_000, 700)
+        rx, ry = rng.uniform(518_000, 542_000, 300), rng.uniform(168_000, 192_000, 300)
+    else:
+        isys, code = M.H3IndexSystem(), 0
+        lx, ly = nyc_points(2000, 61)
+        rx, ry = nyc_points(3000, 62)
+    got = M.grid_ring_join(T(lx, gpu), T(ly, gpu), T(rx, gpu), T(ry, gpu), res, 1, index_system=isys,
+                           max_per_left=keep, left_outer=True)
+    gl, gr, gd = (v.cpu().numpy() for v in got)
+    ol, orr, od = O.ring_join(code, res, 1, lx, ly, rx, ry, max_per_left=keep, left_outer=True)
+    assert (orr == -1).sum() > 100 and (orr >= 0).sum() > 100
+    assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
+    assert np.array_equal(gd.view(np.int64), od.view(np.int64))  # (NaN rows: the same quiet NaN)
+    plain = [v.cpu().numpy() for v in M.grid_ring_join(T(lx, gpu), T(ly, gpu), T(rx, gpu), T(ry, gpu), res, 1,
+                                                       index_system=isys, max_per_left=keep)]
+    assert np.array_equal(plain[1], gr[gr >= 0]) and np.array_equal(plain[0], gl[gr >= 0])
+
+
+@pytest.mark.parametrize("isys_name,res", [("H3", 9), ("BNG", 3)])
+def test_ring_join_final_equals_oracle(gpu, isys_name, res):
+    """SpatialKNN's exactness iteration (mgpu_ring_join_final, GridRingNeighbours.scala:82-90):
+    per landmark the cells of grid_tessellate(st_buffer(landmark, radius)) minus its iterated
+    kRing, joined with the candidates.  The oracle takes the circles' chip tables from the
+    tessellator (as every chip table input) and restates the rest: the 32-gon circle, the
+    kRing difference, the join, distances, order, the left_outer null rows.  Landmarks with
+    radius NaN / 0 have no cells."""
+    rng = np.random.default_rng(91 + res)
+    if isys_name == "BNG":
+        isys, code = M.BNGIndexSystem(), 1
+        lx, ly = rng.uniform(520_000, 540_000, 300), rng.uniform(170_000, 190_000, 300)
+        rx, ry = rng.uniform(518_000, 542_000, 20000), rng.uniform(168_000, 192_000, 20000)
+        radius = rng.uniform(500, 4000, len(lx))
+    else:
+        isys, code = M.H3IndexSystem(), 0
+        lx, ly = nyc_points(400, 63)
+        rx, ry = nyc_points(60000, 64)
+        radius = rng.uniform(0.001, 0.008, len(lx))
+    radius[:5] = [np.nan, 0.0, -1.0, radius[3], radius[4]]
+    kit = rng.integers(1, 4, len(lx)).astype(np.int32)
+    got = M.grid_ring_join_final(T(lx, gpu), T(ly, gpu), radius, kit, T(rx, gpu), T(ry, gpu), res, index_system=isys,
+                                 left_outer=True, left_id_base=3)
+    gl, gr, gd = (v.cpu().numpy() for v in got)
+    # the circles' cells from the tessellator
+    ok = np.nonzero((radius > 0) & np.isfinite(radius))[0]
+    P = M.Polygons.from_lists([(int(i), [[O.jts_circle(lx[i], ly[i], radius[i])]]) for i in ok])
+    chips = M.tessellate(P, isys, res, keep_core_geometries=False)
+    buf = [[] for _ in lx]
+    for c, p in zip(chips.cell.tolist(), chips.polygon_id.tolist()):
+        buf[p].append(c)
+    cells = O.ring_join_final_cells(code, res, lx, ly, radius, kit, buf)
+    assert sum(len(c) for c in cells) > 2 * len(lx)
+    ol, orr, od = O.ring_join(code, res, 0, lx, ly, rx, ry, left_id_base=3, left_outer=True, cells=cells)
+    assert (orr >= 0).sum() > len(lx)
+    assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
+    assert np.array_equal(gd.view(np.int64), od.view(np.int64))
+    assert not np.isin(np.arange(3, 6), gl).any()  # the NaN / 0 / negative radius landmarks 0-2

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build profiling variants of libmosaic_gpu.so: tools/variants.sh NAME "-DFOO=1" [NAME "-D..."]...
-# Each lands in build/variants/NAME/libmosaic_gpu.so (select with MOSAIC_AMD_LIB).  The
+# Each lands in build/ab/NAME/libmosaic_gpu.so (select with MOSAIC_AMD_LIB).  The
 # variants' kernels.hip compiles run in parallel; the host objects are the tree's.
 set -e
 cd "$(dirname "$0")/../mosaic_amd/csrc"
@@ -9,7 +9,7 @@ CXXFLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wno-unused-resu
 pids=()
 names=()
 while [ $# -ge 2 ]; do
-  d=../../build/variants/$1; mkdir -p $d
+  d=../../build/ab/$1; mkdir -p $d
   if [ "${2#host:}" != "$2" ]; then  # NAME "host:-D..." rebuilds capi.cpp (the chip-table builder) instead
     (/opt/rocm/bin/hipcc $CXXFLAGS ${2#host:} -c capi.cpp -o $d/capi.o 2> $d/build.log &&
      /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $d/libmosaic_gpu.so kernels.o $d/capi.o comm.o tessellate.o \
