@@ -108,6 +108,8 @@ int32_t mgpu_ctx_destroy(mgpu_ctx* ctx);
  *   "bin_keys"        1: H3 binned joins over a dense grid take each point's grid entry from
  *                     the binning pass (which projects the point); 0 (default): the join
  *                     projects (C3: binning +1.4 ms, join -0.16 ms per 1.25e8 points)
+ *   "ring_batch"      ring joins hold at most this many candidate pairs in scratch at a time
+ *                     (landmarks in batches; default 2^26)
  *   "spin_us"         synchronous calls poll their stream (yielding the core between polls)
  *                     at most this long, then block in hipStreamSynchronize (default 2000;
  *                     0 = block at once)
@@ -371,7 +373,14 @@ int32_t mgpu_pip_join_fetch(mgpu_ctx* ctx, int64_t capacity, int64_t* out_n_pair
  * batch with near-ties may hold the fast cell at those points.  BNG joins and the
  * correctly rounded mode have no host step, but the call is still required.
  * mgpu_pip_join_finish: MGPU_E_INVALID_ARG when no asynchronous join is pending (another
- * call on the context ended it). */
+ * call on the context ended it).
+ * Graph replays are NOT settled: finish pairs with the host-side mgpu_pip_join_async call
+ * that queued the work, so a captured join replayed from a graph keeps the fast cell at
+ * the points of its tie band (H3, reference libm) and finish after a replay returns
+ * MGPU_E_INVALID_ARG.  A caller replaying graphs either sets h3_libm to
+ * MGPU_LIBM_CORRECTLY_ROUNDED (the device decides every point, no host step) or reads the
+ * replay's queued positions with mgpu_last_near_ties and reruns those batches with
+ * mgpu_pip_join. */
 int32_t mgpu_pip_join_async(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t index_system, int32_t res,
                             const double* x, const double* y, const int64_t* point_id, int64_t point_id_base,
                             int64_t n, int64_t capacity, int64_t* d_n_pairs, int64_t* out_point_id,

@@ -1050,9 +1050,12 @@ void raster_bands(Raster& R) {
 
 // the block table over the level-1 classes: the smallest block edge 2^s (s >= 3) whose
 // table fits kRasterBlkBytes (the join kernels hold it in LDS)
-constexpr size_t kRasterBlkBytes = 40 * 1024;
+#ifndef MGPU_RASTER_BLK_KB
+#define MGPU_RASTER_BLK_KB 40
+#endif
+constexpr size_t kRasterBlkBytes = MGPU_RASTER_BLK_KB * 1024;
 void raster_blocks(Raster& R) {
-  for (uint32_t sh = 3; sh <= 8; sh++) {
+  for (uint32_t sh = MGPU_RASTER_BLK_KB > 64 ? 2 : 3; sh <= 8; sh++) {
     const uint32_t bnx = (R.nx + (1u << sh) - 1) >> sh, bny = (R.ny + (1u << sh) - 1) >> sh;
     if ((size_t)bnx * bny * 2 > kRasterBlkBytes) continue;
     R.bshift = sh, R.bnx = bnx, R.bny = bny;
@@ -1651,6 +1654,9 @@ int32_t mgpu_ctx_set_option(mgpu_ctx* ctx, const char* key, int64_t v) {
   } else if (k == "bin_keys") {
     if (v != 0 && v != 1) return bad();
     o.bin_keys = v;
+  } else if (k == "ring_batch") {
+    if (v < 1) return bad();
+    o.ring_batch = v;
   } else if (k == "spin_us") {
     if (v < 0 || v > 10000000) return bad();
     o.spin_us = v;
@@ -1675,7 +1681,7 @@ int32_t mgpu_ctx_get_option(const mgpu_ctx* ctx, const char* key, int64_t* v) {
   const std::pair<const char*, int64_t> all[] = {
       {"h3_libm", o.h3_libm},       {"pipeline", o.pipeline}, {"bin_count", o.bin_count},
       {"bin_min_mb", o.bin_min_mb}, {"bin_min_points", o.bin_min_points}, {"bin_xcd", o.bin_xcd},
-      {"bin_keys", o.bin_keys},     {"spin_us", o.spin_us},       {"raster", o.raster},     {"raster_bng", o.raster_bng},
+      {"bin_keys", o.bin_keys},     {"spin_us", o.spin_us},   {"ring_batch", o.ring_batch},       {"raster", o.raster},     {"raster_bng", o.raster_bng},
       {"raster_sub", o.raster_sub}, {"raster_milli", o.raster_milli}};
   for (const auto& kv : all)
     if (strcmp(kv.first, key) == 0) {
@@ -2802,6 +2808,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     for (int f = 0; f < 20; f++) grid_entries = std::max<uint64_t>(grid_entries, (uint64_t)cv.dense[f].base + (uint64_t)cv.dense[f].w * cv.dense[f].h);
     const bool keyed = is == MGPU_H3 && cv.probe_mode == mgpu::kProbeDense && o.bin_keys && grid_entries < (1ull << 30);
     const size_t o_key = keyed ? carve((size_t)n * 4) : 0;
+    const size_t o_lb = carve((size_t)K * 8);
     if (off > ctx->bin_bytes) {
       if (ctx->bin_ws) HIP_TRY(hipFree(ctx->bin_ws));
       ctx->bin_ws = nullptr;
@@ -2820,6 +2827,7 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     ba.cnt = (uint32_t*)(bb + o_cnt);
     ba.gsum = (uint32_t*)(bb + o_gs);
     ba.key = keyed ? (uint32_t*)(bb + o_key) : nullptr;
+    ba.lb = (uint64_t*)(bb + o_lb);
     mgpu::JoinArgs j = a;
     j.bin_key = ba.key;
     j.x = ba.bx;

@@ -190,9 +190,12 @@ int32_t mgpu_chips_broadcast(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t roo
   // word is first set negative on the stream, so a failed copy of `mine` still
   // contributes a failure (never a stale OK from an earlier call)
   int32_t agreed = mine;
-  if (hipMemsetAsync(status, 0x80, 4, s) != hipSuccess ||
-      hipMemcpyAsync(status, &mine, 4, hipMemcpyHostToDevice, s) != hipSuccess)
-    agreed = MGPU_E_DEVICE;
+  // (both steps are tried whatever the first gave: a failed memset makes the copied value
+  // a failure itself, so no stale OK from an earlier call can reach the all-reduce)
+  const bool set_ok = hipMemsetAsync(status, 0x80, 4, s) == hipSuccess;
+  const int32_t contrib = set_ok ? mine : (int32_t)MGPU_E_DEVICE;
+  const bool copy_ok = hipMemcpyAsync(status, &contrib, 4, hipMemcpyHostToDevice, s) == hipSuccess;
+  if (!set_ok || !copy_ok) agreed = MGPU_E_DEVICE;
   r = ncclAllReduce(status, status, 1, ncclInt32, ncclMin, c->comm, s);
   if (r != ncclSuccess) {
     if (dst) hipFree(dst);
@@ -237,10 +240,19 @@ int32_t mgpu_pair_offsets(mgpu_ctx* ctx, int64_t local_pairs, int64_t* out_offse
   // a negative count still takes part in the all-gather (as -1): every rank then fails.
   // The slot is set to -1 on the stream first, so a failed copy also contributes -1
   // instead of returning before the collective the other ranks wait in
+  // (the copy is tried even when the memset failed -- then carrying -1 itself -- and a
+  // local failure is reported after the collective, so this rank never relies on the
+  // slot holding the previous call's count)
   const int64_t v = local_pairs < 0 ? -1 : local_pairs;
-  if (hipMemsetAsync(mine, 0xFF, 8, s) == hipSuccess) (void)hipMemcpyAsync(mine, &v, 8, hipMemcpyHostToDevice, s);
+  const bool set_ok = hipMemsetAsync(mine, 0xFF, 8, s) == hipSuccess;
+  const int64_t vv = set_ok ? v : -1;
+  const bool copy_ok = hipMemcpyAsync(mine, &vv, 8, hipMemcpyHostToDevice, s) == hipSuccess;
   ncclResult_t r = ncclAllGather(mine, all, 1, ncclInt64, c->comm, s);
   if (r != ncclSuccess) return comm_failed(ctx, "ncclAllGather(pair counts)", r);
+  if (!set_ok || !copy_ok) {
+    (void)hipStreamSynchronize(s);
+    return mgpu::set_error(MGPU_E_DEVICE, "pair_offsets: staging this rank's count failed");
+  }
   std::vector<int64_t> counts((size_t)c->world);
   HIP_TRY(hipMemcpyAsync(counts.data(), all, counts.size() * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));

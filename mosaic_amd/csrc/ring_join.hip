@@ -162,7 +162,23 @@ __global__ __launch_bounds__(256) void rj_sort_kernel(const int64_t* __restrict_
         R[q] = tr;
       }
   }
-  kept[i] = want + (nul ? nul[i] : 0);
+  if (kept) kept[i] = want + (nul ? nul[i] : 0);
+}
+
+// kept[i]: the landmark's output rows -- its pairs cut to `keep` (0: all), plus its null row
+__global__ __launch_bounds__(256) void rj_kept_kernel(const int64_t* __restrict__ off, int64_t n, int64_t keep,
+                                                      const int8_t* __restrict__ nul, int64_t* __restrict__ kept) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t m = off[i + 1] - off[i];
+  kept[i] = (keep > 0 && keep < m ? keep : m) + (nul ? nul[i] : 0);
+}
+
+// out[i] = off[i] - base (a batch's segment offsets relative to its first pair)
+__global__ __launch_bounds__(256) void rj_rebase_kernel(const int64_t* __restrict__ off, int64_t n, int64_t base,
+                                                        int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = off[i] - base;
 }
 
 // exclusive scan of v[0 .. n) into out[0 .. n] (out[n] = the total), three launches:
@@ -303,28 +319,53 @@ static int32_t cells_join(mgpu_ctx* ctx, hipStream_t s, Scratch& S, int32_t inde
   hipLaunchKernelGGL(rj_pairs_kernel<false>, dim3(grid_of(n_left)), dim3(256), 0, s, a, cnt, nullptr, nullptr, nullptr,
                      nul);
   scan(cnt, off);
-  int64_t total = 0;
-  RJ_TRY(hipMemcpyAsync(&total, off + n_left, 8, hipMemcpyDeviceToHost, s));
-  RJ_TRY(hipStreamSynchronize(s));
-  int64_t* pr;
-  double* pd;
-  RJ_TRY(S.get(&pr, total));
-  RJ_TRY(S.get(&pd, total));
-  hipLaunchKernelGGL(rj_pairs_kernel<true>, dim3(grid_of(n_left)), dim3(256), 0, s, a, nullptr, off, pr, pd, nullptr);
+  // the kept counts follow from the counts (the cut and the null row), so the output
+  // offsets are known before any pair is written
   int64_t *kept, *koff;
   RJ_TRY(S.get(&kept, n_left));
   RJ_TRY(S.get(&koff, n_left + 1));
   const int8_t* nul_out = (flags & MGPU_RING_LEFT_OUTER) ? nul : nullptr;
-  hipLaunchKernelGGL(rj_sort_kernel, dim3(grid_of(n_left)), dim3(256), 0, s, off, n_left, (int64_t)max_per_left, pr, pd,
-                     kept, nul_out);
+  hipLaunchKernelGGL(rj_kept_kernel, dim3(grid_of(n_left)), dim3(256), 0, s, off, n_left, (int64_t)max_per_left, nul_out,
+                     kept);
   scan(kept, koff);
+  std::vector<int64_t> hoff(n_left + 1);
   int64_t n_out = 0;
+  RJ_TRY(hipMemcpyAsync(hoff.data(), off, (n_left + 1) * 8, hipMemcpyDeviceToHost, s));
   RJ_TRY(hipMemcpyAsync(&n_out, koff + n_left, 8, hipMemcpyDeviceToHost, s));
-  if (capacity > 0)
-    hipLaunchKernelGGL(rj_copy_kernel, dim3(grid_of(n_left)), dim3(256), 0, s, off, koff, n_left, pr, pd, left_id_base,
-                       capacity, out_left, out_right, out_dist, nul_out);
-  RJ_TRY(hipGetLastError());
   RJ_TRY(hipStreamSynchronize(s));
+  // the pairs, sorted and cut per landmark, in batches of landmarks holding at most
+  // kBatchPairs candidate pairs (a landmark with more is a batch of its own), so the
+  // scratch stays bounded whatever the density
+  const int64_t kBatchPairs = ctx->opt.ring_batch;  // (option ring_batch)
+  const int64_t biggest = [&] {
+    int64_t m = 0;
+    for (int64_t i = 0; i < n_left; i++) m = std::max(m, hoff[i + 1] - hoff[i]);
+    return m;
+  }();
+  int64_t *pr, *roff;
+  double* pd;
+  RJ_TRY(S.get(&roff, n_left + 1));
+  RJ_TRY(S.get(&pr, std::min(hoff[n_left], std::max(kBatchPairs, biggest))));
+  RJ_TRY(S.get(&pd, std::min(hoff[n_left], std::max(kBatchPairs, biggest))));
+  for (int64_t b0 = 0; b0 < n_left;) {
+    int64_t b1 = b0 + 1;
+    while (b1 < n_left && hoff[b1 + 1] - hoff[b0] <= std::max(kBatchPairs, biggest)) b1++;
+    RjArgs ab = a;
+    ab.lx = a.lx + b0, ab.ly = a.ly + b0, ab.ring_off = a.ring_off + b0, ab.n_left = b1 - b0;
+    // (offsets relative to the batch: the batch's segment starts at pr[0])
+    hipLaunchKernelGGL(rj_rebase_kernel, dim3(grid_of(b1 - b0 + 1)), dim3(256), 0, s, off + b0, b1 - b0 + 1,
+                       hoff[b0], roff);
+    hipLaunchKernelGGL(rj_pairs_kernel<true>, dim3(grid_of(b1 - b0)), dim3(256), 0, s, ab, nullptr, roff, pr, pd,
+                       nullptr);
+    hipLaunchKernelGGL(rj_sort_kernel, dim3(grid_of(b1 - b0)), dim3(256), 0, s, roff, b1 - b0, (int64_t)max_per_left,
+                       pr, pd, nullptr, nullptr);
+    if (capacity > 0)
+      hipLaunchKernelGGL(rj_copy_kernel, dim3(grid_of(b1 - b0)), dim3(256), 0, s, roff, koff + b0, b1 - b0, pr, pd,
+                         left_id_base + b0, capacity, out_left, out_right, out_dist, nul_out ? nul_out + b0 : nullptr);
+    RJ_TRY(hipGetLastError());
+    RJ_TRY(hipStreamSynchronize(s));
+    b0 = b1;
+  }
   if (out_n) *out_n = n_out;
   if (n_out > capacity)
     return mgpu::set_error(MGPU_E_CAPACITY, "ring_join: %lld pairs, capacity %lld", (long long)n_out, (long long)capacity);
@@ -362,8 +403,9 @@ extern "C" int32_t mgpu_ring_join_ex(mgpu_ctx* ctx, int32_t index_system, int32_
   // their ring cells (IndexSystem.kRing / kLoop through mgpu_grid_kring)
   int64_t *ring_off, *ring;
   RJ_TRY(S.get(&ring_off, n_left + 1));
+  // (first guess bounded at 2^24 cells; mgpu_grid_kring reports the exact total when short)
   const int64_t per = loop_only ? (k == 0 ? 1 : 6 * (int64_t)k) : 3 * (int64_t)k * (k + 1) + 1;
-  int64_t ring_cap = n_left * per + 1024, ring_total = 0;
+  int64_t ring_cap = std::min<int64_t>(n_left * per + 1024, (int64_t)1 << 24), ring_total = 0;
   RJ_TRY(S.get(&ring, ring_cap));
   int32_t st = mgpu_grid_kring(ctx, index_system, lc, n_left, k, loop_only, ring, ring_cap, ring_off, &ring_total, stream);
   if (st == MGPU_E_CAPACITY) {

@@ -940,3 +940,20 @@ def test_ring_join_final_equals_oracle(gpu, isys_name, res):
     assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
     assert np.array_equal(gd.view(np.int64), od.view(np.int64))
     assert not np.isin(np.arange(3, 6), gl).any()  # the NaN / 0 / negative radius landmarks 0-2
+
+
+def test_ring_join_batched_equals_oracle(gpu):
+    """Landmarks processed in batches of bounded candidate pairs (option ring_batch, here
+    500 pairs: dozens of batches, some landmarks alone in theirs) give the same rows as
+    the oracle, with the cut, the threshold and the left_outer null rows."""
+    lx, ly = nyc_points(3000, 71)
+    rx, ry = nyc_points(40000, 72)
+    rx[:300], ry[:300] = lx[:300], ly[:300]
+    with M.default_context(gpu).options(ring_batch=500):
+        got = M.grid_ring_join(T(lx, gpu), T(ly, gpu), T(rx, gpu), T(ry, gpu), 9, 1, max_per_left=4,
+                               max_distance=0.004, left_outer=True)
+    gl, gr, gd = (v.cpu().numpy() for v in got)
+    ol, orr, od = O.ring_join(0, 9, 1, lx, ly, rx, ry, max_per_left=4, max_distance=0.004, left_outer=True)
+    assert len(ol) > 3000
+    assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
+    assert np.array_equal(gd.view(np.int64), od.view(np.int64))

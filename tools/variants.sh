@@ -10,7 +10,12 @@ pids=()
 names=()
 while [ $# -ge 2 ]; do
   d=../../build/ab/$1; mkdir -p $d
-  if [ "${2#host:}" != "$2" ]; then  # NAME "host:-D..." rebuilds capi.cpp (the chip-table builder) instead
+  if [ "${2#all:}" != "$2" ]; then  # NAME "all:-D..." rebuilds both kernels.hip and capi.cpp with the flags
+    (/opt/rocm/bin/hipcc $CXXFLAGS ${2#all:} -c capi.cpp -o $d/capi.o 2> $d/build.log &&
+     /opt/rocm/bin/hipcc --offload-arch=gfx950 $CXXFLAGS ${2#all:} -c kernels.hip -o $d/kernels.o 2>> $d/build.log &&
+     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $d/libmosaic_gpu.so $d/kernels.o $d/capi.o comm.o tessellate.o \
+       bng_format.o h3_glibc.o ring_join.o geom_kernels.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib && rm -f $d/capi.o $d/kernels.o) &
+  elif [ "${2#host:}" != "$2" ]; then  # NAME "host:-D..." rebuilds capi.cpp (the chip-table builder) instead
     (/opt/rocm/bin/hipcc $CXXFLAGS ${2#host:} -c capi.cpp -o $d/capi.o 2> $d/build.log &&
      /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $d/libmosaic_gpu.so kernels.o $d/capi.o comm.o tessellate.o \
        bng_format.o h3_glibc.o ring_join.o geom_kernels.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib && rm -f $d/capi.o) &
