@@ -2808,7 +2808,6 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     for (int f = 0; f < 20; f++) grid_entries = std::max<uint64_t>(grid_entries, (uint64_t)cv.dense[f].base + (uint64_t)cv.dense[f].w * cv.dense[f].h);
     const bool keyed = is == MGPU_H3 && cv.probe_mode == mgpu::kProbeDense && o.bin_keys && grid_entries < (1ull << 30);
     const size_t o_key = keyed ? carve((size_t)n * 4) : 0;
-    const size_t o_lb = carve((size_t)K * 8);
     if (off > ctx->bin_bytes) {
       if (ctx->bin_ws) HIP_TRY(hipFree(ctx->bin_ws));
       ctx->bin_ws = nullptr;
@@ -2827,7 +2826,6 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
     ba.cnt = (uint32_t*)(bb + o_cnt);
     ba.gsum = (uint32_t*)(bb + o_gs);
     ba.key = keyed ? (uint32_t*)(bb + o_key) : nullptr;
-    ba.lb = (uint64_t*)(bb + o_lb);
     mgpu::JoinArgs j = a;
     j.bin_key = ba.key;
     j.x = ba.bx;

@@ -137,7 +137,6 @@ struct BinArgs {
   int32_t nbx, nby;                 // nbx * nby <= bin_max()
   int32_t xcd_runs;                 // deal each XCD a contiguous run of binned tiles (option bin_xcd)
   uint32_t* key;                    // [n] H3, dense grid: the binned slot's grid key (JoinArgs.bin_key), or null
-  uint64_t* lb;                     // [bin chunks] look-back words of the fused gather + emit (zeroed by its launcher)
 };
 int64_t bin_chunk();
 int64_t bin_chunks(int64_t n);

@@ -2534,129 +2534,6 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   }
 }
 
-// bin_gather_kernel + tile_scan_kernel + bin_emit_kernel in one pass: a resident grid walks
-// the input chunks (chunk k = block + i * grid), places the chunk's answers in input order
-// in LDS as bin_gather_kernel does, counts its pairs, and takes its output offset by a
-// decoupled look-back over the chunks before it (lb[k] = state << 62 | value: 1 = the
-// chunk's own count, 2 = its inclusive prefix) -- every chunk before k is held by a
-// resident workgroup, so the wait ends -- then writes the pairs, staged in LDS.  The
-// answers never round-trip through HBM in input order (8 + 8 B per point less).
-#ifndef MGPU_BIN_FUSED_EMIT
-#define MGPU_BIN_FUSED_EMIT 1
-#endif
-constexpr uint64_t kLbValue = (1ull << 62) - 1;
-__device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-constexpr int kGeItems = kBinChunk / kBinBlock;  // input points per thread (8)
-constexpr int kGeWin = kBinChunk;                // pairs staged at a time (the answers' LDS, reused)
-__global__ __launch_bounds__(kBinBlock) void bin_gather_emit_kernel(BinArgs b, uint64_t* lb, int64_t n_chunks) {
-  const SplitArgs& sa = b.s;
-  const ChipTableView& t = sa.j.chips;
-  __shared__ uint64_t s_v[kBinChunk];  // the chunk's answers in input order; then the staged pairs
-  __shared__ uint32_t s_off[kBinMax];
-  __shared__ uint32_t s_loc[kBinMax];
-  __shared__ uint32_t s_w[kBinBlock / 64];
-  __shared__ uint64_t s_base;
-  uint32_t* s_poly = (uint32_t*)s_v;                  // [kGeWin]
-  uint16_t* s_pt = (uint16_t*)(s_poly + kGeWin);      // [kGeWin]
-  const int nb = b.nbx * b.nby;
-  const int64_t n = sa.j.n;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int64_t k = blockIdx.x; k < n_chunks; k += gridDim.x) {
-    const int64_t c0 = k * kBinChunk;
-    bin_runs(b, k, s_off, s_loc, s_w);
-    const int64_t left = n - c0;
-    const uint32_t m = left < kBinChunk ? (uint32_t)left : (uint32_t)kBinChunk;
-    for (uint32_t lp = threadIdx.x; lp < m; lp += kBinBlock) {
-      const uint32_t bi = bin_at(s_loc, nb, lp);
-      const uint32_t sl = s_off[bi] + (lp - s_loc[bi]);
-      s_v[b.perm[sl] - (uint32_t)c0] = sa.j.mixed_res[sl];
-    }
-    __syncthreads();
-    // thread i: input points l0 .. l0 + 7 of the chunk
-    const uint32_t l0 = threadIdx.x * kGeItems;
-    uint64_t v[kGeItems];
-    uint32_t npair = 0;
-#pragma unroll
-    for (int q = 0; q < kGeItems; q++) {
-      v[q] = l0 + q < m ? s_v[l0 + q] : 0ull;
-      npair += __popc((uint32_t)(v[q] >> 32));
-    }
-    const uint32_t incl = wave_incl_scan(npair);
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();  // (also: every s_v read above is done before the staging reuses it)
-    uint32_t before = 0, total = 0;
-#pragma unroll
-    for (int w = 0; w < kBinBlock / 64; w++) {
-      before += w < wave ? s_w[w] : 0u;
-      total += s_w[w];
-    }
-    const uint32_t off0 = before + incl - npair;
-    if (threadIdx.x == 0) {
-      // the look-back: publish the count, sum the counts / the first prefix before it
-      lb_store(&lb[k], (1ull << 62) | total);
-      uint64_t excl = 0;
-      for (int64_t j = k - 1; j >= 0; j--) {
-        uint64_t w;
-        while (((w = lb_load(&lb[j])) >> 62) == 0) __builtin_amdgcn_s_sleep(1);
-        excl += w & kLbValue;
-        if ((w >> 62) == 2) break;
-      }
-      lb_store(&lb[k], (2ull << 62) | (excl + total));
-      s_base = excl;
-      sa.chunk_off[k] = excl;
-      sa.chunk_pairs[k] = total;
-      if (k == n_chunks - 1) sa.j.counters[0] = excl + total;
-    }
-    __syncthreads();
-    const uint64_t base = s_base;
-    for (uint32_t w0 = 0; w0 < total; w0 += kGeWin) {
-      if (off0 < w0 + kGeWin && off0 + npair > w0) {
-        uint32_t q = off0;
-#pragma unroll
-        for (int i = 0; i < kGeItems; i++) {
-          const uint32_t first = (uint32_t)v[i], msk = (uint32_t)(v[i] >> 32);
-          if (msk == 1u) {  // one match: first is the polygon id (JoinArgs.poly_answers)
-            if (q >= w0 && q < w0 + kGeWin) {
-              s_poly[emit_swz(q - w0)] = first;
-              s_pt[emit_swz(q - w0)] = (uint16_t)(l0 + i);
-            }
-            q++;
-            continue;
-          }
-          for (uint32_t mm = msk; mm; mm &= mm - 1, q++)
-            if (q >= w0 && q < w0 + kGeWin) {
-              s_poly[emit_swz(q - w0)] = (uint32_t)t.chip_poly[first + __builtin_ctz(mm)];
-              s_pt[emit_swz(q - w0)] = (uint16_t)(l0 + i);
-            }
-        }
-      }
-      __syncthreads();
-      const uint32_t cnt = total - w0 < (uint32_t)kGeWin ? total - w0 : (uint32_t)kGeWin;
-      for (uint32_t i = threadIdx.x; i < cnt; i += kBinBlock) {
-        const uint64_t q = base + w0 + i;
-        if ((int64_t)q >= sa.capacity) break;
-        const int64_t p = c0 + s_pt[emit_swz(i)];
-        sa.out_point[q] = sa.point_id ? sa.point_id[p] : sa.id_base + p;
-        sa.out_poly[q] = (int32_t)s_poly[emit_swz(i)];
-      }
-      __syncthreads();
-    }
-  }
-  // the candidates statistic (the join's per-chunk counts): one workgroup sums them
-  if (blockIdx.x == 0) {
-    const int64_t nbc = (n + kChunk - 1) / kChunk;
-    unsigned long long cand = 0;
-    for (int64_t i = threadIdx.x; i < nbc; i += kBinBlock) cand += sa.j.group_cand[i];
-    cand = wave_sum_u64(cand);
-    if (lane == 0 && cand) atomicAdd(&sa.j.counters[3], cand);
-  }
-}
-
 __global__ __launch_bounds__(256) void scatter_i64_kernel(const int64_t* __restrict__ pos, const int64_t* __restrict__ val,
                                                           int64_t n, int64_t* __restrict__ out) {
   for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) out[pos[k]] = val[k];
@@ -2931,14 +2808,11 @@ int32_t bin_max() { return kBinMax; }
 
 // the binned answers -> ordered pairs: fused (one resident-grid pass with a look-back) or
 // gather, scan, emit
+// (A/B r5, profiles/r5/ab_c3_fused_output.txt: the three in one resident-grid pass with
+// a decoupled look-back over the chunks took 11.1 ms instead of 1.0 on C3 -- a chunk's
+// look-back walks back through the whole grid's round one dependent load at a time)
 static void launch_bin_output(const BinArgs& a, hipStream_t s) {
   const int64_t n = a.s.j.n, K = bin_chunks(n), nc = split_chunks(n);
-  if (MGPU_BIN_FUSED_EMIT && a.lb) {
-    hipMemsetAsync(a.lb, 0, (size_t)K * 8, s);
-    const int64_t grid = std::min<int64_t>(K, (int64_t)resident_blocks((const void*)bin_gather_emit_kernel, kBinBlock, 0));
-    hipLaunchKernelGGL(bin_gather_emit_kernel, dim3((unsigned)std::max<int64_t>(grid, 1)), dim3(kBinBlock), 0, s, a, a.lb, K);
-    return;
-  }
   hipLaunchKernelGGL(bin_gather_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.s.chunk_pairs, a.s.j.group_cand, nc,
                      a.s.chunk_off, a.s.j.counters);
@@ -2979,10 +2853,7 @@ hipError_t launch_binned(int is, const BinArgs& a, hipStream_t s, hipEvent_t aft
 // only the ordered output of a binned join already computed (mgpu_pip_join_fetch)
 hipError_t launch_bin_emit(const BinArgs& a, hipStream_t s) {
   if (a.s.j.n <= 0) return hipSuccess;
-  if (MGPU_BIN_FUSED_EMIT && a.lb)  // (the answers were never written in input order: the fused pass again)
-    launch_bin_output(a, s);
-  else
-    hipLaunchKernelGGL(bin_emit_kernel, dim3((unsigned)split_chunks(a.s.j.n)), dim3(kClsBlock), 0, s, a);
+  hipLaunchKernelGGL(bin_emit_kernel, dim3((unsigned)split_chunks(a.s.j.n)), dim3(kClsBlock), 0, s, a);
   return hipGetLastError();
 }
 
