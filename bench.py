@@ -449,7 +449,7 @@ def main():
     if os.path.exists(vprof):
         try:
             v = json.load(open(vprof)).get("%s_r%d" % (a.config, a.res))
-            if v and v["kernel"].split("<")[0] == kernel.split("<")[0]:
+            if v and v["kernel"].split("<")[0] == kernel.split("<")[0] and v.get("key") == traffic_key(a.option, info):
                 valu = v["valu_insts_per_point"] * n * 2.0 / (1024 * 2.4e9 * stream_ms * 1e-3)
                 out["roofline"]["valu_issue_frac"] = valu
                 out["roofline"]["salu_insts_per_point"] = v["salu_insts_per_point"]

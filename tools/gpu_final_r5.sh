@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-4 final lines: bench.py per config (CPU baseline and PCIe-inclusive included) and a
+# Round-5 final lines: bench.py per config (CPU baseline and PCIe-inclusive included) and a
 # rocprofv3 kernel trace of the same bench command: gpurun_out/final_TAG_<cfg>.json, kt_TAG_<cfg>/
 set -o pipefail
-TAG=${1:-f4}; CFGS=${2:-"c2 c3 c4 c5"}
+TAG=${1:-f5}; CFGS=${2:-"c2 c3 c4 c5"}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for c in $CFGS; do

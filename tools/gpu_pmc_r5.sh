@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-4 counters: per config, the SQ instruction / wave-cycle passes (gpu_pmc3.sh passes 1 2)
+# Round-5 counters: per config, the SQ instruction / wave-cycle passes (gpu_pmc3.sh passes 1 2)
 # and the FETCH_SIZE / WRITE_SIZE traffic passes (gpu_traffic.sh):
-#   tools/gpu_pmc_r4.sh TAG "CFG[:RES] ..."      e.g. "c2 c4:3 c4"
+#   tools/gpu_pmc_r5.sh TAG "CFG[:RES] ..."      e.g. "c2 c4:3 c4"
 set -o pipefail
 TAG=$1; CFGS=$2
 for cr in $CFGS; do
