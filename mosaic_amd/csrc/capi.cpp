@@ -1112,7 +1112,9 @@ uint64_t h3_rect_answer(const H3RasterCtx& X, double xa, double ya, double xb, d
   uint64_t cls = 0;
   for (int k = 0; k < 7; k++) {
     const int64_t a = a0 + da[k], b = b0 + db[k];
-    if (!hex_meets_quad(a, b, QA, HF, d_hex)) continue;
+    // (k = 0, h0: the cell of corner q[0], which lies in its hexagon -- the separating
+    // axis test cannot part them by the margin d_hex >= 1e-9, far above q[0]'s rounding)
+    if (k > 0 && !hex_meets_quad(a, b, QA, HF, d_hex)) continue;
     const uint64_t ua = (uint64_t)(a - D.a0), ub = (uint64_t)(b - D.b0);
     const uint64_t e = (ua < D.w && ub < D.h) ? X.grid[D.base + ub * D.w + ua] : 0;
     const int64_t m = pixel_answer(X.hv, e, xa - mux, ya - muy, xb + mux, yb + muy, pe);

@@ -1046,7 +1046,10 @@ __global__ __launch_bounds__(kBlock) void pip_fix_kernel(JoinArgs a) {
 // point once (16 B read, one pixel load, a 2- or 4-byte code written), the few mixed
 // points go through join_tile's phases gathered into full tiles, and split_emit_kernel
 // writes the ordered pairs from the codes.
-constexpr int kClsBlock = 256;
+#ifndef MGPU_CLS_BLOCK
+#define MGPU_CLS_BLOCK 256  // threads per chunk in the emit kernels (16 points each)
+#endif
+constexpr int kClsBlock = MGPU_CLS_BLOCK;
 constexpr int kClsItems = kChunk / kClsBlock;  // points per thread
 static_assert(kClsItems * (kClsBlock / 64) == 64, "one wave scans a chunk's ballots");
 constexpr uint32_t kCodeMixed32 = 0xFFFFFFFFu;
@@ -2417,7 +2420,7 @@ __global__ __launch_bounds__(kBlock) MGPU_JOIN_ATTR void pip_binned_kernel(JoinA
 // per run) and placed by perm[] into LDS, then written out in input order; the pairs of
 // each split_chunk() of input points are counted on the way (the emit's offsets).
 constexpr int kBinEmitItems = kChunk / kClsBlock;
-static_assert(kBinEmitItems == 16, "four 16-byte answer loads per thread");
+static_assert(kBinEmitItems % 2 == 0, "16-byte answer loads per thread");
 static_assert(kBinChunk % kChunk == 0 && kBinChunk / kChunk <= kBinBlock / 64, "emit chunks inside a bin chunk");
 __global__ __launch_bounds__(kBinBlock) void bin_gather_kernel(BinArgs b) {
   __shared__ uint64_t s_v[kBinChunk];
@@ -2825,10 +2828,13 @@ static void launch_binned_t(const BinArgs& a, hipStream_t s, hipEvent_t after_bi
   hipLaunchKernelGGL(bin_hist_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
   hipLaunchKernelGGL(bin_colscan_kernel, dim3((unsigned)((nb + 255) / 256), (unsigned)G), dim3(256), 0, s, a, K);
   hipLaunchKernelGGL(bin_base_kernel, dim3(1), dim3(kBaseBlock), 0, s, a, G);
-  if (IS == MGPU_H3 && a.key)
+  if (IS == MGPU_H3 && a.key) {
     hipLaunchKernelGGL(bin_scatter_kernel<true>, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
-  else
+  } else {
+    // (a resident grid prefetching its next chunk's points behind the current one's
+    // ranking measured 1.80 vs 1.75 ms on C3: profiles/r5/ab_c3_scatter_pf.txt)
     hipLaunchKernelGGL(bin_scatter_kernel<false>, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
+  }
   if (after_bin) hipEventRecord(after_bin, s);
   const int64_t nc = split_chunks(n), tiles = nc * kChunkTiles;
   const uint32_t per = a.xcd_runs ? (uint32_t)((tiles + 7) / 8) : 0u;
