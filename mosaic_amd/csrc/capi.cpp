@@ -20,6 +20,9 @@
 #include <limits>
 #include <string>
 #include <map>
+#include <functional>
+#include <tuple>
+#include <thread>
 #include <vector>
 
 #include "../../include/mosaic_arrow.h"
@@ -440,9 +443,6 @@ void build_strips(int64_t n_chips, std::vector<uint8_t>& cflags, const std::vect
     // (per chip: each edge's strip range, a count per strip, then the edges placed by a
     // counting sort -- no per-strip vectors)
     std::vector<uint32_t> cnt, pos;
-    std::vector<int> sa_of, sb_of;
-    std::vector<double> rec;
-    std::vector<uint8_t> rring;
     for (int64_t kc = kb; kc < ke; kc++) {
       Strips& L = cs[kc];
       for (int64_t c = kc * G; c < std::min(n_chips, (kc + 1) * G); c++) {
@@ -468,22 +468,15 @@ void build_strips(int64_t n_chips, std::vector<uint8_t>& cflags, const std::vect
         const double inv_h = (H > 0) ? (double)S / H : 0.0;
         st.chip_sy[2 * c] = y0;
         st.chip_sy[2 * c + 1] = inv_h;
+        // (two passes over the chip's edges: counts per strip, then each edge placed in
+        // every strip it spans -- in ring order within each strip)
         cnt.assign(S + 1, 0);
-        rec.clear();
-        rring.clear();
-        sa_of.clear();
-        sb_of.clear();
         for (uint32_t r = r0; r < r1; r++) {
           const uint32_t vb = geo.ring_vtx[r], ve = geo.ring_vtx[r + 1];
           for (uint32_t i = vb + 1; i < ve; i++) {
-            const double p1x = geo.vtx[2 * i], p1y = geo.vtx[2 * i + 1];
-            const double p2x = geo.vtx[2 * i - 2], p2y = geo.vtx[2 * i - 1];
-            rec.insert(rec.end(), {p1x, p1y, p2x, p2y});
-            rring.push_back((uint8_t)(r - r0));
+            const double p1y = geo.vtx[2 * i + 1], p2y = geo.vtx[2 * i - 1];
             const int sa = mgpu::strip_of(std::min(p1y, p2y), y0, inv_h, S);
             const int sb = mgpu::strip_of(std::max(p1y, p2y), y0, inv_h, S);
-            sa_of.push_back(sa);
-            sb_of.push_back(sb);
             for (int q = sa; q <= sb; q++) cnt[q + 1]++;
           }
         }
@@ -492,13 +485,21 @@ void build_strips(int64_t n_chips, std::vector<uint8_t>& cflags, const std::vect
         L.edges.resize(4 * (e_base + cnt[S]));
         L.edge_ring.resize(e_base + cnt[S]);
         pos.assign(cnt.begin(), cnt.end() - 1);
-        // (edges in ring order within each strip, as the per-strip lists had them)
-        for (size_t e = 0; e < rring.size(); e++)
-          for (int q = sa_of[e]; q <= sb_of[e]; q++) {
-            const size_t d = e_base + pos[q]++;
-            std::copy(rec.begin() + 4 * e, rec.begin() + 4 * e + 4, L.edges.begin() + 4 * d);
-            L.edge_ring[d] = rring[e];
+        for (uint32_t r = r0; r < r1; r++) {
+          const uint32_t vb = geo.ring_vtx[r], ve = geo.ring_vtx[r + 1];
+          for (uint32_t i = vb + 1; i < ve; i++) {
+            const double p1x = geo.vtx[2 * i], p1y = geo.vtx[2 * i + 1];
+            const double p2x = geo.vtx[2 * i - 2], p2y = geo.vtx[2 * i - 1];
+            const int sa = mgpu::strip_of(std::min(p1y, p2y), y0, inv_h, S);
+            const int sb = mgpu::strip_of(std::max(p1y, p2y), y0, inv_h, S);
+            for (int q = sa; q <= sb; q++) {
+              const size_t d = e_base + pos[q]++;
+              double* o = L.edges.data() + 4 * d;
+              o[0] = p1x, o[1] = p1y, o[2] = p2x, o[3] = p2y;
+              L.edge_ring[d] = (uint8_t)(r - r0);
+            }
           }
+        }
         for (int q = 0; q < S; q++) L.strip_edge.push_back((uint32_t)(e_base + cnt[q + 1]));
       }
     }
@@ -557,6 +558,12 @@ void build_grid(const mgpu::ChipTableView& hv, uint32_t c, const mgpu::wkb::Flat
   const double ulp = std::nextafter(mag, INFINITY) - mag;
   const double mu_x = 1e-6 + 64 * ulp * h.sx, mu_y = 1e-6 + 64 * ulp * h.sy;
   const uint32_t r0 = hv.part_ring[hv.chip_part[c]], r1 = hv.part_ring[hv.chip_part[c + 1]];
+  // the widened cells' bounds, once per chip (the same expressions as per cell)
+  double bx0[kGrid], bx1[kGrid], by0[kGrid], by1[kGrid];
+  for (int g = 0; g < kGrid; g++) {
+    bx0[g] = e0 + (g - mu_x) / h.sx, bx1[g] = e0 + (g + 1 + mu_x) / h.sx;
+    by0[g] = e1 + (g - mu_y) / h.sy, by1[g] = e1 + (g + 1 + mu_y) / h.sy;
+  }
   for (uint32_t r = r0; r < r1; r++) {
     for (uint32_t i = geo.ring_vtx[r] + 1; i < geo.ring_vtx[r + 1]; i++) {
       const double ax = geo.vtx[2 * i - 2], ay = geo.vtx[2 * i - 1], bx = geo.vtx[2 * i], by = geo.vtx[2 * i + 1];
@@ -564,15 +571,28 @@ void build_grid(const mgpu::ChipTableView& hv, uint32_t c, const mgpu::wkb::Flat
       int gx0 = (int)std::floor((std::min(ax, bx) - e0) * h.sx) - 1, gx1 = (int)std::floor((std::max(ax, bx) - e0) * h.sx) + 1;
       int gy0 = (int)std::floor((std::min(ay, by) - e1) * h.sy) - 1, gy1 = (int)std::floor((std::max(ay, by) - e1) * h.sy) + 1;
       gx0 = std::max(gx0, 0), gy0 = std::max(gy0, 0), gx1 = std::min(gx1, kGrid - 1), gy1 = std::min(gy1, kGrid - 1);
-      for (int gy = gy0; gy <= gy1; gy++)
+      // seg_hits_box per cell (cell gx spans [e0 + gx / sx, e0 + (gx + 1) / sx]; the
+      // clamped last cell also takes everything up to the envelope edge), its terms
+      // dy (cx - ax) per column and dx (cy - ay) per row computed once: the same roundings
+      const double dx = bx - ax, dy = by - ay;
+      const double lx = std::min(ax, bx), hx = std::max(ax, bx), ly = std::min(ay, by), hy = std::max(ay, by);
+      double tx0[kGrid], tx1[kGrid];
+      bool cok[kGrid];
+      for (int gx = gx0; gx <= gx1; gx++) {
+        cok[gx] = !(hx < bx0[gx] || lx > bx1[gx]);
+        tx0[gx] = dy * (bx0[gx] - ax);
+        tx1[gx] = dy * (bx1[gx] - ax);
+      }
+      for (int gy = gy0; gy <= gy1; gy++) {
+        if (hy < by0[gy] || ly > by1[gy]) continue;
+        const double u0 = dx * (by0[gy] - ay), u1 = dx * (by1[gy] - ay);
         for (int gx = gx0; gx <= gx1; gx++) {
-          if (st[gy][gx] == kCellMixed) continue;
-          // cell gx spans [e0 + gx / sx, e0 + (gx + 1) / sx]; the clamped last cell
-          // also takes everything up to the envelope edge
-          const double x0 = e0 + (gx - mu_x) / h.sx, x1 = e0 + (gx + 1 + mu_x) / h.sx;
-          const double y0 = e1 + (gy - mu_y) / h.sy, y1 = e1 + (gy + 1 + mu_y) / h.sy;
-          if (seg_hits_box(ax, ay, bx, by, x0, y0, x1, y1)) st[gy][gx] = kCellMixed;
+          if (st[gy][gx] == kCellMixed || !cok[gx]) continue;
+          const double c0 = u0 - tx0[gx], c1 = u0 - tx1[gx], c2 = u1 - tx0[gx], c3 = u1 - tx1[gx];
+          const int pos = (c0 > 0) + (c1 > 0) + (c2 > 0) + (c3 > 0), neg = (c0 < 0) + (c1 < 0) + (c2 < 0) + (c3 < 0);
+          if (!(pos == 4 || neg == 4)) st[gy][gx] = kCellMixed;
         }
+      }
     }
   }
   // The rest: PointLocator's verdict at the cell centre, which lies at a positive distance
@@ -582,47 +602,47 @@ void build_grid(const mgpu::ChipTableView& hv, uint32_t c, const mgpu::wkb::Flat
   // per row for the row's 16 centres at once instead of a ring walk per centre.  A part
   // is entered when its shell's parity is odd and no hole's is; the chip when some part
   // is (a point on no boundary: the Mod-2 rule does not arise).
-  static thread_local std::vector<double> xs;
-  static thread_local std::vector<uint32_t> ring_first;  // per ring of the chip: its first crossing in xs
+  // (per row: each ring's parity as a 16-column mask -- a crossing at x flips the
+  // columns whose centre lies left of x, a prefix as the centres ascend)
+  double cxp[kGrid];
+  for (int gx = 0; gx < kGrid; gx++) cxp[gx] = e0 + (gx + 0.5) / h.sx;
+  uint32_t par[kStripRings];
+  const uint32_t p0 = hv.chip_part[c], p1 = hv.chip_part[c + 1];
   for (int gy = 0; gy < kGrid; gy++) {
     uint32_t row = 0;
     bool any = false;
     for (int gx = 0; gx < kGrid && !any; gx++) any = st[gy][gx] != kCellMixed;
     if (any) {
       const double cyp = e1 + (gy + 0.5) / h.sy;
-      xs.clear();
-      ring_first.clear();
       for (uint32_t r = r0; r < r1; r++) {
-        ring_first.push_back((uint32_t)xs.size());
+        uint32_t m = 0;
         for (uint32_t i = geo.ring_vtx[r] + 1; i < geo.ring_vtx[r + 1]; i++) {
           const double p1x = geo.vtx[2 * i], p1y = geo.vtx[2 * i + 1], p2x = geo.vtx[2 * i - 2], p2y = geo.vtx[2 * i - 1];
-          if (((p1y > cyp) && (p2y <= cyp)) || ((p2y > cyp) && (p1y <= cyp)))
-            xs.push_back(p1x + (cyp - p1y) * (p2x - p1x) / (p2y - p1y));
+          if (((p1y > cyp) && (p2y <= cyp)) || ((p2y > cyp) && (p1y <= cyp))) {
+            const double x = p1x + (cyp - p1y) * (p2x - p1x) / (p2y - p1y);
+            int k = 0;
+            while (k < kGrid && cxp[k] < x) k++;
+            m ^= (1u << k) - 1u;
+          }
         }
-        std::sort(xs.begin() + ring_first.back(), xs.end());
+        par[r - r0] = m;
       }
-      ring_first.push_back((uint32_t)xs.size());
+      uint32_t in = 0;
+      for (uint32_t p = p0; p < p1; p++) {
+        const uint32_t rb = hv.part_ring[p], re = hv.part_ring[p + 1];
+        if (re == rb || geo.ring_vtx[rb + 1] == geo.ring_vtx[rb]) continue;
+        uint32_t holes = 0;
+        for (uint32_t q = rb + 1; q < re; q++) holes |= par[q - r0];
+        in |= par[rb - r0] & ~holes;
+      }
       for (int gx = 0; gx < kGrid; gx++) {
         uint32_t v = st[gy][gx];
         if (v != kCellMixed) {
-          const double cxp = e0 + (gx + 0.5) / h.sx;
-          auto odd = [&](uint32_t r) {  // ring r (index within the chip): crossings right of cxp
-            const auto b = xs.begin() + ring_first[r], e = xs.begin() + ring_first[r + 1];
-            return ((e - std::upper_bound(b, e, cxp)) & 1) != 0;
-          };
-          bool in = false;
-          for (uint32_t p = hv.chip_part[c]; p < hv.chip_part[c + 1] && !in; p++) {
-            const uint32_t rb = hv.part_ring[p], re = hv.part_ring[p + 1];
-            if (re == rb || geo.ring_vtx[rb + 1] == geo.ring_vtx[rb] || !odd(rb - r0)) continue;
-            bool hole = false;
-            for (uint32_t q = rb + 1; q < re && !hole; q++) hole = odd(q - r0);
-            in = !hole;
-          }
-          v = in ? kCellIn : kCellOut;
+          v = ((in >> gx) & 1u) ? kCellIn : kCellOut;
 #ifdef MGPU_GRID_VERIFY
-          const int loc = pip::chip_locate(hv, c, cxp, cyp);
-          if (loc != (in ? pip::kInterior : pip::kExterior)) {
-            fprintf(stderr, "grid verify: chip %u cell (%d, %d) row parity %d, PointLocator %d\n", c, gx, gy, (int)in, loc);
+          const int loc = pip::chip_locate(hv, c, cxp[gx], cyp);
+          if (loc != (((in >> gx) & 1u) ? pip::kInterior : pip::kExterior)) {
+            fprintf(stderr, "grid verify: chip %u cell (%d, %d) row parity %d, PointLocator %d\n", c, gx, gy, (int)((in >> gx) & 1u), loc);
             abort();
           }
 #endif
@@ -1935,6 +1955,49 @@ struct HostBlob {
   }
 };
 
+// The blob as pieces of its byte stream: [off, off + bytes) from src, then `zero` zero
+// bytes.  build_blob hands them to a sink (the upload stages them straight into pinned
+// buffers: no whole host blob) or assembles the host blob from them.
+struct BlobPiece {
+  size_t off;
+  const uint8_t* src;
+  size_t bytes, zero;
+};
+using BlobSink = std::function<int32_t(size_t total, const std::vector<BlobPiece>& pieces)>;
+
+// The build's multi-GB intermediates freed on a detached thread (returning their pages
+// took ~0.5 s of C3's upload on the box): moved into one heap tuple that thread deletes.
+template <class... V>
+static void release_async(V&... v) {
+  auto* box = new std::tuple<std::decay_t<V>...>(std::move(v)...);
+  try {
+    std::thread([box] { delete box; }).detach();
+  } catch (...) {  // (no thread: free here)
+    delete box;
+  }
+}
+
+// bytes [off, off + n) of the stream the (ascending, contiguous) pieces make, to dst
+static void fill_from_pieces(const std::vector<BlobPiece>& pieces, uint8_t* dst, size_t off, size_t n) {
+  size_t q = std::upper_bound(pieces.begin(), pieces.end(), off,
+                              [](size_t o, const BlobPiece& p) { return o < p.off; }) - pieces.begin() - 1;
+  const size_t end = off + n;
+  for (size_t at = off; at < end; q++) {
+    const BlobPiece& p = pieces[q];
+    const size_t pe = p.off + p.bytes, ze = pe + p.zero;
+    if (at < pe) {
+      const size_t m = std::min(pe, end) - at;
+      memcpy(dst + (at - off), p.src + (at - p.off), m);
+      at += m;
+    }
+    if (at < end && at < ze) {
+      const size_t m = std::min(ze, end) - at;
+      memset(dst + (at - off), 0, m);
+      at += m;
+    }
+  }
+}
+
 // chips per chunk of the parallel blob-build phases (fixed: the result never depends on
 // the thread count or schedule)
 constexpr int64_t kBlobChunk = 1 << 14;
@@ -2015,7 +2078,8 @@ void mark_whole_cells(std::vector<mgpu::HashSlot>& cells, int res,
 // is by mgpu_chips_upload, evaluated in place by mgpu_test_chip_contains_host.
 static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* cell, const int32_t* polygon_id,
                           const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb,
-                          HostBlob& host, BlobHeader& hdr_out, const mgpu_build_opts& bo) {
+                          HostBlob& host, BlobHeader& hdr_out, const mgpu_build_opts& bo,
+                          const BlobSink* sink = nullptr) {
   if (index_system != MGPU_H3 && index_system != MGPU_BNG)
     return fail(MGPU_E_INVALID_ARG, "unknown index system %d (0 = H3, 1 = BNG)", index_system);
   if (n_chips < 0 || n_chips > (int64_t)std::numeric_limits<int32_t>::max())
@@ -2117,17 +2181,41 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   BLOB_MARK("parse");
 
   // cell hash over the distinct cells
+  // (chunks of sorted chips, each starting at a cell's first chip, in parallel)
   std::vector<mgpu::HashSlot> distinct;
-  for (int64_t s = 0; s < n_chips;) {
-    int64_t e = s;
-    uint64_t c = (uint64_t)cell[order[s]];
-    while (e < n_chips && (uint64_t)cell[order[e]] == c) e++;
-    if (e - s > 0xFFFF) return fail(MGPU_E_INVALID_ARG, "more than 65535 chips share cell %lld", (long long)c);
-    uint16_t core = 0;
-    for (int64_t j = 0; j < e - s && j < 16; j++)
-      if (cflags[s + j] & mgpu::kChipCore) core |= (uint16_t)(1u << j);
-    distinct.push_back(mgpu::HashSlot{c, (uint32_t)s, (uint16_t)(e - s), core});
-    s = e;
+  {
+    const int64_t NC = (n_chips + kBlobChunk - 1) / kBlobChunk;
+    std::vector<std::vector<mgpu::HashSlot>> cd(NC);
+    std::vector<int64_t> crowd(NC, -1);  // a cell of more than 65535 chips (its first sorted chip)
+    mgpu::parallel_for(NC, 1, [&](int64_t kb, int64_t ke, int) {
+      for (int64_t k = kb; k < ke; k++) {
+        int64_t s = k * kBlobChunk;
+        const int64_t lim = std::min(n_chips, (k + 1) * kBlobChunk);
+        while (s > 0 && s < lim && cell[order[s]] == cell[order[s - 1]]) s++;  // (the previous chunk's cell)
+        while (s < lim) {
+          int64_t e = s;
+          const uint64_t c = (uint64_t)cell[order[s]];
+          while (e < n_chips && (uint64_t)cell[order[e]] == c) e++;
+          if (e - s > 0xFFFF) {
+            crowd[k] = s;
+            break;
+          }
+          uint16_t core = 0;
+          for (int64_t j = 0; j < e - s && j < 16; j++)
+            if (cflags[s + j] & mgpu::kChipCore) core |= (uint16_t)(1u << j);
+          cd[k].push_back(mgpu::HashSlot{c, (uint32_t)s, (uint16_t)(e - s), core});
+          s = e;
+        }
+      }
+    });
+    size_t nd = 0;
+    for (int64_t k = 0; k < NC; k++) {
+      if (crowd[k] >= 0)
+        return fail(MGPU_E_INVALID_ARG, "more than 65535 chips share cell %lld", (long long)cell[order[crowd[k]]]);
+      nd += cd[k].size();
+    }
+    distinct.reserve(nd);
+    for (int64_t k = 0; k < NC; k++) distinct.insert(distinct.end(), cd[k].begin(), cd[k].end());
   }
   BLOB_MARK("distinct");
   Strips strips;
@@ -2170,22 +2258,40 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   std::vector<std::pair<uint64_t, uint32_t>> keys;
   if (index_system == MGPU_H3 && build_lattice(distinct, keys, &lres, &face_mask, bbox)) {
     probe_mode = mgpu::kProbeLattice;
+    BLOB_MARK("lat:keys");
     mark_whole_cells(distinct, lres, bbox, cflags, cpart, geo);
+    BLOB_MARK("lat:whole");
     parallel_sort(keys, [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) { return a < b; });
-    for (size_t k = 0; k < keys.size(); k++) {
-      if (k && keys[k].first == keys[k - 1].first) {
-        if (keys[k].second != keys[k - 1].second) return fail(MGPU_E_INTERNAL, "lattice key collision");
-        continue;
+    BLOB_MARK("lat:sort");
+    // (per key in parallel: duplicate / collision, the entry's core mask; then in order)
+    const int64_t nk = (int64_t)keys.size();
+    std::vector<uint8_t> kdup(nk);
+    std::vector<uint16_t> kcore(nk);
+    std::atomic<bool> collide{false};
+    mgpu::parallel_for(nk, 4096, [&](int64_t kb, int64_t ke, int) {
+      for (int64_t k = kb; k < ke; k++) {
+        kdup[k] = k && keys[k].first == keys[k - 1].first;
+        if (kdup[k]) {
+          if (keys[k].second != keys[k - 1].second) collide = true;
+          continue;
+        }
+        const mgpu::HashSlot& d = distinct[keys[k].second];
+        uint16_t core = d.core_mask;
+        if (core & mgpu::kCoreWhole) {  // (the whole-cell flag only where the key's face is the cell's home face)
+          int hf, r_;
+          mgpu::h3::IJK hijk;
+          if (!mgpu::h3::h3_home_face_ijk(d.cell, &hf, &hijk, &r_) || (int)(keys[k].first >> 56) != hf)
+            core = (uint16_t)(core & ~mgpu::kCoreWhole);
+        }
+        kcore[k] = core;
       }
+    });
+    if (collide) return fail(MGPU_E_INTERNAL, "lattice key collision");
+    entries.reserve(nk);
+    for (int64_t k = 0; k < nk; k++) {
+      if (kdup[k]) continue;
       const mgpu::HashSlot& d = distinct[keys[k].second];
-      uint16_t core = d.core_mask;
-      if (core & mgpu::kCoreWhole) {  // (the whole-cell flag only where the key's face is the cell's home face)
-        int hf, r_;
-        mgpu::h3::IJK hijk;
-        if (!mgpu::h3::h3_home_face_ijk(d.cell, &hf, &hijk, &r_) || (int)(keys[k].first >> 56) != hf)
-          core = (uint16_t)(core & ~mgpu::kCoreWhole);
-      }
-      entries.push_back(mgpu::HashSlot{keys[k].first, d.first, d.count, core});
+      entries.push_back(mgpu::HashSlot{keys[k].first, d.first, d.count, kcore[k]});
     }
   } else {
     entries = distinct;
@@ -2366,33 +2472,36 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     total = align_up(total + std::max<size_t>(parts[k].bytes, 1), 256);
   }
   hdr.blob_bytes = total;
-  if (!host.alloc(total)) return fail(MGPU_E_INTERNAL, "out of host memory (%zu bytes)", total);
-  // the header, each array and the zero padding behind it, in pieces of <= 64 MiB on the
-  // host threads
-  struct Piece {
-    uint8_t* dst;
-    const uint8_t* src;
-    size_t bytes, zero;
-  };
-  std::vector<Piece> pieces;
-  pieces.push_back({host.data(), (const uint8_t*)&hdr, sizeof hdr, kBlobHeaderBytes - sizeof hdr});
+  // the header, each array and the zero padding behind it, in pieces of <= 64 MiB
+  std::vector<BlobPiece> pieces;
+  pieces.push_back({0, (const uint8_t*)&hdr, sizeof hdr, kBlobHeaderBytes - sizeof hdr});
   for (size_t k = 0; k < parts.size(); k++) {
     const size_t end = k + 1 < parts.size() ? parts[k + 1].off : total;
     const size_t pad = end - parts[k].off - parts[k].bytes;
     for (size_t o = 0; o < parts[k].bytes; o += (64u << 20)) {
       const size_t b = std::min(parts[k].bytes - o, (size_t)64 << 20);
-      pieces.push_back({host.data() + parts[k].off + o, (const uint8_t*)parts[k].src + o, b, 0});
+      pieces.push_back({parts[k].off + o, (const uint8_t*)parts[k].src + o, b, 0});
     }
-    pieces.push_back({host.data() + parts[k].off + parts[k].bytes, nullptr, 0, pad});
+    pieces.push_back({parts[k].off + parts[k].bytes, nullptr, 0, pad});
   }
-  mgpu::parallel_for((int64_t)pieces.size(), 1, [&](int64_t qb, int64_t qe, int) {
-    for (int64_t q = qb; q < qe; q++) {
-      if (pieces[q].bytes) memcpy(pieces[q].dst, pieces[q].src, pieces[q].bytes);
-      if (pieces[q].zero) memset(pieces[q].dst + pieces[q].bytes, 0, pieces[q].zero);
-    }
-  });
-  BLOB_MARK("assemble");
   hdr_out = hdr;
+  auto release = [&] {
+    release_async(order, geo, cpoly, cflags, cpart, cenv, crow, row2chip, distinct, strips, chdr, keys, entries,
+                  grid, raster, cell_ans, slots, cls_poly);
+  };
+  if (sink) {
+    const int32_t st = (*sink)(total, pieces);
+    BLOB_MARK("sink");
+    release();
+    return st;
+  }
+  if (!host.alloc(total)) return fail(MGPU_E_INTERNAL, "out of host memory (%zu bytes)", total);
+  mgpu::parallel_for((int64_t)pieces.size(), 1, [&](int64_t qb, int64_t qe, int) {
+    for (int64_t q = qb; q < qe; q++)
+      fill_from_pieces(pieces, host.data() + pieces[q].off, pieces[q].off, pieces[q].bytes + pieces[q].zero);
+  });
+  release();
+  BLOB_MARK("assemble");
   return MGPU_OK;
 }
 
@@ -2503,12 +2612,19 @@ int32_t mgpu_host_blob_info(const void* host_blob, int64_t bytes, int32_t* index
 
 }  // extern "C"
 
-// Host -> device copy of a large pageable buffer through two pinned 64 MiB staging
-// buffers: the host threads copy one piece in while the DMA engine moves the other
-// (a pageable hipMemcpy of C3's 5.3 GB blob ran at ~4.6 GB/s on the box).
-static hipError_t copy_to_device_staged(void* d, const void* h, size_t bytes) {
+// Host -> device copy of `bytes` bytes that fill(dst, off, n) produces, through two pinned
+// 64 MiB staging buffers: the host threads fill one piece while the DMA engine moves the
+// other (a pageable hipMemcpy of C3's 5.3 GB blob ran at ~4.6 GB/s on the box).
+static hipError_t stage_to_device(void* d, size_t bytes, const std::function<void(uint8_t*, size_t, size_t)>& fill) {
   constexpr size_t kPiece = (size_t)64 << 20;
-  if (bytes <= 2 * kPiece) return hipMemcpy(d, h, bytes, hipMemcpyHostToDevice);
+  if (bytes <= 2 * kPiece) {  // (small: one pageable buffer)
+    std::vector<uint8_t> tmp(bytes);
+    mgpu::parallel_for((int64_t)((bytes + (1 << 20) - 1) >> 20), 1, [&](int64_t b, int64_t en, int) {
+      const size_t lo = (size_t)b << 20, hi = std::min(bytes, (size_t)en << 20);
+      fill(tmp.data() + lo, lo, hi - lo);
+    });
+    return hipMemcpy(d, tmp.data(), bytes, hipMemcpyHostToDevice);
+  }
   void* stage[2] = {nullptr, nullptr};
   hipEvent_t done[2] = {nullptr, nullptr};
   hipStream_t s = nullptr;
@@ -2522,10 +2638,9 @@ static hipError_t copy_to_device_staged(void* d, const void* h, size_t bytes) {
     if (off >= 2 * kPiece) e = hipEventSynchronize(done[k]);  // the piece this buffer held is on the device
     if (e != hipSuccess) break;
     auto* dst = (uint8_t*)stage[k];
-    const auto* src = (const uint8_t*)h + off;
     mgpu::parallel_for((int64_t)((n + (1 << 20) - 1) >> 20), 1, [&](int64_t b, int64_t en, int) {
       const size_t lo = (size_t)b << 20, hi = std::min(n, (size_t)en << 20);
-      memcpy(dst + lo, src + lo, hi - lo);
+      fill(dst + lo, off + lo, hi - lo);
     });
     e = hipMemcpyAsync((uint8_t*)d + off, stage[k], n, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipEventRecord(done[k], s);
@@ -2550,7 +2665,9 @@ int32_t mgpu_chips_upload_blob(mgpu_ctx* ctx, const void* host_blob, int64_t byt
   if (int32_t st = set_device(ctx->device)) return st;
   void* d = nullptr;
   HIP_TRY(hipMalloc(&d, (size_t)bytes));
-  hipError_t e = copy_to_device_staged(d, host_blob, (size_t)bytes);
+  hipError_t e = stage_to_device(d, (size_t)bytes, [&](uint8_t* dst, size_t off, size_t n) {
+    memcpy(dst, (const uint8_t*)host_blob + off, n);
+  });
   if (e != hipSuccess) {
     hipFree(d);
     return fail(MGPU_E_DEVICE, "hipMemcpy: %s", hipGetErrorString(e));
@@ -2566,10 +2683,29 @@ int32_t mgpu_chips_upload(mgpu_ctx* ctx, int32_t index_system, int64_t n_chips, 
   if (!ctx || !out) return fail(MGPU_E_INVALID_ARG, "ctx/out is NULL");
   HostBlob host;
   BlobHeader hdr;
-  if (int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr,
-                              build_opts_of(ctx)))
-    return st;
-  return mgpu_chips_upload_blob(ctx, host.data(), (int64_t)host.size(), out);
+  if (int32_t st = set_device(ctx->device)) return st;
+  // the blob's pieces staged straight to the device (no whole host blob)
+  void* d = nullptr;
+  size_t bytes = 0;
+  const BlobSink sink = [&](size_t total, const std::vector<BlobPiece>& pieces) -> int32_t {
+    BLOB_T0();
+    HIP_TRY(hipMalloc(&d, total));
+    BLOB_MARK("sink:malloc");
+    bytes = total;
+    const hipError_t e = stage_to_device(d, total, [&](uint8_t* dst, size_t off, size_t n) {
+      fill_from_pieces(pieces, dst, off, n);
+    });
+    if (e != hipSuccess) return fail(MGPU_E_DEVICE, "hipMemcpy: %s", hipGetErrorString(e));
+    return MGPU_OK;
+  };
+  BLOB_T0();
+  int32_t st = build_blob(index_system, n_chips, cell, polygon_id, is_core, wkb_offsets, wkb, host, hdr,
+                          build_opts_of(ctx), &sink);
+  BLOB_MARK("upl:build");
+  if (st == MGPU_OK) st = mgpu::adopt_device_blob(ctx, d, (int64_t)bytes, out);
+  BLOB_MARK("upl:adopt");
+  if (st && d) hipFree(d);
+  return st;
 }
 
 int32_t mgpu_chips_destroy(mgpu_chips* chips) {

@@ -1047,7 +1047,7 @@ __global__ __launch_bounds__(kBlock) void pip_fix_kernel(JoinArgs a) {
 // points go through join_tile's phases gathered into full tiles, and split_emit_kernel
 // writes the ordered pairs from the codes.
 #ifndef MGPU_CLS_BLOCK
-#define MGPU_CLS_BLOCK 256  // threads per chunk in the emit kernels (16 points each)
+#define MGPU_CLS_BLOCK 256  // threads per chunk in the emit kernels (16 points each; 512: 8)
 #endif
 constexpr int kClsBlock = MGPU_CLS_BLOCK;
 constexpr int kClsItems = kChunk / kClsBlock;  // points per thread
@@ -1440,6 +1440,7 @@ template <int IS>
 __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_EMIT_WAVES))) void split_emit_kernel(SplitArgs sa) {
   using Code = typename CodeOf<IS>::T;
   constexpr int kWords = kClsItems * (int)sizeof(Code) / 4;  // 32-bit words of a thread's codes
+  static_assert(kWords % 4 == 0 && kWords >= 4, "whole 16-byte code loads per thread (MGPU_CLS_BLOCK 256 or 512)");
   const JoinArgs& a = sa.j;
   const ChipTableView& t = a.chips;
   __shared__ uint32_t s_w[2][kClsBlock / 64];

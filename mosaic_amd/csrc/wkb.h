@@ -57,8 +57,9 @@ struct Reader {
       ok = false;
       return 0;
     }
-    uint64_t v = 0;
-    for (int i = 0; i < 8; i++) v |= (uint64_t)p[le ? i : 7 - i] << (8 * i);
+    uint64_t v;
+    memcpy(&v, p, 8);
+    if (!le) v = __builtin_bswap64(v);  // (a little-endian host)
     p += 8;
     double d;
     memcpy(&d, &v, 8);
@@ -91,8 +92,7 @@ inline bool header(Reader& r, bool& le, uint32_t& type, int& dims, std::string& 
   return r.ok;
 }
 
-inline bool read_polygon(Reader& r, bool le, int dims, Flat& f, GeomInfo& gi, std::string& msg,
-                         std::vector<double>* first_ring = nullptr) {
+inline bool read_polygon(Reader& r, bool le, int dims, Flat& f, GeomInfo& gi, std::string& msg) {
   uint32_t nr = r.u32(le);
   if (!r.ok) {
     msg = "truncated WKB";
@@ -105,15 +105,14 @@ inline bool read_polygon(Reader& r, bool le, int dims, Flat& f, GeomInfo& gi, st
       return false;
     }
     double e[4] = {INFINITY, INFINITY, -INFINITY, -INFINITY};
+    const size_t v0 = f.vtx.size();
+    f.vtx.resize(v0 + 2 * (size_t)n);
+    double* out = f.vtx.data() + v0;
     for (uint32_t i = 0; i < n; i++) {
       double x = r.f64(le), y = r.f64(le);
       for (int d = 2; d < dims; d++) r.f64(le);
-      f.vtx.push_back(x);
-      f.vtx.push_back(y);
-      if (first_ring && k == 0) {
-        first_ring->push_back(x);
-        first_ring->push_back(y);
-      }
+      out[2 * i] = x;
+      out[2 * i + 1] = y;
       e[0] = std::fmin(e[0], x);
       e[1] = std::fmin(e[1], y);
       e[2] = std::fmax(e[2], x);
@@ -164,13 +163,14 @@ inline bool parse(const uint8_t* data, size_t len, Flat& f, GeomInfo& gi, std::s
   gi.multi = type != 3;
   if (type == 3) {
     Reader body = peek;
-    std::vector<double> shell;
     size_t parts_before = f.part_ring.size();
-    if (!read_polygon(body, le, dims, f, gi, msg, &shell)) return false;
+    if (!read_polygon(body, le, dims, f, gi, msg)) return false;
     // Polygon.isRectangle(): no holes, 5-point shell on the envelope, axis-parallel edges
     uint32_t pr = (uint32_t)parts_before - 1;
     uint32_t nrings = f.part_ring[pr + 1] - f.part_ring[pr];
-    if (nrings == 1 && shell.size() == 10) {
+    const uint32_t sr = f.part_ring[pr];  // the shell ring
+    const double* shell = f.vtx.data() + 2 * (size_t)f.ring_vtx[sr];
+    if (nrings == 1 && f.ring_vtx[sr + 1] - f.ring_vtx[sr] == 5) {
       bool ok = true;
       for (int i = 0; i < 5 && ok; i++) {
         double x = shell[2 * i], y = shell[2 * i + 1];
