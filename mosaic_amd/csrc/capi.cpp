@@ -2367,6 +2367,10 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     if (index_system == MGPU_BNG && !build_cell_answers(hv, dense[0], bng_edge, grid, cell_ans)) cell_ans = CellAnswers{};
   }
   BLOB_MARK("raster");
+#ifdef MGPU_BLOB_TIMING
+  fprintf(stderr, "[blob] raster mode %d, %u x %u pixels, %zu classes (one-match below %u)\n", raster.mode, raster.nx,
+          raster.ny, raster.cls.size(), raster.pc[0]);
+#endif
   uint32_t cap = 16;
   while (cap < 2 * entries.size()) cap <<= 1;
   std::vector<mgpu::HashSlot> slots(cap, mgpu::HashSlot{0, 0, 0, 0});

@@ -1135,10 +1135,10 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
         if (pk < a.n && pt_valid(a.valid, a.valid_off, pk)) {
           bool ok = true;
           uint32_t g_ = 0, s_ = 0, b_ = kNoPixel;
-          ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &g_, &s_, use_blk ? &b_ : nullptr);
+          ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &g_, &s_, &b_);  // (see classify_pair_kernel)
           gix[k] = g_;
           sb[k] = s_;
-          bi[k] = b_;
+          bi[k] = use_blk ? b_ : kNoPixel;
           any_bad |= !ok;
         }
       }
@@ -1264,10 +1264,11 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
         if (pj < a.n && pt_valid(a.valid, a.valid_off, pj)) {
           bool ok = true;
           uint32_t g_ = 0, s_ = 0, b_ = kNoPixel;
-          ri[j] = raster_index<IS>(t, X[j], Y[j], &ok, &g_, &s_, use_blk ? &b_ : nullptr);
+          // (always a local's address: a pointer chosen at run time put b_ in scratch)
+          ri[j] = raster_index<IS>(t, X[j], Y[j], &ok, &g_, &s_, &b_);
           gix[j] = g_;
           sb[j] = s_;
-          bi[j] = b_;
+          bi[j] = use_blk ? b_ : kNoPixel;
           any_bad |= !ok;
         }
       }
