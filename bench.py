@@ -19,7 +19,7 @@ mgpu_chips_broadcast, mgpu_pair_offsets; mosaic_amd/csrc/comm.cpp).  torch.distr
 ranks of the barrier-bracketed K steps.
 
 A step is one mgpu_pip_join call, whichever of the library's three pipelines its planner
-picks for the chip table: split (C2, C5: classify_wave_kernel over every
+picks for the chip table: split (C2, C5: classify_pair_kernel over every
 point by its pixel, pip_mixed_kernel for the mixed ones, split_emit_kernel), binned (C3:
 bin_hist / bin_scatter, pip_binned_kernel over the binned points, bin_gather /
 bin_emit) or fused (C4: pip_join_kernel, pip_fix_kernel, tile_scan_kernel,
@@ -370,9 +370,12 @@ def main():
         kernel = "pip_binned_kernel<%s>" % isys.name
         alg_bytes = 24.0 * n
     elif split:
-        # the split pipeline: the dominant kernel is classify_wave_kernel, the one
-        # pass over every point: 16 B read + its code (2 B H3 / 4 B BNG) written per point
-        kernel = "classify_wave_kernel<%s>" % isys.name
+        # the split pipeline: the dominant kernel is the classify pass over every
+        # point: 16 B read + its code (2 B H3 / 4 B BNG) written per point --
+        # classify_pair_kernel (two points per lane, 16-byte loads) when both coordinate
+        # arrays are 16-byte aligned, as torch's allocations are, else classify_wave_kernel
+        pair = x.data_ptr() % 16 == 0 and y.data_ptr() % 16 == 0
+        kernel = "%s<%s>" % ("classify_pair_kernel" if pair else "classify_wave_kernel", isys.name)
         alg_bytes = (16.0 + (2.0 if isys.code == M._native.MGPU_H3 else 4.0)) * n
     else:
         kernel = "pip_join_kernel<%s>" % isys.name

@@ -466,7 +466,10 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   __shared__ uint32_t s_wave_tot[kBlock / 64];
   __shared__ uint32_t s_first[kTile];   // first chip of the point's cell
   __shared__ uint32_t s_mask[kTile];    // bit j: chip first + j matches (j < 32)
-  __shared__ uint16_t s_cnt[kTile];     // chips of the point's cell (0: none)
+  // chips of the point's cell (0: none) -- read by the fix kernels only; the fused
+  // streaming kernel's raster pass lists its mixed points here; the split / binned
+  // streaming tiles use none of it (their LDS sets their occupancy)
+  __shared__ uint16_t s_cnt[(SLOW || G == 0) ? kTile : 1];
   // phases 1-2: candidate list; phase 3: output staging (same bytes)
   constexpr int kCap = G ? kGCandCap : kCandCap, kMix = G ? kGMixCap : kMixCap;
   constexpr int kStash = stash_of<G>();

@@ -515,9 +515,36 @@ def test_pip_join_kats_on_gpu(gpu, nyc_chips_r9):
         assert int(q) in k["objectids"]
 
 
+def assert_device_blob_is_host_blob(d, c):
+    """The upload (blob pieces staged straight to the device through pinned buffers) left
+    exactly the bytes mgpu_chips_host_blob assembles on the host, padding included."""
+    import ctypes
+    from mosaic_amd import _native as N
+    ptr, nbytes = d.device_blob()
+    out, nb = ctypes.c_void_p(), ctypes.c_int64()
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    N.check(N.lib().mgpu_chips_host_blob(c.index_system, len(c), p(c.cell), p(c.polygon_id), p(c.is_core),
+                                         p(c.wkb_offsets), p(c.wkb if c.wkb.size else np.zeros(1, np.uint8)),
+                                         ctypes.byref(out), ctypes.byref(nb)))
+    try:
+        assert nb.value == nbytes
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        piece = 256 << 20
+        buf = np.empty(min(piece, nbytes), np.uint8)
+        for off in range(0, nbytes, piece):
+            n = min(piece, nbytes - off)
+            assert hip.hipMemcpy(buf.ctypes.data, ptr + off, n, 2) == 0  # device to host
+            host = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(out.value + off))
+            assert np.array_equal(buf[:n], host), "device blob differs in [%d, %d)" % (off, off + n)
+    finally:
+        N.lib().mgpu_host_free(out)
+
+
 def test_chip_blob_roundtrip(gpu, nyc_chips_r9):
     """The replicated chip table (what RCCL broadcast carries) joins identically."""
     d = nyc_chips_r9.upload()
+    assert_device_blob_is_host_blob(d, nyc_chips_r9)
     ptr, nbytes = d.device_blob()
     buf = torch.empty(nbytes, dtype=torch.uint8, device=gpu)
     import ctypes
@@ -663,6 +690,7 @@ def test_pip_join_c3_full_table(gpu):
     c = M.tessellate(P, M.H3IndexSystem(), 10, keep_core_geometries=False)
     assert len(c) > 9_000_000 and len(np.unique(c.polygon_id)) == W.N_TRACTS
     d = c.upload()
+    assert_device_blob_is_host_blob(d, c)
     x, y = W.extent_points(W.TRACT_EXTENT, 1_200_000, 31)
     r = M.pip_join(T(x, gpu), T(y, gpu), d, 10)
     gp, gq = r.numpy()

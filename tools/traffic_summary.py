@@ -59,7 +59,7 @@ f_read = bf / (16.0 * N)
 f_write = bw / (8.0 * N)
 # the dominant kernel: classify_kernel in the split pipeline, pip_binned_kernel in the binned
 # one, else the fused pip_join_kernel
-dom = next(k for k in jf_all if k.split("<")[0] in ("classify_kernel", "classify_wave_kernel", "pip_join_kernel",
+dom = next(k for k in jf_all if k.split("<")[0] in ("classify_kernel", "classify_wave_kernel", "classify_pair_kernel", "pip_join_kernel",
                                                      "pip_binned_kernel"))
 jf, nj = jf_all[dom]
 jw, _ = jw_all[dom]

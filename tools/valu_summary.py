@@ -9,7 +9,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DOM = ("classify_wave_kernel", "pip_binned_kernel", "pip_join_kernel")
+DOM = ("classify_wave_kernel", "classify_pair_kernel", "pip_binned_kernel", "pip_join_kernel")
 out_path = os.path.join(ROOT, "profiles", "pmc_valu.json")
 out = json.load(open(out_path)) if os.path.exists(out_path) else {}
 rnd = sys.argv[1]
