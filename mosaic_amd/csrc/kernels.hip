@@ -358,7 +358,14 @@ __device__ __forceinline__ Range chip_probe(const JoinArgs& a, int64_t p, double
     }
     return probe_range(t, h3::lattice_key(f.face, f.ijk));
   }
-  h3::FastHex f = h3::fast_hex2d(lat, lon, res, t.k_res > 0 ? t.k_res : h3::k_of_res(res), kAllFaces);
+  // (cell-id probing: res made opaque here, so the per-resolution predicates of
+  // k_of_res / face_ijk_to_h3_fast are computed on this path instead of being hoisted
+  // into SGPRs across the callers' point loops -- there they spilled to VGPR lanes)
+  int res_o = res;
+#ifdef __HIP_DEVICE_COMPILE__
+  asm volatile("" : "+s"(res_o));
+#endif
+  h3::FastHex f = h3::fast_hex2d(lat, lon, res_o, t.k_res > 0 ? t.k_res : h3::k_of_res(res_o), kAllFaces);
   if (f.tie) {
     if (a.tie_host) {
       if (!SLOW) tie_record(a.tie_queue, a.tie_cap, input_pos(a, p), px, py, h3::lattice_key(f.face, f.ijk));
@@ -369,7 +376,7 @@ __device__ __forceinline__ Range chip_probe(const JoinArgs& a, int64_t p, double
       route_point(a, p, px, py, &f, tie);
     }
   }
-  return probe_range(t, h3::face_ijk_to_h3_fast(f.face, f.ijk, res));
+  return probe_range(t, h3::face_ijk_to_h3_fast(f.face, f.ijk, res_o));
 }
 
 __device__ __forceinline__ bool chip_is_core(const ChipTableView& t, const Range& r, uint32_t j) {
