@@ -61,6 +61,10 @@ struct JoinArgs {
   // binned H3 pipeline over a dense lattice grid: per binned slot, the point's grid entry
   // index (| kKeyDeep) or a kKey* code, written by bin_scatter_kernel (else null)
   const uint32_t* bin_key = nullptr;
+  // binned pipeline (MGPU_BIN_JOIN_COUNTS): the join adds each slot's match count to its
+  // INPUT chunk's pair count here (pos_of[slot] / bin_chunk()), zeroed before launch --
+  // the emit's offsets without a separate gather pass (else null)
+  uint32_t* in_chunk_pairs = nullptr;
 };
 
 // The override pass's scratch (launch_join_redo / launch_split_redo): the units (fused

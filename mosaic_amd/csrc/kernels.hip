@@ -472,7 +472,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
   __shared__ uint32_t s_ncand, s_nmix;
   __shared__ uint32_t s_wave_tot[kBlock / 64];
   __shared__ uint32_t s_first[kTile];   // first chip of the point's cell
-  __shared__ uint32_t s_mask[kTile];    // bit j: chip first + j matches (j < 32)
+  __shared__ __attribute__((aligned(16))) uint32_t s_mask[kTile];  // bit j: chip first + j matches (j < 32)
   // chips of the point's cell (0: none) -- read by the fix kernels only; the fused
   // streaming kernel's raster pass lists its mixed points here; the split / binned
   // streaming tiles use none of it (their LDS sets their occupancy)
@@ -505,6 +505,20 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     if (G == 2)
       for (uint32_t li = threadIdx.x; li < (uint32_t)kTile; li += kBlock)
         s_gidx[li] = li < gcount ? a.mixed_idx[lbase + li] : (uint16_t)0;
+  }
+  // (binned, MGPU_BIN_JOIN_COUNTS: the input positions of slots 4 lane .. 4 lane + 3 load
+  // now, with the tile's first loads, and are used only at its end -- each slot's input
+  // chunk, for the chunk pair counts)
+  uint32_t ckp[G == 1 ? 4 : 1];
+  if (G == 1 && a.in_chunk_pairs) {
+    const uint32_t s0 = 4u * threadIdx.x;
+    if (s0 + 3 < gcount) {
+      const uint4 q = *(const uint4*)(a.pos_of + lbase + s0);  // (perm: 256-byte aligned, lbase % 256 == 0)
+      ckp[0] = q.x, ckp[1] = q.y, ckp[2] = q.z, ckp[3] = q.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; i++) ckp[i] = s0 + i < gcount ? a.pos_of[lbase + s0 + i] : 0u;
+    }
   }
 #define MGPU_PT(li) (G == 2 ? gbase + (int64_t)s_gidx[li] : G == 1 ? lbase + (li) : (int64_t)tile * kTile + (li))
 #define MGPU_VALID(li) (G ? (uint32_t)(li) < gcount : (int64_t)tile * kTile + (li) < a.n)
@@ -903,6 +917,43 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     for (int k = 0; k < kItems; k++) {
       const uint32_t li = threadIdx.x + k * kBlock;
       if (li < gcount) a.mixed_res[lbase + li] = v[k];  // (the slot: the list position / binned point)
+    }
+    if (G == 1 && a.in_chunk_pairs) {
+      // per input chunk pair counts: slots are bin-major, chunk-minor, so the tile's 256
+      // slots hold a few runs of one input chunk each.  Lane l takes slots 4l .. 4l + 3
+      // (their masks from LDS): one wave scan gives every slot's prefix, and the last slot
+      // of each run adds the run's sum -- one atomic per run (kBlock == 64: one wave)
+      const int lane = threadIdx.x & 63;
+      const uint32_t s0 = 4u * (uint32_t)lane;
+      const uint4 mq = *(const uint4*)(s_mask + s0);
+      const uint32_t mv[4] = {mq.x, mq.y, mq.z, mq.w};
+      uint32_t c[4], loc[4], nn[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const bool act = s0 + i < gcount;
+        c[i] = act ? ckp[i] / (uint32_t)kChunk : 0xFFFFFFFFu;  // (kBinChunk == kChunk)
+        nn[i] = act ? (uint32_t)__popc(mv[i]) : 0u;
+        loc[i] = (i ? loc[i - 1] : 0u) + nn[i];
+      }
+      const uint32_t lane_excl = wave_incl_scan(loc[3]) - loc[3];
+      const uint32_t prev_c = __shfl_up(c[3], 1, 64), next_c = __shfl_down(c[0], 1, 64);
+      bool head[4];
+      uint32_t hpre = 0;  // the prefix before the lane's last run head
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        head[i] = c[i] != 0xFFFFFFFFu && (i ? c[i] != c[i - 1] : (lane == 0 || prev_c != c[0]));
+        if (head[i]) hpre = lane_excl + loc[i] - nn[i];
+      }
+      const unsigned long long hl = __ballot(head[0] || head[1] || head[2] || head[3]);
+      const unsigned long long lower = hl & ((1ull << lane) - 1ull);
+      uint32_t start = __shfl(hpre, lower ? 63 - __clzll(lower) : 0, 64);  // (the run in progress)
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        if (head[i]) start = lane_excl + loc[i] - nn[i];
+        const bool tail = c[i] != 0xFFFFFFFFu && (i < 3 ? c[i + 1] != c[i] : (lane == 63 || next_c != c[3]));
+        const uint32_t run = lane_excl + loc[i] - start;
+        if (tail && run) atomicAdd(&a.in_chunk_pairs[c[i]], run);
+      }
     }
     uint32_t tm = 0;
 #pragma unroll
@@ -2324,9 +2375,15 @@ __device__ __forceinline__ uint32_t bin_key_of(const JoinArgs& a, int64_t pos, d
 // chunk's points sorted by bin in LDS, then written as contiguous runs (one per bin) by
 // consecutive lanes: whole cache lines, not one scattered 8-byte store per point.
 template <bool KEY>
+#ifndef MGPU_SCATTER_NOLI
+#define MGPU_SCATTER_NOLI 0
+#endif
 __global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
+  // MGPU_SCATTER_NOLI: the points' chunk indices pass through s_val too (a third pass),
+  // 8 KB less LDS per workgroup (4 instead of 3 per CU)
+  constexpr bool kNoLi = MGPU_SCATTER_NOLI && !KEY;
   __shared__ double s_val[kBinChunk];   // x, then y, in the chunk's bin-sorted order
-  __shared__ uint16_t s_li[kBinChunk];  // the point's index in the chunk
+  __shared__ uint16_t s_li[kNoLi ? 1 : kBinChunk];  // the point's index in the chunk
   __shared__ uint32_t s_off[kBinMax];
   __shared__ uint32_t s_loc[kBinMax];
   __shared__ uint32_t s_rank[kBinMax];
@@ -2373,7 +2430,7 @@ __global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
     if (act) {
       lps[q] = s_loc[bi] + base + (uint32_t)__popcll(peers & below);
       s_val[lps[q]] = px[q];
-      s_li[lps[q]] = (uint16_t)(q * kBinBlock + threadIdx.x);
+      if (!kNoLi) s_li[lps[q]] = (uint16_t)(q * kBinBlock + threadIdx.x);
     }
   }
   __syncthreads();
@@ -2388,7 +2445,7 @@ __global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
       const uint32_t bi = bin_at(s_loc, nb, lp);
       sls[q] = s_off[bi] + (lp - s_loc[bi]);
       MGPU_ST_INTER(s_val[lp], &b.bx[sls[q]]);
-      MGPU_ST_INTER((uint32_t)(c0 + s_li[lp]), &b.perm[sls[q]]);
+      if (!kNoLi) MGPU_ST_INTER((uint32_t)(c0 + s_li[lp]), &b.perm[sls[q]]);
     }
   }
   __syncthreads();
@@ -2399,6 +2456,17 @@ __global__ __launch_bounds__(kBinBlock) void bin_scatter_kernel(BinArgs b) {
 #pragma unroll
   for (int q = 0; q < kBinItems; q++)
     if (sls[q] != 0xFFFFFFFFu) MGPU_ST_INTER(s_val[q * kBinBlock + threadIdx.x], &b.by[sls[q]]);
+  if (kNoLi) {
+    uint32_t* s_pi = (uint32_t*)s_val;  // (the first half of s_val as u32)
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kBinItems; q++)
+      if (lps[q] != 0xFFFFFFFFu) s_pi[lps[q]] = (uint32_t)(c0 + q * kBinBlock + threadIdx.x);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kBinItems; q++)
+      if (sls[q] != 0xFFFFFFFFu) MGPU_ST_INTER(s_pi[q * kBinBlock + threadIdx.x], &b.perm[sls[q]]);
+  }
   if (KEY) {
     // the grid keys, through the same LDS order (the first half of s_val as u32)
     uint32_t* s_key = (uint32_t*)s_val;
@@ -2434,6 +2502,30 @@ __global__ __launch_bounds__(kBlock) MGPU_JOIN_ATTR void pip_binned_kernel(JoinA
 constexpr int kBinEmitItems = kChunk / kClsBlock;
 static_assert(kBinEmitItems % 2 == 0, "16-byte answer loads per thread");
 static_assert(kBinChunk % kChunk == 0 && kBinChunk / kChunk <= kBinBlock / 64, "emit chunks inside a bin chunk");
+// A bin chunk's answers into LDS in input order: its bin runs read whole (consecutive
+// lanes, consecutive slots: coalesced, one page per run), placed by perm[]; every load of
+// a thread's kBgItems slots in flight before its LDS stores
+constexpr int kBgItems = kBinChunk / kBinBlock;  // slots per thread
+__device__ __forceinline__ void bin_gather_lds(const BinArgs& b, int64_t c0, uint32_t m, int nb,
+                                               const uint32_t* s_off, const uint32_t* s_loc, uint64_t* s_v) {
+  uint32_t pp[kBgItems];
+  uint64_t rv[kBgItems];
+#pragma unroll
+  for (int q = 0; q < kBgItems; q++) {
+    const uint32_t lp = q * kBinBlock + threadIdx.x;
+    pp[q] = 0xFFFFFFFFu;
+    if (lp < m) {
+      const uint32_t bi = bin_at(s_loc, nb, lp);
+      const uint32_t sl = s_off[bi] + (lp - s_loc[bi]);
+      pp[q] = b.perm[sl];
+      rv[q] = b.s.j.mixed_res[sl];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kBgItems; q++)
+    if (pp[q] != 0xFFFFFFFFu) s_v[pp[q] - (uint32_t)c0] = rv[q];
+}
+
 __global__ __launch_bounds__(kBinBlock) void bin_gather_kernel(BinArgs b) {
   __shared__ uint64_t s_v[kBinChunk];
   __shared__ uint32_t s_off[kBinMax];
@@ -2445,10 +2537,17 @@ __global__ __launch_bounds__(kBinBlock) void bin_gather_kernel(BinArgs b) {
   bin_runs(b, k, s_off, s_loc, s_w);
   const int64_t left = n - c0;
   const uint32_t m = left < kBinChunk ? (uint32_t)left : (uint32_t)kBinChunk;
-  for (uint32_t lp = threadIdx.x; lp < m; lp += kBinBlock) {
-    const uint32_t bi = bin_at(s_loc, nb, lp);
-    const uint32_t sl = s_off[bi] + (lp - s_loc[bi]);
-    s_v[b.perm[sl] - (uint32_t)c0] = b.s.j.mixed_res[sl];
+#ifndef MGPU_GATHER_UNROLL
+#define MGPU_GATHER_UNROLL 1
+#endif
+  if (MGPU_GATHER_UNROLL) {
+    bin_gather_lds(b, c0, m, nb, s_off, s_loc, s_v);
+  } else {
+    for (uint32_t lp = threadIdx.x; lp < m; lp += kBinBlock) {
+      const uint32_t bi = bin_at(s_loc, nb, lp);
+      const uint32_t sl = s_off[bi] + (lp - s_loc[bi]);
+      s_v[b.perm[sl] - (uint32_t)c0] = b.s.j.mixed_res[sl];
+    }
   }
   __syncthreads();
   constexpr int kPerWave = kChunk / (kBinBlock / 64) * (kBinChunk / kChunk);  // points per wave
@@ -2544,6 +2643,86 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
       sa.out_point[q] = sa.point_id ? sa.point_id[p] : sa.id_base + p;
       sa.out_poly[q] = (int32_t)s_poly[emit_swz(i)];
 #endif
+    }
+    __syncthreads();
+  }
+}
+
+// The binned answers straight to ordered pairs (MGPU_BIN_JOIN_COUNTS: the join counted
+// each input chunk's pairs, the scan made the offsets): per input chunk, its bin runs of
+// answers are read whole (coalesced, one page per run) and placed by perm[] into LDS in
+// input order -- bin_gather_kernel's front half, without writing the answers back out --
+// then emitted as bin_emit_kernel does, 8 consecutive points per thread.
+#ifndef MGPU_BIN_JOIN_COUNTS
+#define MGPU_BIN_JOIN_COUNTS 1
+#endif
+static_assert(kBinChunk == kChunk, "one emit chunk per bin chunk");
+__global__ __launch_bounds__(kBinBlock) void bin_emit_gather_kernel(BinArgs b) {
+  const SplitArgs& sa = b.s;
+  const ChipTableView& t = sa.j.chips;
+  __shared__ uint64_t s_v[kBinChunk];
+  __shared__ uint32_t s_off[kBinMax];
+  __shared__ uint32_t s_loc[kBinMax];
+  __shared__ uint32_t s_w[kBinBlock / 64];
+  __shared__ uint32_t s_poly[kEmitWin];
+  __shared__ uint16_t s_pt[kEmitWin];
+  const int nb = b.nbx * b.nby;
+  const int64_t k = blockIdx.x, n = sa.j.n, c0 = k * kBinChunk;
+  bin_runs(b, k, s_off, s_loc, s_w);
+  const int64_t left = n - c0;
+  const uint32_t m = left < kBinChunk ? (uint32_t)left : (uint32_t)kBinChunk;
+  bin_gather_lds(b, c0, m, nb, s_off, s_loc, s_v);
+  __syncthreads();
+  const int l0 = threadIdx.x * kBgItems;
+  uint64_t v[kBgItems];
+  uint32_t npair = 0;
+#pragma unroll
+  for (int q = 0; q < kBgItems; q++) {
+    v[q] = (uint32_t)(l0 + q) < m ? s_v[l0 + q] : 0ull;
+    npair += __popc((uint32_t)(v[q] >> 32));
+  }
+  // the thread's first pair within the chunk: a block scan of npair
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t incl = wave_incl_scan(npair);
+  __syncthreads();  // (bin_runs' s_w reads are done)
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  uint32_t off0 = incl - npair, total = 0;
+#pragma unroll
+  for (int w = 0; w < kBinBlock / 64; w++) {
+    off0 += w < wave ? s_w[w] : 0u;
+    total += s_w[w];
+  }
+  const uint64_t base = sa.chunk_off[k];
+  for (uint32_t w0 = 0; w0 < total; w0 += kEmitWin) {
+    if (off0 < w0 + kEmitWin && off0 + npair > w0) {
+      uint32_t q = off0;
+#pragma unroll
+      for (int i = 0; i < kBgItems; i++) {
+        const uint32_t first = (uint32_t)v[i], msk = (uint32_t)(v[i] >> 32);
+        if (msk == 1u) {  // one match: first is the polygon id (JoinArgs.poly_answers)
+          if (q >= w0 && q < w0 + kEmitWin) {
+            s_poly[emit_swz(q - w0)] = first;
+            s_pt[emit_swz(q - w0)] = (uint16_t)(l0 + i);
+          }
+          q++;
+          continue;
+        }
+        for (uint32_t mm = msk; mm; mm &= mm - 1, q++)
+          if (q >= w0 && q < w0 + kEmitWin) {
+            s_poly[emit_swz(q - w0)] = (uint32_t)t.chip_poly[first + __builtin_ctz(mm)];
+            s_pt[emit_swz(q - w0)] = (uint16_t)(l0 + i);
+          }
+      }
+    }
+    __syncthreads();
+    const uint32_t cnt = total - w0 < (uint32_t)kEmitWin ? total - w0 : (uint32_t)kEmitWin;
+    for (uint32_t i = threadIdx.x; i < cnt; i += kBinBlock) {
+      const uint64_t q = base + w0 + i;
+      if ((int64_t)q >= sa.capacity) break;
+      const int64_t p = c0 + s_pt[emit_swz(i)];
+      sa.out_point[q] = sa.point_id ? sa.point_id[p] : sa.id_base + p;
+      sa.out_poly[q] = (int32_t)s_poly[emit_swz(i)];
     }
     __syncthreads();
   }
@@ -2828,10 +3007,14 @@ int32_t bin_max() { return kBinMax; }
 // look-back walks back through the whole grid's round one dependent load at a time)
 static void launch_bin_output(const BinArgs& a, hipStream_t s) {
   const int64_t n = a.s.j.n, K = bin_chunks(n), nc = split_chunks(n);
-  hipLaunchKernelGGL(bin_gather_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
+  if (!MGPU_BIN_JOIN_COUNTS)
+    hipLaunchKernelGGL(bin_gather_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, a.s.chunk_pairs, a.s.j.group_cand, nc,
                      a.s.chunk_off, a.s.j.counters);
-  hipLaunchKernelGGL(bin_emit_kernel, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
+  if (MGPU_BIN_JOIN_COUNTS)
+    hipLaunchKernelGGL(bin_emit_gather_kernel, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL(bin_emit_kernel, dim3((unsigned)nc), dim3(kClsBlock), 0, s, a);
 }
 
 template <int IS>
@@ -2847,14 +3030,19 @@ static void launch_binned_t(const BinArgs& a, hipStream_t s, hipEvent_t after_bi
     // ranking measured 1.80 vs 1.75 ms on C3: profiles/r5/ab_c3_scatter_pf.txt)
     hipLaunchKernelGGL(bin_scatter_kernel<false>, dim3((unsigned)K), dim3(kBinBlock), 0, s, a);
   }
-  if (after_bin) hipEventRecord(after_bin, s);
   const int64_t nc = split_chunks(n), tiles = nc * kChunkTiles;
+  JoinArgs j = a.s.j;
+  if (MGPU_BIN_JOIN_COUNTS) {  // the join counts each input chunk's pairs (the emit's offsets)
+    hipMemsetAsync(a.s.chunk_pairs, 0, (size_t)nc * sizeof(uint32_t), s);
+    j.in_chunk_pairs = a.s.chunk_pairs;
+  }
+  if (after_bin) hipEventRecord(after_bin, s);
   const uint32_t per = a.xcd_runs ? (uint32_t)((tiles + 7) / 8) : 0u;
   const int64_t grid = per ? 8 * (int64_t)per : tiles;
-  hipLaunchKernelGGL(pip_binned_kernel<IS>, dim3((unsigned)grid), dim3(kBlock), 0, s, a.s.j, per, (uint32_t)tiles);
+  hipLaunchKernelGGL(pip_binned_kernel<IS>, dim3((unsigned)grid), dim3(kBlock), 0, s, j, per, (uint32_t)tiles);
   if (after_join) hipEventRecord(after_join, s);
   const int64_t fix = tiles < kFixGrid ? tiles : kFixGrid;
-  hipLaunchKernelGGL((pip_mixed_fix_kernel<IS, 1>), dim3((unsigned)fix), dim3(kBlock), 0, s, a.s.j);
+  hipLaunchKernelGGL((pip_mixed_fix_kernel<IS, 1>), dim3((unsigned)fix), dim3(kBlock), 0, s, j);
   launch_bin_output(a, s);
 }
 
@@ -2871,7 +3059,10 @@ hipError_t launch_binned(int is, const BinArgs& a, hipStream_t s, hipEvent_t aft
 // only the ordered output of a binned join already computed (mgpu_pip_join_fetch)
 hipError_t launch_bin_emit(const BinArgs& a, hipStream_t s) {
   if (a.s.j.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(bin_emit_kernel, dim3((unsigned)split_chunks(a.s.j.n)), dim3(kClsBlock), 0, s, a);
+  if (MGPU_BIN_JOIN_COUNTS)
+    hipLaunchKernelGGL(bin_emit_gather_kernel, dim3((unsigned)bin_chunks(a.s.j.n)), dim3(kBinBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL(bin_emit_kernel, dim3((unsigned)split_chunks(a.s.j.n)), dim3(kClsBlock), 0, s, a);
   return hipGetLastError();
 }
 
