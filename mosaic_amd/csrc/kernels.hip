@@ -1498,9 +1498,6 @@ constexpr int kEmitMres = 512;  // mixed results of a chunk staged in LDS (the r
 #ifndef MGPU_EMIT_MR
 #define MGPU_EMIT_MR 1
 #endif
-#ifndef MGPU_EMIT_2P
-#define MGPU_EMIT_2P 0
-#endif
 template <int IS>
 __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_EMIT_WAVES))) void split_emit_kernel(SplitArgs sa) {
   using Code = typename CodeOf<IS>::T;
@@ -1595,74 +1592,6 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   const uint64_t base = sa.chunk_off[blockIdx.x];
   for (uint32_t w0 = 0; w0 < total; w0 += kEmitWin) {
     if (off0 < w0 + kEmitWin && off0 + npair > w0) {
-#if MGPU_EMIT_2P
-      // two passes: every one-match item (from LDS) staged first, in one branch each; the
-      // other matched items (several matches, or an answer beyond LDS) only flagged, then
-      // staged by a second walk that only threads holding one make
-      uint32_t q = off0, multi = 0;
-      r = rank0;
-      auto count_of = [&](Code c, uint32_t rr, bool& one_ok, int32_t& one) -> uint32_t {
-        one_ok = false;
-        if (c == kMixed) {
-          if (rr < kMr) {
-            const uint32_t cn = (uint32_t)__popc((uint32_t)(s_mr[rr] >> 32));
-            one_ok = cn == 1;
-            one = s_mp[rr];
-            return cn;
-          }
-          return (uint32_t)__popc((uint32_t)(a.mixed_res[c0 + rr] >> 32));
-        }
-        if (c == 0) return 0u;
-        if (IS == MGPU_H3) {
-          if ((uint32_t)c < ncp) {
-            one_ok = true;
-            one = s_cp[(uint32_t)c];
-            return 1u;
-          }
-          return c < t.raster_pc[0] ? 1u : c < t.raster_pc[1] ? 2u : c < t.raster_pc[2] ? 3u : c < t.raster_pc[3] ? 4u
-                 : (uint32_t)__popc((uint32_t)(pure(c) >> 32));
-        }
-        return (uint32_t)__popc((uint32_t)c & 0xFFu);
-      };
-#pragma unroll
-      for (int k = 0; k < kClsItems; k++) {
-        const Code c = code(k);
-        const uint32_t rr = r;
-        r += c == kMixed ? 1u : 0u;
-        bool one_ok;
-        int32_t one = 0;
-        const uint32_t cn = count_of(c, rr, one_ok, one);
-        if (one_ok && q - w0 < (uint32_t)kEmitWin) {
-          s_poly[emit_swz(q - w0)] = (uint32_t)one;
-          s_pt[emit_swz(q - w0)] = (uint16_t)(threadIdx.x * kClsItems + k);
-        }
-        if (cn && !one_ok) multi |= 1u << k;
-        q += cn;
-      }
-      if (multi) {
-        q = off0;
-        r = rank0;
-        for (int k = 0; k < kClsItems; k++) {
-          const Code c = code(k);
-          const uint32_t rr = r;
-          r += c == kMixed ? 1u : 0u;
-          bool one_ok;
-          int32_t one = 0;
-          const uint32_t cn = count_of(c, rr, one_ok, one);
-          if ((multi >> k) & 1u) {
-            const uint64_t v = c == kMixed ? mres(rr) : pure(c);
-            const uint32_t first = (uint32_t)v;
-            uint32_t qq = q;
-            for (uint32_t mm = (uint32_t)(v >> 32); mm; mm &= mm - 1, qq++)
-              if (qq - w0 < (uint32_t)kEmitWin) {
-                s_poly[emit_swz(qq - w0)] = (uint32_t)t.chip_poly[first + __builtin_ctz(mm)];
-                s_pt[emit_swz(qq - w0)] = (uint16_t)(threadIdx.x * kClsItems + k);
-              }
-          }
-          q += cn;
-        }
-      }
-#else
       uint32_t q = off0;
       r = rank0;
 #pragma unroll
@@ -1695,7 +1624,6 @@ __global__ __launch_bounds__(kClsBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
             s_pt[emit_swz(q - w0)] = (uint16_t)(threadIdx.x * kClsItems + k);
           }
       }
-#endif
     }
     lds_barrier();
     const uint32_t cnt = total - w0 < (uint32_t)kEmitWin ? total - w0 : (uint32_t)kEmitWin;
