@@ -2218,51 +2218,28 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     for (int64_t k = 0; k < NC; k++) distinct.insert(distinct.end(), cd[k].begin(), cd[k].end());
   }
   BLOB_MARK("distinct");
-  Strips strips;
-  build_strips(n_chips, cflags, cpart, cenv, geo, strips, kBlobChunk);
-  BLOB_MARK("strips");
-  std::vector<mgpu::ChipHdr, NoInit<mgpu::ChipHdr>> chdr(n_chips);  // (every header written below)
-  {
-    // host view of the flattened geometry for the grid classification
-    mgpu::ChipTableView hv{};
-    hv.chip_flags = cflags.data();
-    hv.chip_part = cpart.data();
-    hv.chip_env = cenv.data();
-    hv.part_ring = geo.part_ring.data();
-    hv.ring_vtx = geo.ring_vtx.data();
-    hv.ring_env = geo.ring_env.data();
-    hv.vtx = geo.vtx.data();
-    // chips are independent: headers and classification grids in parallel
-    mgpu::parallel_for(n_chips, 1024, [&](int64_t cb, int64_t ce, int) {
-    for (int64_t c = cb; c < ce; c++) {
-      mgpu::ChipHdr& h = chdr[c];
-      memset(&h, 0, sizeof h);
-      for (int k = 0; k < 4; k++) h.env[k] = cenv[4 * c + k];
-      h.inv_h = strips.chip_sy[2 * c + 1];
-      h.strip_base = strips.chip_strip[c];
-      h.n_strips = (uint16_t)(strips.chip_strip[c + 1] - strips.chip_strip[c]);
-      h.flags = cflags[c];
-      const uint32_t pb = cpart[c], pe = cpart[c + 1];
-      h.single_ring = (pe - pb == 1 && geo.part_ring[pb + 1] - geo.part_ring[pb] == 1 &&
-                       !(cflags[c] & mgpu::kChipMulti)) ? 1 : 0;
-      if (h.n_strips) build_grid(hv, (uint32_t)c, geo, h);
-    }
-    });
-  }
-  BLOB_MARK("headers");
-  // H3: probe by lattice key when possible (chip_table.h)
+  // The cell side (H3 lattice keys and whole cells, the dense grid, the cell hash) needs
+  // only the distinct cells and the parsed geometry: it runs on its own thread while this
+  // one builds the strips and chip headers (independent work; the same results)
   int32_t probe_mode = mgpu::kProbeCellId, lres = -1;
   uint32_t face_mask = (1u << 20) - 1;
   double bbox[4] = {-1e300, -1e300, 1e300, 1e300};
   std::vector<mgpu::HashSlot> entries;
   std::vector<std::pair<uint64_t, uint32_t>> keys;
+  std::vector<uint64_t> grid;
+  mgpu::DenseFace dense[20];
+  memset(dense, 0, sizeof dense);
+  uint32_t bng_edge = 0;
+  uint32_t cap = 16;
+  std::vector<mgpu::HashSlot> slots;
+  uint32_t max_probe = 0;
+  const std::vector<uint8_t> cflags_pre = cflags;  // (build_strips adds kChipNoStrips to cflags meanwhile)
+  auto cell_side = [&]() -> int32_t {
+  // H3: probe by lattice key when possible (chip_table.h)
   if (index_system == MGPU_H3 && build_lattice(distinct, keys, &lres, &face_mask, bbox)) {
     probe_mode = mgpu::kProbeLattice;
-    BLOB_MARK("lat:keys");
-    mark_whole_cells(distinct, lres, bbox, cflags, cpart, geo);
-    BLOB_MARK("lat:whole");
+    mark_whole_cells(distinct, lres, bbox, cflags_pre, cpart, geo);
     parallel_sort(keys, [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) { return a < b; });
-    BLOB_MARK("lat:sort");
     // (per key in parallel: duplicate / collision, the entry's core mask; then in order)
     const int64_t nk = (int64_t)keys.size();
     std::vector<uint8_t> kdup(nk);
@@ -2297,12 +2274,8 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     entries = distinct;
     if (index_system == MGPU_H3 && !distinct.empty()) lres = (int32_t)((distinct[0].cell >> 52) & 15);
   }
-  BLOB_MARK("lattice");
   // dense lattice grid when the chip cells' (a, b) boxes are compact: one load per
   // point instead of a hash probe sequence (misses -- most points -- included)
-  std::vector<uint64_t> grid;
-  mgpu::DenseFace dense[20];
-  memset(dense, 0, sizeof dense);
   if (probe_mode == mgpu::kProbeLattice && !entries.empty()) {
     int64_t amin[20], amax[20], bmin[20], bmax[20];
     for (int f = 0; f < 20; f++) amin[f] = bmin[f] = INT64_MAX, amax[f] = bmax[f] = INT64_MIN;
@@ -2343,9 +2316,68 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
       probe_mode = mgpu::kProbeDense;
     }
   }
-  uint32_t bng_edge = 0;
   if (index_system == MGPU_BNG && build_bng_dense(distinct, &lres, &dense[0], &bng_edge, grid))
     probe_mode = mgpu::kProbeDense;
+  while (cap < 2 * entries.size()) cap <<= 1;
+  slots.assign(cap, mgpu::HashSlot{0, 0, 0, 0});
+  for (const auto& d : entries) {
+    uint32_t h = mgpu::cell_hash(d.cell) & (cap - 1), k = 0;
+    while (slots[h].count) {
+      h = (h + 1) & (cap - 1);
+      k++;
+    }
+    slots[h] = d;
+    max_probe = std::max(max_probe, k);
+  }
+
+    return MGPU_OK;
+  };
+  int32_t side_st = MGPU_OK;
+  std::string side_msg;  // (the error text is thread-local: carried back)
+  std::thread side;
+  try {
+    side = std::thread([&] {
+      side_st = cell_side();
+      if (side_st != MGPU_OK) side_msg = g_err;
+    });
+  } catch (...) {
+    side_st = cell_side();  // (no thread: in turn)
+    if (side_st != MGPU_OK) side_msg = g_err;
+  }
+  Strips strips;
+  build_strips(n_chips, cflags, cpart, cenv, geo, strips, kBlobChunk);
+  BLOB_MARK("strips");
+  std::vector<mgpu::ChipHdr, NoInit<mgpu::ChipHdr>> chdr(n_chips);  // (every header written below)
+  {
+    // host view of the flattened geometry for the grid classification
+    mgpu::ChipTableView hv{};
+    hv.chip_flags = cflags.data();
+    hv.chip_part = cpart.data();
+    hv.chip_env = cenv.data();
+    hv.part_ring = geo.part_ring.data();
+    hv.ring_vtx = geo.ring_vtx.data();
+    hv.ring_env = geo.ring_env.data();
+    hv.vtx = geo.vtx.data();
+    // chips are independent: headers and classification grids in parallel
+    mgpu::parallel_for(n_chips, 1024, [&](int64_t cb, int64_t ce, int) {
+    for (int64_t c = cb; c < ce; c++) {
+      mgpu::ChipHdr& h = chdr[c];
+      memset(&h, 0, sizeof h);
+      for (int k = 0; k < 4; k++) h.env[k] = cenv[4 * c + k];
+      h.inv_h = strips.chip_sy[2 * c + 1];
+      h.strip_base = strips.chip_strip[c];
+      h.n_strips = (uint16_t)(strips.chip_strip[c + 1] - strips.chip_strip[c]);
+      h.flags = cflags[c];
+      const uint32_t pb = cpart[c], pe = cpart[c + 1];
+      h.single_ring = (pe - pb == 1 && geo.part_ring[pb + 1] - geo.part_ring[pb] == 1 &&
+                       !(cflags[c] & mgpu::kChipMulti)) ? 1 : 0;
+      if (h.n_strips) build_grid(hv, (uint32_t)c, geo, h);
+    }
+    });
+  }
+  if (side.joinable()) side.join();
+  if (side_st != MGPU_OK) return fail(side_st, "%s", side_msg.c_str());
+  BLOB_MARK("cells");
   BLOB_MARK("dense");
   // pixel index over the dense grid (chip_table.h, build_raster_*), BNG cell answer grids
   Raster raster;
@@ -2371,20 +2403,6 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   fprintf(stderr, "[blob] raster mode %d, %u x %u pixels, %zu classes (one-match below %u)\n", raster.mode, raster.nx,
           raster.ny, raster.cls.size(), raster.pc[0]);
 #endif
-  uint32_t cap = 16;
-  while (cap < 2 * entries.size()) cap <<= 1;
-  std::vector<mgpu::HashSlot> slots(cap, mgpu::HashSlot{0, 0, 0, 0});
-  uint32_t max_probe = 0;
-  for (const auto& d : entries) {
-    uint32_t h = mgpu::cell_hash(d.cell) & (cap - 1), k = 0;
-    while (slots[h].count) {
-      h = (h + 1) & (cap - 1);
-      k++;
-    }
-    slots[h] = d;
-    max_probe = std::max(max_probe, k);
-  }
-
   BLOB_MARK("hash");
   // lonlat classes with one match -> their polygon (ChipTableView::raster_cls_poly)
   std::vector<int32_t> cls_poly;
