@@ -1,7 +1,5 @@
 #!/bin/bash
-# Round-5 final bench lines on the final build, after its counters are in profiles/ (each
-# line attaches its keyed traffic and VALU profile): C2-C5 with kernel traces, C4 at 500M.
+# Round-5 final bench lines on the final build, part 1, after its counters are in profiles/
+# (each line attaches its keyed traffic and VALU profile): C2, C5, C4 with kernel traces.
 set -o pipefail
-bash tools/gpu_final_r5.sh f5w "c2 c3 c4 c5" || exit 1
-timeout -k 10 600 python3 -u bench.py --config c4 --points 500000000 --res 3 > gpurun_out/final_f5w_c4_500m_r3.json 2> gpurun_out/final_f5w_c4_500m_r3.err || { echo "c4 500m failed"; tail -5 gpurun_out/final_f5w_c4_500m_r3.err; exit 1; }
-python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print('c4 500M r3', '%.3e'%d['value'], '%.3f ms'%d['ms_per_step'], d.get('kernels_ms'), 'frac %.3f'%d['roofline']['frac'], 'traffic', d['roofline'].get('traffic'))" gpurun_out/final_f5w_c4_500m_r3.json
+bash tools/gpu_final_r5.sh f5w "c2 c5 c4"
