@@ -404,8 +404,11 @@ bool build_lattice(const std::vector<mgpu::HashSlot>& cells, std::vector<std::pa
 // the edge in its strip.
 // An allocator whose resize() leaves new elements uninitialised (the builders write every
 // element, in parallel; a zero-filling resize of a GB-sized array is a serial pass).
+// the builder's per-chip arrays (huge_alloc.h)
 template <class T>
-struct NoInit : std::allocator<T> {
+using HVec = std::vector<T, mgpu::HugeAlloc<T>>;
+template <class T>
+struct NoInit : mgpu::HugeAlloc<T> {
   template <class U>
   struct rebind {
     using other = NoInit<U>;
@@ -424,15 +427,15 @@ struct NoInit : std::allocator<T> {
 };
 
 struct Strips {
-  std::vector<uint32_t> chip_strip;
-  std::vector<double> chip_sy;
-  std::vector<uint32_t> strip_edge{0};
+  HVec<uint32_t> chip_strip;
+  HVec<double> chip_sy;
+  HVec<uint32_t> strip_edge{0};
   std::vector<double, NoInit<double>> edges;
-  std::vector<uint8_t> edge_ring;
+  HVec<uint8_t> edge_ring;
 };
 
-void build_strips(int64_t n_chips, std::vector<uint8_t>& cflags, const std::vector<uint32_t>& cpart,
-                  const std::vector<double>& cenv, const mgpu::wkb::Flat& geo, Strips& st, int64_t G) {
+void build_strips(int64_t n_chips, HVec<uint8_t>& cflags, const HVec<uint32_t>& cpart,
+                  const HVec<double>& cenv, const mgpu::wkb::Flat& geo, Strips& st, int64_t G) {
   st.chip_strip.assign(n_chips + 1, 0);
   st.chip_sy.assign(2 * (size_t)n_chips, 0.0);
   // chunks of G chips in parallel, each into its own strip / edge lists (chip_strip then
@@ -2004,8 +2007,8 @@ constexpr int64_t kBlobChunk = 1 << 14;
 
 // std::sort of v by cmp (a strict total order) on the host threads: chunks sorted in
 // parallel, then pairwise merge rounds
-template <class T, class Cmp>
-static void parallel_sort(std::vector<T>& v, Cmp cmp) {
+template <class V, class Cmp>
+static void parallel_sort(V& v, Cmp cmp) {
   const int64_t n = (int64_t)v.size();
   const int64_t P = mgpu::parallel_slots(n, 1 << 16);
   if (P <= 1) {
@@ -2017,7 +2020,7 @@ static void parallel_sort(std::vector<T>& v, Cmp cmp) {
   mgpu::parallel_for(P, 1, [&](int64_t kb, int64_t ke, int) {
     for (int64_t k = kb; k < ke; k++) std::sort(v.begin() + b[k], v.begin() + b[k + 1], cmp);
   });
-  std::vector<T> tmp(v.size());
+  V tmp(v.size());
   for (int64_t w = 1; w < P; w *= 2) {
     const int64_t jobs = (P + 2 * w - 1) / (2 * w);
     mgpu::parallel_for(jobs, 1, [&](int64_t jb, int64_t je, int) {
@@ -2045,7 +2048,7 @@ static void parallel_sort(std::vector<T>& v, Cmp cmp) {
 // res >= 6 and |lat| <= 75) without a candidate (kernels.hip phase1_item).
 // (profiles/r4_whole_cell_ab.txt: C3 candidates 68.5M -> 55.6M per 1e8 points.)
 void mark_whole_cells(std::vector<mgpu::HashSlot>& cells, int res,
-                      const double bbox[4], const std::vector<uint8_t>& cflags, const std::vector<uint32_t>& cpart,
+                      const double bbox[4], const HVec<uint8_t>& cflags, const HVec<uint32_t>& cpart,
                       const mgpu::wkb::Flat& geo) {
   if (res < 6 || !(bbox[1] >= -75.0 && bbox[3] <= 75.0)) return;
   mgpu::parallel_for((int64_t)cells.size(), 4096, [&](int64_t b, int64_t e, int) {
@@ -2090,7 +2093,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   BLOB_T0();
   // chips sorted by (cell, polygon id, input row): chunks sorted in parallel, merged in
   // parallel rounds
-  std::vector<int64_t> order(n_chips);
+  HVec<int64_t> order(n_chips);
   for (int64_t i = 0; i < n_chips; i++) order[i] = i;
   parallel_sort(order, [&](int64_t a, int64_t b) {
     if (cell[a] != cell[b]) return cell[a] < cell[b];
@@ -2102,12 +2105,12 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   // the chips' WKB parsed in parallel: each chunk of sorted chips into its own flat
   // geometry, then the chunks concatenated with their offsets shifted
   mgpu::wkb::Flat geo;  // parts / rings / vertices of all chips, in sorted order
-  std::vector<int32_t> cpoly(n_chips);
-  std::vector<uint8_t> cflags(n_chips);
-  std::vector<uint32_t> cpart(n_chips + 1);
-  std::vector<double> cenv(4 * (size_t)n_chips);
-  std::vector<int64_t> crow(n_chips);
-  std::vector<uint32_t> row2chip(n_chips);
+  HVec<int32_t> cpoly(n_chips);
+  HVec<uint8_t> cflags(n_chips);
+  HVec<uint32_t> cpart(n_chips + 1);
+  HVec<double> cenv(4 * (size_t)n_chips);
+  HVec<int64_t> crow(n_chips);
+  HVec<uint32_t> row2chip(n_chips);
   {
     const int64_t G = kBlobChunk, NC = (n_chips + G - 1) / G;
     std::vector<mgpu::wkb::Flat> cf(NC);
@@ -2233,7 +2236,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   uint32_t cap = 16;
   std::vector<mgpu::HashSlot> slots;
   uint32_t max_probe = 0;
-  const std::vector<uint8_t> cflags_pre = cflags;  // (build_strips adds kChipNoStrips to cflags meanwhile)
+  const HVec<uint8_t> cflags_pre = cflags;  // (build_strips adds kChipNoStrips to cflags meanwhile)
   auto cell_side = [&]() -> int32_t {
   // H3: probe by lattice key when possible (chip_table.h)
   if (index_system == MGPU_H3 && build_lattice(distinct, keys, &lres, &face_mask, bbox)) {

@@ -19,16 +19,20 @@
 #include <string>
 #include <vector>
 
+#include "huge_alloc.h"
+
 namespace mgpu {
 namespace wkb {
 
 // Flattened polygons: part -> rings [part_ring[p], part_ring[p+1]),
 // ring -> vertices [ring_vtx[r], ring_vtx[r+1]) in vtx (x, y pairs).
 struct Flat {
-  std::vector<uint32_t> part_ring{0};
-  std::vector<uint32_t> ring_vtx{0};
-  std::vector<double> ring_env;  // minx, miny, maxx, maxy per ring
-  std::vector<double> vtx;
+  template <class T>
+  using Vec = std::vector<T, HugeAlloc<T>>;  // (multi-GB for large tables: huge_alloc.h)
+  Vec<uint32_t> part_ring{0};
+  Vec<uint32_t> ring_vtx{0};
+  Vec<double> ring_env;  // minx, miny, maxx, maxy per ring
+  Vec<double> vtx;
 };
 
 struct GeomInfo {
