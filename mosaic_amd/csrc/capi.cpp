@@ -936,14 +936,17 @@ struct QuadAxes {
     }
   }
 };
-bool hex_meets_quad(int64_t a, int64_t b, const QuadAxes& Q, const HexFrame& F, double d) {
+// (first: the axis tried first -- the hexagon normal facing a neighbour separates it from
+// a quad inside the centre cell at once; the answer does not depend on the order)
+bool hex_meets_quad(int64_t a, int64_t b, const QuadAxes& Q, const HexFrame& F, double d, int first = 0) {
   const double cx = (double)a - 0.5 * (double)b, cy = (double)b * mgpu::h3::kSin60;
   double hv[6][2];
   for (int k = 0; k < 6; k++) {
     hv[k][0] = cx + F.off[k][0];
     hv[k][1] = cy + F.off[k][1];
   }
-  for (int k = 0; k < 7; k++) {
+  for (int i = 0; i < 7; i++) {
+    const int k = i == 0 ? first : (i <= first ? i - 1 : i);
     if (!Q.valid[k]) continue;
     double h0 = 1e300, h1 = -1e300;
     for (int p = 0; p < 6; p++) {
@@ -1128,6 +1131,7 @@ uint64_t h3_rect_answer(const H3RasterCtx& X, double xa, double ya, double xb, d
   // every cell a point of the rectangle can take is h0 or a neighbour (L < 1/2) whose
   // hexagon meets the quad; all must give the same polygon list
   static const int da[7] = {0, 1, -1, 0, 0, 1, -1}, db[7] = {0, 0, 0, 1, -1, 1, -1};
+  static const int kFacing[7] = {0, 0, 0, 2, 2, 1, 1};  // (the normal toward neighbour k: 0, 120, 60 degrees)
   static const HexFrame HF;
   const QuadAxes QA(q, HF);
   const mgpu::DenseFace& D = X.dense[c[0]->face];
@@ -1137,7 +1141,7 @@ uint64_t h3_rect_answer(const H3RasterCtx& X, double xa, double ya, double xb, d
     const int64_t a = a0 + da[k], b = b0 + db[k];
     // (k = 0, h0: the cell of corner q[0], which lies in its hexagon -- the separating
     // axis test cannot part them by the margin d_hex >= 1e-9, far above q[0]'s rounding)
-    if (k > 0 && !hex_meets_quad(a, b, QA, HF, d_hex)) continue;
+    if (k > 0 && !hex_meets_quad(a, b, QA, HF, d_hex, kFacing[k])) continue;
     const uint64_t ua = (uint64_t)(a - D.a0), ub = (uint64_t)(b - D.b0);
     const uint64_t e = (ua < D.w && ub < D.h) ? X.grid[D.base + ub * D.w + ua] : 0;
     const int64_t m = pixel_answer(X.hv, e, xa - mux, ya - muy, xb + mux, yb + muy, pe);
