@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <unordered_map>
+#include <unordered_set>
 #include <chrono>
 #include <sched.h>
 #include <array>
@@ -699,7 +700,7 @@ struct Raster {
   // sub_n x sub_n sub-pixel classes at sub[b * sub_n^2 ..] (BNG: sub-pixel edge sub_w metres)
   uint32_t sub_n = 0, sub_w = 0;
   std::vector<mgpu::RankWord> rank;
-  std::vector<uint16_t> sub;
+  std::vector<uint16_t, NoInit<uint16_t>> sub;
   // lonlat: band[k] = the refined pixels before raster rows k << band_shift (rank unused)
   uint32_t band_shift = 0;
   std::vector<uint32_t> band;
@@ -915,7 +916,8 @@ struct HexFrame {  // the hexagon's vertex offsets (circumradius R at 30 + 60 k 
 struct QuadAxes {
   double n[7][2], lo[7], hi[7];
   bool valid[7];
-  QuadAxes(const double q[4][2], const HexFrame& F) {
+  // (el[e]: the length of edge q[e] -> q[(e + 1) % 4], as std::hypot gives it)
+  QuadAxes(const double q[4][2], const HexFrame& F, const double el[4]) {
     for (int k = 0; k < 7; k++) {
       valid[k] = true;
       if (k < 3) {
@@ -923,7 +925,7 @@ struct QuadAxes {
       } else {
         const int e = k - 3;
         const double ex = q[(e + 1) % 4][0] - q[e][0], ey = q[(e + 1) % 4][1] - q[e][1];
-        const double l = std::hypot(ex, ey);
+        const double l = el[e];
         valid[k] = l > 0;
         n[k][0] = valid[k] ? -ey / l : 0.0, n[k][1] = valid[k] ? ex / l : 0.0;
       }
@@ -974,10 +976,11 @@ constexpr uint64_t kAnsMixed = ~0ULL;
 // share a class, represented by the first such answer), ordered by their number of
 // matches so a class id tells its pair count (pc[k]: the first class with more than
 // k + 1 matches)
-void raster_classes(const mgpu::ChipTableView& hv, const std::vector<uint64_t>& a1, const std::vector<uint64_t>& a2,
-                    Raster& R) {
+using AnsVec = std::vector<uint64_t, NoInit<uint64_t>>;  // (level 2's answers: every one written, in parallel)
+void raster_classes(const mgpu::ChipTableView& hv, const std::vector<uint64_t>& a1, const AnsVec& a2, Raster& R) {
   R.cells.assign(a1.size(), mgpu::kPixMixed);
-  R.sub.assign(a2.size(), mgpu::kPixMixed);
+  R.sub.clear();
+  R.sub.resize(a2.size());  // (every slot written below)
   R.cls.assign(1, 0);
   auto slot = [&](size_t i) -> uint16_t& { return i < a1.size() ? R.cells[i] : R.sub[i - a1.size()]; };
   auto polys_of = [&](uint64_t v) {
@@ -986,18 +989,34 @@ void raster_classes(const mgpu::ChipTableView& hv, const std::vector<uint64_t>& 
     return ps;
   };
   // distinct answers -> their polygon lists -> classes
-  // (a hash of the distinct answers; neighbouring pixels mostly repeat the previous one)
+  // (a hash of the distinct answers; neighbouring pixels mostly repeat the previous one).
+  // The classes and their representatives follow the answers' first appearance in pixel
+  // order: each chunk lists its distinct answers in the order they first appear in it,
+  // and the chunks' lists, read in chunk order with the ones seen dropped, are that order.
+  const size_t n_all = a1.size() + a2.size();
+  constexpr int64_t kChunk = 1 << 20;
+  std::vector<std::vector<uint64_t>> firsts((n_all + kChunk - 1) / kChunk);
+  mgpu::parallel_for((int64_t)firsts.size(), 1, [&](int64_t cb, int64_t ce, int) {
+    for (int64_t ch = cb; ch < ce; ch++) {
+      std::unordered_set<uint64_t> seen;
+      uint64_t last = kAnsMixed;
+      for (size_t i = (size_t)ch * kChunk; i < std::min(n_all, (size_t)(ch + 1) * kChunk); i++) {
+        const uint64_t v = i < a1.size() ? a1[i] : a2[i - a1.size()];
+        if (v == last) continue;
+        last = v;
+        if (v == kAnsMixed || (v >> 32) == 0 || !seen.insert(v).second) continue;
+        firsts[ch].push_back(v);
+      }
+    }
+  });
   std::unordered_map<uint64_t, int32_t> answer_key;
   answer_key.reserve(1 << 16);
   std::map<std::vector<int32_t>, int32_t> list_key;
   std::vector<uint64_t> rep;  // per list: the representative answer
   std::vector<std::vector<int32_t>> lists;
-  uint64_t last = kAnsMixed;
-  for (size_t i = 0; i < a1.size() + a2.size(); i++) {
-    const uint64_t v = i < a1.size() ? a1[i] : a2[i - a1.size()];
-    if (v == last) continue;
-    last = v;
-    if (v == kAnsMixed || (v >> 32) == 0 || answer_key.count(v)) continue;
+  for (const auto& fc : firsts)
+  for (const uint64_t v : fc) {
+    if (answer_key.count(v)) continue;
     auto ps = polys_of(v);
     auto it = list_key.find(ps);
     if (it == list_key.end()) {
@@ -1018,22 +1037,22 @@ void raster_classes(const mgpu::ChipTableView& hv, const std::vector<uint64_t>& 
     cls_of[k] = (int32_t)R.cls.size();
     R.cls.push_back(rep[k]);
   }
-  const size_t n_all = a1.size() + a2.size();
   mgpu::parallel_for((int64_t)n_all, 1 << 16, [&](int64_t b, int64_t e, int) {
     uint64_t lv = kAnsMixed;
     int32_t lc = -1;
     for (int64_t i = b; i < e; i++) {
       const uint64_t v = (size_t)i < a1.size() ? a1[i] : a2[i - a1.size()];
-      if (v == kAnsMixed) continue;
-      if ((v >> 32) == 0) {
-        slot((size_t)i) = mgpu::kPixEmpty;
-        continue;
+      uint16_t out = mgpu::kPixMixed;
+      if (v != kAnsMixed && (v >> 32) == 0) {
+        out = mgpu::kPixEmpty;
+      } else if (v != kAnsMixed) {
+        if (v != lv) {
+          lv = v;
+          lc = cls_of[answer_key.find(v)->second];
+        }
+        if (lc >= 0) out = (uint16_t)lc;
       }
-      if (v != lv) {
-        lv = v;
-        lc = cls_of[answer_key.find(v)->second];
-      }
-      if (lc >= 0) slot((size_t)i) = (uint16_t)lc;
+      slot((size_t)i) = out;
     }
   });
   auto pc = [](uint64_t v) { return __builtin_popcountll(v >> 32); };
@@ -1104,7 +1123,9 @@ void raster_blocks(Raster& R) {
 // whose corners c (projected at exactly those points, in the order (xa, ya), (xb, ya),
 // (xb, yb), (xa, yb)) are given; the certificate is checked on the rectangle widened by
 // (mux, muy) -- its corners lie within ~1e-6 of its size of c, a deviation the margins
-// below carry -- or kAnsMixed.
+// below carry -- or kAnsMixed.  (el: the four edge lengths when the caller has them --
+// a grid of sub-pixels shares each edge between two of them -- else computed here; the
+// side lengths enter both the diameter L and the quad's edge normals)
 struct H3RasterCtx {
   const mgpu::ChipTableView& hv;
   int res;
@@ -1114,11 +1135,16 @@ struct H3RasterCtx {
 };
 uint64_t h3_rect_answer(const H3RasterCtx& X, double xa, double ya, double xb, double yb, const Corner* c[4],
                         double mux, double muy, std::vector<int32_t>& polys, std::vector<int32_t>& ref,
-                        PixelEdges* pe = nullptr) {
-  double q[4][2], L = 0;
+                        PixelEdges* pe = nullptr, const double* el = nullptr) {
+  double q[4][2], e4[4];
   for (int p = 0; p < 4; p++) q[p][0] = c[p]->x, q[p][1] = c[p]->y;
-  for (int p = 0; p < 4; p++)
-    for (int r = p + 1; r < 4; r++) L = std::max(L, std::hypot(q[p][0] - q[r][0], q[p][1] - q[r][1]));
+  // (|a - b| = |b - a| exactly: the sides and the two diagonals are the six corner pairs)
+  for (int e = 0; e < 4; e++)
+    e4[e] = el ? el[e] : std::hypot(q[(e + 1) % 4][0] - q[e][0], q[(e + 1) % 4][1] - q[e][1]);
+  double L = 0;
+  for (int e = 0; e < 4; e++) L = std::max(L, e4[e]);
+  L = std::max(L, std::hypot(q[0][0] - q[2][0], q[0][1] - q[2][1]));
+  L = std::max(L, std::hypot(q[1][0] - q[3][0], q[1][1] - q[3][1]));
   const double ang = std::hypot(xb - xa + 2 * mux, yb - ya + 2 * muy) * kPi / 180.0;  // angular diagonal bound
   const double d_face = 1e-12 + 8.0 * ang * ang + 8e-6 * ang;
   const double d_hex = 1e-9 * (1.0 + std::fabs(q[0][0]) + std::fabs(q[0][1])) + 8.0 * L * L / X.k_res + 8e-6 * L;
@@ -1133,7 +1159,7 @@ uint64_t h3_rect_answer(const H3RasterCtx& X, double xa, double ya, double xb, d
   static const int da[7] = {0, 1, -1, 0, 0, 1, -1}, db[7] = {0, 0, 0, 1, -1, 1, -1};
   static const int kFacing[7] = {0, 0, 0, 2, 2, 1, 1};  // (the normal toward neighbour k: 0, 120, 60 degrees)
   static const HexFrame HF;
-  const QuadAxes QA(q, HF);
+  const QuadAxes QA(q, HF, e4);
   const mgpu::DenseFace& D = X.dense[c[0]->face];
   bool first = true;
   uint64_t cls = 0;
@@ -1191,6 +1217,9 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
     return iy + f >= R.ny ? std::max(R.y0 + R.ny * sy, bbox[3]) : R.y0 + (iy + f) * sy;
   };
   const H3RasterCtx X{hv, res, k_res, dense, grid};
+#ifdef MGPU_BLOB_TIMING
+  const auto rl0 = std::chrono::steady_clock::now();
+#endif
   // level 1: corners on the pixel grid, two rows at a time
   std::vector<uint64_t> a1((size_t)R.nx * R.ny, kAnsMixed);
   {
@@ -1216,10 +1245,10 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
   }
 #ifdef MGPU_BLOB_TIMING
   auto rt0 = std::chrono::steady_clock::now();
-  fprintf(stderr, "[raster] level 1 done: %u x %u pixels\n", R.nx, R.ny);
+  fprintf(stderr, "[raster] level 1: %u x %u pixels, %.3f s\n", R.nx, R.ny, std::chrono::duration<double>(rt0 - rl0).count());
 #endif
   // level 2: the mixed pixels cut into S x S sub-pixels
-  std::vector<uint64_t> a2;
+  AnsVec a2;
 #ifdef MGPU_BLOB_TIMING
   int64_t t_corner_ns_total = 0;
 #endif
@@ -1234,7 +1263,7 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
   if (S >= 2 && !mixed.empty()) {
     R.sub_n = (uint32_t)S;
     mixed_rank(mixed, a1.size(), R.rank);
-    a2.assign(mixed.size() * S * S, kAnsMixed);
+    a2.resize(mixed.size() * S * S);  // (every answer written below)
     const double mux = 1e-6 * sx / S + 64 * ulp, muy = 1e-6 * sy / S + 64 * ulp;
     const double pmux = 1e-6 * sx + 64 * ulp, pmuy = 1e-6 * sy + 64 * ulp;  // (level 1's widening: holds every sub-pixel's)
 #ifdef MGPU_BLOB_TIMING
@@ -1249,6 +1278,7 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
       std::vector<int32_t> polys, ref;
       std::vector<Corner> cg((size_t)(S + 1) * (S + 1));
       std::vector<SinCos> scx(S + 1);
+      std::vector<double> hl((size_t)(S + 1) * S), vl((size_t)S * (S + 1));  // sub-pixel side lengths
       PixelEdges pe;
       for (int64_t k = kb; k < ke; k++) {
         const uint32_t ix = mixed[k] % R.nx, iy = mixed[k] / R.nx;
@@ -1264,13 +1294,20 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
 #ifdef MGPU_BLOB_TIMING
         t_corner_ns += (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tc0).count();
 #endif
+        for (int v = 0; v <= S; v++)
+          for (int u = 0; u <= S; u++) {
+            const Corner& o = cg[v * (S + 1) + u];
+            if (u < S) hl[v * S + u] = std::hypot(cg[v * (S + 1) + u + 1].x - o.x, cg[v * (S + 1) + u + 1].y - o.y);
+            if (v < S) vl[v * (S + 1) + u] = std::hypot(cg[(v + 1) * (S + 1) + u].x - o.x, cg[(v + 1) * (S + 1) + u].y - o.y);
+          }
         for (int v = 0; v < S; v++)
           for (int u = 0; u < S; u++) {
             const Corner* c[4] = {&cg[v * (S + 1) + u], &cg[v * (S + 1) + u + 1], &cg[(v + 1) * (S + 1) + u + 1],
                                   &cg[(v + 1) * (S + 1) + u]};
+            const double el[4] = {hl[v * S + u], vl[v * (S + 1) + u + 1], hl[(v + 1) * S + u], vl[v * (S + 1) + u]};
             a2[(size_t)k * S * S + v * S + u] = h3_rect_answer(X, xe(ix, (double)u / S), ye(iy, (double)v / S),
                                                                xe(ix, (double)(u + 1) / S), ye(iy, (double)(v + 1) / S), c,
-                                                               mux, muy, polys, ref, &pe);
+                                                               mux, muy, polys, ref, &pe, el);
           }
       }
     });
