@@ -864,11 +864,23 @@ Corner h3_corner_sc(const SinCos& lon, const SinCos& lat, int res, double k_res)
   Corner o;
   const double slat = lat.s, clat = lat.c, slon = lon.s, clon = lon.c;
   const double vx = clon * clat, vy = slon * clat, vz = slat;
+  // the squared chords to the 20 face centres (a vector loop over the centres' columns),
+  // then the nearest (the first of equals) and the next -- the second smallest of the 20
+  struct FaceCols {
+    double x[20], y[20], z[20];
+    FaceCols() {
+      for (int f = 0; f < 20; f++) x[f] = H3T_FACE_CENTER_POINT[f][0], y[f] = H3T_FACE_CENTER_POINT[f][1], z[f] = H3T_FACE_CENTER_POINT[f][2];
+    }
+  };
+  static const FaceCols FC;
+  double sq[20];
+  for (int f = 0; f < 20; f++) {
+    const double dx = FC.x[f] - vx, dy = FC.y[f] - vy, dz = FC.z[f] - vz;
+    sq[f] = dx * dx + dy * dy + dz * dz;
+  }
   double best = 5.0, second = 5.0;
   for (int f = 0; f < 20; f++) {
-    const double dx = H3T_FACE_CENTER_POINT[f][0] - vx, dy = H3T_FACE_CENTER_POINT[f][1] - vy,
-                 dz = H3T_FACE_CENTER_POINT[f][2] - vz;
-    const double s = dx * dx + dy * dy + dz * dz;
+    const double s = sq[f];
     if (s < best) {
       second = best;
       best = s;
@@ -954,6 +966,66 @@ bool hex_meets_quad(int64_t a, int64_t b, const QuadAxes& Q, const HexFrame& F, 
     for (int p = 0; p < 6; p++) {
       const double v = hv[p][0] * Q.n[k][0] + hv[p][1] * Q.n[k][1];
       h0 = std::min(h0, v), h1 = std::max(h1, v);
+    }
+    if (h1 + d < Q.lo[k] || Q.hi[k] + d < h0) return false;
+  }
+  return true;
+}
+
+// The hexagon side of the test on the hexagon's own three normals does not depend on the
+// quad: the seven hexagons around one lattice position keep their extents along them in
+// a per-thread cache (neighbouring sub-pixels mostly share that position), computed by
+// hex_meets_quad's own expressions, so the answers are the same.
+struct HexAxisCache {
+  int64_t a0 = INT64_MIN, b0 = INT64_MIN;
+  double lo[7][3], hi[7][3];
+};
+static const int kHexDa[7] = {0, 1, -1, 0, 0, 1, -1}, kHexDb[7] = {0, 0, 0, 1, -1, 1, -1};
+void hex_axis_fill(HexAxisCache& C, int64_t a0, int64_t b0, const HexFrame& F) {
+  C.a0 = a0, C.b0 = b0;
+  for (int h = 0; h < 7; h++) {
+    const int64_t a = a0 + kHexDa[h], b = b0 + kHexDb[h];
+    const double cx = (double)a - 0.5 * (double)b, cy = (double)b * mgpu::h3::kSin60;
+    double hv[6][2];
+    for (int k = 0; k < 6; k++) {
+      hv[k][0] = cx + F.off[k][0];
+      hv[k][1] = cy + F.off[k][1];
+    }
+    for (int k = 0; k < 3; k++) {
+      double h0 = 1e300, h1 = -1e300;
+      for (int p = 0; p < 6; p++) {
+        const double v = hv[p][0] * F.nrm[k][0] + hv[p][1] * F.nrm[k][1];
+        h0 = std::min(h0, v), h1 = std::max(h1, v);
+      }
+      C.lo[h][k] = h0, C.hi[h][k] = h1;
+    }
+  }
+}
+// hex_meets_quad for hexagon h of the cache's position (the same axes in the same order)
+bool hex_meets_quad_cached(const HexAxisCache& C, int h, const QuadAxes& Q, const HexFrame& F, double d, int first) {
+  bool have_hv = false;
+  double hv[6][2];
+  for (int i = 0; i < 7; i++) {
+    const int k = i == 0 ? first : (i <= first ? i - 1 : i);
+    if (!Q.valid[k]) continue;
+    double h0, h1;
+    if (k < 3) {
+      h0 = C.lo[h][k], h1 = C.hi[h][k];
+    } else {
+      if (!have_hv) {
+        const int64_t a = C.a0 + kHexDa[h], b = C.b0 + kHexDb[h];
+        const double cx = (double)a - 0.5 * (double)b, cy = (double)b * mgpu::h3::kSin60;
+        for (int p = 0; p < 6; p++) {
+          hv[p][0] = cx + F.off[p][0];
+          hv[p][1] = cy + F.off[p][1];
+        }
+        have_hv = true;
+      }
+      h0 = 1e300, h1 = -1e300;
+      for (int p = 0; p < 6; p++) {
+        const double v = hv[p][0] * Q.n[k][0] + hv[p][1] * Q.n[k][1];
+        h0 = std::min(h0, v), h1 = std::max(h1, v);
+      }
     }
     if (h1 + d < Q.lo[k] || Q.hi[k] + d < h0) return false;
   }
@@ -1135,7 +1207,7 @@ struct H3RasterCtx {
 };
 uint64_t h3_rect_answer(const H3RasterCtx& X, double xa, double ya, double xb, double yb, const Corner* c[4],
                         double mux, double muy, std::vector<int32_t>& polys, std::vector<int32_t>& ref,
-                        PixelEdges* pe = nullptr, const double* el = nullptr) {
+                        PixelEdges* pe = nullptr, const double* el = nullptr, HexAxisCache* hc = nullptr) {
   double q[4][2], e4[4];
   for (int p = 0; p < 4; p++) q[p][0] = c[p]->x, q[p][1] = c[p]->y;
   // (|a - b| = |b - a| exactly: the sides and the two diagonals are the six corner pairs)
@@ -1156,10 +1228,12 @@ uint64_t h3_rect_answer(const H3RasterCtx& X, double xa, double ya, double xb, d
   const int64_t a0 = h0.i - h0.k, b0 = h0.j - h0.k;
   // every cell a point of the rectangle can take is h0 or a neighbour (L < 1/2) whose
   // hexagon meets the quad; all must give the same polygon list
-  static const int da[7] = {0, 1, -1, 0, 0, 1, -1}, db[7] = {0, 0, 0, 1, -1, 1, -1};
+  static const int* da = kHexDa;
+  static const int* db = kHexDb;
   static const int kFacing[7] = {0, 0, 0, 2, 2, 1, 1};  // (the normal toward neighbour k: 0, 120, 60 degrees)
   static const HexFrame HF;
   const QuadAxes QA(q, HF, e4);
+  if (hc && (hc->a0 != a0 || hc->b0 != b0)) hex_axis_fill(*hc, a0, b0, HF);
   const mgpu::DenseFace& D = X.dense[c[0]->face];
   bool first = true;
   uint64_t cls = 0;
@@ -1167,7 +1241,8 @@ uint64_t h3_rect_answer(const H3RasterCtx& X, double xa, double ya, double xb, d
     const int64_t a = a0 + da[k], b = b0 + db[k];
     // (k = 0, h0: the cell of corner q[0], which lies in its hexagon -- the separating
     // axis test cannot part them by the margin d_hex >= 1e-9, far above q[0]'s rounding)
-    if (k > 0 && !hex_meets_quad(a, b, QA, HF, d_hex, kFacing[k])) continue;
+    if (k > 0 && !(hc ? hex_meets_quad_cached(*hc, k, QA, HF, d_hex, kFacing[k]) : hex_meets_quad(a, b, QA, HF, d_hex, kFacing[k])))
+      continue;
     const uint64_t ua = (uint64_t)(a - D.a0), ub = (uint64_t)(b - D.b0);
     const uint64_t e = (ua < D.w && ub < D.h) ? X.grid[D.base + ub * D.w + ua] : 0;
     const int64_t m = pixel_answer(X.hv, e, xa - mux, ya - muy, xb + mux, yb + muy, pe);
@@ -1280,6 +1355,7 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
       std::vector<SinCos> scx(S + 1);
       std::vector<double> hl((size_t)(S + 1) * S), vl((size_t)S * (S + 1));  // sub-pixel side lengths
       PixelEdges pe;
+      HexAxisCache hc;
       for (int64_t k = kb; k < ke; k++) {
         const uint32_t ix = mixed[k] % R.nx, iy = mixed[k] / R.nx;
         pe.reset(xe(ix, 0) - pmux, ye(iy, 0) - pmuy, xe(ix, 1) + pmux, ye(iy, 1) + pmuy);
@@ -1307,7 +1383,7 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
             const double el[4] = {hl[v * S + u], vl[v * (S + 1) + u + 1], hl[(v + 1) * S + u], vl[v * (S + 1) + u]};
             a2[(size_t)k * S * S + v * S + u] = h3_rect_answer(X, xe(ix, (double)u / S), ye(iy, (double)v / S),
                                                                xe(ix, (double)(u + 1) / S), ye(iy, (double)(v + 1) / S), c,
-                                                               mux, muy, polys, ref, &pe, el);
+                                                               mux, muy, polys, ref, &pe, el, &hc);
           }
       }
     });
