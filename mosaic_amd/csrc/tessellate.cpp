@@ -336,6 +336,8 @@ struct Grid {
   // ring, or several (H3: a cell cut at the antimeridian); empty = no geometry
   virtual int64_t cell_id(long i, long j) const = 0;
   virtual std::vector<std::vector<Pt>> boundary(long i, long j) const = 0;
+  // the same, for a cell whose id the caller has (cell_id(i, j))
+  virtual std::vector<std::vector<Pt>> boundary_of(long i, long j, int64_t) const { return boundary(i, j); }
   // a cell whose reference geometry is a clockwise ring (H3's south polar cap)
   virtual bool cw_ring(int64_t) const { return false; }
   // the cell's centre in input coords (H3: h3ToGeo; BNG: the square's centre)
@@ -391,12 +393,23 @@ struct H3Grid : Grid {
   // neighbour's projection moves them by a second-order amount, a fraction of a
   // cell only at coarse resolutions
   double far_distance() const override { return res <= 4 ? 1.25 : 0.75; }
+  // (keep and center_input both want the id's centre, mostly for the same cell in a row:
+  // the last one is kept -- a grid belongs to one thread)
+  mutable uint64_t cc_id = 0;
+  mutable mgpu::h3b::LatLon cc_val{};
+  const mgpu::h3b::LatLon& id_center(int64_t id) const {
+    if ((uint64_t)id != cc_id || cc_id == 0) {
+      cc_val = mgpu::h3b::cell_center((uint64_t)id);
+      cc_id = (uint64_t)id;
+    }
+    return cc_val;
+  }
   bool keep(int64_t id, long i, long j) const override {
     if (mgpu::h3b::h3_to_face_ijk((uint64_t)id).face != face) return false;
     // near an icosahedron vertex the lattice positions beyond a pentagon's missing
     // sector map to ids of cells elsewhere: the id's centre must be this position
     const Pt g = to_geo(center(i, j));
-    const auto c = mgpu::h3b::cell_center((uint64_t)id);
+    const auto c = id_center(id);
     const double dlat = g.y - mgpu::h3b::to_degrees(c.lat), dlon = g.x - mgpu::h3b::to_degrees(c.lon);
     double spacing = 20.0;  // ~ res-0 centre spacing in degrees
     for (int r = 0; r < res; r++) spacing /= 2.6457513110645906;
@@ -435,9 +448,13 @@ struct H3Grid : Grid {
     if (!id) return {};
     return h3_cell_rings((uint64_t)id, res);
   }
+  std::vector<std::vector<Pt>> boundary_of(long, long, int64_t id) const override {
+    if (!id) return {};
+    return h3_cell_rings((uint64_t)id, res);
+  }
   bool cw_ring(int64_t id) const override { return (uint64_t)id == pole_cell(false, res); }
   Pt center_input(long, long, int64_t id) const override {
-    const auto c = mgpu::h3b::cell_center((uint64_t)id);
+    const auto c = id_center(id);
     return {mgpu::h3b::to_degrees(c.lon), mgpu::h3b::to_degrees(c.lat)};
   }
   double row_y(long j) const override { return j * mgpu::h3::kSin60; }
@@ -765,13 +782,13 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
     if (v != CoreRule::kCore) {
       rule->st.demoted++;
       Chip ch{id, pid, 0, {}};
-      write_cell_wkb(reversed(rings ? *rings : g.boundary(i, j)), ch.wkb);
+      write_cell_wkb(reversed(rings ? *rings : g.boundary_of(i, j, id)), ch.wkb);
       out.push_back(std::move(ch));
       return;
     }
     Chip ch{id, pid, 1, {}};
     if (keep_core) {
-      const auto rs = rings ? *rings : g.boundary(i, j);
+      const auto rs = rings ? *rings : g.boundary_of(i, j, id);
       write_cell_wkb(g.cw_ring(id) ? reversed(rs) : rs, ch.wkb);
     }
     out.push_back(std::move(ch));
@@ -849,7 +866,7 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
       whole(cid, c.first, c.second, nullptr);
       continue;
     }
-    const auto rings = g.boundary(c.first, c.second);
+    const auto rings = g.boundary_of(c.first, c.second, cid);
     if (rings.empty()) continue;
     double cminx = INFINITY, cminy = INFINITY, cmaxx = -INFINITY, cmaxy = -INFINITY;
     for (auto& r : rings)
