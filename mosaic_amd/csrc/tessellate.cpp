@@ -78,9 +78,12 @@ std::vector<Pt> clip_ring(const std::vector<Pt>& ring, const std::vector<Pt>& cl
     Pt a = clip[e], b = clip[e + 1];
     auto side = [&](Pt p) { return (b.x - a.x) * (p.y - a.y) - (b.y - a.y) * (p.x - a.x); };
     out.clear();
+    // (the previous vertex and its side carried over from the last step: the same values)
+    Pt prev = in.back();
+    double sp = side(prev);
     for (size_t i = 0; i < in.size(); i++) {
-      Pt cur = in[i], prev = in[(i + in.size() - 1) % in.size()];
-      double sc = side(cur), sp = side(prev);
+      const Pt cur = in[i];
+      const double sc = side(cur);
       if (sc >= 0) {
         if (sp < 0) {
           double t = sp / (sp - sc);
@@ -91,6 +94,7 @@ std::vector<Pt> clip_ring(const std::vector<Pt>& ring, const std::vector<Pt>& cl
         double t = sp / (sp - sc);
         out.push_back({prev.x + t * (cur.x - prev.x), prev.y + t * (cur.y - prev.y)});
       }
+      prev = cur, sp = sc;
     }
     in.swap(out);
   }
@@ -797,10 +801,14 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
   // from its centre to a walked sample (samples <= 0.2 apart)
   std::unordered_map<std::pair<long, long>, float, PairHash> border;
   std::vector<std::pair<long, long>> nb;
+  // (a cell seen before skips the hypot when max(|dx|, |dy|) -- which the faithfully
+  // rounded hypot cannot fall below -- already rounds to at least its distance)
   auto touch = [&](const std::pair<long, long>& c, Pt s) {
     const Pt cc = g.center(c.first, c.second);
-    const float d = (float)std::hypot(s.x - cc.x, s.y - cc.y);
+    const double dx = s.x - cc.x, dy = s.y - cc.y;
     auto it = border.find(c);
+    if (it != border.end() && (float)std::max(std::fabs(dx), std::fabs(dy)) >= it->second) return;
+    const float d = (float)std::hypot(dx, dy);
     if (it == border.end()) border.emplace(c, d);
     else if (d < it->second) it->second = d;
   };
