@@ -438,7 +438,7 @@ def main():
             if (p.get("res") == a.res and p.get("config", "c2") == a.config and p.get("points") and same_kernel
                     and p.get("key") == traffic_key(a.option, info)):
                 # measured per launch on p["points"] points of this workload (rocprofv3 PMC
-                # passes, tools/gpu_traffic.sh); scaled to this launch's size if it differs
+                # passes, tools/gpu.sh traffic); scaled to this launch's size if it differs
                 out["roofline"]["traffic"] = p["hbm_bytes_per_launch"] * n / p["points"]
                 out["roofline"]["traffic_source"] = "profiles/%s (%s%s)" % (
                     name, p.get("round", "?"), "" if p["points"] == n else ", measured on %d points, scaled" % p["points"])

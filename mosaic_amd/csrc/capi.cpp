@@ -23,6 +23,7 @@
 #include <map>
 #include <functional>
 #include <tuple>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -2085,13 +2086,29 @@ struct BlobPiece {
 };
 using BlobSink = std::function<int32_t(size_t total, const std::vector<BlobPiece>& pieces)>;
 
-// The build's multi-GB intermediates freed on a detached thread (returning their pages
-// took ~0.5 s of C3's upload on the box): moved into one heap tuple that thread deletes.
+// The build's multi-GB intermediates freed off the caller's thread (returning their pages
+// took ~0.5 s of C3's upload on the box): moved into one heap tuple a releaser thread
+// deletes.  At most one release is pending per process: the next build_blob (and process
+// exit) joins it first, so back-to-back uploads never hold two tables' intermediates.
+namespace {
+struct PendingRelease {
+  std::mutex mu;
+  std::thread th;
+  void join() {
+    std::lock_guard<std::mutex> g(mu);
+    if (th.joinable()) th.join();
+  }
+  ~PendingRelease() { join(); }
+};
+PendingRelease g_release;
+}  // namespace
 template <class... V>
 static void release_async(V&... v) {
   auto* box = new std::tuple<std::decay_t<V>...>(std::move(v)...);
+  std::lock_guard<std::mutex> g(g_release.mu);
+  if (g_release.th.joinable()) g_release.th.join();
   try {
-    std::thread([box] { delete box; }).detach();
+    g_release.th = std::thread([box] { delete box; });
   } catch (...) {  // (no thread: free here)
     delete box;
   }
@@ -2200,6 +2217,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
                           const uint8_t* is_core, const int64_t* wkb_offsets, const uint8_t* wkb,
                           HostBlob& host, BlobHeader& hdr_out, const mgpu_build_opts& bo,
                           const BlobSink* sink = nullptr) {
+  g_release.join();  // (the previous build's intermediates, before this one allocates)
   if (index_system != MGPU_H3 && index_system != MGPU_BNG)
     return fail(MGPU_E_INVALID_ARG, "unknown index system %d (0 = H3, 1 = BNG)", index_system);
   if (n_chips < 0 || n_chips > (int64_t)std::numeric_limits<int32_t>::max())

@@ -23,6 +23,9 @@ struct CommState {
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
   void* scratch = nullptr;  // device: the broadcast header, the gathered counts
+  // pinned host staging of the values copied to / from `scratch` (a status word, a count):
+  // an asynchronous copy never reads a stack local that dies before the copy runs
+  int64_t* host = nullptr;
 };
 constexpr size_t kScratch = 4096;  // >= the blob header + a status word; the counts
 
@@ -63,6 +66,10 @@ int32_t mgpu_comm_init(mgpu_ctx* ctx, const uint8_t* unique_id, int32_t rank, in
   c->rank = rank;
   c->world = world;
   hipError_t e = hipMalloc(&c->scratch, kScratch);
+  if (e == hipSuccess) {
+    e = hipHostMalloc((void**)&c->host, 64, hipHostMallocDefault);
+    if (e != hipSuccess) hipFree(c->scratch);
+  }
   if (e != hipSuccess) {
     delete c;
     return mgpu::set_error(MGPU_E_DEVICE, "hipMalloc: %s", hipGetErrorString(e));
@@ -70,6 +77,7 @@ int32_t mgpu_comm_init(mgpu_ctx* ctx, const uint8_t* unique_id, int32_t rank, in
   ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
   if (r != ncclSuccess) {
     hipFree(c->scratch);
+    hipHostFree(c->host);
     delete c;
     return mgpu::set_error(MGPU_E_DEVICE, "ncclCommInitRank(rank %d of %d): %s", rank, world, ncclGetErrorString(r));
   }
@@ -83,6 +91,7 @@ int32_t mgpu_comm_destroy(mgpu_ctx* ctx) {
   hipSetDevice(ctx->device);
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->scratch) hipFree(c->scratch);
+  if (c->host) hipHostFree(c->host);
   delete c;
   ctx->comm = nullptr;
   return MGPU_OK;
@@ -103,11 +112,14 @@ int32_t mgpu_comm_info(mgpu_ctx* ctx, int32_t* rank, int32_t* world) {
 // agreement and return an error.  A failed RCCL call aborts the communicator
 // (ncclCommAbort): later calls on the context fail instead of hanging.
 namespace {
-int32_t comm_failed(mgpu_ctx* ctx, const char* what, ncclResult_t r) {
+// (the stream is drained first: copies staged through c->host may still be pending)
+int32_t comm_failed(mgpu_ctx* ctx, const char* what, ncclResult_t r, hipStream_t s) {
   CommState* c = state(ctx);
   int32_t st = mgpu::set_error(MGPU_E_DEVICE, "%s: %s (communicator aborted)", what, ncclGetErrorString(r));
   if (c->comm) ncclCommAbort(c->comm);
+  (void)hipStreamSynchronize(s);
   if (c->scratch) hipFree(c->scratch);
+  if (c->host) hipHostFree(c->host);
   delete c;
   ctx->comm = nullptr;
   return st;
@@ -175,7 +187,7 @@ int32_t mgpu_chips_broadcast(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t roo
   void* hdr_dev = (is_root && root_ok) ? chips->blob : c->scratch;
   if (is_root && !root_ok) (void)hipMemsetAsync(c->scratch, 0, (size_t)mgpu::kBlobHeaderSize, s);
   ncclResult_t r = ncclBroadcast(hdr_dev, hdr_dev, (size_t)mgpu::kBlobHeaderSize, ncclUint8, root, c->comm, s);
-  if (r != ncclSuccess) return comm_failed(ctx, "ncclBroadcast(header)", r);
+  if (r != ncclSuccess) return comm_failed(ctx, "ncclBroadcast(header)", r, s);
   int64_t bytes = 0;
   void* dst = nullptr;
   int32_t mine = MGPU_OK;
@@ -192,18 +204,24 @@ int32_t mgpu_chips_broadcast(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t roo
   int32_t agreed = mine;
   // (both steps are tried whatever the first gave: a failed memset makes the copied value
   // a failure itself, so no stale OK from an earlier call can reach the all-reduce)
+  // (staged through the pinned c->host, read by the copy whenever it runs; the stream is
+  // synchronised below before the word is reused or any return)
   const bool set_ok = hipMemsetAsync(status, 0x80, 4, s) == hipSuccess;
-  const int32_t contrib = set_ok ? mine : (int32_t)MGPU_E_DEVICE;
-  const bool copy_ok = hipMemcpyAsync(status, &contrib, 4, hipMemcpyHostToDevice, s) == hipSuccess;
+  int32_t* contrib = (int32_t*)c->host;
+  *contrib = set_ok ? mine : (int32_t)MGPU_E_DEVICE;
+  const bool copy_ok = hipMemcpyAsync(status, contrib, 4, hipMemcpyHostToDevice, s) == hipSuccess;
   if (!set_ok || !copy_ok) agreed = MGPU_E_DEVICE;
   r = ncclAllReduce(status, status, 1, ncclInt32, ncclMin, c->comm, s);
   if (r != ncclSuccess) {
     if (dst) hipFree(dst);
-    return comm_failed(ctx, "ncclAllReduce(status)", r);
+    return comm_failed(ctx, "ncclAllReduce(status)", r, s);
   }
+  int32_t* back = (int32_t*)(c->host + 1);
+  *back = MGPU_OK;
   int32_t all = MGPU_OK;
-  if (hipMemcpyAsync(&all, status, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
-    all = MGPU_E_DEVICE;
+  const bool back_ok = hipMemcpyAsync(back, status, 4, hipMemcpyDeviceToHost, s) == hipSuccess;
+  if (hipStreamSynchronize(s) != hipSuccess || !back_ok) all = MGPU_E_DEVICE;
+  else all = *back;
   if (agreed != MGPU_OK && all == MGPU_OK) all = agreed;
   if (all != MGPU_OK) {
     // every rank skips the bulk broadcast
@@ -216,7 +234,7 @@ int32_t mgpu_chips_broadcast(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t roo
   r = ncclBroadcast(buf, buf, (size_t)bytes, ncclUint8, root, c->comm, s);
   if (r != ncclSuccess) {
     if (dst) hipFree(dst);
-    return comm_failed(ctx, "ncclBroadcast(blob)", r);
+    return comm_failed(ctx, "ncclBroadcast(blob)", r, s);
   }
   if (hipStreamSynchronize(s) != hipSuccess) {
     if (dst) hipFree(dst);
@@ -243,19 +261,19 @@ int32_t mgpu_pair_offsets(mgpu_ctx* ctx, int64_t local_pairs, int64_t* out_offse
   // (the copy is tried even when the memset failed -- then carrying -1 itself -- and a
   // local failure is reported after the collective, so this rank never relies on the
   // slot holding the previous call's count)
+  // (the count is staged through the pinned c->host; every return after the copy has
+  // synchronised the stream)
   const int64_t v = local_pairs < 0 ? -1 : local_pairs;
   const bool set_ok = hipMemsetAsync(mine, 0xFF, 8, s) == hipSuccess;
-  const int64_t vv = set_ok ? v : -1;
-  const bool copy_ok = hipMemcpyAsync(mine, &vv, 8, hipMemcpyHostToDevice, s) == hipSuccess;
+  c->host[0] = set_ok ? v : -1;
+  const bool copy_ok = hipMemcpyAsync(mine, c->host, 8, hipMemcpyHostToDevice, s) == hipSuccess;
   ncclResult_t r = ncclAllGather(mine, all, 1, ncclInt64, c->comm, s);
-  if (r != ncclSuccess) return comm_failed(ctx, "ncclAllGather(pair counts)", r);
-  if (!set_ok || !copy_ok) {
-    (void)hipStreamSynchronize(s);
-    return mgpu::set_error(MGPU_E_DEVICE, "pair_offsets: staging this rank's count failed");
-  }
+  if (r != ncclSuccess) return comm_failed(ctx, "ncclAllGather(pair counts)", r, s);
   std::vector<int64_t> counts((size_t)c->world);
-  HIP_TRY(hipMemcpyAsync(counts.data(), all, counts.size() * 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  const bool back_ok = hipMemcpyAsync(counts.data(), all, counts.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess;
+  const bool sync_ok = hipStreamSynchronize(s) == hipSuccess;
+  if (!set_ok || !copy_ok) return mgpu::set_error(MGPU_E_DEVICE, "pair_offsets: staging this rank's count failed");
+  if (!back_ok || !sync_ok) return mgpu::set_error(MGPU_E_DEVICE, "pair_offsets: reading the gathered counts failed");
   int64_t off = 0, tot = 0;
   for (int k = 0; k < c->world; k++) {
     if (counts[k] < 0) return mgpu::set_error(MGPU_E_INVALID_ARG, "pair_offsets: negative count on rank %d", k);

@@ -1152,6 +1152,7 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   using Code = typename CodeOf<IS>::T;
   constexpr int kW = kCfyBlock / 64;        // waves per workgroup
   constexpr int kItems = kChunk / 64;       // points per lane per chunk
+  static_assert(kItems % kCfyBatch == 0, "MGPU_CFY_BATCH must divide the points per lane of a chunk");
   const JoinArgs& a = sa.j;
   const ChipTableView& t = a.chips;
   extern __shared__ uint16_t s_blk[];       // [raster_bny * raster_bnx] (IS == H3), then the row bands
@@ -1281,6 +1282,7 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   constexpr int kPairItems = kChunk / 128;                       // pair items per lane per chunk
   constexpr int kPB = kCfyBatch / 2 > 0 ? kCfyBatch / 2 : 1;      // pair items in flight
   constexpr int kPts = 2 * kPB;
+  static_assert(kPairItems % kPB == 0, "MGPU_CFY_BATCH / 2 must divide the pair items per lane of a chunk");
   const JoinArgs& a = sa.j;
   const ChipTableView& t = a.chips;
   extern __shared__ uint16_t s_blk[];

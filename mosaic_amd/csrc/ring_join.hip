@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <unordered_set>
 #include <vector>
 
 #include "capi_internal.h"
@@ -328,33 +329,45 @@ static int32_t cells_join(mgpu_ctx* ctx, hipStream_t s, Scratch& S, int32_t inde
   hipLaunchKernelGGL(rj_kept_kernel, dim3(grid_of(n_left)), dim3(256), 0, s, off, n_left, (int64_t)max_per_left, nul_out,
                      kept);
   scan(kept, koff);
-  std::vector<int64_t> hoff(n_left + 1);
-  int64_t n_out = 0;
-  RJ_TRY(hipMemcpyAsync(hoff.data(), off, (n_left + 1) * 8, hipMemcpyDeviceToHost, s));
+  // the output's size (kept pairs) and the candidate pairs' total: a short output fails
+  // here, before any pair is generated (the caller retries at the reported size)
+  int64_t n_out = 0, n_pairs = 0;
   RJ_TRY(hipMemcpyAsync(&n_out, koff + n_left, 8, hipMemcpyDeviceToHost, s));
+  RJ_TRY(hipMemcpyAsync(&n_pairs, off + n_left, 8, hipMemcpyDeviceToHost, s));
   RJ_TRY(hipStreamSynchronize(s));
+  if (out_n) *out_n = n_out;
+  if (n_out > capacity)
+    return mgpu::set_error(MGPU_E_CAPACITY, "ring_join: %lld pairs, capacity %lld", (long long)n_out, (long long)capacity);
+  if (n_out == 0) return MGPU_OK;
   // the pairs, sorted and cut per landmark, in batches of landmarks holding at most
   // kBatchPairs candidate pairs (a landmark with more is a batch of its own), so the
-  // scratch stays bounded whatever the density
+  // scratch stays bounded whatever the density; the per-landmark offsets come to the host
+  // only when the pairs need more than one batch
   const int64_t kBatchPairs = ctx->opt.ring_batch;  // (option ring_batch)
-  const int64_t biggest = [&] {
-    int64_t m = 0;
-    for (int64_t i = 0; i < n_left; i++) m = std::max(m, hoff[i + 1] - hoff[i]);
-    return m;
-  }();
+  std::vector<int64_t> hoff;
+  int64_t biggest = 0;
+  if (n_pairs > kBatchPairs) {
+    hoff.resize(n_left + 1);
+    RJ_TRY(hipMemcpyAsync(hoff.data(), off, (n_left + 1) * 8, hipMemcpyDeviceToHost, s));
+    RJ_TRY(hipStreamSynchronize(s));
+    for (int64_t i = 0; i < n_left; i++) biggest = std::max(biggest, hoff[i + 1] - hoff[i]);
+  }
   int64_t *pr, *roff;
   double* pd;
   RJ_TRY(S.get(&roff, n_left + 1));
-  RJ_TRY(S.get(&pr, std::min(hoff[n_left], std::max(kBatchPairs, biggest))));
-  RJ_TRY(S.get(&pd, std::min(hoff[n_left], std::max(kBatchPairs, biggest))));
+  RJ_TRY(S.get(&pr, std::min(n_pairs, std::max(kBatchPairs, biggest))));
+  RJ_TRY(S.get(&pd, std::min(n_pairs, std::max(kBatchPairs, biggest))));
   for (int64_t b0 = 0; b0 < n_left;) {
-    int64_t b1 = b0 + 1;
-    while (b1 < n_left && hoff[b1 + 1] - hoff[b0] <= std::max(kBatchPairs, biggest)) b1++;
+    int64_t b1 = n_left;
+    if (!hoff.empty()) {
+      b1 = b0 + 1;
+      while (b1 < n_left && hoff[b1 + 1] - hoff[b0] <= std::max(kBatchPairs, biggest)) b1++;
+    }
     RjArgs ab = a;
     ab.lx = a.lx + b0, ab.ly = a.ly + b0, ab.ring_off = a.ring_off + b0, ab.n_left = b1 - b0;
     // (offsets relative to the batch: the batch's segment starts at pr[0])
     hipLaunchKernelGGL(rj_rebase_kernel, dim3(grid_of(b1 - b0 + 1)), dim3(256), 0, s, off + b0, b1 - b0 + 1,
-                       hoff[b0], roff);
+                       hoff.empty() ? (int64_t)0 : hoff[b0], roff);
     hipLaunchKernelGGL(rj_pairs_kernel<true>, dim3(grid_of(b1 - b0)), dim3(256), 0, s, ab, nullptr, roff, pr, pd,
                        nullptr);
     hipLaunchKernelGGL(rj_sort_kernel, dim3(grid_of(b1 - b0)), dim3(256), 0, s, roff, b1 - b0, (int64_t)max_per_left,
@@ -366,9 +379,6 @@ static int32_t cells_join(mgpu_ctx* ctx, hipStream_t s, Scratch& S, int32_t inde
     RJ_TRY(hipStreamSynchronize(s));
     b0 = b1;
   }
-  if (out_n) *out_n = n_out;
-  if (n_out > capacity)
-    return mgpu::set_error(MGPU_E_CAPACITY, "ring_join: %lld pairs, capacity %lld", (long long)n_out, (long long)capacity);
   return MGPU_OK;
 }
 
@@ -521,7 +531,9 @@ extern "C" int32_t mgpu_ring_join_final(mgpu_ctx* ctx, int32_t index_system, int
     RJ_TRY(S.get(&dsub, sub.size()));
     RJ_TRY(S.get(&doff, sub.size() + 1));
     RJ_TRY(hipMemcpy(dsub, sub.data(), sub.size() * 8, hipMemcpyHostToDevice));
-    int64_t cap = (int64_t)sub.size() * (3 * (int64_t)k * (k + 1) + 1) + 1024, total = 0;
+    // (first guess bounded at 2^24 cells, as mgpu_ring_join_ex's; the exact total on a retry)
+    int64_t cap = std::min<int64_t>((int64_t)sub.size() * (3 * (int64_t)k * (k + 1) + 1) + 1024, (int64_t)1 << 24),
+            total = 0;
     RJ_TRY(S.get(&dring, cap));
     int32_t st = mgpu_grid_kring(ctx, index_system, dsub, (int64_t)sub.size(), k, 0, dring, cap, doff, &total, stream);
     if (st == MGPU_E_CAPACITY) {
@@ -535,16 +547,17 @@ extern "C" int32_t mgpu_ring_join_final(mgpu_ctx* ctx, int32_t index_system, int
     RJ_TRY(hipMemcpy(ho.data(), doff, ho.size() * 8, hipMemcpyDeviceToHost));
     for (size_t q = 0; q < who.size(); q++) iterated[who[q]].assign(hr.begin() + ho[q], hr.begin() + ho[q + 1]);
   }
-  // array_except: the distinct tessellation cells outside the iterated ring
+  // array_except: the distinct tessellation cells outside the iterated ring, in their
+  // first-seen order (a hash set of the cells seen: linear per landmark)
   std::vector<int64_t> ring, ring_off{0};
+  std::unordered_set<int64_t> seen;
   for (int64_t i = 0; i < n_left; i++) {
     std::vector<int64_t> it = iterated[i];
     std::sort(it.begin(), it.end());
-    std::vector<int64_t> seen;
+    seen.clear();
     for (int64_t c : cells[i]) {
       if (std::binary_search(it.begin(), it.end(), c)) continue;
-      if (std::find(seen.begin(), seen.end(), c) != seen.end()) continue;
-      seen.push_back(c);
+      if (!seen.insert(c).second) continue;
       ring.push_back(c);
     }
     ring_off.push_back((int64_t)ring.size());
