@@ -442,11 +442,28 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
 int32_t mgpu_tessellate_ex(int32_t index_system, int32_t res, int64_t n_polys, const int32_t* polygon_id,
                            const int64_t* poly_part_off, const int64_t* part_ring_off, const int64_t* ring_off,
                            const double* xy, int32_t keep_core_geometries, int32_t core_rule, mgpu_tess** out);
+/* mgpu_tessellate_geom: mgpu_tessellate_ex with the input geometries' types and the way
+ * border chips are cut.  poly_type[n_polys] (NULL: MULTIPOLYGON iff several parts) holds
+ * each geometry's WKB type, 3 = POLYGON or 6 = MULTIPOLYGON: coerceChipGeometry
+ * (IndexSystem.scala:293-303) re-nodes a chip whose type differs from its polygon's.
+ * chip_geometry: MGPU_CHIPS_OVERLAY (default) -- `polygon INTERSECTION cell` as JTS
+ * OverlayNG computes it (RobustLineIntersector nodes, minimal result rings, separate pieces;
+ * mosaic_amd/csrc/jts_overlay.h); MGPU_CHIPS_SUTHERLAND_HODGMAN -- rounds 1-5's ring clip
+ * (its own crossing arithmetic, pieces bridged along the cell boundary), kept to count what
+ * the overlay changes. */
+#define MGPU_CHIPS_OVERLAY 0
+#define MGPU_CHIPS_SUTHERLAND_HODGMAN 1
+int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys, const int32_t* polygon_id,
+                             const int64_t* poly_part_off, const int64_t* part_ring_off, const int64_t* ring_off,
+                             const double* xy, const uint8_t* poly_type, int32_t keep_core_geometries,
+                             int32_t core_rule, int32_t chip_geometry, mgpu_tess** out);
 int32_t mgpu_tess_result_stats(const mgpu_tess* t, int64_t* out6);
 /* mgpu_tess_result_core_stats: the first n of {rows, core rows, demoted, promoted,
  * dropped, ambiguous, carved tests, band tests, core rows whose centre is < r deep,
  * border rows whose centre is >= r deep, chip cells outside the band (dropped),
- * DP-sensitive rows, unresolved rows, polygons with an empty buffer(-r)}. */
+ * DP-sensitive rows, unresolved rows, polygons with an empty buffer(-r), border chips cut
+ * by the overlay, ... of several pieces, ... re-noded by coerceChipGeometry, nodes that
+ * re-noding added, ... whose overlay also gave lines / points}. */
 int32_t mgpu_tess_result_core_stats(const mgpu_tess* t, int64_t* out, int32_t n);
 int32_t mgpu_tess_result_sizes(const mgpu_tess* t, int64_t* n_chips, int64_t* wkb_bytes);
 int32_t mgpu_tess_result_copy(const mgpu_tess* t, int64_t* cell, int32_t* polygon_id, uint8_t* is_core,

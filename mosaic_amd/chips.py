@@ -105,14 +105,18 @@ class Polygons:
 
     polygon p -> parts [poly_part_off[p], poly_part_off[p+1]);
     part q -> rings [part_ring_off[q], part_ring_off[q+1]) (first ring = shell);
-    ring r -> vertices xy[ring_off[r]:ring_off[r+1]] (x = lon/easting, y = lat/northing)."""
+    ring r -> vertices xy[ring_off[r]:ring_off[r+1]] (x = lon/easting, y = lat/northing);
+    poly_type[p] (optional): the geometry's WKB type, 3 = POLYGON, 6 = MULTIPOLYGON (None:
+    MULTIPOLYGON iff several parts) -- coerceChipGeometry depends on it."""
 
-    def __init__(self, poly_id, poly_part_off, part_ring_off, ring_off, xy):
+    def __init__(self, poly_id, poly_part_off, part_ring_off, ring_off, xy, poly_type=None):
         self.poly_id = np.ascontiguousarray(poly_id, dtype=np.int32)
         self.poly_part_off = np.ascontiguousarray(poly_part_off, dtype=np.int64)
         self.part_ring_off = np.ascontiguousarray(part_ring_off, dtype=np.int64)
         self.ring_off = np.ascontiguousarray(ring_off, dtype=np.int64)
         self.xy = np.ascontiguousarray(xy, dtype=np.float64).reshape(-1, 2)
+        self.poly_type = None if poly_type is None else np.ascontiguousarray(poly_type, dtype=np.uint8)
+        assert self.poly_type is None or self.poly_type.shape[0] == self.poly_id.shape[0]
 
     def __len__(self):
         return self.poly_id.shape[0]
@@ -120,10 +124,11 @@ class Polygons:
     @classmethod
     def from_npz(cls, path):
         z = np.load(path, allow_pickle=False)
-        return cls(z["poly_id"], z["poly_part_off"], z["part_ring_off"], z["ring_off"], z["xy"])
+        return cls(z["poly_id"], z["poly_part_off"], z["part_ring_off"], z["ring_off"], z["xy"],
+                   z["poly_type"] if "poly_type" in z.files else None)
 
     @classmethod
-    def from_lists(cls, polys):
+    def from_lists(cls, polys, poly_type=None):
         """polys: list of (id, [part: [ring: [(x, y), ...]]])."""
         ids, pp, pr, ro, xy = [], [0], [0], [0], []
         for pid, parts in polys:
@@ -134,7 +139,7 @@ class Polygons:
                     ro.append(len(xy))
                 pr.append(len(ro) - 1)
             pp.append(len(pr) - 1)
-        return cls(ids, pp, pr, ro, np.array(xy, dtype=np.float64).reshape(-1, 2))
+        return cls(ids, pp, pr, ro, np.array(xy, dtype=np.float64).reshape(-1, 2), poly_type)
 
     def select(self, idx):
         out = []
@@ -146,7 +151,7 @@ class Polygons:
                     rings.append([tuple(v) for v in self.xy[self.ring_off[r]:self.ring_off[r + 1]]])
                 parts.append(rings)
             out.append((int(self.poly_id[p]), parts))
-        return Polygons.from_lists(out)
+        return Polygons.from_lists(out, None if self.poly_type is None else self.poly_type[list(idx)])
 
     def bounds(self):
         return self.xy[:, 0].min(), self.xy[:, 1].min(), self.xy[:, 0].max(), self.xy[:, 1].max()
@@ -154,25 +159,32 @@ class Polygons:
 
 CORE_RULES = {"mosaicfill": 0, "clip": 1, "distance": 2}
 CORE_STATS = ("rows", "core", "demoted", "promoted", "dropped", "ambiguous", "carved_tests", "band_tests",
-              "core_below_r", "border_above_r", "band_dropped", "dp_sensitive", "unresolved", "carved_empty")
+              "core_below_r", "border_above_r", "band_dropped", "dp_sensitive", "unresolved", "carved_empty",
+              "overlay_chips", "multi_piece", "coerced", "coerce_nodes", "lower_dim")
+CHIP_GEOMETRY = {"overlay": 0, "sutherland_hodgman": 1}
 
 
-def tessellate(polygons, index_system, resolution, keep_core_geometries=True, core_rule="mosaicfill"):
+def tessellate(polygons, index_system, resolution, keep_core_geometries=True, core_rule="mosaicfill",
+               chip_geometry="overlay"):
     """grid_tessellateexplode over a polygon set -> ChipTable (host C++ builder).
 
     ``core_rule``: "mosaicfill" (default, the reference's: core iff the cell is in
     polyfill(buffer(-r)); a border-set cell the polygon holds whole is a border chip of the
     whole cell; near r the sets follow JTS's chorded buffers), "clip" (every wholly covered
     cell is core) or "distance" (round 4's form of the reference's rule: exact distances) --
-    include/mosaic_gpu.h MGPU_CORE_*.  The table's ``core_stats``: CORE_STATS
+    include/mosaic_gpu.h MGPU_CORE_*.  ``chip_geometry``: "overlay" (default: border chips
+    as JTS OverlayNG cuts them, mosaic_amd/csrc/jts_overlay.h) or "sutherland_hodgman" (the
+    ring clip of rounds 1-5).  The table's ``core_stats``: CORE_STATS
     (mgpu_tess_result_core_stats)."""
     res = index_system.get_resolution(resolution)
     L = N.lib()
     h = ctypes.c_void_p()
     p = polygons
-    st = L.mgpu_tessellate_ex(index_system.code, res, len(p), p.poly_id.ctypes.data, p.poly_part_off.ctypes.data,
-                              p.part_ring_off.ctypes.data, p.ring_off.ctypes.data, p.xy.ctypes.data,
-                              1 if keep_core_geometries else 0, CORE_RULES[core_rule], ctypes.byref(h))
+    st = L.mgpu_tessellate_geom(index_system.code, res, len(p), p.poly_id.ctypes.data, p.poly_part_off.ctypes.data,
+                                p.part_ring_off.ctypes.data, p.ring_off.ctypes.data, p.xy.ctypes.data,
+                                None if p.poly_type is None else p.poly_type.ctypes.data,
+                                1 if keep_core_geometries else 0, CORE_RULES[core_rule],
+                                CHIP_GEOMETRY[chip_geometry], ctypes.byref(h))
     N.check(st, "tessellation failed")
     try:
         stats = np.zeros(len(CORE_STATS), np.int64)

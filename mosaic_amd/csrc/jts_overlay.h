@@ -1,0 +1,707 @@
+// Border-chip geometry as JTS 1.20 OverlayNG computes `polygon INTERSECTION cell` in its
+// floating-precision mode (Geometry.intersection -> OverlayNGRobust: MCIndexNoder with an
+// IntersectionAdder over RobustLineIntersector, validated noding), restated for one cell.
+// JTS is a Maven dependency of the reference (pom.xml:98-102), absent here; its call sites:
+// IndexSystem.getBorderChips (core/index/IndexSystem.scala:184-188) ->
+// MosaicGeometryJTS.intersection (core/geometry/MosaicGeometryJTS.scala:139-152, multi-part
+// results through compactCollection :277-315) -> coerceChipGeometry (IndexSystem.scala:293-303).
+//
+// What decides the chip's point set, and is restated exactly:
+//  * every node where a polygon segment meets a cell segment is RobustLineIntersector's
+//    point for the two ORIGINAL segments: an endpoint when one lies on the other segment
+//    (Orientation.index == 0, CGAlgorithmsDD's filtered / double-double sign), else
+//    Intersection.intersection (homogeneous coordinates about the midpoint of the two
+//    envelopes' overlap, every product rounded on its own), replaced by the nearest
+//    endpoint when it falls outside either segment's envelope; collinear overlaps node at
+//    the overlap's endpoints (computeCollinearIntersection);
+//  * the noded edges between those nodes, each kept when it lies in the other geometry's
+//    interior -- a polygon edge in the cell, a cell edge in the polygon, a shared edge when
+//    both interiors lie on one side -- located at its nodes by the angular sectors of the
+//    other geometry's edges there (OverlayLabeller's propagation around a node; exact
+//    orientation tests), and by point location when it touches none of them;
+//  * the result rings as OverlayNG's PolygonBuilder forms them: minimal rings (at a node
+//    with several result edges the ring turns into the face on its right), shells
+//    clockwise, holes counter-clockwise, each hole in the smallest shell holding it -- so
+//    a chip that falls apart is a MULTIPOLYGON of separate pieces, never one ring bridged
+//    along the cell boundary;
+//  * coerceChipGeometry's `difference(indexGeom.getBoundary)` when the chip's type differs
+//    from the polygon's (a MULTIPOLYGON zone giving a one-piece chip, a POLYGON giving
+//    several) or the overlay also produced lines / points (the polygon touching the cell
+//    from outside: OverlayNG's non-strict mode keeps them, compactCollection makes a
+//    GEOMETRYCOLLECTION): that second overlay re-nodes the chip's edges against the cell's
+//    boundary segments, and a chip edge that crosses a cell segment within rounding -- a
+//    crossing node a few ulps outside the cell -- gains that node.
+// Not restated (documented in DESIGN.md): OverlayNGRobust's fallbacks when the validating
+// noder rejects the floating noding (snapping / snap-rounding noders), the ring start
+// vertex of OverlayNG's output (bytes, not the point set), and compactCollection's union of
+// the pieces (disjoint pieces: no new node).
+#pragma once
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+#include "jts_orient.h"
+
+namespace mgpu {
+namespace ovl {
+
+struct P {
+  double x, y;
+};
+inline bool eq(P a, P b) { return a.x == b.x && a.y == b.y; }
+inline bool less(P a, P b) { return a.x < b.x || (a.x == b.x && a.y < b.y); }
+inline int orient(P a, P b, P c) { return mgpu::pip::orientation(a.x, a.y, b.x, b.y, c.x, c.y); }
+
+// Envelope.intersects(p1, p2, q)
+inline bool env_has(P p1, P p2, P q) {
+  return q.x >= (p1.x < p2.x ? p1.x : p2.x) && q.x <= (p1.x > p2.x ? p1.x : p2.x) &&
+         q.y >= (p1.y < p2.y ? p1.y : p2.y) && q.y <= (p1.y > p2.y ? p1.y : p2.y);
+}
+// Envelope.intersects(p1, p2, q1, q2)
+inline bool env_meet(P p1, P p2, P q1, P q2) {
+  double minq = std::min(q1.x, q2.x), maxq = std::max(q1.x, q2.x), minp = std::min(p1.x, p2.x),
+         maxp = std::max(p1.x, p2.x);
+  if (minp > maxq || maxp < minq) return false;
+  minq = std::min(q1.y, q2.y), maxq = std::max(q1.y, q2.y), minp = std::min(p1.y, p2.y), maxp = std::max(p1.y, p2.y);
+  return !(minp > maxq || maxp < minq);
+}
+
+// Intersection.intersection (JTS 1.20 algorithm/Intersection.java); false = parallel (null)
+inline bool hom_intersection(P p1, P p2, P q1, P q2, P* out) {
+  const double minX0 = p1.x < p2.x ? p1.x : p2.x, minY0 = p1.y < p2.y ? p1.y : p2.y;
+  const double maxX0 = p1.x > p2.x ? p1.x : p2.x, maxY0 = p1.y > p2.y ? p1.y : p2.y;
+  const double minX1 = q1.x < q2.x ? q1.x : q2.x, minY1 = q1.y < q2.y ? q1.y : q2.y;
+  const double maxX1 = q1.x > q2.x ? q1.x : q2.x, maxY1 = q1.y > q2.y ? q1.y : q2.y;
+  const double intMinX = minX0 > minX1 ? minX0 : minX1, intMaxX = maxX0 < maxX1 ? maxX0 : maxX1;
+  const double intMinY = minY0 > minY1 ? minY0 : minY1, intMaxY = maxY0 < maxY1 ? maxY0 : maxY1;
+  const double midx = (intMinX + intMaxX) / 2.0, midy = (intMinY + intMaxY) / 2.0;
+  const double p1x = p1.x - midx, p1y = p1.y - midy, p2x = p2.x - midx, p2y = p2.y - midy;
+  const double q1x = q1.x - midx, q1y = q1.y - midy, q2x = q2.x - midx, q2y = q2.y - midy;
+  const double px = p1y - p2y, py = p2x - p1x, pw = p1x * p2y - p2x * p1y;
+  const double qx = q1y - q2y, qy = q2x - q1x, qw = q1x * q2y - q2x * q1y;
+  const double x = py * qw - qy * pw, y = qx * pw - px * qw, w = px * qy - qx * py;
+  const double xi = x / w, yi = y / w;
+  if (std::isnan(xi) || std::isinf(xi) || std::isnan(yi) || std::isinf(yi)) return false;
+  *out = {xi + midx, yi + midy};
+  return true;
+}
+
+// Distance.pointToSegment (Coordinate.distance = Math.hypot)
+inline double point_to_segment(P p, P a, P b) {
+  if (a.x == b.x && a.y == b.y) return std::hypot(p.x - a.x, p.y - a.y);
+  const double len2 = (b.x - a.x) * (b.x - a.x) + (b.y - a.y) * (b.y - a.y);
+  const double r = ((p.x - a.x) * (b.x - a.x) + (p.y - a.y) * (b.y - a.y)) / len2;
+  if (r <= 0.0) return std::hypot(p.x - a.x, p.y - a.y);
+  if (r >= 1.0) return std::hypot(p.x - b.x, p.y - b.y);
+  const double s = ((a.y - p.y) * (b.x - a.x) - (a.x - p.x) * (b.y - a.y)) / len2;
+  return std::fabs(s) * std::sqrt(len2);
+}
+
+// RobustLineIntersector.nearestEndpoint
+inline P nearest_endpoint(P p1, P p2, P q1, P q2) {
+  P best = p1;
+  double m = point_to_segment(p1, q1, q2), d;
+  if ((d = point_to_segment(p2, q1, q2)) < m) m = d, best = p2;
+  if ((d = point_to_segment(q1, p1, p2)) < m) m = d, best = q1;
+  if ((d = point_to_segment(q2, p1, p2)) < m) m = d, best = q2;
+  return best;
+}
+
+// RobustLineIntersector.computeIntersect: n points (0, 1 or 2 for a collinear overlap)
+struct Hit {
+  int n = 0;
+  bool proper = false;
+  P pt[2];
+};
+inline Hit line_intersect(P p1, P p2, P q1, P q2) {
+  Hit h;
+  if (!env_meet(p1, p2, q1, q2)) return h;
+  const int Pq1 = orient(p1, p2, q1), Pq2 = orient(p1, p2, q2);
+  if ((Pq1 > 0 && Pq2 > 0) || (Pq1 < 0 && Pq2 < 0)) return h;
+  const int Qp1 = orient(q1, q2, p1), Qp2 = orient(q1, q2, p2);
+  if ((Qp1 > 0 && Qp2 > 0) || (Qp1 < 0 && Qp2 < 0)) return h;
+  if (Pq1 == 0 && Pq2 == 0 && Qp1 == 0 && Qp2 == 0) {  // computeCollinearIntersection
+    const bool q1inP = env_has(p1, p2, q1), q2inP = env_has(p1, p2, q2);
+    const bool p1inQ = env_has(q1, q2, p1), p2inQ = env_has(q1, q2, p2);
+    auto two = [&](P a, P b, bool point) {
+      h.pt[0] = a, h.pt[1] = b, h.n = point ? 1 : 2;
+    };
+    if (q1inP && q2inP) two(q1, q2, false);
+    else if (p1inQ && p2inQ) two(p1, p2, false);
+    else if (q1inP && p1inQ) two(q1, p1, eq(q1, p1) && !q2inP && !p2inQ);
+    else if (q1inP && p2inQ) two(q1, p2, eq(q1, p2) && !q2inP && !p1inQ);
+    else if (q2inP && p1inQ) two(q2, p1, eq(q2, p1) && !q1inP && !p2inQ);
+    else if (q2inP && p2inQ) two(q2, p2, eq(q2, p2) && !q1inP && !p1inQ);
+    return h;
+  }
+  h.n = 1;
+  if (Pq1 == 0 || Pq2 == 0 || Qp1 == 0 || Qp2 == 0) {
+    if (eq(p1, q1) || eq(p1, q2)) h.pt[0] = p1;
+    else if (eq(p2, q1) || eq(p2, q2)) h.pt[0] = p2;
+    else if (Pq1 == 0) h.pt[0] = q1;
+    else if (Pq2 == 0) h.pt[0] = q2;
+    else if (Qp1 == 0) h.pt[0] = p1;
+    else h.pt[0] = p2;
+    return h;
+  }
+  h.proper = true;
+  P ip;
+  if (!hom_intersection(p1, p2, q1, q2, &ip)) ip = nearest_endpoint(p1, p2, q1, q2);
+  // isInSegmentEnvelopes, else the nearest endpoint
+  if (!(env_has(p1, p2, ip) && env_has(q1, q2, ip))) ip = nearest_endpoint(p1, p2, q1, q2);
+  h.pt[0] = ip;
+  return h;
+}
+
+// Octant.octant and SegmentPointComparator.compare: the order of nodes along a segment
+inline int octant(double dx, double dy) {
+  const double adx = std::fabs(dx), ady = std::fabs(dy);
+  if (dx >= 0) {
+    if (dy >= 0) return adx >= ady ? 0 : 1;
+    return adx >= ady ? 7 : 6;
+  }
+  if (dy >= 0) return adx >= ady ? 3 : 2;
+  return adx >= ady ? 4 : 5;
+}
+inline int rel(double a, double b) { return a < b ? -1 : (a > b ? 1 : 0); }
+inline int cmp_value(int a, int b) { return a < 0 ? -1 : a > 0 ? 1 : b < 0 ? -1 : b > 0 ? 1 : 0; }
+inline int seg_compare(int oct, P p0, P p1) {
+  if (eq(p0, p1)) return 0;
+  const int xs = rel(p0.x, p1.x), ys = rel(p0.y, p1.y);
+  switch (oct) {
+    case 0: return cmp_value(xs, ys);
+    case 1: return cmp_value(ys, xs);
+    case 2: return cmp_value(ys, -xs);
+    case 3: return cmp_value(-xs, ys);
+    case 4: return cmp_value(-xs, -ys);
+    case 5: return cmp_value(-ys, -xs);
+    case 6: return cmp_value(-ys, xs);
+    default: return cmp_value(xs, -ys);
+  }
+}
+
+// Is direction d strictly inside the counter-clockwise sweep from direction a to
+// direction b (all about the origin point o; a and b not parallel-same)?  Exact: the
+// directions are the points A, B, D themselves.
+inline int half(P o, P ref, P d) {  // 0: d in [ref, ref + 180), 1: otherwise
+  const int s = orient(o, ref, d);
+  if (s > 0) return 0;
+  if (s < 0) return 1;
+  // collinear with the ray o -> ref: same direction (0) or opposite (1)
+  return ((d.x - o.x) * (ref.x - o.x) + (d.y - o.y) * (ref.y - o.y)) > 0 ? 0 : 1;
+}
+// ccw angle from ref to u is smaller than to v
+inline bool ccw_before(P o, P ref, P u, P v) {
+  const int hu = half(o, ref, u), hv = half(o, ref, v);
+  if (hu != hv) return hu < hv;
+  return orient(o, u, v) > 0;
+}
+// strictly between: a < d < b in ccw angle from a (d not on either ray)
+inline bool in_sector(P o, P a, P b, P d) {
+  if (orient(o, a, d) == 0 && half(o, a, d) == 0) return false;
+  if (orient(o, b, d) == 0 && half(o, b, d) == 0) return false;
+  if (eq(a, b) || (orient(o, a, b) == 0 && half(o, a, b) == 0)) return true;  // (a full turn)
+  return ccw_before(o, a, d, b);
+}
+
+// One cell overlay.  Cell rings: closed, counter-clockwise (each a part of the cell).
+// Subject: parts of rings (first = shell), closed; only segments meeting the cell's
+// envelope take part.
+struct Overlay {
+  struct Seg {  // an input segment near the cell
+    P a, b;
+    int geom;     // 0 = subject, 1 = cell
+    int ring;     // ring id within its geometry (subject: global ring index)
+    bool int_left;  // the geometry's interior lies left of a -> b
+  };
+  struct Edge {  // a noded sub-edge
+    int u, v;      // node ids
+    int geom, ring;
+    bool int_left;
+    int partner = -1;  // the coincident edge of the other geometry
+    bool in_result = false, res_left = false;  // result interior left of u -> v
+  };
+  std::vector<Seg> segs;
+  std::vector<std::vector<P>> seg_nodes;  // per seg: nodes found
+  std::vector<P> nodes;                   // node coordinates (sorted unique)
+  std::vector<uint8_t> on_geom;           // per node: bit 0 subject, bit 1 cell boundary
+  std::vector<Edge> edges;
+  // subject part / hole bookkeeping of rings: ring -> part, is hole, is ccw
+  std::vector<int> ring_part;
+  std::vector<uint8_t> ring_hole;
+  bool lower_dim = false;  // the overlay also produced lines / points (touching)
+
+  void clear() {
+    segs.clear();
+    seg_nodes.clear();
+    nodes.clear();
+    on_geom.clear();
+    edges.clear();
+    lower_dim = false;
+  }
+  int node_id(P p) const {
+    auto it = std::lower_bound(nodes.begin(), nodes.end(), p, less);
+    return (int)(it - nodes.begin());
+  }
+};
+
+// shoelace about the first vertex (absolute coordinates would cancel a chip's area away)
+inline double signed_area(const std::vector<P>& r) {
+  if (r.size() < 4) return 0;
+  const double x0 = r[0].x, y0 = r[0].y;
+  double a = 0;
+  for (size_t i = 1; i + 2 < r.size(); i++)
+    a += (r[i].x - x0) * (r[i + 1].y - y0) - (r[i + 1].x - x0) * (r[i].y - y0);
+  return 0.5 * a;
+}
+
+// Orientation.isCCW (JTS 1.20): the first highest point after a rising segment, the cap
+// there by orientation index (or a flat cap's direction); a flat ring is not ccw
+inline bool is_ccw(const std::vector<P>& ring) {
+  const int n = (int)ring.size() - 1;
+  if (n < 3) return false;
+  P upHi = ring[0], upLow{};
+  double prevY = upHi.y;
+  int iUpHi = 0;
+  for (int i = 1; i <= n; i++) {
+    const double py = ring[i].y;
+    if (py > prevY && py >= upHi.y) {
+      upHi = ring[i];
+      iUpHi = i;
+      upLow = ring[i - 1];
+    }
+    prevY = py;
+  }
+  if (iUpHi == 0) return false;
+  int iDownLow = iUpHi;
+  do {
+    iDownLow = (iDownLow + 1) % n;
+  } while (iDownLow != iUpHi && ring[iDownLow].y == upHi.y);
+  const P downLow = ring[iDownLow];
+  const P downHi = ring[iDownLow > 0 ? iDownLow - 1 : n - 1];
+  if (eq(upHi, downHi)) {
+    if (eq(upLow, upHi) || eq(downLow, upHi) || eq(upLow, downLow)) return false;
+    return orient(upLow, upHi, downLow) > 0;
+  }
+  return downHi.x - upHi.x < 0;
+}
+
+// JTS PointLocation.locateInRing (RayCrossingCounter): 1 interior, 0 boundary, -1 exterior
+inline int locate_in_ring(P p, const std::vector<P>& ring) {
+  int crossings = 0;
+  for (size_t i = 1; i < ring.size(); i++) {
+    const P p1 = ring[i - 1], p2 = ring[i];
+    if (p1.x < p.x && p2.x < p.x) continue;
+    if (eq(p, p2)) return 0;
+    if (p1.y == p.y && p2.y == p.y) {
+      double mn = p1.x, mx = p2.x;
+      if (mn > mx) std::swap(mn, mx);
+      if (p.x >= mn && p.x <= mx) return 0;
+      continue;
+    }
+    if ((p1.y > p.y && p2.y <= p.y) || (p2.y > p.y && p1.y <= p.y)) {
+      int o = orient(p1, p2, p);
+      if (o == 0) return 0;
+      if (p2.y < p1.y) o = -o;
+      if (o > 0) crossings++;
+    }
+  }
+  return (crossings & 1) ? 1 : -1;
+}
+
+// The result of one overlay: pieces (rings; ring 0 = shell, clockwise; holes ccw)
+using Rings = std::vector<std::vector<P>>;
+
+// polygon (parts of closed rings) INTERSECTION cell (closed ccw rings), as OverlayNG
+// (header).  `whole_subject_rings[r]` must hold every subject ring (for point location);
+// ring_ccw[r] its orientation.  Returns the pieces; *lower_dim when the overlay also
+// produced lines or points.
+struct Clipper {
+  Overlay o;
+  // scratch
+  std::vector<int> out_start, out_list, cell_edge_begin;
+  std::vector<uint8_t> used;
+
+  void build(const std::vector<std::vector<std::vector<P>>>& parts, const std::vector<uint8_t>& ring_ccw,
+             const std::vector<std::vector<P>>& cell, std::vector<Rings>& pieces, bool* lower_dim) {
+    o.clear();
+    pieces.clear();
+    double cx0 = INFINITY, cy0 = INFINITY, cx1 = -INFINITY, cy1 = -INFINITY;
+    for (auto& r : cell)
+      for (auto& p : r) {
+        cx0 = std::min(cx0, p.x), cx1 = std::max(cx1, p.x);
+        cy0 = std::min(cy0, p.y), cy1 = std::max(cy1, p.y);
+      }
+    // 1. segments near the cell (repeated points dropped, as EdgeNodingBuilder does)
+    o.ring_part.clear();
+    o.ring_hole.clear();
+    int ring_id = 0;
+    std::vector<const std::vector<P>*> sub_rings;
+    for (size_t pi = 0; pi < parts.size(); pi++)
+      for (size_t ri = 0; ri < parts[pi].size(); ri++, ring_id++) {
+        const auto& r = parts[pi][ri];
+        sub_rings.push_back(&r);
+        o.ring_part.push_back((int)pi);
+        o.ring_hole.push_back(ri > 0);
+        // interior of the polygon left of the ring's direction: shell ccw, hole cw
+        const bool il = (ri == 0) == (bool)ring_ccw[ring_id];
+        for (size_t k = 0; k + 1 < r.size(); k++) {
+          const P a = r[k], b = r[k + 1];
+          if (eq(a, b)) continue;
+          if (std::max(a.x, b.x) < cx0 || std::min(a.x, b.x) > cx1 || std::max(a.y, b.y) < cy0 ||
+              std::min(a.y, b.y) > cy1)
+            continue;
+          o.segs.push_back({a, b, 0, ring_id, il});
+        }
+      }
+    const size_t n_sub = o.segs.size();
+    for (size_t ci = 0; ci < cell.size(); ci++)
+      for (size_t k = 0; k + 1 < cell[ci].size(); k++)
+        if (!eq(cell[ci][k], cell[ci][k + 1])) o.segs.push_back({cell[ci][k], cell[ci][k + 1], 1, (int)ci, true});
+    // 2. noding: every subject segment against every cell segment (IntersectionAdder)
+    o.seg_nodes.assign(o.segs.size(), {});
+    for (size_t i = 0; i < n_sub; i++)
+      for (size_t j = n_sub; j < o.segs.size(); j++) {
+        const Hit h = line_intersect(o.segs[i].a, o.segs[i].b, o.segs[j].a, o.segs[j].b);
+        for (int q = 0; q < h.n; q++) {
+          o.seg_nodes[i].push_back(h.pt[q]);
+          o.seg_nodes[j].push_back(h.pt[q]);
+        }
+      }
+    // 3. sub-edges between consecutive nodes along each segment
+    std::vector<P> pts;
+    std::vector<std::pair<P, P>> sub;  // (from, to) coordinates
+    std::vector<int> sub_seg;
+    for (size_t i = 0; i < o.segs.size(); i++) {
+      const Overlay::Seg& s = o.segs[i];
+      auto& nd = o.seg_nodes[i];
+      const int oc = octant(s.b.x - s.a.x, s.b.y - s.a.y);
+      std::sort(nd.begin(), nd.end(), [&](P p, P q) { return seg_compare(oc, p, q) < 0; });
+      pts.clear();
+      pts.push_back(s.a);
+      for (P p : nd)
+        if (!eq(p, pts.back()) && !eq(p, s.b)) pts.push_back(p);
+      pts.push_back(s.b);
+      for (size_t k = 0; k + 1 < pts.size(); k++) {
+        sub.push_back({pts[k], pts[k + 1]});
+        sub_seg.push_back((int)i);
+      }
+    }
+    // node ids
+    o.nodes.clear();
+    for (auto& e : sub) {
+      o.nodes.push_back(e.first);
+      o.nodes.push_back(e.second);
+    }
+    std::sort(o.nodes.begin(), o.nodes.end(), less);
+    o.nodes.erase(std::unique(o.nodes.begin(), o.nodes.end(), eq), o.nodes.end());
+    o.on_geom.assign(o.nodes.size(), 0);
+    o.edges.clear();
+    cell_edge_begin.assign(cell.size() + 1, (int)sub.size());
+    for (size_t k = sub.size(); k-- > 0;) {
+      const Overlay::Seg& s = o.segs[sub_seg[k]];
+      if (s.geom == 1) cell_edge_begin[s.ring] = (int)k;
+    }
+    for (size_t ci = cell.size(); ci-- > 0;)
+      if (cell_edge_begin[ci] > cell_edge_begin[ci + 1]) cell_edge_begin[ci] = cell_edge_begin[ci + 1];
+    for (size_t k = 0; k < sub.size(); k++) {
+      const Overlay::Seg& s = o.segs[sub_seg[k]];
+      Overlay::Edge e;
+      e.u = o.node_id(sub[k].first);
+      e.v = o.node_id(sub[k].second);
+      e.geom = s.geom, e.ring = s.ring, e.int_left = s.int_left;
+      o.on_geom[e.u] |= (uint8_t)(1 << s.geom);
+      o.on_geom[e.v] |= (uint8_t)(1 << s.geom);
+      o.edges.push_back(e);
+    }
+    // incidence (both directions) per node
+    const int nn = (int)o.nodes.size(), ne = (int)o.edges.size();
+    out_start.assign(nn + 1, 0);
+    for (auto& e : o.edges) out_start[e.u + 1]++, out_start[e.v + 1]++;
+    for (int q = 0; q < nn; q++) out_start[q + 1] += out_start[q];
+    out_list.assign(out_start[nn], 0);
+    {
+      std::vector<int> fill(out_start.begin(), out_start.end() - 1);
+      for (int k = 0; k < ne; k++) {
+        out_list[fill[o.edges[k].u]++] = k;
+        out_list[fill[o.edges[k].v]++] = k;
+      }
+    }
+    // 4. coincident edges of the two geometries (EdgeMerger)
+    for (int q = 0; q < nn; q++)
+      for (int a = out_start[q]; a < out_start[q + 1]; a++)
+        for (int b = a + 1; b < out_start[q + 1]; b++) {
+          Overlay::Edge &e = o.edges[out_list[a]], &f = o.edges[out_list[b]];
+          if (e.geom == f.geom) continue;
+          if ((e.u == f.u && e.v == f.v) || (e.u == f.v && e.v == f.u)) {
+            e.partner = out_list[b];
+            f.partner = out_list[a];
+          }
+        }
+    // 5. location of each edge in the other geometry
+    // the ring neighbours of a node on one ring of geometry g: the other endpoints of that
+    // ring's edges incident to the node (prev: the edge ending there, next: starting)
+    auto ring_at = [&](int node, int geom, int ring, P* prev, P* next) {
+      bool hp = false, hn = false;
+      for (int a = out_start[node]; a < out_start[node + 1]; a++) {
+        const Overlay::Edge& e = o.edges[out_list[a]];
+        if (e.geom != geom || e.ring != ring) continue;
+        if (e.v == node && !hp) *prev = o.nodes[e.u], hp = true;
+        if (e.u == node && !hn) *next = o.nodes[e.v], hn = true;
+      }
+      return hp && hn;
+    };
+    // is direction node -> w inside the area enclosed by ring (g, ring) at node?
+    auto in_ring_sector = [&](int node, int geom, int ring, bool ccw, P w) {
+      P prev{}, next{};
+      if (!ring_at(node, geom, ring, &prev, &next)) return false;
+      const P X = o.nodes[node];
+      // enclosed area left of travel (ccw): from next ccw to prev; else from prev to next
+      return ccw ? in_sector(X, next, prev, w) : in_sector(X, prev, next, w);
+    };
+    // rings of geometry g through a node
+    auto rings_at = [&](int node, int geom, std::vector<int>& rs) {
+      rs.clear();
+      for (int a = out_start[node]; a < out_start[node + 1]; a++) {
+        const Overlay::Edge& e = o.edges[out_list[a]];
+        if (e.geom == geom && std::find(rs.begin(), rs.end(), e.ring) == rs.end()) rs.push_back(e.ring);
+      }
+    };
+    std::vector<int> rs;
+    // subject interior at node (on the subject's boundary) in direction w: per part through
+    // the node, inside its shell's sector (or inside the shell) and outside its holes' sectors
+    auto subject_sector = [&](int node, P w) {
+      rings_at(node, 0, rs);
+      std::vector<int> prts;
+      for (int r : rs)
+        if (std::find(prts.begin(), prts.end(), o.ring_part[r]) == prts.end()) prts.push_back(o.ring_part[r]);
+      for (int pt : prts) {
+        bool in = true;
+        bool shell_here = false;
+        for (int r : rs) {
+          if (o.ring_part[r] != pt) continue;
+          const bool s = in_ring_sector(node, 0, r, ring_ccw[r], w);
+          if (!o.ring_hole[r]) shell_here = true, in = in && s;
+          else in = in && !s;
+        }
+        (void)shell_here;
+        if (in) return true;
+      }
+      return false;
+    };
+    auto cell_sector = [&](int node, P w) {
+      rings_at(node, 1, rs);
+      for (int r : rs)
+        if (in_ring_sector(node, 1, r, true, w)) return true;
+      return false;
+    };
+    auto locate_cell = [&](P p) {  // not on the cell's boundary here
+      for (auto& r : cell)
+        if (locate_in_ring(p, r) >= 0) return true;
+      return false;
+    };
+    auto locate_subject = [&](P p) {
+      int ring = 0;
+      for (size_t pi = 0; pi < parts.size(); pi++) {
+        bool in = false;
+        for (size_t ri = 0; ri < parts[pi].size(); ri++, ring++) {
+          const int l = locate_in_ring(p, *sub_rings[ring]);
+          if (ri == 0) in = l >= 0;
+          else if (in && l > 0) in = false;
+        }
+        if (in) return true;
+      }
+      return false;
+    };
+    // located edges: at a node of the other geometry by its sectors; a subject edge touching
+    // no cell node by point location in the cell (both ends, locateEdgeBothEnds)
+    std::vector<int8_t> loc(ne, -1);
+    for (int k = 0; k < ne; k++) {
+      const Overlay::Edge& e = o.edges[k];
+      if (e.partner >= 0) continue;
+      const int other = 1 - e.geom;
+      const P U = o.nodes[e.u], V = o.nodes[e.v];
+      if (o.on_geom[e.u] & (1 << other)) loc[k] = (other ? cell_sector(e.u, V) : subject_sector(e.u, V)) ? 1 : 0;
+      else if (o.on_geom[e.v] & (1 << other)) loc[k] = (other ? cell_sector(e.v, U) : subject_sector(e.v, U)) ? 1 : 0;
+      else if (other == 1) loc[k] = (locate_cell(U) && locate_cell(V)) ? 1 : 0;
+    }
+    // a cell edge touching no subject node lies where its ring's previous edge does (the
+    // location changes only at subject nodes; a cell ring's edges are consecutive, in ring
+    // order); a ring without any subject node: one point location in the subject
+    for (size_t ci = 0; ci < cell.size(); ci++) {
+      const int k0 = cell_edge_begin[ci], k1 = cell_edge_begin[ci + 1], m = k1 - k0;
+      if (m <= 0) continue;
+      int start = -1;
+      for (int k = k0; k < k1 && start < 0; k++)
+        if (loc[k] >= 0 || o.edges[k].partner >= 0) start = k;
+      if (start < 0) {
+        const int8_t l = locate_subject(o.nodes[o.edges[k0].u]) ? 1 : 0;
+        for (int k = k0; k < k1; k++) loc[k] = l;
+        continue;
+      }
+      int8_t cur = o.edges[start].partner >= 0 ? -1 : loc[start];
+      for (int t = 1; t < m; t++) {
+        const int k = k0 + (start - k0 + t) % m;
+        if (o.edges[k].partner >= 0) {
+          cur = -1;
+          continue;
+        }
+        if (loc[k] >= 0) cur = loc[k];
+        else if (cur >= 0) loc[k] = cur;
+      }
+      // (edges after a shared edge with no located edge before them: one more pass)
+      for (int t = 0; t < m; t++) {
+        const int k = k0 + (start - k0 + t) % m;
+        if (loc[k] < 0 && o.edges[k].partner < 0) loc[k] = locate_subject(o.nodes[o.edges[k].u]) ? 1 : 0;
+      }
+    }
+    for (int k = 0; k < ne; k++) {
+      Overlay::Edge& e = o.edges[k];
+      if (e.partner < 0 && loc[k] == 1) {
+        e.in_result = true;
+        e.res_left = e.int_left;
+      }
+    }
+    // shared edges: in the result when both interiors lie on the same side
+    for (int k = 0; k < ne; k++) {
+      Overlay::Edge& e = o.edges[k];
+      if (e.partner < 0 || e.geom != 0) continue;
+      const Overlay::Edge& f = o.edges[e.partner];
+      const bool f_left = (f.u == e.u) ? f.int_left : !f.int_left;  // f's interior side on e's direction
+      if (f_left == e.int_left) {
+        e.in_result = true;
+        e.res_left = e.int_left;
+      } else {
+        o.lower_dim = true;  // a touching line (non-strict OverlayNG keeps it)
+      }
+    }
+    // isolated touching points: a node on both boundaries with no result edge
+    // 6. result edges directed with the result interior on their right (shells clockwise)
+    std::vector<std::pair<int, int>> res;  // (from, to) node ids
+    for (auto& e : o.edges)
+      if (e.in_result) res.push_back(e.res_left ? std::make_pair(e.v, e.u) : std::make_pair(e.u, e.v));
+    {
+      std::vector<uint8_t> touched(nn, 0);
+      for (auto& r : res) touched[r.first] = touched[r.second] = 1;
+      for (int q = 0; q < nn; q++)
+        if (o.on_geom[q] == 3 && !touched[q]) o.lower_dim = true;
+    }
+    *lower_dim = o.lower_dim;
+    if (res.empty()) return;
+    // 7. minimal rings: at each node leave by the first out-edge counter-clockwise from the
+    // reversed incoming direction (the face on the right)
+    const int nr = (int)res.size();
+    std::vector<int> rs_start(nn + 1, 0), rs_list(nr);
+    for (auto& r : res) rs_start[r.first + 1]++;
+    for (int q = 0; q < nn; q++) rs_start[q + 1] += rs_start[q];
+    {
+      std::vector<int> fill(rs_start.begin(), rs_start.end() - 1);
+      for (int k = 0; k < nr; k++) rs_list[fill[res[k].first]++] = k;
+    }
+    used.assign(nr, 0);
+    std::vector<std::vector<P>> rings;
+    for (int k0 = 0; k0 < nr; k0++) {
+      if (used[k0]) continue;
+      std::vector<P> ring;
+      int k = k0;
+      bool ok = true;
+      while (true) {
+        used[k] = 1;
+        ring.push_back(o.nodes[res[k].first]);
+        const int X = res[k].second;
+        if (X == res[k0].first && (rs_start[X + 1] - rs_start[X] == 1)) break;
+        // choose the next edge
+        int best = -1;
+        const P Xp = o.nodes[X], back = o.nodes[res[k].first];
+        // (an edge straight back the way we came turns by a full circle: last)
+        auto straight_back = [&](P d) {
+          return orient(Xp, back, d) == 0 && half(Xp, back, d) == 0;
+        };
+        for (int a = rs_start[X]; a < rs_start[X + 1]; a++) {
+          const int c = rs_list[a];
+          const P d = o.nodes[res[c].second];
+          if (best < 0) {
+            best = c;
+            continue;
+          }
+          const P bd = o.nodes[res[best].second];
+          const bool sb = straight_back(d), sbb = straight_back(bd);
+          if (sb != sbb) {
+            if (!sb) best = c;
+            continue;
+          }
+          if (ccw_before(Xp, back, d, bd)) best = c;
+        }
+        if (best == k0) break;
+        if (best < 0 || used[best]) {
+          ok = false;
+          break;
+        }
+        k = best;
+      }
+      if (!ok || ring.size() < 3) continue;
+      ring.push_back(ring[0]);
+      rings.push_back(std::move(ring));
+    }
+    // 8. shells (clockwise) and holes (ccw); each hole to the smallest shell holding it
+    std::vector<int> shells, holes;
+    std::vector<double> area(rings.size());
+    // (OverlayEdgeRing: a ring is a hole iff Orientation.isCCW)
+    for (size_t i = 0; i < rings.size(); i++) {
+      area[i] = std::fabs(signed_area(rings[i]));
+      if (!is_ccw(rings[i])) shells.push_back((int)i);
+      else holes.push_back((int)i);
+    }
+    if (shells.empty()) return;
+    std::vector<Rings> out(shells.size());
+    for (size_t s = 0; s < shells.size(); s++) out[s].push_back(rings[shells[s]]);
+    for (int h : holes) {
+      int best = -1;
+      for (size_t s = 0; s < shells.size(); s++) {
+        const auto& sh = rings[shells[s]];
+        // a hole vertex not on the shell
+        int l = 0;
+        for (auto& p : rings[h]) {
+          l = locate_in_ring(p, sh);
+          if (l != 0) break;
+        }
+        if (l > 0 && (best < 0 || area[shells[s]] < area[shells[best]])) best = (int)s;
+      }
+      if (best >= 0) out[best].push_back(rings[h]);
+    }
+    pieces = std::move(out);
+  }
+};
+
+// coerceChipGeometry's difference with the cell boundary: each chip edge re-noded against
+// the cell's segments (RobustLineIntersector; the chip edge first as IntersectionAdder's
+// segment pair puts it); a node strictly inside an edge splits it
+inline void renode_with_cell(std::vector<Rings>& pieces, const std::vector<std::vector<P>>& cell) {
+  std::vector<P> nd, out;
+  for (auto& piece : pieces)
+    for (auto& ring : piece) {
+      out.clear();
+      for (size_t k = 0; k + 1 < ring.size(); k++) {
+        const P a = ring[k], b = ring[k + 1];
+        out.push_back(a);
+        nd.clear();
+        for (auto& cr : cell)
+          for (size_t j = 0; j + 1 < cr.size(); j++) {
+            const Hit h = line_intersect(a, b, cr[j], cr[j + 1]);
+            for (int q = 0; q < h.n; q++)
+              if (!eq(h.pt[q], a) && !eq(h.pt[q], b)) nd.push_back(h.pt[q]);
+          }
+        if (nd.empty()) continue;
+        const int oc = octant(b.x - a.x, b.y - a.y);
+        std::sort(nd.begin(), nd.end(), [&](P p, P q) { return seg_compare(oc, p, q) < 0; });
+        for (size_t q = 0; q < nd.size(); q++)
+          if (q == 0 || !eq(nd[q], nd[q - 1])) out.push_back(nd[q]);
+      }
+      out.push_back(out[0]);
+      ring.swap(out);
+    }
+}
+
+}  // namespace ovl
+}  // namespace mgpu

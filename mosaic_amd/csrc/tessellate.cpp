@@ -53,6 +53,7 @@
 #include "h3_core.h"
 #include "h3_boundary.h"
 #include "jts_buffer.h"
+#include "jts_overlay.h"
 #include "parallel.h"
 #include "wkb.h"
 
@@ -60,9 +61,7 @@ namespace {
 
 thread_local std::string t_err;
 
-struct Pt {
-  double x, y;
-};
+using Pt = mgpu::ovl::P;
 
 double ring_area(const std::vector<Pt>& r) {
   double a = 0;
@@ -114,12 +113,27 @@ bool point_in_ring(const std::vector<Pt>& r, Pt p) {
 
 struct Polygon {
   std::vector<std::vector<std::vector<Pt>>> parts;  // part -> rings (first = shell)
+  std::vector<uint8_t> ring_ccw;                    // per ring (parts' rings in order)
+  bool multi = false;                               // a MULTIPOLYGON (else a POLYGON)
 };
 
-double orient(Pt a, Pt b, Pt c) { return (b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x); }
+// how border chips are cut (mgpu_tessellate_geom's chip_geometry)
+enum ChipGeometry { kChipOverlay = 0, kChipSutherlandHodgman = 1 };
+
+struct GeomStats {
+  int64_t overlay_chips = 0;   // border chips cut by the overlay
+  int64_t multi_piece = 0;     // ... that fell apart into several pieces
+  int64_t coerced = 0;         // ... re-noded by coerceChipGeometry's difference
+  int64_t coerce_nodes = 0;    // nodes that difference added
+  int64_t lower_dim = 0;       // ... whose overlay also gave lines / points
+};
+
+thread_local mgpu::ovl::Clipper t_clip;
+
+double cross3(Pt a, Pt b, Pt c) { return (b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x); }
 
 bool segments_touch(Pt a, Pt b, Pt c, Pt d) {
-  double o1 = orient(a, b, c), o2 = orient(a, b, d), o3 = orient(c, d, a), o4 = orient(c, d, b);
+  double o1 = cross3(a, b, c), o2 = cross3(a, b, d), o3 = cross3(c, d, a), o4 = cross3(c, d, b);
   if (((o1 > 0 && o2 < 0) || (o1 < 0 && o2 > 0)) && ((o3 > 0 && o4 < 0) || (o3 < 0 && o4 > 0))) return true;
   auto on = [](Pt p, Pt q, Pt r) {  // r on segment pq given collinear
     return std::min(p.x, q.x) <= r.x && r.x <= std::max(p.x, q.x) && std::min(p.y, q.y) <= r.y &&
@@ -131,14 +145,14 @@ bool segments_touch(Pt a, Pt b, Pt c, Pt d) {
 // convex ccw closed polygon: p inside or on the boundary
 bool in_convex(const std::vector<Pt>& cell, Pt p) {
   for (size_t i = 0; i + 1 < cell.size(); i++)
-    if (orient(cell[i], cell[i + 1], p) < 0) return false;
+    if (cross3(cell[i], cell[i + 1], p) < 0) return false;
   return true;
 }
 
 bool is_convex(const std::vector<Pt>& c) {  // closed ccw ring
   const size_t n = c.size() - 1;
   for (size_t i = 0; i < n; i++)
-    if (orient(c[(i + n - 1) % n], c[i], c[(i + 1) % n]) < 0) return false;
+    if (cross3(c[(i + n - 1) % n], c[i], c[(i + 1) % n]) < 0) return false;
   return true;
 }
 
@@ -157,11 +171,11 @@ std::vector<std::vector<Pt>> convex_pieces(const std::vector<Pt>& cell) {
     bool cut = false;
     for (int k = 0; k < m && !cut; k++) {
       const int a = idx[(k + m - 1) % m], b = idx[k], c = idx[(k + 1) % m];
-      if (orient(cell[a], cell[b], cell[c]) <= 0) continue;
+      if (cross3(cell[a], cell[b], cell[c]) <= 0) continue;
       bool empty = true;
       for (int q : idx)
-        if (q != a && q != b && q != c && orient(cell[a], cell[b], cell[q]) >= 0 &&
-            orient(cell[b], cell[c], cell[q]) >= 0 && orient(cell[c], cell[a], cell[q]) >= 0)
+        if (q != a && q != b && q != c && cross3(cell[a], cell[b], cell[q]) >= 0 &&
+            cross3(cell[b], cell[c], cell[q]) >= 0 && cross3(cell[c], cell[a], cell[q]) >= 0)
           empty = false;
       if (!empty) continue;
       pieces.push_back({a, b, c});
@@ -774,7 +788,7 @@ bool cell_in_polygon(const std::vector<Pt>& cellb, const std::vector<std::vector
 
 // `lat_rings`: every ring in the grid's lattice space (densified for H3)
 void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<std::vector<Pt>>& lat_rings, int32_t pid,
-                        bool keep_core, CoreRule* rule, std::vector<Chip>& out) {
+                        bool keep_core, CoreRule* rule, int chip_geometry, GeomStats& gs, std::vector<Chip>& out) {
   // a cell the polygon holds whole: core -- unless mosaicFill's rule (rule != null) puts
   // it in the border set (then its chip is the whole cell, not core)
   auto whole = [&](int64_t id, long i, long j, const std::vector<std::vector<Pt>>* rings) {
@@ -909,6 +923,43 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
     // Mod-2 rule puts a point on such a seam in the interior, as for the whole cell)
     std::vector<mgpu::wkb::Polygon> parts;
     double area = 0;
+    if (chip_geometry == kChipOverlay) {
+      // polygon INTERSECTION cell as JTS OverlayNG computes it, then coerceChipGeometry
+      // (jts_overlay.h)
+      std::vector<mgpu::ovl::Rings> pcs;
+      bool lower = false;
+      t_clip.build(poly.parts, poly.ring_ccw, rings, pcs, &lower);
+      for (auto& pc : pcs)
+        for (size_t k = 0; k < pc.size(); k++) area += (k == 0 ? 1.0 : -1.0) * std::fabs(mgpu::ovl::signed_area(pc[k]));
+      if (pcs.empty() || area <= 0) continue;  // empty chip (lines / points only): dropped
+      gs.overlay_chips++;
+      if (pcs.size() > 1) gs.multi_piece++;
+      if (lower) gs.lower_dim++;
+      if (lower || poly.multi != (pcs.size() > 1)) {
+        size_t before = 0, after = 0;
+        for (auto& pc : pcs)
+          for (auto& r : pc) before += r.size();
+        mgpu::ovl::renode_with_cell(pcs, rings);
+        for (auto& pc : pcs)
+          for (auto& r : pc) after += r.size();
+        gs.coerced++;
+        gs.coerce_nodes += (int64_t)(after - before);
+      }
+      for (auto& pc : pcs) {
+        mgpu::wkb::Polygon wp;
+        for (auto& r : pc) {
+          std::vector<double> flat;
+          flat.reserve(2 * r.size());
+          for (auto& q : r) {
+            flat.push_back(q.x);
+            flat.push_back(q.y);
+          }
+          wp.push_back(std::move(flat));
+        }
+        parts.push_back(std::move(wp));
+      }
+    }
+    if (chip_geometry == kChipSutherlandHodgman)
     for (auto& piece : pieces)
     for (auto& part : poly.parts) {
       mgpu::wkb::Polygon out_part;
@@ -1036,6 +1087,7 @@ bool h3_faces(const Polygon& poly, int res, std::vector<std::vector<Pt>>& dense,
 struct mgpu_tess {
   std::vector<Chip> chips;
   CoreStats core_stats;
+  GeomStats geom_stats;
 };
 
 namespace {
@@ -1097,7 +1149,21 @@ int32_t mgpu_tessellate(int32_t index_system, int32_t res, int64_t n_polys, cons
 int32_t mgpu_tessellate_ex(int32_t index_system, int32_t res, int64_t n_polys, const int32_t* polygon_id,
                            const int64_t* poly_part_off, const int64_t* part_ring_off, const int64_t* ring_off,
                            const double* xy, int32_t keep_core_geometries, int32_t core_rule, mgpu_tess** out) {
+  return mgpu_tessellate_geom(index_system, res, n_polys, polygon_id, poly_part_off, part_ring_off, ring_off, xy,
+                              nullptr, keep_core_geometries, core_rule, MGPU_CHIPS_OVERLAY, out);
+}
+
+int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys, const int32_t* polygon_id,
+                             const int64_t* poly_part_off, const int64_t* part_ring_off, const int64_t* ring_off,
+                             const double* xy, const uint8_t* poly_type, int32_t keep_core_geometries,
+                             int32_t core_rule, int32_t chip_geometry, mgpu_tess** out) {
   if (!out || n_polys < 0) return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellate: bad arguments");
+  if (chip_geometry != MGPU_CHIPS_OVERLAY && chip_geometry != MGPU_CHIPS_SUTHERLAND_HODGMAN)
+    return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellate: unknown chip geometry %d", chip_geometry);
+  for (int64_t p = 0; poly_type && p < n_polys; p++)
+    if (poly_type[p] != 3 && poly_type[p] != 6)
+      return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellate: polygon type %d (3 = POLYGON, 6 = MULTIPOLYGON)",
+                             (int)poly_type[p]);
   if (core_rule != MGPU_CORE_MOSAICFILL && core_rule != MGPU_CORE_CLIP && core_rule != MGPU_CORE_DISTANCE)
     return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellate: unknown core rule %d", core_rule);
   if (int32_t st = mgpu_check_resolution(index_system, res)) return st;
@@ -1109,6 +1175,7 @@ int32_t mgpu_tessellate_ex(int32_t index_system, int32_t res, int64_t n_polys, c
   std::vector<std::vector<Chip>> per(n_polys);
   std::vector<uint8_t> bad_poly(n_polys, 0);
   std::vector<CoreStats> pstats(n_polys);
+  std::vector<GeomStats> gstats(n_polys);
   mgpu::parallel_for(n_polys, 64, [&](int64_t pb, int64_t pe, int) {
     for (int64_t p = pb; p < pe; p++) {
       Polygon poly;
@@ -1125,6 +1192,11 @@ int32_t mgpu_tessellate_ex(int32_t index_system, int32_t res, int64_t n_polys, c
         if (!rings.empty()) poly.parts.push_back(std::move(rings));
       }
       if (poly.parts.empty()) continue;
+      // the geometry's type decides coerceChipGeometry (a MULTIPOLYGON unless told, when it
+      // has several parts); each ring's orientation gives the interior's side of its edges
+      poly.multi = poly_type ? poly_type[p] == 6 : poly.parts.size() > 1;
+      for (auto& part : poly.parts)
+        for (auto& ring : part) poly.ring_ccw.push_back(mgpu::ovl::is_ccw(ring));
       // mosaicFill's core set (CoreRule) unless the clip rule was asked for
       CoreRule rule_storage;
       CoreRule* rule = nullptr;
@@ -1162,7 +1234,8 @@ int32_t mgpu_tessellate_ex(int32_t index_system, int32_t res, int64_t n_polys, c
             for (auto& q : r) lr.push_back(g.to_lattice(q));
             lat_rings.push_back(std::move(lr));
           }
-          tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, rule, per[p]);
+          tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, rule, chip_geometry,
+                             gstats[p], per[p]);
         }
         // a cell reached twice (two lattice positions around a pentagon map to one id):
         // its chip is computed from the id, so the copies are equal -- keep the first
@@ -1181,7 +1254,8 @@ int32_t mgpu_tessellate_ex(int32_t index_system, int32_t res, int64_t n_polys, c
             for (auto& q : ring) lr.push_back(g.to_lattice(q));
             lat_rings.push_back(std::move(lr));
           }
-        tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, rule, per[p]);
+        tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, rule, chip_geometry,
+                           gstats[p], per[p]);
       }
       if (rule) pstats[p] = rule->st;
     }
@@ -1197,6 +1271,13 @@ int32_t mgpu_tessellate_ex(int32_t index_system, int32_t res, int64_t n_polys, c
                              "first, as the reference's alignToGrid does)", polygon_id[p]);
   }
   mgpu_tess* t = new mgpu_tess();
+  for (auto& q : gstats) {
+    t->geom_stats.overlay_chips += q.overlay_chips;
+    t->geom_stats.multi_piece += q.multi_piece;
+    t->geom_stats.coerced += q.coerced;
+    t->geom_stats.coerce_nodes += q.coerce_nodes;
+    t->geom_stats.lower_dim += q.lower_dim;
+  }
   for (auto& q : pstats) {
     t->core_stats.demoted += q.demoted;
     t->core_stats.promoted += q.promoted;
@@ -1268,7 +1349,9 @@ int32_t mgpu_tess_result_core_stats(const mgpu_tess* t, int64_t* out, int32_t n)
   const CoreStats& s = t->core_stats;
   const int64_t v[] = {(int64_t)t->chips.size(), core, s.demoted, s.promoted, s.dropped, s.ambiguous,
                        s.carved_tests, s.band_tests, s.core_below_r, s.border_above_r, s.band_dropped,
-                       s.dp_sensitive, s.unresolved, s.carved_empty};
+                       s.dp_sensitive, s.unresolved, s.carved_empty, t->geom_stats.overlay_chips,
+                       t->geom_stats.multi_piece, t->geom_stats.coerced, t->geom_stats.coerce_nodes,
+                       t->geom_stats.lower_dim};
   for (int32_t i = 0; i < n; i++) out[i] = i < (int32_t)(sizeof(v) / sizeof(v[0])) ? v[i] : 0;
   return MGPU_OK;
 }

@@ -52,9 +52,14 @@ def wkt_to_wkb(wkt, **kw):
 
 
 def ring_area(r):
+    """shoelace about the ring's first vertex (absolute lon / lat products would cancel a
+    small chip's area into rounding noise)"""
+    if len(r) < 2:
+        return 0.0
+    x0, y0 = r[0]
     a = 0.0
     for (x1, y1), (x2, y2) in zip(r[:-1], r[1:]):
-        a += x1 * y2 - x2 * y1
+        a += (x1 - x0) * (y2 - y0) - (x2 - x0) * (y1 - y0)
     return 0.5 * a
 
 
@@ -127,3 +132,70 @@ def brute_force_pairs(polys, x, y, oracle):
             if oracle.st_contains(w, x[i], y[i]):
                 pairs.add((int(i), pid))
     return pairs
+
+
+def crossing_adversaries(P, table, cell_rings_of, ulps=3, steps=4, max_chips=None, grid_step=None):
+    """Points a few ulps from every place a polygon edge crosses a cell edge (the
+    reference's chip vertices there come from JTS's RobustLineIntersector: oracle/
+    jts_overlay.py): points on the ORIGINAL polygon segment near the crossing (rounded
+    a + t (b - a) for t around the crossing's parameter, `steps` each way, 2^-50 apart) and
+    the crossing node's ulp neighbourhood (+-`ulps` in x and y).  grid_step (BNG): also the
+    0.01-m points on the square line nearest the crossing, 3 each way.
+    -> (x, y) float64 arrays."""
+    import jts_overlay as JO
+    idx = {int(p): i for i, p in enumerate(P.poly_id)}
+    rows = np.nonzero(~table.is_core.astype(bool))[0]
+    if max_chips is not None:
+        rows = rows[:: max(1, len(rows) // max_chips)]
+    xs, ys = [], []
+    cache = {}
+    for i in rows:
+        k = idx[int(table.polygon_id[i])]
+        if k not in cache:
+            cache[k] = [[tuple(map(float, v)) for v in P.xy[P.ring_off[r]:P.ring_off[r + 1]]]
+                        for q in range(P.poly_part_off[k], P.poly_part_off[k + 1])
+                        for r in range(P.part_ring_off[q], P.part_ring_off[q + 1])]
+        w = bytes(table.wkb[table.wkb_offsets[i]:table.wkb_offsets[i + 1]])
+        cell = cell_rings_of(table.cell[i], w)
+        cx = [p[0] for r in cell for p in r]
+        cy = [p[1] for r in cell for p in r]
+        x0, x1, y0, y1 = min(cx), max(cx), min(cy), max(cy)
+        csegs = [(r[j], r[j + 1]) for r in cell for j in range(len(r) - 1)]
+        for ring in cache[k]:
+            for j in range(len(ring) - 1):
+                a, b = ring[j], ring[j + 1]
+                if a == b or max(a[0], b[0]) < x0 or min(a[0], b[0]) > x1 or max(a[1], b[1]) < y0 or min(a[1], b[1]) > y1:
+                    continue
+                for c, d in csegs:
+                    pts, proper = JO.line_intersection(a, b, c, d)
+                    if not proper:
+                        continue
+                    X = pts[0]
+                    ax = 0 if abs(b[0] - a[0]) >= abs(b[1] - a[1]) else 1
+                    t = (X[ax] - a[ax]) / (b[ax] - a[ax])
+                    for s in range(-steps, steps + 1):
+                        tt = t + s * 2.0 ** -50
+                        xs.append(a[0] + tt * (b[0] - a[0]))
+                        ys.append(a[1] + tt * (b[1] - a[1]))
+                    for dx in range(-ulps, ulps + 1):
+                        for dy in range(-ulps, ulps + 1):
+                            px, py = X
+                            for _ in range(abs(dx)):
+                                px = np.nextafter(px, np.inf if dx > 0 else -np.inf)
+                            for _ in range(abs(dy)):
+                                py = np.nextafter(py, np.inf if dy > 0 else -np.inf)
+                            xs.append(float(px))
+                            ys.append(float(py))
+                    if grid_step:
+                        # the square line the crossing lies on (vertical: x fixed, else y fixed)
+                        if c[0] == d[0]:
+                            base = round(X[1], 2)
+                            for s in range(-3, 4):
+                                xs.append(c[0])
+                                ys.append(round(base + s * grid_step, 2))
+                        else:
+                            base = round(X[0], 2)
+                            for s in range(-3, 4):
+                                xs.append(round(base + s * grid_step, 2))
+                                ys.append(c[1])
+    return np.array(xs, np.float64), np.array(ys, np.float64)

@@ -652,6 +652,36 @@ def test_pip_join_c4_answer_grid_edges(gpu):
     assert np.array_equal(gp, op) and np.array_equal(gq, oq)
 
 
+@pytest.mark.parametrize("pipeline", [0, 1, 2])
+def test_pip_join_overlay_crossing_adversaries(gpu, nyc_zones, nyc_chips_r9, pipeline):
+    """Round 6's border chips (JTS OverlayNG's cut, jts_overlay.h) through every pipeline on
+    points a few ulps from the polygon-edge x cell-edge crossings (their chip vertices are
+    RobustLineIntersector's nodes): NYC r9 (a 1,500-chip sample) and the London-like
+    districts at BNG r4 with 0.01-m points on the square lines -- every pair equals the
+    oracle's over the same table."""
+    import bench_workloads as W
+    from geom_util import crossing_adversaries
+    from test_tessellate_host import _bng_cell_rings, _h3_cell_rings
+    import jts_overlay as JO
+    c = nyc_chips_r9
+    x, y = crossing_adversaries(nyc_zones, c, lambda cell, w: _h3_cell_rings(cell), max_chips=1500)
+    ctx = M.default_context(gpu)
+    with ctx.options(pipeline=pipeline):
+        r = M.pip_join(T(x, gpu), T(y, gpu), c, 9)
+    op, oq = oracle_join(c, x, y)
+    gp, gq = r.numpy()
+    assert len(op) > 1000 and np.array_equal(gp, op) and np.array_equal(gq, oq)
+    L = W.london_districts()
+    cb = M.tessellate(L, M.BNGIndexSystem(), 4)
+    x, y = crossing_adversaries(L, cb, lambda cell, w: _bng_cell_rings([q for pc in JO.wkb_rings(w) for q in pc], 100.0),
+                                max_chips=3000, grid_step=0.01)
+    with ctx.options(pipeline=pipeline):
+        r = M.pip_join(T(x, gpu), T(y, gpu), cb, 4, index_system=M.BNGIndexSystem())
+    op, oq = oracle_join(cb, x, y, res=4, isys=1)
+    gp, gq = r.numpy()
+    assert len(op) > 1000 and np.array_equal(gp, op) and np.array_equal(gq, oq)
+
+
 def test_pip_join_c5_skewed_fractal(gpu):
     """C5: points concentrated on the boundaries of 49k-vertex fractal polygons."""
     import bench_workloads as W

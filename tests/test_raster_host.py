@@ -207,21 +207,29 @@ def test_whole_cell_shortcut_tracts_r10():
     print("whole-cell answers: %.3f of the points" % frac)
 
 
-def test_nyc_r9_blob_bytes_pinned(nyc_chips_r9):
-    """The NYC r9 chip-table blob (mgpu_chips_host_blob: headers, strips, lattice grid,
-    pixel index with its 16x16 sub-pixels) is byte-for-byte the one round 5's builder
-    produced before its speed-ups (per-pixel edge lists, shared corner sines, row-parity
-    verdicts, hashed classes): sha256 prefix of the whole blob."""
+def _blob_hash(c):
     import ctypes
     import hashlib
     from mosaic_amd import _native as N
-    c = nyc_chips_r9
     out, nb = ctypes.c_void_p(), ctypes.c_int64()
     p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
     N.check(N.lib().mgpu_chips_host_blob(0, len(c), p(c.cell), p(c.polygon_id), p(c.is_core), p(c.wkb_offsets),
                                          p(c.wkb), ctypes.byref(out), ctypes.byref(nb)))
     try:
-        h = hashlib.sha256(ctypes.string_at(out.value, nb.value)).hexdigest()[:16]
+        return nb.value, hashlib.sha256(ctypes.string_at(out.value, nb.value)).hexdigest()[:16]
     finally:
         N.lib().mgpu_host_free(out)
-    assert (nb.value, h) == (86778112, "a145d3f4556f4f6a")
+
+
+def test_nyc_r9_blob_bytes_pinned(nyc_zones, nyc_chips_r9):
+    """The NYC r9 chip-table blob (mgpu_chips_host_blob: headers, strips, lattice grid,
+    pixel index with its 16x16 sub-pixels) is byte-for-byte the one round 5's builder
+    produced before its speed-ups (per-pixel edge lists, shared corner sines, row-parity
+    verdicts, hashed classes): sha256 prefix of the whole blob of round 5's chips (the
+    Sutherland-Hodgman clip, kept as chip_geometry="sutherland_hodgman").  Round 6's chips
+    (the JTS overlay: one zero-area row fewer, other crossing vertices, separate pieces)
+    give their own pinned blob."""
+    import mosaic_amd as M
+    sh = M.tessellate(nyc_zones, M.H3IndexSystem(), 9, chip_geometry="sutherland_hodgman")
+    assert _blob_hash(sh) == (86778112, "a145d3f4556f4f6a")
+    assert _blob_hash(nyc_chips_r9) == (86478336, "8235ff6347457b25")

@@ -322,8 +322,12 @@ def _assert_rule(P, res, expect=None):
     return clip, mf
 
 
-@pytest.mark.parametrize("res,expect", [(8, (2795, 29, 125, 0)), (9, (11890, 2229, 1713, 0)),
-                                        (10, (64041, 34257, 7469, 0))])
+# (rows: round 5's Sutherland-Hodgman clip gave 2795 / 11890 / 64041 -- 2 / 1 / 17 rows whose
+# polygon only touches the cell (exact intersection area 0: the overlay gives no chip, as
+# MosaicChip.isEmpty drops the reference's), and at r10 it missed 4 real chips (exact areas
+# 7.8e-16 .. 5.4e-13 deg^2) whose shoelace cancelled to <= 0: test_overlay_rows_vs_clip)
+@pytest.mark.parametrize("res,expect", [(8, (2793, 29, 125, 0)), (9, (11889, 2229, 1713, 0)),
+                                        (10, (64028, 34257, 7469, 0))])
 def test_mosaicfill_rule_nyc(nyc_zones, res, expect):
     """NYC taxi zones: mosaicFill's flags (core set = polyfill(buffer(-r)), JTS's chorded
     buffer) vs the clip's (every wholly covered cell): the same rows; at res 9, 1,713 of
@@ -381,7 +385,9 @@ def test_mosaicfill_rule_coarse_cells():
     _, _, pent = cell_geometry([(1 << 59) | (bc << 45) | 0x1FFFFFFFFFFF for bc in (14,)])
     P = M.Polygons.from_lists([(2, _star(pent[0, 0], pent[0, 1], 1.0, 3.0, 30, 2)),
                                (4, _star(-40.0, -30.0, 6.0, 12.0, 50, 4))])
-    res = 4
+    # (res 3: at res 4 the dropped rows of round 5 were the clip's zero-area slivers of cells
+    # the polygon only touches -- no chip under the overlay, test_overlay_rows_vs_clip)
+    res = 3
     clip = M.tessellate(P, M.H3IndexSystem(), res, core_rule="clip")
     mf = M.tessellate(P, M.H3IndexSystem(), res)
     st = mf.core_stats
@@ -568,3 +574,184 @@ def test_jts_buffer_flags_pair_impact(nyc_zones, res):
     assert not (a - b)  # core only adds matches (points of the cell outside the polygon)
     if sticks_out == 0:
         assert a == b
+
+
+# ---------------------------------------------------------------- border chips as JTS cuts them
+# (round 6) mosaic_amd/csrc/jts_overlay.h restates `polygon INTERSECTION cell` as OverlayNG
+# computes it (IndexSystem.scala:184-188, MosaicGeometryJTS.scala:139-152) and
+# coerceChipGeometry's re-noding (IndexSystem.scala:293-303); oracle/jts_overlay.py restates
+# the node arithmetic independently (exact orientation, Intersection.intersection in IEEE
+# doubles).  Parity with JTS itself is unpinned beyond the published algorithm.
+import jts_overlay as JO  # noqa: E402  (oracle/, test infrastructure)
+
+
+def _h3_cell_rings(cell):
+    buf = (ctypes.c_uint8 * 8192)()
+    n = ctypes.c_int64()
+    _native.check(_native.lib().mgpu_test_h3_cell_wkb_host(ctypes.c_int64(int(cell)), buf, 8192, ctypes.byref(n)))
+    return [r for pc in JO.wkb_rings(bytes(buf[:n.value])) for r in pc]
+
+
+def _bng_cell_rings(chip_rings, edge):
+    xs = [p[0] for r in chip_rings for p in r]
+    ys = [p[1] for r in chip_rings for p in r]
+    i, j = float(np.floor((min(xs) + max(xs)) / 2 / edge)), float(np.floor((min(ys) + max(ys)) / 2 / edge))
+    x, y = i * edge, j * edge
+    return [[(x, y), (x + edge, y), (x + edge, y + edge), (x, y + edge), (x, y)]]
+
+
+def _poly_rings(P, k):
+    return [[tuple(map(float, v)) for v in P.xy[P.ring_off[r]:P.ring_off[r + 1]]]
+            for q in range(P.poly_part_off[k], P.poly_part_off[k + 1])
+            for r in range(P.part_ring_off[q], P.part_ring_off[q + 1])]
+
+
+def _check_overlay_chips(P, c, cell_rings_of, is_multi, limit=None):
+    """every border chip of c against oracle/jts_overlay.check_chip -> (chips, crossings, coerce nodes)"""
+    idx = {int(p): i for i, p in enumerate(P.poly_id)}
+    cache = {}
+    n = cross = coerce = 0
+    rows = np.nonzero(~c.is_core.astype(bool))[0]
+    if limit is not None:
+        rows = rows[:: max(1, len(rows) // limit)]
+    for i in rows:
+        k = idx[int(c.polygon_id[i])]
+        if k not in cache:
+            cache[k] = _poly_rings(P, k)
+        w = _wkb(c, i)
+        a, b = JO.check_chip(w, cache[k], cell_rings_of(c.cell[i], w), is_multi(k))
+        n, cross, coerce = n + 1, cross + a, coerce + b
+    return n, cross, coerce
+
+
+def test_overlay_chip_vertices_nyc_r9(nyc_zones, nyc_chips_r9):
+    """Every NYC r9 border chip (9,660; the zones are MULTIPOLYGONs): its vertices are polygon
+    vertices, cell vertices, RobustLineIntersector's nodes of the two ORIGINAL segments (the
+    independent restatement's, bit for bit), or coerceChipGeometry's re-noding nodes -- only
+    in the one-piece chips, whose type differs from the zone's; every proper crossing node
+    is a vertex."""
+    P, c = nyc_zones, nyc_chips_r9
+    assert P.poly_type is not None and (P.poly_type == 6).all()
+    n, cross, coerce = _check_overlay_chips(P, c, lambda cell, w: _h3_cell_rings(cell), lambda k: True)
+    st = c.core_stats
+    print("chips", n, "crossing vertices", cross, "coerce vertices", coerce, st)
+    assert n == st["overlay_chips"] + st["demoted"] and cross > 15000
+    assert coerce == st["coerce_nodes"] > 0 and st["coerced"] == st["overlay_chips"] - st["multi_piece"]
+
+
+def test_overlay_chip_vertices_bng_and_tracts():
+    """The same on BNG squares (London-like districts, POLYGONs, edges along the extent's km
+    lines: collinear overlaps) at res 3 and 4, and on tract-like POLYGONs at H3 r10 (a sample):
+    no re-noding unless a chip falls apart into pieces."""
+    import bench_workloads as W
+    L = W.london_districts(n_cells=40)
+    for res in (3, 4):
+        edge = 10.0 ** (6 - res)
+        c = M.tessellate(L, M.BNGIndexSystem(), res)
+        n, cross, coerce = _check_overlay_chips(
+            L, c, lambda cell, w: _bng_cell_rings([r for pc in JO.wkb_rings(w) for r in pc], edge), lambda k: False)
+        st = c.core_stats
+        assert n > 100 and cross > 100 and coerce == st["coerce_nodes"], (res, n, cross, coerce, st)
+        assert st["coerced"] == st["multi_piece"] + st["lower_dim"]
+    T = W.tract_polygons(n_cells=60)
+    c = M.tessellate(T, M.H3IndexSystem(), 10)
+    n, cross, coerce = _check_overlay_chips(T, c, lambda cell, w: _h3_cell_rings(cell), lambda k: False, limit=3000)
+    assert n > 1000 and cross > 1000 and coerce == 0 or c.core_stats["multi_piece"] > 0
+
+
+def test_overlay_separate_pieces_and_holes():
+    """A U-shaped polygon whose two arms cross one cell: OverlayNG's result is a MULTIPOLYGON
+    of two separate pieces (round 5's clip bridged them into one ring along the cell
+    boundary); a polygon with a hole inside the cell keeps it as the chip's hole.  Points
+    between the arms and in the hole: no pair, by either table."""
+    res = 4
+    edge = 100.0
+    x0, y0 = 530000.0, 180000.0
+    # arms 20 m wide, 40 m apart, crossing the square [x0, x0 + 100] x [y0, y0 + 100]
+    u = [(x0 + 10, y0 - 50), (x0 + 90, y0 - 50), (x0 + 90, y0 + 150), (x0 + 70, y0 + 150), (x0 + 70, y0 - 30),
+         (x0 + 30, y0 - 30), (x0 + 30, y0 + 150), (x0 + 10, y0 + 150), (x0 + 10, y0 - 50)]
+    h_shell = [(x0 - 150, y0 + 150 + 200), (x0 - 150, y0 + 150 + 50), (x0 + 250, y0 + 150 + 50),
+               (x0 + 250, y0 + 150 + 200), (x0 - 150, y0 + 150 + 200)]
+    hole = [(x0 + 40, y0 + 230), (x0 + 60, y0 + 230), (x0 + 60, y0 + 270), (x0 + 40, y0 + 270), (x0 + 40, y0 + 230)]
+    P = M.Polygons.from_lists([(1, [[u[::-1]]]), (2, [[h_shell[::-1], hole]])], poly_type=np.array([3, 3]))
+    new = M.tessellate(P, M.BNGIndexSystem(), res)
+    old = M.tessellate(P, M.BNGIndexSystem(), res, chip_geometry="sutherland_hodgman")
+    ucell = O.bng_point_to_index(x0 + 50, y0 + 50, res)
+    hcell = O.bng_point_to_index(x0 + 50, y0 + 250, res)
+    i = [k for k in range(len(new)) if new.cell[k] == ucell and new.polygon_id[k] == 1][0]
+    pieces = JO.wkb_rings(_wkb(new, i))
+    assert len(pieces) == 2 and all(len(pc) == 1 for pc in pieces)
+    assert _wkb(new, i)[1:5] == b"\x00\x00\x00\x06"  # big-endian MULTIPOLYGON
+    for pc in pieces:  # shells clockwise (OverlayNG)
+        assert JO.orient(pc[0][0], pc[0][1], pc[0][2]) <= 0 or len(pc[0]) > 4
+    j = [k for k in range(len(old)) if old.cell[k] == ucell and old.polygon_id[k] == 1][0]
+    assert len(JO.wkb_rings(_wkb(old, j))) == 1  # round 5: one bridged ring
+    i = [k for k in range(len(new)) if new.cell[k] == hcell and new.polygon_id[k] == 2][0]
+    pieces = JO.wkb_rings(_wkb(new, i))
+    assert len(pieces) == 1 and len(pieces[0]) == 2  # shell + the hole
+    # containment over the chips equals containment in the polygons
+    rng = np.random.default_rng(6)
+    px = np.concatenate([x0 + rng.uniform(0, 100, 4000), x0 + rng.uniform(0, 100, 4000)])
+    py = np.concatenate([y0 + rng.uniform(0, 100, 4000), y0 + 200 + rng.uniform(0, 100, 4000)])
+    want = brute_force_pairs(P, px, py, O)
+    assert len(want) > 1000
+    for t in (new, old):
+        pts, polys = O.pip_join(1, res, px, py, t.cell, t.polygon_id, t.is_core, t.wkb_offsets, t.wkb)
+        assert set(zip(pts.tolist(), polys.tolist())) == want
+
+
+def test_overlay_rows_vs_clip(nyc_zones):
+    """Rows round 5's Sutherland-Hodgman clip and the overlay disagree on (NYC r10): the
+    clip's extra rows have an exact (rational) intersection area of 0 -- the polygon only
+    touches the cell, OverlayNG gives lines / points, which coerceChipGeometry and
+    MosaicChip.isEmpty drop; the overlay's extra rows are real chips (exact area > 0) whose
+    shoelace in absolute coordinates had cancelled to <= 0 in the clip."""
+    from fractions import Fraction as F
+
+    def area(r):
+        x0, y0 = r[0]
+        return sum((r[q][0] - x0) * (r[q + 1][1] - y0) - (r[q + 1][0] - x0) * (r[q][1] - y0)
+                   for q in range(len(r) - 1)) / 2
+
+    def clip_exact(ring, cell):  # exact rational clip against the convex ccw cell: the area
+        pts = [(F(x), F(y)) for x, y in ring[:-1]]
+        c = [(F(x), F(y)) for x, y in cell]
+        for e in range(len(c) - 1):
+            a, b = c[e], c[e + 1]
+            side = lambda p: (b[0] - a[0]) * (p[1] - a[1]) - (b[1] - a[1]) * (p[0] - a[0])  # noqa: E731
+            out = []
+            if not pts:
+                break
+            prev = pts[-1]
+            sp = side(prev)
+            for cur in pts:
+                sc = side(cur)
+                if (sc >= 0) != (sp >= 0):
+                    t = sp / (sp - sc)
+                    out.append((prev[0] + t * (cur[0] - prev[0]), prev[1] + t * (cur[1] - prev[1])))
+                if sc >= 0:
+                    out.append(cur)
+                prev, sp = cur, sc
+            pts = out
+        return abs(area(pts + [pts[0]])) if len(pts) >= 3 else F(0)
+
+    P = nyc_zones
+    old = M.tessellate(P, M.H3IndexSystem(), 10, chip_geometry="sutherland_hodgman")
+    new = M.tessellate(P, M.H3IndexSystem(), 10)
+    ko = {(int(old.polygon_id[i]), int(old.cell[i])) for i in range(len(old))}
+    kn = {(int(new.polygon_id[i]), int(new.cell[i])) for i in range(len(new))}
+    idx = {int(p): i for i, p in enumerate(P.poly_id)}
+
+    def exact(pid, cell):
+        k, tot = idx[pid], F(0)
+        cr = _h3_cell_rings(cell)
+        assert len(cr) == 1
+        for q in range(P.poly_part_off[k], P.poly_part_off[k + 1]):
+            for j, r in enumerate(range(P.part_ring_off[q], P.part_ring_off[q + 1])):
+                ring = [tuple(map(float, v)) for v in P.xy[P.ring_off[r]:P.ring_off[r + 1]]]
+                tot += clip_exact(ring, cr[0]) * (1 if j == 0 else -1)
+        return tot
+
+    assert (len(ko - kn), len(kn - ko)) == (17, 4)
+    assert all(exact(*k) == 0 for k in ko - kn)
+    assert all(exact(*k) > 0 for k in kn - ko)

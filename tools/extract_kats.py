@@ -254,6 +254,8 @@ def main():
         polys.append((int(f["properties"]["objectid"]), [[[(float(x), float(y)) for x, y, *_ in ring] for ring in p] for p in parts]))
     arr = zones_to_arrays(polys)
     arr["zone_name"] = np.array([f["properties"]["zone"] for f in zones])
+    # the geometry's WKB type (3 POLYGON, 6 MULTIPOLYGON): coerceChipGeometry depends on it
+    arr["poly_type"] = np.array([6 if f["geometry"]["type"] == "MultiPolygon" else 3 for f in zones], np.uint8)
     np.savez_compressed(os.path.join(OUT, "nyc_taxi_zones.npz"), **arr)
     lon_fc = json.load(open(REF + "/notebooks/data/London_Postcode_Zones.geojson"))
     lpolys = []
@@ -262,6 +264,7 @@ def main():
         parts = g["coordinates"] if g["type"] == "MultiPolygon" else [g["coordinates"]]
         lpolys.append((k + 1, [[[(float(x), float(y)) for x, y, *_ in ring] for ring in p] for p in parts]))
     larr = zones_to_arrays(lpolys)
+    larr["poly_type"] = np.array([6 if f["geometry"]["type"] == "MultiPolygon" else 3 for f in lon_fc["features"]], np.uint8)
     larr["name"] = np.array([str(f["properties"].get("Name", f["properties"].get("name", k))) for k, f in enumerate(lon_fc["features"])])
     np.savez_compressed(os.path.join(OUT, "london_postcode_zones.npz"), **larr)
     print("h3 kats:", len(h3), "pip kats:", len(pip), "bng kats:", len(bng["point_to_index"]),
