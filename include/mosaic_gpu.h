@@ -468,6 +468,12 @@ int32_t mgpu_tess_result_core_stats(const mgpu_tess* t, int64_t* out, int32_t n)
 int32_t mgpu_tess_result_sizes(const mgpu_tess* t, int64_t* n_chips, int64_t* wkb_bytes);
 int32_t mgpu_tess_result_copy(const mgpu_tess* t, int64_t* cell, int32_t* polygon_id, uint8_t* is_core,
                               int64_t* wkb_offsets, uint8_t* wkb);
+/* The rows the core rule left undecided (core_stats' ambiguous): n, their WKB bytes, and
+ * when cell != NULL per row its cell, polygon, {kind (1 DP-sensitive band membership, 2 a
+ * centre on a buffer curve), kept (the table holds the row), core}, and its chip -- the
+ * one the table holds, or the one a dropped row would carry -- to count the pairs at stake. */
+int32_t mgpu_tess_result_undecided(const mgpu_tess* t, int64_t* n, int64_t* wkb_bytes, int64_t* cell, int32_t* poly,
+                                   uint8_t* kind_kept_core, int64_t* wkb_offsets, uint8_t* wkb);
 int32_t mgpu_tess_destroy(mgpu_tess* t);
 
 /* TEST ONLY -- not an interface of the reference.  Builds the chip table on the host

@@ -33,7 +33,7 @@ EXPORTS = (
     "mgpu_bng_format_device", "mgpu_format_cells_device", "mgpu_grid_kring",
     "mgpu_chips_upload", "mgpu_chips_destroy", "mgpu_chips_device_blob", "mgpu_chips_from_device_blob",
     "mgpu_chips_info", "mgpu_st_contains", "mgpu_pip_join", "mgpu_pip_join_async", "mgpu_pip_join_finish", "mgpu_ctx_reserve",
-    "mgpu_last_near_ties",    "mgpu_pip_join_host", "mgpu_tessellate", "mgpu_tess_result_sizes", "mgpu_tess_result_copy", "mgpu_tessellate_ex", "mgpu_tessellate_geom", "mgpu_tess_result_stats", "mgpu_tess_result_core_stats",
+    "mgpu_last_near_ties",    "mgpu_pip_join_host", "mgpu_tessellate", "mgpu_tess_result_sizes", "mgpu_tess_result_copy", "mgpu_tessellate_ex", "mgpu_tessellate_geom", "mgpu_tess_result_undecided", "mgpu_tess_result_stats", "mgpu_tess_result_core_stats",
     "mgpu_tess_destroy", "mgpu_test_chip_contains_host", "mgpu_test_raster_host", "mgpu_test_cell_answers_host", "mgpu_test_whole_cells_host", "mgpu_pip_join_fetch",
     "mgpu_chips_host_blob", "mgpu_host_free", "mgpu_host_blob_info", "mgpu_chips_upload_blob",
     "mgpu_comm_unique_id", "mgpu_comm_init", "mgpu_comm_info", "mgpu_comm_destroy", "mgpu_chips_broadcast",
@@ -140,6 +140,7 @@ def lib():
         "mgpu_tessellate": (I32, [I32, I32, I64, P, P, P, P, P, I32, ctypes.POINTER(P)]),
         "mgpu_tessellate_ex": (I32, [I32, I32, I64, P, P, P, P, P, I32, I32, ctypes.POINTER(P)]),
         "mgpu_tessellate_geom": (I32, [I32, I32, I64, P, P, P, P, P, P, I32, I32, I32, ctypes.POINTER(P)]),
+        "mgpu_tess_result_undecided": (I32, [P, P, P, P, P, P, P, P]),
         "mgpu_tess_result_stats": (I32, [P, P]),
         "mgpu_tess_result_core_stats": (I32, [P, P, I32]),
         "mgpu_tess_result_sizes": (I32, [P, ctypes.POINTER(I64), ctypes.POINTER(I64)]),

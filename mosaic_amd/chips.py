@@ -198,8 +198,18 @@ def tessellate(polygons, index_system, resolution, keep_core_geometries=True, co
         wkb = np.zeros(max(b.value, 1), np.uint8)
         N.check(L.mgpu_tess_result_copy(h, cell.ctypes.data, pid.ctypes.data, core.ctypes.data, off.ctypes.data,
                                         wkb.ctypes.data))
+        nu, ub = ctypes.c_int64(), ctypes.c_int64()
+        N.check(L.mgpu_tess_result_undecided(h, ctypes.byref(nu), ctypes.byref(ub), None, None, None, None, None))
+        ucell, upoly = np.zeros(nu.value, np.int64), np.zeros(nu.value, np.int32)
+        ukkc, uoff, uwkb = np.zeros((nu.value, 3), np.uint8), np.zeros(nu.value + 1, np.int64), np.zeros(max(ub.value, 1), np.uint8)
+        N.check(L.mgpu_tess_result_undecided(h, ctypes.byref(nu), ctypes.byref(ub), ucell.ctypes.data, upoly.ctypes.data,
+                                             ukkc.ctypes.data, uoff.ctypes.data, uwkb.ctypes.data))
     finally:
         L.mgpu_tess_destroy(h)
     t = ChipTable(cell, pid, core, off, wkb[:b.value], index_system.code)
     t.core_stats = dict(zip(CORE_STATS, stats.tolist()))
+    # the rows the core rule left undecided: kind (1 DP-sensitive, 2 on a buffer curve), kept,
+    # core, and the chip the row carries (or would carry, when dropped)
+    t.undecided = ChipTable(ucell, upoly, ukkc[:, 2], uoff, uwkb[:ub.value], index_system.code)
+    t.undecided.kind, t.undecided.kept = ukkc[:, 0].copy(), ukkc[:, 1].copy()
     return t

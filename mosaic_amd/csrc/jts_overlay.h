@@ -223,7 +223,7 @@ struct Overlay {
     bool in_result = false, res_left = false;  // result interior left of u -> v
   };
   std::vector<Seg> segs;
-  std::vector<std::vector<P>> seg_nodes;  // per seg: nodes found
+  std::vector<std::pair<int, P>> seg_nodes;  // (seg, node found on it)
   std::vector<P> nodes;                   // node coordinates (sorted unique)
   std::vector<uint8_t> on_geom;           // per node: bit 0 subject, bit 1 cell boundary
   std::vector<Edge> edges;
@@ -310,6 +310,76 @@ inline int locate_in_ring(P p, const std::vector<P>& ring) {
   return (crossings & 1) ? 1 : -1;
 }
 
+// A polygon's segments bucketed on a uniform grid (one per polygon, built once): the
+// segments whose envelope meets a box, each once, in (ring, index) order -- the overlay
+// then visits the segments near a cell instead of all of them.
+struct SegGrid {
+  double x0 = 0, y0 = 0, inv = 1;
+  long nx = 0, ny = 0;
+  std::vector<uint32_t> start;
+  std::vector<uint64_t> items;  // ring << 32 | index
+  mutable std::vector<uint64_t> out;
+
+  void build(const std::vector<std::vector<std::vector<P>>>& parts, double cell) {
+    double minx = INFINITY, miny = INFINITY, maxx = -INFINITY, maxy = -INFINITY;
+    size_t nseg = 0;
+    for (auto& part : parts)
+      for (auto& r : part)
+        for (auto& p : r) {
+          minx = std::min(minx, p.x), maxx = std::max(maxx, p.x);
+          miny = std::min(miny, p.y), maxy = std::max(maxy, p.y);
+          nseg++;
+        }
+    if (!(minx <= maxx)) return;
+    double s = std::max({cell, (maxx - minx) / 1024.0, (maxy - miny) / 1024.0, 1e-300});
+    // (at most ~4 buckets per segment on average)
+    s = std::max(s, std::sqrt((maxx - minx) * (maxy - miny) / (4.0 * (double)nseg + 1.0)));
+    inv = 1.0 / s;
+    x0 = minx, y0 = miny;
+    nx = (long)((maxx - minx) * inv) + 1;
+    ny = (long)((maxy - miny) * inv) + 1;
+    start.assign((size_t)(nx * ny + 1), 0);
+    for (int pass = 0; pass < 2; pass++) {
+      std::vector<uint32_t> fill;
+      if (pass) {
+        for (size_t q = 1; q < start.size(); q++) start[q] += start[q - 1];
+        items.assign(start.back(), 0);
+        fill.assign(start.begin(), start.end() - 1);
+      }
+      uint32_t ring = 0;
+      for (auto& part : parts)
+        for (auto& r : part) {
+          for (size_t k = 0; k + 1 < r.size(); k++) {
+            const long i0 = col(std::min(r[k].x, r[k + 1].x)), i1 = col(std::max(r[k].x, r[k + 1].x));
+            const long j0 = row(std::min(r[k].y, r[k + 1].y)), j1 = row(std::max(r[k].y, r[k + 1].y));
+            for (long j = j0; j <= j1; j++)
+              for (long i = i0; i <= i1; i++) {
+                const size_t q = (size_t)(j * nx + i);
+                if (pass) items[fill[q]++] = ((uint64_t)ring << 32) | (uint64_t)k;
+                else start[q + 1]++;
+              }
+          }
+          ring++;
+        }
+    }
+  }
+  long col(double x) const { return std::min(std::max((long)std::floor((x - x0) * inv), 0L), nx - 1); }
+  long row(double y) const { return std::min(std::max((long)std::floor((y - y0) * inv), 0L), ny - 1); }
+  // the segments in buckets meeting [bx0, bx1] x [by0, by1], sorted, each once
+  const std::vector<uint64_t>& query(double bx0, double by0, double bx1, double by1) const {
+    out.clear();
+    if (start.empty()) return out;
+    for (long j = row(by0); j <= row(by1); j++)
+      for (long i = col(bx0); i <= col(bx1); i++) {
+        const size_t c = (size_t)(j * nx + i);
+        out.insert(out.end(), items.begin() + start[c], items.begin() + start[c + 1]);
+      }
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out;
+  }
+};
+
 // The result of one overlay: pieces (rings; ring 0 = shell, clockwise; holes ccw)
 using Rings = std::vector<std::vector<P>>;
 
@@ -320,11 +390,19 @@ using Rings = std::vector<std::vector<P>>;
 struct Clipper {
   Overlay o;
   // scratch
-  std::vector<int> out_start, out_list, cell_edge_begin;
+  std::vector<int> out_start, out_list, cell_edge_begin, fill, prts, rs;
   std::vector<uint8_t> used;
+  std::vector<P> pts;
+  std::vector<std::pair<P, P>> sub;  // (from, to) coordinates
+  std::vector<int> sub_seg;
+  std::vector<int8_t> loc;
+  std::vector<int> cand;  // candidate subject segments (ring << 32 | k) from the grid
+  std::vector<uint64_t> cand64;
+  std::vector<const std::vector<P>*> sub_rings;
 
   void build(const std::vector<std::vector<std::vector<P>>>& parts, const std::vector<uint8_t>& ring_ccw,
-             const std::vector<std::vector<P>>& cell, std::vector<Rings>& pieces, bool* lower_dim) {
+             const std::vector<std::vector<P>>& cell, std::vector<Rings>& pieces, bool* lower_dim,
+             const SegGrid* grid = nullptr) {
     o.clear();
     pieces.clear();
     double cx0 = INFINITY, cy0 = INFINITY, cx1 = -INFINITY, cy1 = -INFINITY;
@@ -337,51 +415,61 @@ struct Clipper {
     o.ring_part.clear();
     o.ring_hole.clear();
     int ring_id = 0;
-    std::vector<const std::vector<P>*> sub_rings;
+    sub_rings.clear();
     for (size_t pi = 0; pi < parts.size(); pi++)
       for (size_t ri = 0; ri < parts[pi].size(); ri++, ring_id++) {
-        const auto& r = parts[pi][ri];
-        sub_rings.push_back(&r);
+        sub_rings.push_back(&parts[pi][ri]);
         o.ring_part.push_back((int)pi);
         o.ring_hole.push_back(ri > 0);
-        // interior of the polygon left of the ring's direction: shell ccw, hole cw
-        const bool il = (ri == 0) == (bool)ring_ccw[ring_id];
-        for (size_t k = 0; k + 1 < r.size(); k++) {
-          const P a = r[k], b = r[k + 1];
-          if (eq(a, b)) continue;
-          if (std::max(a.x, b.x) < cx0 || std::min(a.x, b.x) > cx1 || std::max(a.y, b.y) < cy0 ||
-              std::min(a.y, b.y) > cy1)
-            continue;
-          o.segs.push_back({a, b, 0, ring_id, il});
-        }
       }
+    // interior of the polygon left of the ring's direction: shell ccw, hole cw
+    auto add_seg = [&](int rid, size_t k) {
+      const auto& r = *sub_rings[rid];
+      const P a = r[k], b = r[k + 1];
+      if (eq(a, b)) return;
+      if (std::max(a.x, b.x) < cx0 || std::min(a.x, b.x) > cx1 || std::max(a.y, b.y) < cy0 || std::min(a.y, b.y) > cy1)
+        return;
+      o.segs.push_back({a, b, 0, rid, (o.ring_hole[rid] == 0) == (bool)ring_ccw[rid]});
+    };
+    if (grid) {
+      for (uint64_t c : grid->query(cx0, cy0, cx1, cy1)) add_seg((int)(c >> 32), (size_t)(c & 0xFFFFFFFFu));
+    } else {
+      for (int rid = 0; rid < ring_id; rid++)
+        for (size_t k = 0; k + 1 < sub_rings[rid]->size(); k++) add_seg(rid, k);
+    }
     const size_t n_sub = o.segs.size();
     for (size_t ci = 0; ci < cell.size(); ci++)
       for (size_t k = 0; k + 1 < cell[ci].size(); k++)
         if (!eq(cell[ci][k], cell[ci][k + 1])) o.segs.push_back({cell[ci][k], cell[ci][k + 1], 1, (int)ci, true});
     // 2. noding: every subject segment against every cell segment (IntersectionAdder)
-    o.seg_nodes.assign(o.segs.size(), {});
+    o.seg_nodes.clear();
     for (size_t i = 0; i < n_sub; i++)
       for (size_t j = n_sub; j < o.segs.size(); j++) {
         const Hit h = line_intersect(o.segs[i].a, o.segs[i].b, o.segs[j].a, o.segs[j].b);
         for (int q = 0; q < h.n; q++) {
-          o.seg_nodes[i].push_back(h.pt[q]);
-          o.seg_nodes[j].push_back(h.pt[q]);
+          o.seg_nodes.push_back({(int)i, h.pt[q]});
+          o.seg_nodes.push_back({(int)j, h.pt[q]});
         }
       }
-    // 3. sub-edges between consecutive nodes along each segment
-    std::vector<P> pts;
-    std::vector<std::pair<P, P>> sub;  // (from, to) coordinates
-    std::vector<int> sub_seg;
+    // 3. sub-edges between consecutive nodes along each segment (nodes by segment, then
+    // in SegmentPointComparator order along it)
+    std::sort(o.seg_nodes.begin(), o.seg_nodes.end(), [&](const std::pair<int, P>& u, const std::pair<int, P>& v) {
+      if (u.first != v.first) return u.first < v.first;
+      const Overlay::Seg& s = o.segs[u.first];
+      return seg_compare(octant(s.b.x - s.a.x, s.b.y - s.a.y), u.second, v.second) < 0;
+    });
+    pts.clear();
+    sub.clear();
+    sub_seg.clear();
+    size_t nq = 0;
     for (size_t i = 0; i < o.segs.size(); i++) {
       const Overlay::Seg& s = o.segs[i];
-      auto& nd = o.seg_nodes[i];
-      const int oc = octant(s.b.x - s.a.x, s.b.y - s.a.y);
-      std::sort(nd.begin(), nd.end(), [&](P p, P q) { return seg_compare(oc, p, q) < 0; });
       pts.clear();
       pts.push_back(s.a);
-      for (P p : nd)
+      for (; nq < o.seg_nodes.size() && o.seg_nodes[nq].first == (int)i; nq++) {
+        const P p = o.seg_nodes[nq].second;
         if (!eq(p, pts.back()) && !eq(p, s.b)) pts.push_back(p);
+      }
       pts.push_back(s.b);
       for (size_t k = 0; k + 1 < pts.size(); k++) {
         sub.push_back({pts[k], pts[k + 1]});
@@ -421,12 +509,10 @@ struct Clipper {
     for (auto& e : o.edges) out_start[e.u + 1]++, out_start[e.v + 1]++;
     for (int q = 0; q < nn; q++) out_start[q + 1] += out_start[q];
     out_list.assign(out_start[nn], 0);
-    {
-      std::vector<int> fill(out_start.begin(), out_start.end() - 1);
-      for (int k = 0; k < ne; k++) {
-        out_list[fill[o.edges[k].u]++] = k;
-        out_list[fill[o.edges[k].v]++] = k;
-      }
+    fill.assign(out_start.begin(), out_start.end() - 1);
+    for (int k = 0; k < ne; k++) {
+      out_list[fill[o.edges[k].u]++] = k;
+      out_list[fill[o.edges[k].v]++] = k;
     }
     // 4. coincident edges of the two geometries (EdgeMerger)
     for (int q = 0; q < nn; q++)
@@ -468,12 +554,11 @@ struct Clipper {
         if (e.geom == geom && std::find(rs.begin(), rs.end(), e.ring) == rs.end()) rs.push_back(e.ring);
       }
     };
-    std::vector<int> rs;
     // subject interior at node (on the subject's boundary) in direction w: per part through
     // the node, inside its shell's sector (or inside the shell) and outside its holes' sectors
     auto subject_sector = [&](int node, P w) {
       rings_at(node, 0, rs);
-      std::vector<int> prts;
+      prts.clear();
       for (int r : rs)
         if (std::find(prts.begin(), prts.end(), o.ring_part[r]) == prts.end()) prts.push_back(o.ring_part[r]);
       for (int pt : prts) {
@@ -516,7 +601,7 @@ struct Clipper {
     };
     // located edges: at a node of the other geometry by its sectors; a subject edge touching
     // no cell node by point location in the cell (both ends, locateEdgeBothEnds)
-    std::vector<int8_t> loc(ne, -1);
+    loc.assign(ne, -1);
     for (int k = 0; k < ne; k++) {
       const Overlay::Edge& e = o.edges[k];
       if (e.partner >= 0) continue;

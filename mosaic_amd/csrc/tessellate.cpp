@@ -115,6 +115,8 @@ struct Polygon {
   std::vector<std::vector<std::vector<Pt>>> parts;  // part -> rings (first = shell)
   std::vector<uint8_t> ring_ccw;                    // per ring (parts' rings in order)
   bool multi = false;                               // a MULTIPOLYGON (else a POLYGON)
+  std::vector<const std::vector<Pt>*> ring_ptr;     // per ring (parts' rings in order)
+  mgpu::ovl::SegGrid grid;                          // the rings' segments, bucketed
 };
 
 // how border chips are cut (mgpu_tessellate_geom's chip_geometry)
@@ -531,6 +533,16 @@ struct Chip {
   std::vector<uint8_t> wkb;
 };
 
+// a row the core rule left undecided (mgpu_tess_result_undecided): kind 1 DP-sensitive,
+// 2 unresolved; kept = whether the table holds it; its chip (the border chip the table
+// holds, or the one a dropped row would have) for counting the pairs at stake
+struct Undecided {
+  int64_t cell;
+  int32_t poly;
+  uint8_t kind, kept, core;
+  std::vector<uint8_t> wkb;
+};
+
 // ---------------------------------------------------------------- mosaicFill's core set
 // The reference flags a chip core in two places (core/Mosaic.scala:61-99):
 //  * getCoreChips (IndexSystem.scala:208-213): every cell of polyfill(buffer(-r)) -- a
@@ -665,6 +677,9 @@ struct CoreRule {
   int carved_state = 0;  // 0 not built, 1 non-empty, 2 empty
   mgpu::jtsbuf::DepthField carved, band;
   bool band_built = false;
+  // the last decide()'s undecided kind: 0 none, 1 DP-sensitive (band membership within the
+  // band simplification's 0.01 r), 2 unresolved (a centre within 1e-9 r of a buffer curve)
+  int last_flag = 0;
   enum Verdict { kCore, kBorder, kDrop };
 
   std::vector<mgpu::jtsbuf::Rings> parts() const {
@@ -698,6 +713,7 @@ struct CoreRule {
   // the reference's flag of a chip cell with centre c; inside: the clip's knowledge (1 in,
   // 0 out, -1 unknown).  Every caller holds a cell with a non-empty chip.
   Verdict decide(Pt c, int inside) {
+    last_flag = 0;
     const double q = 1.1 * r;
     double d = seg.min_dist(c, q);
     const bool in = inside >= 0 ? inside == 1 : seg.inside(c);
@@ -721,7 +737,8 @@ struct CoreRule {
       ensure_carved();
       st.carved_tests++;
       core = carved_state == 1 && carved.depth(p) >= 1;
-      if (carved_state == 1 && carved.outline_dist(p, 1e-9 * r, 1e-7 * r) < INFINITY) st.unresolved++, st.ambiguous++;
+      if (carved_state == 1 && carved.outline_dist(p, 1e-9 * r, 1e-7 * r) < INFINITY)
+        st.unresolved++, st.ambiguous++, last_flag = 2;
       if (core && d < r) st.core_below_r++;
       if (!core && d >= r) st.border_above_r++;
     }
@@ -734,8 +751,8 @@ struct CoreRule {
     st.band_tests++;
     const bool in_band = band.depth(p) >= 1;
     const double near = band.outline_dist(p, 0.01 * r * (1 + 1e-6), 1e-7 * r);  // simplify(0.01 r)
-    if (near < 1e-9 * r) st.unresolved++, st.ambiguous++;
-    else if (near < INFINITY) st.dp_sensitive++, st.ambiguous++;
+    if (near < 1e-9 * r) st.unresolved++, st.ambiguous++, last_flag = 2;
+    else if (near < INFINITY) st.dp_sensitive++, st.ambiguous++, last_flag = 1;
     if (!in_band) st.band_dropped++;
     return in_band ? kBorder : kDrop;
   }
@@ -764,18 +781,18 @@ bool cell_in_polygon(const std::vector<Pt>& cellb, const std::vector<std::vector
     cminy = std::min(cminy, p.y);
     cmaxy = std::max(cmaxy, p.y);
   }
-  for (auto& part : poly.parts)
-    for (auto& ring : part)
-      for (size_t i = 0; i + 1 < ring.size(); i++) {
-        Pt a = ring[i], b = ring[i + 1];
-        if (std::max(a.x, b.x) < cminx || std::min(a.x, b.x) > cmaxx || std::max(a.y, b.y) < cminy ||
-            std::min(a.y, b.y) > cmaxy)
-          continue;
-        for (auto& pc : pieces)
-          if (in_convex(pc, a)) return false;
-        for (size_t k = 0; k + 1 < cellb.size(); k++)
-          if (segments_touch(a, b, cellb[k], cellb[k + 1])) return false;
-      }
+  for (uint64_t c : poly.grid.query(cminx, cminy, cmaxx, cmaxy)) {
+    const auto& ring = *poly.ring_ptr[c >> 32];
+    const size_t i = (size_t)(c & 0xFFFFFFFFu);
+    Pt a = ring[i], b = ring[i + 1];
+    if (std::max(a.x, b.x) < cminx || std::min(a.x, b.x) > cmaxx || std::max(a.y, b.y) < cminy ||
+        std::min(a.y, b.y) > cmaxy)
+      continue;
+    for (auto& pc : pieces)
+      if (in_convex(pc, a)) return false;
+    for (size_t k = 0; k + 1 < cellb.size(); k++)
+      if (segments_touch(a, b, cellb[k], cellb[k + 1])) return false;
+  }
   for (auto& part : poly.parts) {
     if (!point_in_ring(part[0], cc)) continue;
     bool in_hole = false;
@@ -788,11 +805,17 @@ bool cell_in_polygon(const std::vector<Pt>& cellb, const std::vector<std::vector
 
 // `lat_rings`: every ring in the grid's lattice space (densified for H3)
 void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<std::vector<Pt>>& lat_rings, int32_t pid,
-                        bool keep_core, CoreRule* rule, int chip_geometry, GeomStats& gs, std::vector<Chip>& out) {
+                        bool keep_core, CoreRule* rule, int chip_geometry, GeomStats& gs, std::vector<Chip>& out,
+                        std::vector<Undecided>& und) {
   // a cell the polygon holds whole: core -- unless mosaicFill's rule (rule != null) puts
   // it in the border set (then its chip is the whole cell, not core)
   auto whole = [&](int64_t id, long i, long j, const std::vector<std::vector<Pt>>* rings) {
     const auto v = rule ? rule->decide(g.center_input(i, j, id), 1) : CoreRule::kCore;
+    if (rule && rule->last_flag) {
+      Undecided u{id, pid, (uint8_t)rule->last_flag, (uint8_t)(v != CoreRule::kDrop), (uint8_t)(v == CoreRule::kCore), {}};
+      write_cell_wkb(reversed(rings ? *rings : g.boundary_of(i, j, id)), u.wkb);
+      und.push_back(std::move(u));
+    }
     if (v == CoreRule::kDrop) {
       rule->st.dropped++;
       return;
@@ -928,7 +951,7 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
       // (jts_overlay.h)
       std::vector<mgpu::ovl::Rings> pcs;
       bool lower = false;
-      t_clip.build(poly.parts, poly.ring_ccw, rings, pcs, &lower);
+      t_clip.build(poly.parts, poly.ring_ccw, rings, pcs, &lower, &poly.grid);
       for (auto& pc : pcs)
         for (size_t k = 0; k < pc.size(); k++) area += (k == 0 ? 1.0 : -1.0) * std::fabs(mgpu::ovl::signed_area(pc[k]));
       if (pcs.empty() || area <= 0) continue;  // empty chip (lines / points only): dropped
@@ -999,6 +1022,12 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
       // (its chip is the whole cell, core, even where the polygon does not cover it); one
       // whose centre is beyond the border band is never visited
       const auto v = rule->decide(g.center_input(c.first, c.second, cid), -1);
+      if (rule->last_flag) {
+        Undecided u{cid, pid, (uint8_t)rule->last_flag, (uint8_t)(v != CoreRule::kDrop), (uint8_t)(v == CoreRule::kCore),
+                    {}};
+        mgpu::wkb::write_polygons(u.wkb, parts);
+        und.push_back(std::move(u));
+      }
       if (v == CoreRule::kDrop) {
         rule->st.dropped++;
         continue;
@@ -1088,6 +1117,7 @@ struct mgpu_tess {
   std::vector<Chip> chips;
   CoreStats core_stats;
   GeomStats geom_stats;
+  std::vector<Undecided> undecided;
 };
 
 namespace {
@@ -1176,6 +1206,7 @@ int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys,
   std::vector<uint8_t> bad_poly(n_polys, 0);
   std::vector<CoreStats> pstats(n_polys);
   std::vector<GeomStats> gstats(n_polys);
+  std::vector<std::vector<Undecided>> pund(n_polys);
   mgpu::parallel_for(n_polys, 64, [&](int64_t pb, int64_t pe, int) {
     for (int64_t p = pb; p < pe; p++) {
       Polygon poly;
@@ -1196,7 +1227,16 @@ int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys,
       // has several parts); each ring's orientation gives the interior's side of its edges
       poly.multi = poly_type ? poly_type[p] == 6 : poly.parts.size() > 1;
       for (auto& part : poly.parts)
-        for (auto& ring : part) poly.ring_ccw.push_back(mgpu::ovl::is_ccw(ring));
+        for (auto& ring : part) {
+          poly.ring_ccw.push_back(mgpu::ovl::is_ccw(ring));
+          poly.ring_ptr.push_back(&ring);
+        }
+      {
+        // the segment grid's buckets about one cell (H3: the centre spacing at res)
+        double cell = index_system == MGPU_H3 ? 20.0 : BngGrid(res).edge;
+        for (int r = 0; index_system == MGPU_H3 && r < res; r++) cell /= 2.6457513110645906;
+        poly.grid.build(poly.parts, cell);
+      }
       // mosaicFill's core set (CoreRule) unless the clip rule was asked for
       CoreRule rule_storage;
       CoreRule* rule = nullptr;
@@ -1235,7 +1275,7 @@ int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys,
             lat_rings.push_back(std::move(lr));
           }
           tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, rule, chip_geometry,
-                             gstats[p], per[p]);
+                             gstats[p], per[p], pund[p]);
         }
         // a cell reached twice (two lattice positions around a pentagon map to one id):
         // its chip is computed from the id, so the copies are equal -- keep the first
@@ -1255,7 +1295,7 @@ int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys,
             lat_rings.push_back(std::move(lr));
           }
         tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, rule, chip_geometry,
-                           gstats[p], per[p]);
+                           gstats[p], per[p], pund[p]);
       }
       if (rule) pstats[p] = rule->st;
     }
@@ -1271,6 +1311,8 @@ int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys,
                              "first, as the reference's alignToGrid does)", polygon_id[p]);
   }
   mgpu_tess* t = new mgpu_tess();
+  for (auto& v : pund)
+    for (auto& u : v) t->undecided.push_back(std::move(u));
   for (auto& q : gstats) {
     t->geom_stats.overlay_chips += q.overlay_chips;
     t->geom_stats.multi_piece += q.multi_piece;
@@ -1353,6 +1395,28 @@ int32_t mgpu_tess_result_core_stats(const mgpu_tess* t, int64_t* out, int32_t n)
                        t->geom_stats.multi_piece, t->geom_stats.coerced, t->geom_stats.coerce_nodes,
                        t->geom_stats.lower_dim};
   for (int32_t i = 0; i < n; i++) out[i] = i < (int32_t)(sizeof(v) / sizeof(v[0])) ? v[i] : 0;
+  return MGPU_OK;
+}
+
+int32_t mgpu_tess_result_undecided(const mgpu_tess* t, int64_t* n, int64_t* wkb_bytes, int64_t* cell, int32_t* poly,
+                                   uint8_t* kind_kept_core, int64_t* wkb_offsets, uint8_t* wkb) {
+  if (!t || !n) return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellation result is NULL");
+  *n = (int64_t)t->undecided.size();
+  int64_t b = 0;
+  for (auto& u : t->undecided) b += (int64_t)u.wkb.size();
+  if (wkb_bytes) *wkb_bytes = b;
+  if (!cell) return MGPU_OK;
+  int64_t off = 0;
+  for (size_t i = 0; i < t->undecided.size(); i++) {
+    const Undecided& u = t->undecided[i];
+    cell[i] = u.cell;
+    poly[i] = u.poly;
+    kind_kept_core[3 * i] = u.kind, kind_kept_core[3 * i + 1] = u.kept, kind_kept_core[3 * i + 2] = u.core;
+    wkb_offsets[i] = off;
+    if (!u.wkb.empty()) memcpy(wkb + off, u.wkb.data(), u.wkb.size());
+    off += (int64_t)u.wkb.size();
+  }
+  wkb_offsets[t->undecided.size()] = off;
   return MGPU_OK;
 }
 
