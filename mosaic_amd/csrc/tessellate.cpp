@@ -768,6 +768,49 @@ struct PairHash {
   size_t operator()(const std::pair<long, long>& p) const { return std::hash<long>()(p.first * 1000003L ^ p.second); }
 };
 
+// lattice cell -> smallest squared distance from its centre to a walked boundary sample:
+// open addressing (the walk looks a cell up ~7 times per sample)
+struct CellDist {
+  struct Slot {
+    long i, j;
+    float d2;
+    bool used;
+  };
+  std::vector<Slot> t;
+  size_t n = 0, mask = 0;
+  static size_t h(long i, long j) {
+    uint64_t k = (uint64_t)i * 0x9E3779B97F4A7C15ull ^ ((uint64_t)j + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full;
+    return (size_t)(k ^ (k >> 29));
+  }
+  void clear() {
+    t.assign(1024, Slot{0, 0, 0.f, false});
+    mask = 1023;
+    n = 0;
+  }
+  Slot* find(long i, long j) {
+    for (size_t q = h(i, j) & mask;; q = (q + 1) & mask) {
+      if (!t[q].used) return nullptr;
+      if (t[q].i == i && t[q].j == j) return &t[q];
+    }
+  }
+  void put(long i, long j, float d2) {
+    if (2 * (n + 1) > t.size()) {
+      std::vector<Slot> old;
+      old.swap(t);
+      t.assign(old.size() * 2, Slot{0, 0, 0.f, false});
+      mask = t.size() - 1;
+      n = 0;
+      for (auto& s : old)
+        if (s.used) put(s.i, s.j, s.d2);
+    }
+    size_t q = h(i, j) & mask;
+    while (t[q].used) q = (q + 1) & mask;
+    t[q] = Slot{i, j, d2, true};
+    n++;
+  }
+};
+thread_local CellDist t_border;
+
 // Exact test that the cell lies in the interior of one part of the polygon: no ring
 // vertex in/on the cell, no ring edge touching a cell edge, the cell centre inside
 // the shell and outside every hole.  Such a cell's chip IS the cell geometry
@@ -836,18 +879,19 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
   };
   // 2. border cells: walk every edge in lattice space; per cell the smallest distance
   // from its centre to a walked sample (samples <= 0.2 apart)
-  std::unordered_map<std::pair<long, long>, float, PairHash> border;
+  // (squared distances: the test against far_distance only chooses between two exact
+  // constructions of the same chip -- a cell the boundary never reaches gives the same
+  // row either way -- so its rounding at the threshold does not matter)
+  CellDist& border = t_border;
+  border.clear();
   std::vector<std::pair<long, long>> nb;
-  // (a cell seen before skips the hypot when max(|dx|, |dy|) -- which the faithfully
-  // rounded hypot cannot fall below -- already rounds to at least its distance)
   auto touch = [&](const std::pair<long, long>& c, Pt s) {
     const Pt cc = g.center(c.first, c.second);
     const double dx = s.x - cc.x, dy = s.y - cc.y;
-    auto it = border.find(c);
-    if (it != border.end() && (float)std::max(std::fabs(dx), std::fabs(dy)) >= it->second) return;
-    const float d = (float)std::hypot(dx, dy);
-    if (it == border.end()) border.emplace(c, d);
-    else if (d < it->second) it->second = d;
+    const float d2 = (float)(dx * dx + dy * dy);
+    CellDist::Slot* it = border.find(c.first, c.second);
+    if (!it) border.put(c.first, c.second, d2);
+    else if (d2 < it->d2) it->d2 = d2;
   };
   for (auto& r : lat_rings)
     for (size_t i = 0; i + 1 < r.size(); i++) {
@@ -884,7 +928,7 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
       std::sort(xs.begin(), xs.end());
       for (size_t k = 0; k + 1 < xs.size(); k += 2)
         for (long i = g.col_of(xs[k], j, true); i <= g.col_of(xs[k + 1], j, false); i++)
-          if (!border.count({i, j})) interior.push_back({i, j});
+          if (!border.find(i, j)) interior.push_back({i, j});
     }
   }
   for (auto& c : interior) {
@@ -896,13 +940,15 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
   // neighbour of a walked cell): then it lies wholly inside or outside, decided by its
   // centre, without its exact geometry
   std::vector<std::pair<long, long>> bl;
-  bl.reserve(border.size());
-  for (auto& kv : border) bl.push_back(kv.first);
+  bl.reserve(border.n);
+  for (auto& sl : border.t)
+    if (sl.used) bl.push_back({sl.i, sl.j});
   std::sort(bl.begin(), bl.end());
   for (auto& c : bl) {
     const int64_t cid = g.cell_id(c.first, c.second);
     if (!cid || !g.keep(cid, c.first, c.second)) continue;
-    if (border[c] > g.far_distance()) {
+    const double far = g.far_distance();
+    if ((double)border.find(c.first, c.second)->d2 > far * far) {
       const Pt cc = g.center(c.first, c.second);
       bool in = false;
       for (auto& r : lat_rings)
