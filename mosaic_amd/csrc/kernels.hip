@@ -194,6 +194,9 @@ constexpr int kMixCap = kTile / 2;  // mixed-cell candidates (phase 2b), after t
 #else
 #define MGPU_ST_INTER(v, ptr) (*(ptr) = (v))
 #endif
+#ifndef MGPU_EDGE_PAR
+#define MGPU_EDGE_PAR 0  // (the edge-parallel walk over LDS-staged runs: A/B round 6)
+#endif
 #ifndef MGPU_SPLIT_WALK
 #define MGPU_SPLIT_WALK 1  // (A/B r3, profiles/r3_split_walk_ab.txt: C3 binned join -3.8%, C4 r4 -1.6%)
 #endif
@@ -816,6 +819,105 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #ifdef MGPU_STATS
   uint32_t st_edges = 0;
 #endif
+  bool walked = false;
+#if MGPU_EDGE_PAR
+  // north_star's ray-crossing test over LDS-staged vertex runs: the walks' strip edge runs
+  // (each strip a contiguous run of edge records in JTS's visiting order) are laid end to
+  // end in LDS -- per flat position its walk -- and every lane of the wave tests one edge
+  // per step, loads for several steps in flight, whatever walk it belongs to; the rings'
+  // boundary / parity bits gather per walk by LDS atomics (order-free: OR / XOR), then the
+  // walk's lane applies PointLocator's verdict.  s_buf's candidate lists are dead here once
+  // each walk lane holds its candidate, so the runs reuse its bytes.
+  if (!SLOW && kBlock == 64 && nmix > 0 && nmix <= 64) {
+    constexpr uint32_t kBufBytes = sizeof(s_buf);
+    constexpr uint32_t kWalkBytes = 64 * (8 + 8 + 4 + 4 + 4 + 4 + 1);
+    constexpr uint32_t kFlatCap = kBufBytes > kWalkBytes ? kBufBytes - kWalkBytes : 0;
+    const uint32_t lane = threadIdx.x;
+    uint32_t pj = 0, ch = 0, eb = 0, ne = 0;
+    int li = 0;
+    bool one = false;
+    uint8_t fl = 0;
+    double px = 0.0, py = 0.0;
+    if (lane < nmix) {
+      const uint32_t c = s_mix[lane];
+      pj = s_cand_pj[c];
+      li = pj & 1023;
+      ch = s_first[li] + (pj >> 10);
+      if (point_stash<G>() || c < (uint32_t)kStash) {
+        const double2 q = s_cand_xy[point_stash<G>() ? (uint32_t)li : c];
+        px = q.x;
+        py = q.y;
+      } else {
+        px = a.x[MGPU_PT(li)];
+        py = a.y[MGPU_PT(li)];
+      }
+      const ChipHdr& H = t.chip_hdr[ch];
+      const uint32_t strip = H.strip_base + (uint32_t)strip_of(py, H.env[1], H.inv_h, (int)H.n_strips);
+      one = H.single_ring != 0;
+      fl = H.flags;
+      eb = t.strip_edge[strip];
+      ne = t.strip_edge[strip + 1] - eb;
+    }
+    uint32_t inc = ne;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t u = (uint32_t)__shfl_up((int)inc, d);
+      if ((int)lane >= d) inc += u;
+    }
+    const uint32_t total = (uint32_t)__shfl((int)inc, 63), off = inc - ne;
+    if (total <= kFlatCap) {
+      __syncthreads();  // (every walk lane has read its candidate: s_buf is free)
+      double* s_wx = (double*)s_buf;
+      double* s_wy = s_wx + 64;
+      uint32_t* s_web = (uint32_t*)(s_wy + 64);
+      uint32_t* s_woff = s_web + 64;
+      uint32_t* s_bnd = s_woff + 64;
+      uint32_t* s_par = s_bnd + 64;
+      uint8_t* s_wone = (uint8_t*)(s_par + 64);
+      uint8_t* s_walk = s_wone + 64;  // [kFlatCap]: the walk of each flat edge
+      s_wx[lane] = px;
+      s_wy[lane] = py;
+      s_web[lane] = eb;
+      s_woff[lane] = off;
+      s_bnd[lane] = 0;
+      s_par[lane] = 0;
+      s_wone[lane] = one ? 1 : 0;
+      for (uint32_t k = 0; k < ne; k++) s_walk[off + k] = (uint8_t)lane;
+      __syncthreads();
+      const double4* E4 = (const double4*)t.edges;
+#ifndef MGPU_EDGE_PAR_STEPS
+#define MGPU_EDGE_PAR_STEPS 4
+#endif
+      constexpr int kS = MGPU_EDGE_PAR_STEPS;
+      const uint32_t e_safe = s_web[s_walk[0]];  // (a valid record for the idle lanes' loads)
+      for (uint32_t f0 = 0; f0 < total; f0 += 64 * kS) {
+        double4 R[kS];
+        uint32_t wm[kS], we[kS];
+#pragma unroll
+        for (int k = 0; k < kS; k++) {
+          const uint32_t f = f0 + lane + 64u * k;
+          wm[k] = f < total ? s_walk[f] : 0u;
+          we[k] = f < total ? s_web[wm[k]] + (f - s_woff[wm[k]]) : 0u;
+          R[k] = E4[f < total ? we[k] : e_safe];
+        }
+#pragma unroll
+        for (int k = 0; k < kS; k++) {
+          const uint32_t f = f0 + lane + 64u * k;
+          if (f >= total) continue;
+          const int bits = pip::count_segment(R[k].x, R[k].y, R[k].z, R[k].w, s_wx[wm[k]], s_wy[wm[k]]);
+          if (!bits) continue;
+          const uint32_t rb = s_wone[wm[k]] ? 1u : 1u << t.edge_ring[we[k]];
+          if (bits & pip::kRingOnSegment) atomicOr(&s_bnd[wm[k]], rb);
+          if (bits & 2) atomicXor(&s_par[wm[k]], rb);
+        }
+      }
+      __syncthreads();
+      if (lane < nmix && pip::strip_verdict(t, ch, one, fl, s_bnd[lane], s_par[lane], px, py))
+        atomicOr(&s_mask[li], 1u << (pj >> 10));
+      walked = true;
+    }
+  }
+#endif
+  if (!walked) {
 #if MGPU_SPLIT_WALK
   // few walks (binned tiles: ~16): a group of 4 (<= 16 walks) or 2 (<= 32) lanes shares
   // each walk, every lane taking every L-th block of the strip's edges; the partial
@@ -884,6 +986,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
     }
     if (hit) atomicOr(&s_mask[li], 1u << (pj >> 10));
   }
+  }  // (!walked)
 #ifdef MGPU_STATS
   if (threadIdx.x == 0) {
     atomicAdd(&a.counters[8], (unsigned long long)s_nmix);
