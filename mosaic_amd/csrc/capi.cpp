@@ -69,8 +69,8 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // offsets, so a byte copy of the blob on another GPU (RCCL broadcast) is a
 // complete chip table there.
 constexpr uint64_t kBlobMagic = 0x4d4f534149434850ULL;  // "MOSAICHP"
-constexpr int kBlobArrays = 27;
-constexpr uint32_t kBlobVersion = 12;  // 12: BNG cell answer grids
+constexpr int kBlobArrays = 29;
+constexpr uint32_t kBlobVersion = 13;  // 12: BNG cell answer grids; 13: palette-compressed second level
 struct BlobHeader {
   uint64_t magic;
   uint32_t version, hash_mask, max_probe, n_chips, n_cells;
@@ -95,6 +95,7 @@ struct BlobHeader {
   uint32_t raster_bshift, raster_bnx, raster_bny, raster_ncls;
   uint32_t raster_band_shift, raster_nband;
   uint32_t cell_ans_g, cell_ans_sw;
+  uint32_t raster_pal, pad5;  // 1: the second level is palette-compressed
 };
 constexpr size_t kBlobHeaderBytes = 1024;
 static_assert(sizeof(BlobHeader) <= kBlobHeaderBytes, "header too large");
@@ -157,6 +158,8 @@ mgpu::ChipTableView view_from_header(const BlobHeader& h, uint8_t* base) {
   v.cell_ans_row = h.cell_ans_g ? (const uint32_t*)(base + h.off[25]) : nullptr;
   v.cell_ans = (const uint16_t*)(base + h.off[26]);
   v.raster_sub = (const uint16_t*)(base + h.off[21]);
+  v.raster_pal = h.raster_pal ? (const uint64_t*)(base + h.off[27]) : nullptr;
+  v.raster_idx2 = (const uint8_t*)(base + h.off[28]);
   v.raster_bshift = h.raster_bshift;
   v.raster_bnx = h.raster_bnx;
   v.raster_bny = h.raster_bny;
@@ -705,6 +708,11 @@ struct Raster {
   // lonlat: band[k] = the refined pixels before raster rows k << band_shift (rank unused)
   uint32_t band_shift = 0;
   std::vector<uint32_t> band;
+  // lonlat with bands, palette-compressed second level (raster_palette): per refined block
+  // pal[b] = its <= 4 classes (16 bits each) or kPalFull | the index of its full block in
+  // sub (which then keeps only those); idx2[b * sub_n^2 / 4 ..] = 2-bit palette indices
+  std::vector<uint64_t> pal;
+  std::vector<uint8_t> idx2;
   // blocks of 2^bshift x 2^bshift pixels: the class when all of them share it, else mixed
   uint32_t bshift = 0, bnx = 0, bny = 0;
   std::vector<uint16_t> blk;
@@ -1166,6 +1174,62 @@ void raster_bands(Raster& R) {
   R.rank.clear();
 }
 
+// The second level palette-compressed (lonlat with bands): a refined mixed pixel's 256
+// sub-pixels hold few distinct classes (a zone boundary: its two zones and "mixed"), so
+// each block keeps <= 4 classes in one 8-byte palette word and 2 bits per sub-pixel -- 72
+// bytes instead of 512, the whole level 7x smaller (C2: 68 MB -> ~10 MB); a block with more
+// classes keeps its full u16 layout (pal = kPalFull | its index among those).
+#ifndef MGPU_RASTER_PAL
+#define MGPU_RASTER_PAL 1
+#endif
+void raster_palette(Raster& R) {
+  if (!MGPU_RASTER_PAL || R.band.empty() || R.sub_n == 0 || (R.sub_n * R.sub_n) % 4) return;
+  const size_t S2 = (size_t)R.sub_n * R.sub_n, nb = R.sub.size() / S2;
+  R.pal.assign(nb, 0);
+  R.idx2.assign(nb * S2 / 4, 0);
+  std::vector<uint8_t> full(nb, 0);
+  mgpu::parallel_for((int64_t)nb, 1024, [&](int64_t bb, int64_t be, int) {
+    for (int64_t b = bb; b < be; b++) {
+      const uint16_t* c = R.sub.data() + (size_t)b * S2;
+      uint16_t p[4];
+      int n = 0;
+      bool ok = true;
+      for (size_t i = 0; i < S2 && ok; i++) {
+        int k = 0;
+        while (k < n && p[k] != c[i]) k++;
+        if (k == n) {
+          if (n == 4) ok = false;
+          else p[n++] = c[i];
+        }
+      }
+      if (!ok) {
+        full[b] = 1;
+        continue;
+      }
+      for (int k = n; k < 4; k++) p[k] = p[0];
+      // 15 bits a class (the bands need fewer than 0x7FFF classes), "mixed" as 0x7FFF: the
+      // word's top bit stays kPalFull's
+      auto c15 = [](uint16_t c) { return (uint64_t)(c == mgpu::kPixMixed ? 0x7FFFu : c); };
+      R.pal[b] = c15(p[0]) | c15(p[1]) << 16 | c15(p[2]) << 32 | c15(p[3]) << 48;
+      uint8_t* q = R.idx2.data() + (size_t)b * S2 / 4;
+      for (size_t i = 0; i < S2; i++) {
+        int k = 0;
+        while (p[k] != c[i]) k++;
+        q[i >> 2] |= (uint8_t)(k << (2 * (i & 3)));
+      }
+    }
+  });
+  // the full blocks, in order, are all the second level keeps
+  uint64_t nf = 0;
+  for (size_t b = 0; b < nb; b++)
+    if (full[b]) {
+      if (nf != b) std::memmove(R.sub.data() + nf * S2, R.sub.data() + b * S2, S2 * 2);
+      R.pal[b] = mgpu::kPalFull | nf++;
+    }
+  R.sub.resize(nf * S2);
+  R.sub.shrink_to_fit();
+}
+
 // the block table over the level-1 classes: the smallest block edge 2^s (s >= 3) whose
 // table fits kRasterBlkBytes (the join kernels hold it in LDS)
 #ifndef MGPU_RASTER_BLK_KB
@@ -1397,6 +1461,7 @@ bool build_raster_h3(const mgpu::ChipTableView& hv, int res, double k_res, const
   raster_classes(hv, a1, a2, R);
   raster_blocks(R);
   raster_bands(R);
+  raster_palette(R);
 #ifdef MGPU_BLOB_TIMING
   fprintf(stderr, "[raster] classes, blocks, bands %.3f s\n", std::chrono::duration<double>(std::chrono::steady_clock::now() - rt0).count());
 #endif
@@ -2585,6 +2650,8 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
       {raster.band.data(), raster.band.size() * 4, 0},
       {cell_ans.row.data(), cell_ans.row.size() * 4, 0},
       {cell_ans.ans.data(), cell_ans.ans.size() * 2, 0},
+      {raster.pal.data(), raster.pal.size() * 8, 0},
+      {raster.idx2.data(), raster.idx2.size(), 0},
   };
   size_t total = kBlobHeaderBytes;
   BlobHeader hdr{};
@@ -2626,6 +2693,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   hdr.raster_nband = (uint32_t)raster.band.size();
   hdr.cell_ans_g = cell_ans.g;
   hdr.cell_ans_sw = cell_ans.sw;
+  hdr.raster_pal = raster.pal.empty() ? 0u : 1u;
   for (size_t k = 0; k < parts.size(); k++) {
     parts[k].off = total;
     hdr.off[k] = total;

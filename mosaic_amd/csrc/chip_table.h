@@ -204,6 +204,13 @@ struct ChipTableView {
   const uint32_t* cell_ans_row;  // [dense rows], or null: no answer grids
   const uint16_t* cell_ans;
   const uint16_t* raster_sub;
+  // lonlat with bands, palette-compressed (capi.cpp raster_palette; null: raster_sub holds
+  // every block): block b's sub-pixel i has class (raster_pal[b] >> 16 k) & 0x7FFF (0x7FFF
+  // = kPixMixed), k = the 2 bits (i & 3) of byte raster_idx2[b * sub_n^2 / 4 + i / 4];
+  // raster_pal[b] with kPalFull: its classes are raster_sub[(raster_pal[b] & 0xFFFFFFFF) *
+  // sub_n^2 + i]
+  const uint64_t* raster_pal;
+  const uint8_t* raster_idx2;
   // lonlat: blocks of 2^bshift x 2^bshift pixels, raster_blk[(iy >> bshift) * bnx + (ix >>
   // bshift)] = the class all of the block's pixels share, else kPixMixed (a table small
   // enough for LDS: the streaming kernels answer most points without a global load);
@@ -228,6 +235,7 @@ MGPU_HDI_FWD uint32_t grid_count(uint64_t e, bool ans) {
 MGPU_HDI_FWD uint32_t cell_ans_index(uint64_t e) { return (uint32_t)((e >> 36) & 0x7FF) | (uint32_t)(e >> 63) << 11; }
 constexpr uint16_t kPixEmpty = 0;
 constexpr uint16_t kPixMixed = 0xFFFF;
+constexpr uint64_t kPalFull = 1ull << 63;
 
 enum ProbeMode { kProbeCellId = 0, kProbeLattice = 1, kProbeDense = 2 };
 

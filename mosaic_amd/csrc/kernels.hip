@@ -194,8 +194,12 @@ constexpr int kMixCap = kTile / 2;  // mixed-cell candidates (phase 2b), after t
 #else
 #define MGPU_ST_INTER(v, ptr) (*(ptr) = (v))
 #endif
+// the edge-parallel walk over LDS-staged runs (below): 0 off, 1 every tile mode, 2 the split
+// pipeline's mixed tiles only -- A/B round 6 (profiles/r6/ab_edgepar.txt): C5 mixed 0.353 ->
+// 0.263 ms per 1e8 points (long fractal strips), C3 binned join 3.49 -> 3.51, C4 fused join
+// 1.664 -> 1.683 (short strips: the flat layout costs them registers and an LDS round trip)
 #ifndef MGPU_EDGE_PAR
-#define MGPU_EDGE_PAR 0  // (the edge-parallel walk over LDS-staged runs: A/B round 6)
+#define MGPU_EDGE_PAR 2
 #endif
 #ifndef MGPU_SPLIT_WALK
 #define MGPU_SPLIT_WALK 1  // (A/B r3, profiles/r3_split_walk_ab.txt: C3 binned join -3.8%, C4 r4 -1.6%)
@@ -821,6 +825,7 @@ __device__ __forceinline__ void join_tile(const JoinArgs& a, const uint32_t tile
 #endif
   bool walked = false;
 #if MGPU_EDGE_PAR
+  if (MGPU_EDGE_PAR == 1 || G == 2)
   // north_star's ray-crossing test over LDS-staged vertex runs: the walks' strip edge runs
   // (each strip a contiguous run of edge records in JTS's visiting order) are laid end to
   // end in LDS -- per flat position its walk -- and every lane of the wave tests one edge

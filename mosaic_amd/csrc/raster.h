@@ -82,7 +82,16 @@ MGPU_HDI uint32_t raster_class(const ChipTableView& t, uint32_t ri, uint32_t sub
     uint32_t cl = t.raster[ri];
     if (cl >= 0x8000u && cl != kPixMixed) {
       const uint64_t b = (uint64_t)(band ? band : t.raster_band)[sub >> 16] + (cl & 0x7FFFu);
-      cl = t.raster_sub[b * t.raster_sub_n * t.raster_sub_n + (sub & 0xFFFFu)];
+      const uint32_t i = sub & 0xFFFFu, s2 = t.raster_sub_n * t.raster_sub_n;
+      if (t.raster_pal) {
+        // (the palette word and the index byte load together: both hang off b)
+        const uint64_t P = t.raster_pal[b];
+        const uint32_t q = t.raster_idx2[b * (s2 >> 2) + (i >> 2)];
+        const uint32_t c = (uint32_t)(P >> (16 * ((q >> (2 * (i & 3))) & 3))) & 0x7FFFu;
+        cl = (P & kPalFull) ? t.raster_sub[(P & 0xFFFFFFFFull) * s2 + i] : (c == 0x7FFFu ? kPixMixed : c);
+      } else {
+        cl = t.raster_sub[b * s2 + i];
+      }
     }
     return cl;
   }
