@@ -1865,6 +1865,9 @@ int32_t mgpu_ctx_set_option(mgpu_ctx* ctx, const char* key, int64_t v) {
   } else if (k == "ring_batch") {
     if (v < 1) return bad();
     o.ring_batch = v;
+  } else if (k == "bng_split") {
+    if (v != 0 && v != 1) return bad();
+    o.bng_split = v;
   } else if (k == "spin_us") {
     if (v < 0 || v > 10000000) return bad();
     o.spin_us = v;
@@ -1890,6 +1893,7 @@ int32_t mgpu_ctx_get_option(const mgpu_ctx* ctx, const char* key, int64_t* v) {
       {"h3_libm", o.h3_libm},       {"pipeline", o.pipeline}, {"bin_count", o.bin_count},
       {"bin_min_mb", o.bin_min_mb}, {"bin_min_points", o.bin_min_points}, {"bin_xcd", o.bin_xcd},
       {"bin_keys", o.bin_keys},     {"spin_us", o.spin_us},   {"ring_batch", o.ring_batch},       {"raster", o.raster},     {"raster_bng", o.raster_bng},
+      {"bng_split", o.bng_split},
       {"raster_sub", o.raster_sub}, {"raster_milli", o.raster_milli}};
   for (const auto& kv : all)
     if (strcmp(kv.first, key) == 0) {
@@ -3109,8 +3113,12 @@ static int32_t join_impl(mgpu_ctx* ctx, const mgpu_chips* chips, int32_t is, int
   HIP_TRY(hipMemsetAsync(ctx->tq, 0, 16, s));
   // the split pipeline (kernels.h SplitArgs) when the chip table has a pixel index for
   // this resolution and no cell holds more than 32 chips
+  // (BNG dense tables without a pixel index: the grid entry is the code -- a cell whose
+  // chips are all core answers its points, the rest are mixed; option bng_split)
+  const bool bng_grid = is == MGPU_BNG && chips->view.raster_mode == mgpu::kRasterNone &&
+                        chips->view.probe_mode == mgpu::kProbeDense && o.bng_split;
   const bool split = (o.pipeline == MGPU_PIPELINE_AUTO || o.pipeline == MGPU_PIPELINE_SPLIT) && n > 0 &&
-                     chips->view.raster_mode != mgpu::kRasterNone && a.res_match &&
+                     (chips->view.raster_mode != mgpu::kRasterNone || bng_grid) && a.res_match &&
                      (is == MGPU_H3 || res == chips->view.res) && chips->view.max_cell_chips <= 32;
   mgpu::SplitArgs sa{};
   if (split) {

@@ -1233,6 +1233,39 @@ struct CodeOf<MGPU_BNG> {
 };
 
 
+// BNG without a pixel index (option bng_split): the point's dense grid entry is its code.
+// A cell whose chips are all core (at most 8) answers every point in it; a cell flagged
+// with an answer grid (chip_table.h cell_ans) answers from the point's square unless that
+// square is mixed; the other cells' points (border chips) are mixed -- the mixed tiles run
+// the whole join for them.  Cells off the dense box go through the id + hash probe.
+// Returns the match mask over the chips from *first, or kPixMixed.
+__device__ __forceinline__ uint32_t bng_grid_class(const JoinArgs& a, int64_t p, double px, double py, bool* ok,
+                                                     uint32_t* first) {
+  const ChipTableView& t = a.chips;
+  bool tie = false;
+  uint32_t gi = kNoEntry;
+  Range r = chip_probe<MGPU_BNG, false>(a, p, px, py, ok, &tie, &gi);
+  if (!*ok) return kPixEmpty;
+  uint64_t e = 0;
+  if (gi != kNoEntry) {
+    e = t.grid[gi];
+    r = grid_range(e, t.cell_ans_row != nullptr);
+  }
+  *first = r.first;
+  if (r.count == 0) return kPixEmpty;
+  if (r.count <= 8 && (r.core & ((1u << r.count) - 1u)) == (1u << r.count) - 1u) return (1u << r.count) - 1u;
+  if (t.cell_ans_row && (e & kCellAnsFlag)) {
+    const uint32_t eI = (uint32_t)bng::d2i(px), nI = (uint32_t)bng::d2i(py), ed = t.bng_edge;
+    const uint32_t col = div_fix(eI, ed, t.bng_inv_edge), row = div_fix(nI, ed, t.bng_inv_edge);
+    const uint32_t u = div_fix(eI - col * ed, t.cell_ans_sw, t.cell_ans_inv_sw);
+    const uint32_t v = div_fix(nI - row * ed, t.cell_ans_sw, t.cell_ans_inv_sw);
+    const uint32_t ai = t.cell_ans_row[row - (uint32_t)t.dense[0].b0] + cell_ans_index(e);
+    const uint16_t m = t.cell_ans[((size_t)ai * t.cell_ans_g + v) * t.cell_ans_g + u];
+    if (m != kCellAnsMixed && m < 256u) return m;
+  }
+  return kPixMixed;
+}
+
 // One wave per chunk of kChunk points: a lane takes every 64th point of the chunk
 // (item-major, so consecutive lanes read consecutive points), and the chunk's mixed
 // points are ranked in point order by a running wave count plus the item's ballot -- no
@@ -1266,6 +1299,7 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   extern __shared__ uint16_t s_blk[];       // [raster_bny * raster_bnx] (IS == H3), then the row bands
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool use_blk = IS == MGPU_H3 && t.raster_blk != nullptr;
+  const bool bng_grid = IS == MGPU_BNG && t.raster_mode == kRasterNone;  // (bng_grid_class)
   const uint32_t nblk = use_blk ? t.raster_bnx * t.raster_bny : 0u;
   uint32_t* s_band = (uint32_t*)(s_blk + ((nblk + 1) & ~1u));
   if (use_blk)
@@ -1305,7 +1339,12 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
         if (pk < a.n && pt_valid(a.valid, a.valid_off, pk)) {
           bool ok = true;
           uint32_t g_ = 0, s_ = 0, b_ = kNoPixel;
-          ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &g_, &s_, &b_);  // (see classify_pair_kernel)
+          if (IS == MGPU_BNG && bng_grid) {
+            const uint32_t m = bng_grid_class(a, pk, bx[k], by[k], &ok, &g_);
+            ri[k] = m == kPixMixed ? kRasterFull : m;  // (the class itself, below)
+          } else {
+            ri[k] = raster_index<IS>(t, bx[k], by[k], &ok, &g_, &s_, &b_);  // (see classify_pair_kernel)
+          }
           gix[k] = g_;
           sb[k] = s_;
           bi[k] = use_blk ? b_ : kNoPixel;
@@ -1332,10 +1371,14 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
         cl[k] = ri[k] < kRasterFull ? (bi[k] != kNoPixel && s_blk[bi[k]] != kPixMixed ? s_blk[bi[k]] : kPixMixed)
                                     : kPixEmpty;  // (LDS, then every non-uniform block point mixed: no global loads)
 #else
-        cl[k] = ri[k] < kRasterFull ? raster_class_blk(t, s_blk, ri[k], bi[k], sb[k], s_band)
-                                    : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
+        if (IS == MGPU_BNG && bng_grid)
+          cl[k] = ri[k] == kRasterFull ? kPixMixed : (ri[k] == kNoPixel ? kPixEmpty : ri[k]);
+        else
+          cl[k] = ri[k] < kRasterFull ? raster_class_blk(t, s_blk, ri[k], bi[k], sb[k], s_band)
+                                      : (ri[k] == kRasterFull ? kPixMixed : kPixEmpty);
 #endif
-        ge[k] = (IS == MGPU_BNG && ri[k] < kRasterFull) ? t.grid[gix[k]] : 0ull;
+        if (IS == MGPU_BNG && bng_grid) ge[k] = gix[k];  // (the first chip)
+        else ge[k] = (IS == MGPU_BNG && ri[k] < kRasterFull) ? t.grid[gix[k]] : 0ull;
       }
 #pragma unroll
       for (int k = 0; k < kCfyBatch; k++) {
@@ -1396,6 +1439,7 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
   extern __shared__ uint16_t s_blk[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool use_blk = IS == MGPU_H3 && t.raster_blk != nullptr;
+  const bool bng_grid = IS == MGPU_BNG && t.raster_mode == kRasterNone;  // (bng_grid_class)
   const uint32_t nblk = use_blk ? t.raster_bnx * t.raster_bny : 0u;
   uint32_t* s_band = (uint32_t*)(s_blk + ((nblk + 1) & ~1u));
   if (use_blk)
@@ -1435,8 +1479,13 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
         if (pj < a.n && pt_valid(a.valid, a.valid_off, pj)) {
           bool ok = true;
           uint32_t g_ = 0, s_ = 0, b_ = kNoPixel;
-          // (always a local's address: a pointer chosen at run time put b_ in scratch)
-          ri[j] = raster_index<IS>(t, X[j], Y[j], &ok, &g_, &s_, &b_);
+          if (IS == MGPU_BNG && bng_grid) {
+            const uint32_t m = bng_grid_class(a, pj, X[j], Y[j], &ok, &g_);
+            ri[j] = m == kPixMixed ? kRasterFull : m;
+          } else {
+            // (always a local's address: a pointer chosen at run time put b_ in scratch)
+            ri[j] = raster_index<IS>(t, X[j], Y[j], &ok, &g_, &s_, &b_);
+          }
           gix[j] = g_;
           sb[j] = s_;
           bi[j] = use_blk ? b_ : kNoPixel;
@@ -1447,9 +1496,14 @@ __global__ __launch_bounds__(kCfyBlock) __attribute__((amdgpu_waves_per_eu(MGPU_
       uint64_t ge[kPts];
 #pragma unroll
       for (int j = 0; j < kPts; j++) {
-        cl[j] = ri[j] < kRasterFull ? raster_class_blk(t, s_blk, ri[j], bi[j], sb[j], s_band)
-                                    : (ri[j] == kRasterFull ? kPixMixed : kPixEmpty);
-        ge[j] = (IS == MGPU_BNG && ri[j] < kRasterFull) ? t.grid[gix[j]] : 0ull;
+        if (IS == MGPU_BNG && bng_grid) {
+          cl[j] = ri[j] == kRasterFull ? kPixMixed : (ri[j] == kNoPixel ? kPixEmpty : ri[j]);
+          ge[j] = gix[j];  // (the first chip)
+        } else {
+          cl[j] = ri[j] < kRasterFull ? raster_class_blk(t, s_blk, ri[j], bi[j], sb[j], s_band)
+                                      : (ri[j] == kRasterFull ? kPixMixed : kPixEmpty);
+          ge[j] = (IS == MGPU_BNG && ri[j] < kRasterFull) ? t.grid[gix[j]] : 0ull;
+        }
       }
       Code code[kPts];
       bool mixed[kPts];

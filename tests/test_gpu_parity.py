@@ -632,6 +632,35 @@ def test_pip_join_c4_london_districts_bng(gpu):
         assert len(gp) > 0.95 * len(x)  # the districts tile the extent
 
 
+@pytest.mark.parametrize("res", [3, 4])
+def test_pip_join_bng_split_grid_codes(gpu, res):
+    """BNG through the split pipeline with the dense grid entry as the code (option
+    bng_split, round 6): a cell of core chips answers its points, an answer-grid square
+    (res 3) answers its points, the rest are mixed -- pairs equal the oracle's and the
+    fused pipeline's (bng_split = 0), on uniform points plus chip vertices / edge points and
+    whole-metre points on square lines."""
+    import bench_workloads as W
+    from test_raster_host import adversarial_points as chip_adversaries
+    P = W.london_districts()
+    c = M.tessellate(P, M.BNGIndexSystem(), res)
+    rng = np.random.default_rng(71 + res)
+    a = chip_adversaries(c, rng, 1500)
+    x0, y0 = W.london_points(400_000, 17 + res)
+    sq = rng.integers(50300, 56100, 20000).astype(np.float64) * 10.0
+    nn = rng.integers(155000, 201000, 20000).astype(np.float64)
+    x = np.concatenate([x0, a[:, 0], sq, np.nextafter(sq, -np.inf)])
+    y = np.concatenate([y0, a[:, 1], nn, nn])
+    op, oq = oracle_join(c, x, y, res=res, isys=1)
+    ctx = M.default_context(gpu)
+    d = c.upload(ctx)
+    for split in (1, 0):
+        with ctx.options(bng_split=split):
+            r = M.pip_join(T(x, gpu), T(y, gpu), d, res, index_system=M.BNGIndexSystem())
+        assert r.stats["pipeline"] == (1 if split else 0), (split, r.stats["pipeline"])
+        gp, gq = r.numpy()
+        assert np.array_equal(gp, op) and np.array_equal(gq, oq), (res, split)
+
+
 def test_pip_join_c4_answer_grid_edges(gpu):
     """C4 res 3 joins through the cells' answer grids (10 m squares): chip vertices and
     edge points (and their ulp neighbours), whole-metre points on square lines and just
