@@ -113,7 +113,7 @@ int32_t mgpu_ctx_destroy(mgpu_ctx* ctx);
  *   "spin_us"         synchronous calls poll their stream (yielding the core between polls)
  *                     at most this long, then block in hipStreamSynchronize (default 2000;
  *                     0 = block at once)
- *   "bng_split"       1 (default) / 0: a BNG table on a dense grid without a pixel index
+ *   "bng_split"       1 / 0 (default): a BNG table on a dense grid without a pixel index
  *                     joins through the split pipeline with the grid entry as the code (a
  *                     cell of core chips, or an answer-grid square, answers its points; the
  *                     rest go to the mixed tiles) / through the fused pipeline

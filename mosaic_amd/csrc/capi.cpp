@@ -1180,7 +1180,7 @@ void raster_bands(Raster& R) {
 // bytes instead of 512, the whole level 7x smaller (C2: 68 MB -> ~10 MB); a block with more
 // classes keeps its full u16 layout (pal = kPalFull | its index among those).
 #ifndef MGPU_RASTER_PAL
-#define MGPU_RASTER_PAL 1
+#define MGPU_RASTER_PAL 0  // (A/B round 6, profiles/r6/ab_palette_edgepar.txt: C2 classify 0.59 -> 0.70 ms with it -- rejected)
 #endif
 void raster_palette(Raster& R) {
   if (!MGPU_RASTER_PAL || R.band.empty() || R.sub_n == 0 || (R.sub_n * R.sub_n) % 4) return;

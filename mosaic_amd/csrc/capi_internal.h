@@ -19,7 +19,7 @@ struct mgpu_options {
   int64_t bin_keys = 0;                   // ... H3: grid keys computed by the scatter kernel (A/B r5: slower)
   int64_t spin_us = 2000;                 // synchronous calls: poll (yielding) this long, then block
   int64_t ring_batch = (int64_t)1 << 26;   // ring joins: candidate pairs held in scratch at a time
-  int64_t bng_split = 1;                  // BNG dense tables: the split pipeline, the grid entry as the code
+  int64_t bng_split = 0;                  // BNG dense tables: the split pipeline, the grid entry as the code (A/B r6: C4 2.43 vs 2.17 ms fused -- off)
   // the chip-table builder of mgpu_chips_upload on this context (mgpu_build_opts)
   int64_t raster = 1, raster_bng = 0, raster_sub = 16, raster_milli = 250;
 };

@@ -227,10 +227,10 @@ def test_nyc_r9_blob_bytes_pinned(nyc_zones, nyc_chips_r9):
     produced before its speed-ups (per-pixel edge lists, shared corner sines, row-parity
     verdicts, hashed classes): sha256 prefix of the whole blob, for round 5's chips (the
     Sutherland-Hodgman clip, kept as chip_geometry="sutherland_hodgman") and round 6's (the
-    JTS overlay: one zero-area row fewer, other crossing vertices, separate pieces).  Round
-    6's blob format (version 13) palette-compresses the second level (86.8 MB -> 28.0 MB for
-    round 5's chips; before it, those were 86778112 bytes, a145d3f4556f4f6a)."""
+    JTS overlay: one zero-area row fewer, other crossing vertices, separate pieces).  (The
+    palette-compressed second level, MGPU_RASTER_PAL=1, gives 28048896 / 9b2d36e77e294e9d
+    and 27949568 / 615fde4ca9269ef5 -- off: slower on C2)"""
     import mosaic_amd as M
     sh = M.tessellate(nyc_zones, M.H3IndexSystem(), 9, chip_geometry="sutherland_hodgman")
-    assert _blob_hash(sh) == (28048896, "9b2d36e77e294e9d")
-    assert _blob_hash(nyc_chips_r9) == (27949568, "615fde4ca9269ef5")
+    assert _blob_hash(sh) == (86778112, "a145d3f4556f4f6a")
+    assert _blob_hash(nyc_chips_r9) == (86478336, "8235ff6347457b25")
