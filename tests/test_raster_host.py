@@ -227,10 +227,11 @@ def test_nyc_r9_blob_bytes_pinned(nyc_zones, nyc_chips_r9):
     produced before its speed-ups (per-pixel edge lists, shared corner sines, row-parity
     verdicts, hashed classes): sha256 prefix of the whole blob, for round 5's chips (the
     Sutherland-Hodgman clip, kept as chip_geometry="sutherland_hodgman") and round 6's (the
-    JTS overlay: one zero-area row fewer, other crossing vertices, separate pieces).  (The
-    palette-compressed second level, MGPU_RASTER_PAL=1, gives 28048896 / 9b2d36e77e294e9d
-    and 27949568 / 615fde4ca9269ef5 -- off: slower on C2)"""
+    JTS overlay: one zero-area row fewer, other crossing vertices, separate pieces).  Blob
+    version 13 adds the (empty) palette arrays: round 5's bytes were 86778112 /
+    a145d3f4556f4f6a; the palette-compressed second level (MGPU_RASTER_PAL=1) gives
+    28048896 / 9b2d36e77e294e9d and 27949568 / 615fde4ca9269ef5 -- off: slower on C2 (§4)."""
     import mosaic_amd as M
     sh = M.tessellate(nyc_zones, M.H3IndexSystem(), 9, chip_geometry="sutherland_hodgman")
-    assert _blob_hash(sh) == (86778112, "a145d3f4556f4f6a")
-    assert _blob_hash(nyc_chips_r9) == (86478336, "8235ff6347457b25")
+    assert _blob_hash(sh) == (86778624, '22e5b22b2ea161e5')
+    assert _blob_hash(nyc_chips_r9) == (86478848, 'fa0a071a53ada4f2')
