@@ -241,7 +241,7 @@ struct Overlay {
     lower_dim = false;
   }
   int node_id(P p) const {
-    auto it = std::lower_bound(nodes.begin(), nodes.end(), p, less);
+    auto it = std::lower_bound(nodes.begin(), nodes.end(), p, [](P a, P b) { return less(a, b); });
     return (int)(it - nodes.begin());
   }
 };
@@ -378,6 +378,56 @@ struct SegGrid {
     out.erase(std::unique(out.begin(), out.end()), out.end());
     return out;
   }
+  // the segments a rightward ray from (px, py) can meet or (px, py) can lie on: a segment
+  // whose envelope spans py and reaches x >= px is in py's bucket row at or right of
+  // px's bucket (clamping keeps both monotone) -- sorted, each once
+  const std::vector<uint64_t>& ray_right(double px, double py) const {
+    out.clear();
+    if (start.empty()) return out;
+    const long j = row(py);
+    for (long i = col(px); i < nx; i++) {
+      const size_t c = (size_t)(j * nx + i);
+      out.insert(out.end(), items.begin() + start[c], items.begin() + start[c + 1]);
+    }
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out;
+  }
+  // PointLocation.locateInRing (locate_in_ring below) of p in every ring at once, from the
+  // ray_right segments only (the others are skipped by its first test or cross nothing):
+  // loc[ring] = 1 interior, 0 boundary, -1 exterior
+  void locate_rings(P p, const std::vector<const std::vector<P>*>& rings, std::vector<int8_t>& loc,
+                    std::vector<int>& cross) const {
+    loc.assign(rings.size(), -1);
+    cross.assign(rings.size(), 0);
+    for (uint64_t c : ray_right(p.x, p.y)) {
+      const size_t r = (size_t)(c >> 32), k = (size_t)(c & 0xFFFFFFFFu);
+      if (loc[r] == 0) continue;
+      const P p1 = (*rings[r])[k], p2 = (*rings[r])[k + 1];
+      if (p1.x < p.x && p2.x < p.x) continue;
+      if (eq(p, p2)) {
+        loc[r] = 0;
+        continue;
+      }
+      if (p1.y == p.y && p2.y == p.y) {
+        double mn = p1.x, mx = p2.x;
+        if (mn > mx) std::swap(mn, mx);
+        if (p.x >= mn && p.x <= mx) loc[r] = 0;
+        continue;
+      }
+      if ((p1.y > p.y && p2.y <= p.y) || (p2.y > p.y && p1.y <= p.y)) {
+        int o = orient(p1, p2, p);
+        if (o == 0) {
+          loc[r] = 0;
+          continue;
+        }
+        if (p2.y < p1.y) o = -o;
+        if (o > 0) cross[r]++;
+      }
+    }
+    for (size_t r = 0; r < rings.size(); r++)
+      if (loc[r] != 0) loc[r] = (cross[r] & 1) ? 1 : -1;
+  }
 };
 
 // The result of one overlay: pieces (rings; ring 0 = shell, clockwise; holes ccw)
@@ -399,6 +449,8 @@ struct Clipper {
   std::vector<int> cand;  // candidate subject segments (ring << 32 | k) from the grid
   std::vector<uint64_t> cand64;
   std::vector<const std::vector<P>*> sub_rings;
+  std::vector<int8_t> rloc;
+  std::vector<int> rcross;
 
   void build(const std::vector<std::vector<std::vector<P>>>& parts, const std::vector<uint8_t>& ring_ccw,
              const std::vector<std::vector<P>>& cell, std::vector<Rings>& pieces, bool* lower_dim,
@@ -482,8 +534,9 @@ struct Clipper {
       o.nodes.push_back(e.first);
       o.nodes.push_back(e.second);
     }
-    std::sort(o.nodes.begin(), o.nodes.end(), less);
-    o.nodes.erase(std::unique(o.nodes.begin(), o.nodes.end(), eq), o.nodes.end());
+    // (lambdas: the comparisons inline)
+    std::sort(o.nodes.begin(), o.nodes.end(), [](P a, P b) { return less(a, b); });
+    o.nodes.erase(std::unique(o.nodes.begin(), o.nodes.end(), [](P a, P b) { return eq(a, b); }), o.nodes.end());
     o.on_geom.assign(o.nodes.size(), 0);
     o.edges.clear();
     cell_edge_begin.assign(cell.size() + 1, (int)sub.size());
@@ -587,11 +640,12 @@ struct Clipper {
       return false;
     };
     auto locate_subject = [&](P p) {
+      if (grid) grid->locate_rings(p, sub_rings, rloc, rcross);
       int ring = 0;
       for (size_t pi = 0; pi < parts.size(); pi++) {
         bool in = false;
         for (size_t ri = 0; ri < parts[pi].size(); ri++, ring++) {
-          const int l = locate_in_ring(p, *sub_rings[ring]);
+          const int l = grid ? rloc[ring] : locate_in_ring(p, *sub_rings[ring]);
           if (ri == 0) in = l >= 0;
           else if (in && l > 0) in = false;
         }

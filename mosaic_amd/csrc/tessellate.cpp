@@ -238,17 +238,9 @@ uint64_t pole_cell(bool north, int res) {
 }
 
 // a cell's rings (Grid::boundary) as chip WKB: a Polygon, or a MultiPolygon of its parts
-void write_cell_wkb(const std::vector<std::vector<Pt>>& rings, std::vector<uint8_t>& out) {
-  std::vector<mgpu::wkb::Polygon> parts(rings.size());
-  for (size_t k = 0; k < rings.size(); k++) {
-    std::vector<double> flat;
-    for (auto& p : rings[k]) {
-      flat.push_back(p.x);
-      flat.push_back(p.y);
-    }
-    parts[k].push_back(std::move(flat));
-  }
-  mgpu::wkb::write_polygons(out, parts);
+// (every ring its own polygon; each ring reversed when `rev`)
+void write_cell_wkb(const std::vector<std::vector<Pt>>& rings, std::vector<uint8_t>& out, bool rev = false) {
+  mgpu::wkb::write_polygons_pts<true>(out, rings, rev);
 }
 
 // JTS Intersection.intersection (JTS 1.20 algorithm/Intersection.java, what
@@ -368,11 +360,23 @@ struct Grid {
   virtual long row_of(double y, bool up) const = 0;
   virtual double col_x(long i, long j) const = 0;
   virtual long col_of(double x, long j, bool up) const = 0;
+  // lattice cells (i0..i1, j0..j1) holding every cell_at of a point in the lattice-space
+  // box and the neighbours of those cells
+  virtual void cell_window(double xmin, double ymin, double xmax, double ymax, long* i0, long* j0, long* i1,
+                           long* j1) const = 0;
 };
 
 struct H3Grid : Grid {
   int face, res;
-  explicit H3Grid(int f, int r) : face(f), res(r) {}
+  // a lattice position inside the face triangle's inscribed circle (radius 1 in res-0
+  // units; the vertices, where the pentagons sit, lie at 2), with a margin: no overage and
+  // no pentagon near, so the id at that position is this face's cell centred there
+  double inscribed2;
+  explicit H3Grid(int f, int r) : face(f), res(r) {
+    double q = 0.95;
+    for (int i = 0; i < r; i++) q *= mgpu::h3::kSqrt7;
+    inscribed2 = q * q;
+  }
   Pt to_lattice(Pt p) const override {
     double lat = p.y * M_PI / 180.0, lon = p.x * M_PI / 180.0;
     // project onto THIS face (the polygon's), even slightly beyond its edge
@@ -425,6 +429,8 @@ struct H3Grid : Grid {
     return cc_val;
   }
   bool keep(int64_t id, long i, long j) const override {
+    const Pt v = center(i, j);
+    if (v.x * v.x + v.y * v.y < inscribed2) return true;
     if (mgpu::h3b::h3_to_face_ijk((uint64_t)id).face != face) return false;
     // near an icosahedron vertex the lattice positions beyond a pentagon's missing
     // sector map to ids of cells elsewhere: the id's centre must be this position
@@ -487,6 +493,15 @@ struct H3Grid : Grid {
     double v = x + 0.5 * j;
     return up ? (long)std::ceil(v) : (long)std::floor(v);
   }
+  // (a point's cell centre lies within 0.58 of it: row within 1, column within 1 + half
+  // a row; neighbours one more)
+  void cell_window(double xmin, double ymin, double xmax, double ymax, long* i0, long* j0, long* i1,
+                   long* j1) const override {
+    *j0 = (long)std::floor(ymin / mgpu::h3::kSin60) - 3;
+    *j1 = (long)std::ceil(ymax / mgpu::h3::kSin60) + 3;
+    *i0 = (long)std::floor(xmin + 0.5 * (double)*j0) - 3;
+    *i1 = (long)std::ceil(xmax + 0.5 * (double)*j1) + 3;
+  }
 };
 
 struct BngGrid : Grid {
@@ -523,6 +538,11 @@ struct BngGrid : Grid {
   double col_x(long i, long) const override { return i + 0.5; }
   long col_of(double x, long, bool up) const override {
     return up ? (long)std::ceil(x - 0.5) : (long)std::floor(x - 0.5);
+  }
+  void cell_window(double xmin, double ymin, double xmax, double ymax, long* i0, long* j0, long* i1,
+                   long* j1) const override {
+    *i0 = (long)std::floor(xmin) - 2, *j0 = (long)std::floor(ymin) - 2;
+    *i1 = (long)std::floor(xmax) + 2, *j1 = (long)std::floor(ymax) + 2;
   }
 };
 
@@ -768,8 +788,9 @@ struct PairHash {
   size_t operator()(const std::pair<long, long>& p) const { return std::hash<long>()(p.first * 1000003L ^ p.second); }
 };
 
-// lattice cell -> smallest squared distance from its centre to a walked boundary sample:
-// open addressing (the walk looks a cell up ~7 times per sample)
+// lattice cell -> smallest squared distance from its centre to a walked boundary sample
+// (the walk looks a cell up ~7 times per sample): a dense window of the lattice around the
+// polygon when that is small (-1: not walked), else open addressing
 struct CellDist {
   struct Slot {
     long i, j;
@@ -778,11 +799,48 @@ struct CellDist {
   };
   std::vector<Slot> t;
   size_t n = 0, mask = 0;
+  bool dense = false, overflow = false;
+  long wi0 = 0, wj0 = 0, wni = 0, wnj = 0;
+  std::vector<float> w;
+  void clear_dense(long i0, long j0, long i1, long j1) {
+    dense = true;
+    overflow = false;
+    wi0 = i0, wj0 = j0, wni = i1 - i0 + 1, wnj = j1 - j0 + 1;
+    w.assign((size_t)(wni * wnj), -1.f);
+  }
+  float* cell(long i, long j) {
+    const long a = i - wi0, b = j - wj0;
+    return (a >= 0 && a < wni && b >= 0 && b < wnj) ? &w[(size_t)(a * wnj + b)] : nullptr;
+  }
+  // the smallest squared distance walked for (i, j), or -1
+  float get(long i, long j) {
+    if (dense) {
+      const float* c = cell(i, j);
+      return c ? *c : -1.f;
+    }
+    const Slot* q = find(i, j);
+    return q ? q->d2 : -1.f;
+  }
+  void touch(long i, long j, float d2) {
+    if (dense) {
+      float* c = cell(i, j);
+      if (!c) {  // (cell_window should hold every cell the walk reaches: then hash it)
+        overflow = true;
+        return;
+      }
+      if (*c < 0 || d2 < *c) *c = d2;
+      return;
+    }
+    Slot* it = find(i, j);
+    if (!it) put(i, j, d2);
+    else if (d2 < it->d2) it->d2 = d2;
+  }
   static size_t h(long i, long j) {
     uint64_t k = (uint64_t)i * 0x9E3779B97F4A7C15ull ^ ((uint64_t)j + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full;
     return (size_t)(k ^ (k >> 29));
   }
   void clear() {
+    dense = overflow = false;
     t.assign(1024, Slot{0, 0, 0.f, false});
     mask = 1023;
     n = 0;
@@ -836,12 +894,25 @@ bool cell_in_polygon(const std::vector<Pt>& cellb, const std::vector<std::vector
     for (size_t k = 0; k + 1 < cellb.size(); k++)
       if (segments_touch(a, b, cellb[k], cellb[k + 1])) return false;
   }
+  // point_in_ring of the centre in every ring at once, over the segments a rightward ray
+  // from it can cross (SegGrid::ray_right; the others add no crossing): the same terms
+  thread_local std::vector<uint8_t> par;
+  par.assign(poly.ring_ptr.size(), 0);
+  for (uint64_t c : poly.grid.ray_right(cc.x, cc.y)) {
+    const auto& ring = *poly.ring_ptr[c >> 32];
+    const size_t k = (size_t)(c & 0xFFFFFFFFu);
+    const Pt ri = ring[k + 1], rj = ring[k];
+    if (((ri.y > cc.y) != (rj.y > cc.y)) && (cc.x < (rj.x - ri.x) * (cc.y - ri.y) / (rj.y - ri.y) + ri.x))
+      par[c >> 32] ^= 1;
+  }
+  size_t r0 = 0;
   for (auto& part : poly.parts) {
-    if (!point_in_ring(part[0], cc)) continue;
-    bool in_hole = false;
-    for (size_t r = 1; r < part.size(); r++)
-      if (point_in_ring(part[r], cc)) in_hole = true;
-    if (!in_hole) return true;
+    const size_t r1 = r0 + part.size();
+    bool in = par[r0] != 0;
+    for (size_t r = r0 + 1; in && r < r1; r++)
+      if (par[r]) in = false;
+    if (in) return true;
+    r0 = r1;
   }
   return false;
 }
@@ -856,7 +927,7 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
     const auto v = rule ? rule->decide(g.center_input(i, j, id), 1) : CoreRule::kCore;
     if (rule && rule->last_flag) {
       Undecided u{id, pid, (uint8_t)rule->last_flag, (uint8_t)(v != CoreRule::kDrop), (uint8_t)(v == CoreRule::kCore), {}};
-      write_cell_wkb(reversed(rings ? *rings : g.boundary_of(i, j, id)), u.wkb);
+      write_cell_wkb(rings ? *rings : g.boundary_of(i, j, id), u.wkb, true);
       und.push_back(std::move(u));
     }
     if (v == CoreRule::kDrop) {
@@ -866,14 +937,14 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
     if (v != CoreRule::kCore) {
       rule->st.demoted++;
       Chip ch{id, pid, 0, {}};
-      write_cell_wkb(reversed(rings ? *rings : g.boundary_of(i, j, id)), ch.wkb);
+      write_cell_wkb(rings ? *rings : g.boundary_of(i, j, id), ch.wkb, true);
       out.push_back(std::move(ch));
       return;
     }
     Chip ch{id, pid, 1, {}};
     if (keep_core) {
       const auto rs = rings ? *rings : g.boundary_of(i, j, id);
-      write_cell_wkb(g.cw_ring(id) ? reversed(rs) : rs, ch.wkb);
+      write_cell_wkb(rs, ch.wkb, g.cw_ring(id));
     }
     out.push_back(std::move(ch));
   };
@@ -883,53 +954,66 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
   // constructions of the same chip -- a cell the boundary never reaches gives the same
   // row either way -- so its rounding at the threshold does not matter)
   CellDist& border = t_border;
+  double xmin = INFINITY, ymin = INFINITY, xmax = -INFINITY, ymax = -INFINITY;
+  double walk_len = 0;
+  for (auto& r : lat_rings)
+    for (size_t i = 0; i < r.size(); i++) {
+      xmin = std::min(xmin, r[i].x), xmax = std::max(xmax, r[i].x);
+      ymin = std::min(ymin, r[i].y), ymax = std::max(ymax, r[i].y);
+      if (i + 1 < r.size()) walk_len += std::fabs(r[i + 1].x - r[i].x) + std::fabs(r[i + 1].y - r[i].y);
+    }
   border.clear();
+  if (xmin <= xmax) {
+    // the dense window when it is not much larger than the cells the walk visits
+    long i0, j0, i1, j1;
+    g.cell_window(xmin, ymin, xmax, ymax, &i0, &j0, &i1, &j1);
+    if ((double)(i1 - i0 + 1) * (double)(j1 - j0 + 1) <= 64.0 * walk_len + 65536.0) border.clear_dense(i0, j0, i1, j1);
+  }
   std::vector<std::pair<long, long>> nb;
   auto touch = [&](const std::pair<long, long>& c, Pt s) {
     const Pt cc = g.center(c.first, c.second);
     const double dx = s.x - cc.x, dy = s.y - cc.y;
-    const float d2 = (float)(dx * dx + dy * dy);
-    CellDist::Slot* it = border.find(c.first, c.second);
-    if (!it) border.put(c.first, c.second, d2);
-    else if (d2 < it->d2) it->d2 = d2;
+    border.touch(c.first, c.second, (float)(dx * dx + dy * dy));
   };
-  for (auto& r : lat_rings)
-    for (size_t i = 0; i + 1 < r.size(); i++) {
-      Pt a = r[i], b = r[i + 1];
-      double len = std::hypot(b.x - a.x, b.y - a.y);
-      int steps = std::max(1, (int)std::ceil(len / 0.2));
-      for (int s = 0; s <= steps; s++) {
-        double t = (double)s / steps;
-        const Pt q{a.x + t * (b.x - a.x), a.y + t * (b.y - a.y)};
-        auto c = g.cell_at(q);
-        touch(c, q);
-        nb.clear();
-        g.neighbors(c.first, c.second, nb);
-        for (auto& n : nb) touch(n, q);
-      }
-    }
-  // 3. interior cells: even-odd scanline over lattice rows
-  double ymin = INFINITY, ymax = -INFINITY;
-  for (auto& r : lat_rings)
-    for (auto& p : r) {
-      ymin = std::min(ymin, p.y);
-      ymax = std::max(ymax, p.y);
-    }
-  std::vector<std::pair<long, long>> interior;
-  if (ymin <= ymax) {
-    for (long j = g.row_of(ymin, true); j <= g.row_of(ymax, false); j++) {
-      double y = g.row_y(j);
-      std::vector<double> xs;
-      for (auto& r : lat_rings)
-        for (size_t i = 0; i + 1 < r.size(); i++) {
-          Pt a = r[i], b = r[i + 1];
-          if ((a.y > y) != (b.y > y)) xs.push_back(a.x + (y - a.y) * (b.x - a.x) / (b.y - a.y));
+  auto walk = [&]() {
+    for (auto& r : lat_rings)
+      for (size_t i = 0; i + 1 < r.size(); i++) {
+        Pt a = r[i], b = r[i + 1];
+        double len = std::hypot(b.x - a.x, b.y - a.y);
+        int steps = std::max(1, (int)std::ceil(len / 0.2));
+        for (int s = 0; s <= steps; s++) {
+          double t = (double)s / steps;
+          const Pt q{a.x + t * (b.x - a.x), a.y + t * (b.y - a.y)};
+          auto c = g.cell_at(q);
+          touch(c, q);
+          nb.clear();
+          g.neighbors(c.first, c.second, nb);
+          for (auto& n : nb) touch(n, q);
         }
-      std::sort(xs.begin(), xs.end());
-      for (size_t k = 0; k + 1 < xs.size(); k += 2)
-        for (long i = g.col_of(xs[k], j, true); i <= g.col_of(xs[k + 1], j, false); i++)
-          if (!border.find(i, j)) interior.push_back({i, j});
-    }
+      }
+  };
+  walk();
+  if (border.overflow) {
+    border.clear();
+    walk();
+  }
+  // 3. interior cells: even-odd scanline over lattice rows (each row's sorted crossings
+  // kept: they also place the far border cells below)
+  std::vector<std::pair<long, long>> interior;
+  const long row0 = ymin <= ymax ? g.row_of(ymin, true) : 0, row1 = ymin <= ymax ? g.row_of(ymax, false) : -1;
+  std::vector<std::vector<double>> row_xs((size_t)std::max(0L, row1 - row0 + 1));
+  for (long j = row0; j <= row1; j++) {
+    double y = g.row_y(j);
+    std::vector<double>& xs = row_xs[(size_t)(j - row0)];
+    for (auto& r : lat_rings)
+      for (size_t i = 0; i + 1 < r.size(); i++) {
+        Pt a = r[i], b = r[i + 1];
+        if ((a.y > y) != (b.y > y)) xs.push_back(a.x + (y - a.y) * (b.x - a.x) / (b.y - a.y));
+      }
+    std::sort(xs.begin(), xs.end());
+    for (size_t k = 0; k + 1 < xs.size(); k += 2)
+      for (long i = g.col_of(xs[k], j, true); i <= g.col_of(xs[k + 1], j, false); i++)
+        if (border.get(i, j) < 0) interior.push_back({i, j});
   }
   for (auto& c : interior) {
     int64_t id = g.cell_id(c.first, c.second);
@@ -940,19 +1024,29 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
   // neighbour of a walked cell): then it lies wholly inside or outside, decided by its
   // centre, without its exact geometry
   std::vector<std::pair<long, long>> bl;
-  bl.reserve(border.n);
-  for (auto& sl : border.t)
-    if (sl.used) bl.push_back({sl.i, sl.j});
-  std::sort(bl.begin(), bl.end());
+  if (border.dense) {
+    for (long a = 0; a < border.wni; a++)  // (in (i, j) order already)
+      for (long b = 0; b < border.wnj; b++)
+        if (border.w[(size_t)(a * border.wnj + b)] >= 0) bl.push_back({border.wi0 + a, border.wj0 + b});
+  } else {
+    bl.reserve(border.n);
+    for (auto& sl : border.t)
+      if (sl.used) bl.push_back({sl.i, sl.j});
+    std::sort(bl.begin(), bl.end());
+  }
   for (auto& c : bl) {
     const int64_t cid = g.cell_id(c.first, c.second);
     if (!cid || !g.keep(cid, c.first, c.second)) continue;
     const double far = g.far_distance();
-    if ((double)border.find(c.first, c.second)->d2 > far * far) {
+    if ((double)border.get(c.first, c.second) > far * far) {
+      // no ring comes within 0.65 of the centre (samples <= 0.2 apart): the even-odd count
+      // of its row's crossings right of it places it (the centre is on its row: col_x, row_y)
       const Pt cc = g.center(c.first, c.second);
       bool in = false;
-      for (auto& r : lat_rings)
-        if (point_in_ring(r, cc)) in = !in;
+      if (c.second >= row0 && c.second <= row1) {
+        const auto& xs = row_xs[(size_t)(c.second - row0)];
+        in = ((xs.end() - std::upper_bound(xs.begin(), xs.end(), cc.x)) & 1) != 0;
+      }
       if (!in) continue;
       whole(cid, c.first, c.second, nullptr);
       continue;
@@ -990,12 +1084,12 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
     // (a concave cell is clipped piece by piece: the chip is then a MULTIPOLYGON whose
     // parts meet along the pieces' diagonals -- the same point set, and PointLocator's
     // Mod-2 rule puts a point on such a seam in the interior, as for the whole cell)
-    std::vector<mgpu::wkb::Polygon> parts;
+    std::vector<mgpu::wkb::Polygon> parts;  // (Sutherland-Hodgman)
+    std::vector<mgpu::ovl::Rings> pcs;      // (overlay)
     double area = 0;
     if (chip_geometry == kChipOverlay) {
       // polygon INTERSECTION cell as JTS OverlayNG computes it, then coerceChipGeometry
       // (jts_overlay.h)
-      std::vector<mgpu::ovl::Rings> pcs;
       bool lower = false;
       t_clip.build(poly.parts, poly.ring_ccw, rings, pcs, &lower, &poly.grid);
       for (auto& pc : pcs)
@@ -1013,19 +1107,6 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
           for (auto& r : pc) after += r.size();
         gs.coerced++;
         gs.coerce_nodes += (int64_t)(after - before);
-      }
-      for (auto& pc : pcs) {
-        mgpu::wkb::Polygon wp;
-        for (auto& r : pc) {
-          std::vector<double> flat;
-          flat.reserve(2 * r.size());
-          for (auto& q : r) {
-            flat.push_back(q.x);
-            flat.push_back(q.y);
-          }
-          wp.push_back(std::move(flat));
-        }
-        parts.push_back(std::move(wp));
       }
     }
     if (chip_geometry == kChipSutherlandHodgman)
@@ -1062,7 +1143,11 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
       }
       if (shell_ok) parts.push_back(std::move(out_part));
     }
-    if (parts.empty() || area <= 0) continue;  // empty chip: dropped
+    if ((chip_geometry == kChipOverlay ? pcs.empty() : parts.empty()) || area <= 0) continue;  // empty chip: dropped
+    auto write_chip = [&](std::vector<uint8_t>& w) {
+      if (chip_geometry == kChipOverlay) mgpu::wkb::write_polygons_pts<false>(w, pcs, false);
+      else mgpu::wkb::write_polygons(w, parts);
+    };
     if (rule) {
       // mosaicFill's sets: a cell whose centre is deep enough inside is in the core set
       // (its chip is the whole cell, core, even where the polygon does not cover it); one
@@ -1071,7 +1156,7 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
       if (rule->last_flag) {
         Undecided u{cid, pid, (uint8_t)rule->last_flag, (uint8_t)(v != CoreRule::kDrop), (uint8_t)(v == CoreRule::kCore),
                     {}};
-        mgpu::wkb::write_polygons(u.wkb, parts);
+        write_chip(u.wkb);
         und.push_back(std::move(u));
       }
       if (v == CoreRule::kDrop) {
@@ -1081,13 +1166,13 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
       if (v == CoreRule::kCore) {
         rule->st.promoted++;
         Chip ch{cid, pid, 1, {}};
-        if (keep_core) write_cell_wkb(g.cw_ring(cid) ? reversed(rings) : rings, ch.wkb);
+        if (keep_core) write_cell_wkb(rings, ch.wkb, g.cw_ring(cid));
         out.push_back(std::move(ch));
         continue;
       }
     }
     Chip ch{cid, pid, 0, {}};
-    mgpu::wkb::write_polygons(ch.wkb, parts);
+    write_chip(ch.wkb);
     out.push_back(std::move(ch));
   }
 }
@@ -1118,10 +1203,13 @@ std::vector<Pt> densify(const std::vector<Pt>& r, double step) {
 // H3: every face whose cells can meet the polygon, with the polygon's rings densified
 // (returns false when the polygon is too large for the per-face projection)
 bool h3_faces(const Polygon& poly, int res, std::vector<std::vector<Pt>>& dense, std::vector<int>& faces) {
-  // centre spacing of res-r cells ~ 0.3 / sqrt7^r rad; pieces of a tenth of it
+  // centre spacing of res-r cells ~ 0.3 / sqrt7^r rad; pieces of a tenth of it, or of half
+  // of it from res 5 (a lon/lat edge bows off its lattice chord by ~L^2 k / 8 with k the
+  // curvature in cells^-1, < 1e-3 there: far below the walk's 0.07 margin -- and the walk
+  // samples every 0.2 along the chords anyway)
   double cell = 0.3;
   for (int i = 0; i < res; i++) cell /= 2.6457513110645906;
-  const double step = std::min(1.0, 0.1 * cell * 180.0 / M_PI);
+  const double step = std::min(1.0, (res >= 5 ? 0.5 : 0.1) * cell * 180.0 / M_PI);
   // a cell centred on face g can reach a point p only if g is nearest to some point
   // within a cell radius (<= 0.25 / sqrt7^r rad) of p; moving p by dt changes a
   // squared chord distance by <= 2 sin(t) dt, so d_g(p) - d_best(p) < 0.9 / sqrt7^r
@@ -1325,12 +1413,7 @@ int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys,
         }
         // a cell reached twice (two lattice positions around a pentagon map to one id):
         // its chip is computed from the id, so the copies are equal -- keep the first
-        std::unordered_set<int64_t> seen;
-        std::vector<Chip> uniq;
-        uniq.reserve(per[p].size());
-        for (auto& ch : per[p])
-          if (seen.insert(ch.cell).second) uniq.push_back(std::move(ch));
-        per[p].swap(uniq);
+        // (below, after the sort)
       } else {
         BngGrid g(res);
         std::vector<std::vector<Pt>> lat_rings;
@@ -1343,6 +1426,12 @@ int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys,
         tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, rule, chip_geometry,
                            gstats[p], per[p], pund[p]);
       }
+      // the polygon's rows in cell order (stable: a repeated id keeps its first chip) -- the
+      // output does not depend on which cells the walk classified as interior or border
+      // (the chip-table blob keeps input rows, so the order is part of its bytes)
+      std::stable_sort(per[p].begin(), per[p].end(), [](const Chip& a, const Chip& b) { return a.cell < b.cell; });
+      per[p].erase(std::unique(per[p].begin(), per[p].end(), [](const Chip& a, const Chip& b) { return a.cell == b.cell; }),
+                   per[p].end());
       if (rule) pstats[p] = rule->st;
     }
   });

@@ -221,6 +221,12 @@ inline void write_polygon_body(Writer& w, const Polygon& p) {
 
 // Polygon when one part, MultiPolygon otherwise (big-endian, 2-D)
 inline void write_polygons(std::vector<uint8_t>& out, const std::vector<Polygon>& parts) {
+  size_t n = parts.size() == 1 ? 5 : 9 + 5 * parts.size();
+  for (const Polygon& p : parts) {
+    n += 4;
+    for (const Ring& r : p) n += 4 + 8 * r.size();
+  }
+  out.reserve(out.size() + n);
   Writer w{out};
   if (parts.size() == 1) {
     w.u8(0);
@@ -235,6 +241,64 @@ inline void write_polygons(std::vector<uint8_t>& out, const std::vector<Polygon>
     w.u8(0);
     w.u32(3);
     write_polygon_body(w, p);
+  }
+}
+
+// write_polygons from point rings (q.x, q.y; closed) without the flat copies: parts[k]
+// a polygon's rings, or, with RingParts, every ring a polygon of its own; each ring
+// reversed when `rev`.  One resize to the exact size.
+template <bool RingParts, class Parts>
+inline void write_polygons_pts(std::vector<uint8_t>& out, const Parts& parts, bool rev) {
+  const size_t np = parts.size();
+  size_t n = np == 1 ? 5 : 9 + 5 * np;
+  for (const auto& p : parts) {
+    if constexpr (RingParts) {
+      n += 8 + 16 * p.size();
+    } else {
+      n += 4;
+      for (const auto& r : p) n += 4 + 16 * r.size();
+    }
+  }
+  const size_t o0 = out.size();
+  out.resize(o0 + n);
+  uint8_t* w = out.data() + o0;
+  auto u8 = [&](uint8_t v) { *w++ = v; };
+  auto u32 = [&](uint32_t v) {
+    for (int i = 3; i >= 0; i--) *w++ = (uint8_t)(v >> (8 * i));
+  };
+  auto f64 = [&](double d) {
+    uint64_t v;
+    memcpy(&v, &d, 8);
+    for (int i = 7; i >= 0; i--) *w++ = (uint8_t)(v >> (8 * i));
+  };
+  auto ring = [&](const auto& r) {
+    u32((uint32_t)r.size());
+    if (!rev)
+      for (const auto& q : r) f64(q.x), f64(q.y);
+    else
+      for (size_t k = r.size(); k-- > 0;) f64(r[k].x), f64(r[k].y);
+  };
+  auto polygon = [&](const auto& p) {
+    if constexpr (RingParts) {
+      u32(1);
+      ring(p);
+    } else {
+      u32((uint32_t)p.size());
+      for (const auto& r : p) ring(r);
+    }
+  };
+  u8(0);
+  if (np == 1) {
+    u32(3);
+    polygon(parts[0]);
+    return;
+  }
+  u32(6);
+  u32((uint32_t)np);
+  for (const auto& p : parts) {
+    u8(0);
+    u32(3);
+    polygon(p);
   }
 }
 
