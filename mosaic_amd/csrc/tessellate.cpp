@@ -546,11 +546,14 @@ struct BngGrid : Grid {
   }
 };
 
+// a row; its WKB is bytes [woff, woff + wlen) of its polygon's arena (one allocation per
+// polygon, not per row: 9.4M rows on C3)
 struct Chip {
   int64_t cell;
   int32_t poly;
   uint8_t core;
-  std::vector<uint8_t> wkb;
+  uint32_t wlen;
+  uint64_t woff;
 };
 
 // a row the core rule left undecided (mgpu_tess_result_undecided): kind 1 DP-sensitive,
@@ -919,6 +922,7 @@ bool cell_in_polygon(const std::vector<Pt>& cellb, const std::vector<std::vector
 
 // `lat_rings`: every ring in the grid's lattice space (densified for H3)
 void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<std::vector<Pt>>& lat_rings, int32_t pid,
+                        std::vector<uint8_t>& arena,
                         bool keep_core, CoreRule* rule, int chip_geometry, GeomStats& gs, std::vector<Chip>& out,
                         std::vector<Undecided>& und) {
   // a cell the polygon holds whole: core -- unless mosaicFill's rule (rule != null) puts
@@ -936,17 +940,19 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
     }
     if (v != CoreRule::kCore) {
       rule->st.demoted++;
-      Chip ch{id, pid, 0, {}};
-      write_cell_wkb(rings ? *rings : g.boundary_of(i, j, id), ch.wkb, true);
-      out.push_back(std::move(ch));
+      Chip ch{id, pid, 0, 0, arena.size()};
+      write_cell_wkb(rings ? *rings : g.boundary_of(i, j, id), arena, true);
+      ch.wlen = (uint32_t)(arena.size() - ch.woff);
+      out.push_back(ch);
       return;
     }
-    Chip ch{id, pid, 1, {}};
+    Chip ch{id, pid, 1, 0, arena.size()};
     if (keep_core) {
       const auto rs = rings ? *rings : g.boundary_of(i, j, id);
-      write_cell_wkb(rs, ch.wkb, g.cw_ring(id));
+      write_cell_wkb(rs, arena, g.cw_ring(id));
+      ch.wlen = (uint32_t)(arena.size() - ch.woff);
     }
-    out.push_back(std::move(ch));
+    out.push_back(ch);
   };
   // 2. border cells: walk every edge in lattice space; per cell the smallest distance
   // from its centre to a walked sample (samples <= 0.2 apart)
@@ -1165,15 +1171,17 @@ void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<st
       }
       if (v == CoreRule::kCore) {
         rule->st.promoted++;
-        Chip ch{cid, pid, 1, {}};
-        if (keep_core) write_cell_wkb(rings, ch.wkb, g.cw_ring(cid));
-        out.push_back(std::move(ch));
+        Chip ch{cid, pid, 1, 0, arena.size()};
+        if (keep_core) write_cell_wkb(rings, arena, g.cw_ring(cid));
+        ch.wlen = (uint32_t)(arena.size() - ch.woff);
+        out.push_back(ch);
         continue;
       }
     }
-    Chip ch{cid, pid, 0, {}};
-    write_chip(ch.wkb);
-    out.push_back(std::move(ch));
+    Chip ch{cid, pid, 0, 0, arena.size()};
+    write_chip(arena);
+    ch.wlen = (uint32_t)(arena.size() - ch.woff);
+    out.push_back(ch);
   }
 }
 
@@ -1249,6 +1257,8 @@ bool h3_faces(const Polygon& poly, int res, std::vector<std::vector<Pt>>& dense,
 
 struct mgpu_tess {
   std::vector<Chip> chips;
+  std::vector<uint32_t> chip_arena;          // chips[i]'s polygon (its arena)
+  std::vector<std::vector<uint8_t>> arenas;  // per polygon
   CoreStats core_stats;
   GeomStats geom_stats;
   std::vector<Undecided> undecided;
@@ -1337,6 +1347,7 @@ int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys,
   // polygons are independent: tessellate them in parallel into per-polygon chip lists,
   // then concatenate in input order (the output does not depend on the schedule)
   std::vector<std::vector<Chip>> per(n_polys);
+  std::vector<std::vector<uint8_t>> arena(n_polys);
   std::vector<uint8_t> bad_poly(n_polys, 0);
   std::vector<CoreStats> pstats(n_polys);
   std::vector<GeomStats> gstats(n_polys);
@@ -1408,7 +1419,7 @@ int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys,
             for (auto& q : r) lr.push_back(g.to_lattice(q));
             lat_rings.push_back(std::move(lr));
           }
-          tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, rule, chip_geometry,
+          tessellate_polygon(g, poly, lat_rings, polygon_id[p], arena[p], keep_core_geometries != 0, rule, chip_geometry,
                              gstats[p], per[p], pund[p]);
         }
         // a cell reached twice (two lattice positions around a pentagon map to one id):
@@ -1423,7 +1434,7 @@ int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys,
             for (auto& q : ring) lr.push_back(g.to_lattice(q));
             lat_rings.push_back(std::move(lr));
           }
-        tessellate_polygon(g, poly, lat_rings, polygon_id[p], keep_core_geometries != 0, rule, chip_geometry,
+        tessellate_polygon(g, poly, lat_rings, polygon_id[p], arena[p], keep_core_geometries != 0, rule, chip_geometry,
                            gstats[p], per[p], pund[p]);
       }
       // the polygon's rows in cell order (stable: a repeated id keeps its first chip) -- the
@@ -1472,10 +1483,13 @@ int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys,
   size_t total = 0;
   for (auto& v : per) total += v.size();
   t->chips.reserve(total);
-  for (auto& v : per) {
-    for (auto& c : v) t->chips.push_back(std::move(c));
-    std::vector<Chip>().swap(v);
+  t->chip_arena.reserve(total);
+  for (int64_t p = 0; p < n_polys; p++) {
+    t->chips.insert(t->chips.end(), per[p].begin(), per[p].end());
+    t->chip_arena.insert(t->chip_arena.end(), per[p].size(), (uint32_t)p);
+    std::vector<Chip>().swap(per[p]);
   }
+  t->arenas.swap(arena);
   *out = t;
   return MGPU_OK;
 }
@@ -1483,7 +1497,7 @@ int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys,
 int32_t mgpu_tess_result_sizes(const mgpu_tess* t, int64_t* n_chips, int64_t* wkb_bytes) {
   if (!t) return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellation result is NULL");
   int64_t b = 0;
-  for (auto& c : t->chips) b += (int64_t)c.wkb.size();
+  for (auto& c : t->chips) b += (int64_t)c.wlen;
   if (n_chips) *n_chips = (int64_t)t->chips.size();
   if (wkb_bytes) *wkb_bytes = b;
   return MGPU_OK;
@@ -1492,17 +1506,23 @@ int32_t mgpu_tess_result_sizes(const mgpu_tess* t, int64_t* n_chips, int64_t* wk
 int32_t mgpu_tess_result_copy(const mgpu_tess* t, int64_t* cell, int32_t* polygon_id, uint8_t* is_core,
                               int64_t* wkb_offsets, uint8_t* wkb) {
   if (!t) return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellation result is NULL");
+  const int64_t n = (int64_t)t->chips.size();
   int64_t off = 0;
-  for (size_t i = 0; i < t->chips.size(); i++) {
-    const Chip& c = t->chips[i];
-    cell[i] = c.cell;
-    polygon_id[i] = c.poly;
-    is_core[i] = c.core;
+  for (int64_t i = 0; i < n; i++) {
     wkb_offsets[i] = off;
-    if (!c.wkb.empty()) memcpy(wkb + off, c.wkb.data(), c.wkb.size());
-    off += (int64_t)c.wkb.size();
+    off += (int64_t)t->chips[i].wlen;
   }
-  wkb_offsets[t->chips.size()] = off;
+  wkb_offsets[n] = off;
+  // (the columns and the bytes in parallel: first-touch of the caller's fresh pages too)
+  mgpu::parallel_for(n, 1 << 15, [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; i++) {
+      const Chip& c = t->chips[i];
+      cell[i] = c.cell;
+      polygon_id[i] = c.poly;
+      is_core[i] = c.core;
+      if (c.wlen) memcpy(wkb + wkb_offsets[i], t->arenas[t->chip_arena[i]].data() + c.woff, c.wlen);
+    }
+  });
   return MGPU_OK;
 }
 
