@@ -366,7 +366,7 @@ struct Grid {
                            long* j1) const = 0;
 };
 
-struct H3Grid : Grid {
+struct H3Grid final : Grid {
   int face, res;
   // a lattice position inside the face triangle's inscribed circle (radius 1 in res-0
   // units; the vertices, where the pentagons sit, lie at 2), with a margin: no overage and
@@ -504,7 +504,7 @@ struct H3Grid : Grid {
   }
 };
 
-struct BngGrid : Grid {
+struct BngGrid final : Grid {
   int res;
   double edge;
   // edge sizes of BNGIndexSystem.sizeMap: 10^(6-r) m, quadrant resolutions 10^(7-|r|) / 2 m
@@ -719,11 +719,16 @@ struct CoreRule {
     }
     return o;
   }
+  // a centre decided core by its exact distance (>= 1.05 r deep): a point of buffer(-r)
+  bool have_deep = false;
+  mgpu::jtsbuf::XY deep{};
   void ensure_carved() {
     if (carved_state) return;
     mgpu::jtsbuf::carved_field(parts(), r, carved);
     carved.build_index(r);
-    carved_state = carved.any_positive(1e-7 * r) ? 1 : 2;
+    // non-empty when a known deep centre lies in it (the usual case: interior cells come
+    // first), else the probe of every curve segment's sides
+    carved_state = (have_deep && carved.depth(deep) >= 1) || carved.any_positive(1e-7 * r) ? 1 : 2;
     if (carved_state == 2) st.carved_empty++;
   }
   void ensure_band() {
@@ -754,6 +759,7 @@ struct CoreRule {
     bool core;
     if (d >= 1.05 * r) {
       core = true;
+      if (!have_deep) have_deep = true, deep = p;
     } else if (d < 0.97 * r) {
       core = false;
     } else {
@@ -921,7 +927,9 @@ bool cell_in_polygon(const std::vector<Pt>& cellb, const std::vector<std::vector
 }
 
 // `lat_rings`: every ring in the grid's lattice space (densified for H3)
-void tessellate_polygon(const Grid& g, const Polygon& poly, const std::vector<std::vector<Pt>>& lat_rings, int32_t pid,
+// (G: H3Grid or BngGrid -- final, so the per-sample calls bind statically)
+template <class G>
+void tessellate_polygon(const G& g, const Polygon& poly, const std::vector<std::vector<Pt>>& lat_rings, int32_t pid,
                         std::vector<uint8_t>& arena,
                         bool keep_core, CoreRule* rule, int chip_geometry, GeomStats& gs, std::vector<Chip>& out,
                         std::vector<Undecided>& und) {
