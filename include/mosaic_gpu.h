@@ -478,6 +478,8 @@ int32_t mgpu_tess_result_copy(const mgpu_tess* t, int64_t* cell, int32_t* polygo
  * one the table holds, or the one a dropped row would carry -- to count the pairs at stake. */
 int32_t mgpu_tess_result_undecided(const mgpu_tess* t, int64_t* n, int64_t* wkb_bytes, int64_t* cell, int32_t* poly,
                                    uint8_t* kind_kept_core, int64_t* wkb_offsets, uint8_t* wkb);
+/* frees the result (its memory returns on a helper thread, joined by the next
+ * mgpu_tessellate* call and at unload: at most one result is in release at a time) */
 int32_t mgpu_tess_destroy(mgpu_tess* t);
 
 /* TEST ONLY -- not an interface of the reference.  Builds the chip table on the host

@@ -451,6 +451,11 @@ struct Clipper {
   std::vector<const std::vector<P>*> sub_rings;
   std::vector<int8_t> rloc;
   std::vector<int> rcross;
+  // (the result-ring stage's scratch, reused across calls)
+  std::vector<std::pair<int, int>> res;
+  std::vector<uint8_t> touched;
+  std::vector<int> rs_start, rs_list, rs_fill, shells, holes;
+  std::vector<double> rarea;
 
   void build(const std::vector<std::vector<std::vector<P>>>& parts, const std::vector<uint8_t>& ring_ccw,
              const std::vector<std::vector<P>>& cell, std::vector<Rings>& pieces, bool* lower_dim,
@@ -717,11 +722,11 @@ struct Clipper {
     }
     // isolated touching points: a node on both boundaries with no result edge
     // 6. result edges directed with the result interior on their right (shells clockwise)
-    std::vector<std::pair<int, int>> res;  // (from, to) node ids
+    res.clear();  // (from, to) node ids
     for (auto& e : o.edges)
       if (e.in_result) res.push_back(e.res_left ? std::make_pair(e.v, e.u) : std::make_pair(e.u, e.v));
     {
-      std::vector<uint8_t> touched(nn, 0);
+      touched.assign(nn, 0);
       for (auto& r : res) touched[r.first] = touched[r.second] = 1;
       for (int q = 0; q < nn; q++)
         if (o.on_geom[q] == 3 && !touched[q]) o.lower_dim = true;
@@ -731,12 +736,13 @@ struct Clipper {
     // 7. minimal rings: at each node leave by the first out-edge counter-clockwise from the
     // reversed incoming direction (the face on the right)
     const int nr = (int)res.size();
-    std::vector<int> rs_start(nn + 1, 0), rs_list(nr);
+    rs_start.assign(nn + 1, 0);
+    rs_list.assign(nr, 0);
     for (auto& r : res) rs_start[r.first + 1]++;
     for (int q = 0; q < nn; q++) rs_start[q + 1] += rs_start[q];
     {
-      std::vector<int> fill(rs_start.begin(), rs_start.end() - 1);
-      for (int k = 0; k < nr; k++) rs_list[fill[res[k].first]++] = k;
+      rs_fill.assign(rs_start.begin(), rs_start.end() - 1);
+      for (int k = 0; k < nr; k++) rs_list[rs_fill[res[k].first]++] = k;
     }
     used.assign(nr, 0);
     std::vector<std::vector<P>> rings;
@@ -784,8 +790,10 @@ struct Clipper {
       rings.push_back(std::move(ring));
     }
     // 8. shells (clockwise) and holes (ccw); each hole to the smallest shell holding it
-    std::vector<int> shells, holes;
-    std::vector<double> area(rings.size());
+    shells.clear();
+    holes.clear();
+    std::vector<double>& area = rarea;
+    area.assign(rings.size(), 0.0);
     // (OverlayEdgeRing: a ring is a hole iff Orientation.isCCW)
     for (size_t i = 0; i < rings.size(); i++) {
       area[i] = std::fabs(signed_area(rings[i]));

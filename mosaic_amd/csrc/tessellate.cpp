@@ -44,6 +44,8 @@
 #include <cstring>
 #include <set>
 #include <string>
+#include <mutex>
+#include <thread>
 #include <unordered_set>
 #include <vector>
 
@@ -645,14 +647,26 @@ struct SegIndex {
     t = std::min(1.0, std::max(0.0, t));
     return std::hypot(u.x + t * dx - p.x, u.y + t * dy - p.y);
   }
-  // distance from p to the nearest boundary segment, or INFINITY when none is within q
+  // distance from p to the nearest boundary segment, or INFINITY when none is within q.
+  // (seg_dist's hypot only for a segment whose squared distance is within 1e-9 of the
+  // smallest so far: the segment with the least hypot is always among them -- both round
+  // within a few ulps of the exact distance -- so the minimum is seg_dist's, bit for bit)
   double min_dist(Pt p, double q) const {
     if (a.empty()) return INFINITY;
-    double best = INFINITY;
+    double best = INFINITY, best2 = INFINITY;
     for (long j = row(p.y - q); j <= row(p.y + q); j++)
       for (long i = col(p.x - q); i <= col(p.x + q); i++) {
         const size_t c = (size_t)(j * nx + i);
-        for (uint32_t k = start[c]; k < start[c + 1]; k++) best = std::min(best, seg_dist(p, a[items[k]], b[items[k]]));
+        for (uint32_t k = start[c]; k < start[c + 1]; k++) {
+          const Pt u = a[items[k]], v = b[items[k]];
+          const double dx = v.x - u.x, dy = v.y - u.y, l2 = dx * dx + dy * dy;
+          double t = l2 > 0 ? ((p.x - u.x) * dx + (p.y - u.y) * dy) / l2 : 0.0;
+          t = std::min(1.0, std::max(0.0, t));
+          const double ex = u.x + t * dx - p.x, ey = u.y + t * dy - p.y, d2 = ex * ex + ey * ey;
+          if (d2 > best2 * (1.0 + 1e-9)) continue;
+          best = std::min(best, std::hypot(ex, ey));
+          best2 = std::min(best2, d2);
+        }
       }
     return best <= q ? best : INFINITY;
   }
@@ -1263,6 +1277,18 @@ bool h3_faces(const Polygon& poly, int res, std::vector<std::vector<Pt>>& dense,
 
 }  // namespace
 
+// the previous result's release (mgpu_tess_destroy)
+struct TessRelease {
+  std::mutex mu;
+  std::thread th;
+  void join() {
+    std::lock_guard<std::mutex> g(mu);
+    if (th.joinable()) th.join();
+  }
+  ~TessRelease() { join(); }
+};
+static TessRelease g_tess_release;
+
 struct mgpu_tess {
   std::vector<Chip> chips;
   std::vector<uint32_t> chip_arena;          // chips[i]'s polygon (its arena)
@@ -1340,6 +1366,7 @@ int32_t mgpu_tessellate_geom(int32_t index_system, int32_t res, int64_t n_polys,
                              const double* xy, const uint8_t* poly_type, int32_t keep_core_geometries,
                              int32_t core_rule, int32_t chip_geometry, mgpu_tess** out) {
   if (!out || n_polys < 0) return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellate: bad arguments");
+  g_tess_release.join();  // (the previous result's memory back before this one allocates)
   if (chip_geometry != MGPU_CHIPS_OVERLAY && chip_geometry != MGPU_CHIPS_SUTHERLAND_HODGMAN)
     return mgpu::set_error(MGPU_E_INVALID_ARG, "tessellate: unknown chip geometry %d", chip_geometry);
   for (int64_t p = 0; poly_type && p < n_polys; p++)
@@ -1584,7 +1611,16 @@ int32_t mgpu_tess_result_undecided(const mgpu_tess* t, int64_t* n, int64_t* wkb_
 }
 
 int32_t mgpu_tess_destroy(mgpu_tess* t) {
-  delete t;
+  if (!t) return MGPU_OK;
+  // (9.4M rows on C3: 0.2 s of page returns -- handed to a helper thread, joined by the
+  // next tessellation and at exit, so at most one result is being freed at a time)
+  std::lock_guard<std::mutex> g(g_tess_release.mu);
+  if (g_tess_release.th.joinable()) g_tess_release.th.join();
+  try {
+    g_tess_release.th = std::thread([t] { delete t; });
+  } catch (...) {
+    delete t;
+  }
   return MGPU_OK;
 }
 
