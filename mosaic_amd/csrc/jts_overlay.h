@@ -214,6 +214,7 @@ struct Overlay {
     int geom;     // 0 = subject, 1 = cell
     int ring;     // ring id within its geometry (subject: global ring index)
     bool int_left;  // the geometry's interior lies left of a -> b
+    int k = 0;      // the segment's index in its ring
   };
   struct Edge {  // a noded sub-edge
     int u, v;      // node ids
@@ -453,9 +454,163 @@ struct Clipper {
   std::vector<int> rcross;
   // (the result-ring stage's scratch, reused across calls)
   std::vector<std::pair<int, int>> res;
+  std::vector<P> tmp_chain, tmp_cycle, tmp_sorted;
   std::vector<uint8_t> touched;
   std::vector<int> rs_start, rs_list, rs_fill, shells, holes;
   std::vector<double> rarea;
+
+  // the one-chain shortcut below (off: always the general noded graph)
+  bool fast = true;
+
+  // The commonest border cell: one ring of the subject crosses the cell's one ring twice,
+  // both proper crossings (interiors of both segments, points off every endpoint), and the
+  // subject's segments between them -- the same ring, in ring order -- are the only ones
+  // inside.  The general graph below then labels exactly those subject edges and the cell
+  // arc on the interior's side, and walks one ring: here it is written down directly, in
+  // the order and from the node the graph's walk starts at (the first result edge in edge
+  // order).  False (nothing written) when the configuration is anything else.
+  bool one_crossing_chain(const std::vector<std::vector<std::vector<P>>>& parts, const std::vector<std::vector<P>>& cell,
+                          std::vector<Rings>& pieces) {
+    const int n_sub = (int)o.segs.size() - [&] {
+      int c = 0;
+      for (auto& sg : o.segs) c += sg.geom == 1;
+      return c;
+    }();
+    // the two crossings: (subject seg, cell seg, point), in seg_nodes order
+    const int s0 = o.seg_nodes[0].first, c0 = o.seg_nodes[1].first, s1 = o.seg_nodes[2].first, c1 = o.seg_nodes[3].first;
+    const P h0 = o.seg_nodes[0].second, h1 = o.seg_nodes[2].second;
+    if (eq(h0, h1)) return false;
+    for (int q = 0; q < 2; q++) {
+      const P h = q ? h1 : h0;
+      const Overlay::Seg &ss = o.segs[q ? s1 : s0], &cs = o.segs[q ? c1 : c0];
+      if (eq(h, ss.a) || eq(h, ss.b) || eq(h, cs.a) || eq(h, cs.b)) return false;
+    }
+    const std::vector<P>& cr = cell[0];
+    const int ring = o.segs[s0].ring;
+    if (o.segs[s1].ring != ring) return false;
+    const std::vector<P>& R = *sub_rings[ring];
+    const int nr = (int)R.size() - 1;  // segments of the ring
+    // locations of the subject segs' start points (no crossing: the whole seg is there)
+    int entry = -1, exit_ = -1;  // subject seg indices in o.segs
+    P in_pt{}, out_pt{};
+    int in_cell = -1, out_cell = -1;
+    int n_inside = 0;
+    for (int i = 0; i < n_sub; i++) {
+      const int l = locate_in_ring(o.segs[i].a, cr);
+      if (l == 0) return false;
+      const bool a_in = l > 0;
+      const bool hit0 = i == s0, hit1 = i == s1;
+      if (hit0 && hit1) {  // both crossings on one seg: it enters and leaves
+        if (a_in) return false;
+        // the first along the seg enters
+        const int oc = octant(o.segs[i].b.x - o.segs[i].a.x, o.segs[i].b.y - o.segs[i].a.y);
+        const bool first0 = seg_compare(oc, h0, h1) < 0;
+        entry = exit_ = i;
+        in_pt = first0 ? h0 : h1, in_cell = first0 ? c0 : c1;
+        out_pt = first0 ? h1 : h0, out_cell = first0 ? c1 : c0;
+      } else if (hit0 || hit1) {
+        const P h = hit0 ? h0 : h1;
+        const int c = hit0 ? c0 : c1;
+        if (!a_in) {
+          if (entry >= 0) return false;
+          entry = i, in_pt = h, in_cell = c;
+        } else {
+          if (exit_ >= 0) return false;
+          exit_ = i, out_pt = h, out_cell = c;
+        }
+      } else if (a_in) {
+        if (o.segs[i].ring != ring) return false;
+        n_inside++;
+      }
+    }
+    if (entry < 0 || exit_ < 0) return false;
+    const int ke = o.segs[entry].k, kx = o.segs[exit_].k;
+    // the chain: entry's end, the ring's vertices up to exit's start (degenerate segments
+    // skipped, as the graph's segments are); every seg strictly between is inside
+    std::vector<P>& chain = tmp_chain;
+    chain.clear();
+    chain.push_back(in_pt);
+    int n_between = 0;
+    if (entry != exit_) {
+      for (int k = (ke + 1) % nr;; k = (k + 1) % nr) {
+        if (!eq(R[k], chain.back())) chain.push_back(R[k]);
+        if (k == kx) break;
+        if (!eq(R[k], R[k + 1])) n_between++;
+        if ((int)chain.size() > nr + 2) return false;
+      }
+    }
+    if (n_between != n_inside) return false;
+    chain.push_back(out_pt);
+    // the cell side: cell segs are o.segs[n_sub ..], in ring order; the arc clockwise (the
+    // result's interior on the right) from the chain's last point to its first
+    const bool int_left = o.segs[entry].int_left;  // (one ring: one orientation)
+    std::vector<P>& cyc = tmp_cycle;
+    cyc.clear();
+    P first = chain.front(), last = chain.back();
+    int c_first = in_cell, c_last = out_cell;
+    if (int_left) {  // result direction: the chain reversed
+      std::reverse(chain.begin(), chain.end());
+      std::swap(first, last);
+      std::swap(c_first, c_last);
+    }
+    for (auto& q : chain) cyc.push_back(q);
+    const int nc = (int)o.segs.size() - n_sub;
+    const int jl = c_last - n_sub, jf = c_first - n_sub;
+    bool direct = false;  // both on one cell seg with `first` before `last` clockwise
+    if (jl == jf) {
+      const Overlay::Seg& cs = o.segs[c_last];
+      const int oc = octant(cs.b.x - cs.a.x, cs.b.y - cs.a.y);
+      direct = seg_compare(oc, first, last) < 0;  // clockwise = against the seg's direction
+    }
+    if (!direct) {
+      // clockwise from `last`: the start of its seg, then the previous segs' starts, down
+      // to the end of first's seg
+      int j = jl;
+      for (int guard = 0; guard <= nc; guard++) {
+        cyc.push_back(o.segs[n_sub + j].a);
+        j = (j + nc - 1) % nc;
+        if (j == jf) break;
+        if (guard == nc) return false;
+      }
+    }
+    if (cyc.size() < 3) return false;
+    // distinct nodes (the graph would merge equal ones)
+    tmp_sorted.assign(cyc.begin(), cyc.end());
+    std::sort(tmp_sorted.begin(), tmp_sorted.end(), [](P a, P b) { return less(a, b); });
+    for (size_t q = 1; q < tmp_sorted.size(); q++)
+      if (eq(tmp_sorted[q], tmp_sorted[q - 1])) return false;
+    // the walk starts at the first result edge in edge order: the subject edges come first,
+    // by seg (o.segs order), each seg's sub-edges along it; a result edge runs (v, u) when
+    // the interior is left of the subject direction, so it starts at the sub-edge's end
+    int first_seg = entry;
+    if (exit_ < first_seg) first_seg = exit_;
+    for (int i = 0; i < n_sub; i++)
+      if (i < first_seg && o.segs[i].ring == ring && locate_in_ring(o.segs[i].a, cr) > 0) {
+        first_seg = i;
+        break;
+      }
+    P u, v;  // the first inside sub-edge of first_seg, in subject direction
+    if (first_seg == entry && entry == exit_) u = in_pt, v = out_pt;
+    else if (first_seg == entry) u = in_pt, v = o.segs[entry].b;
+    else if (first_seg == exit_) u = o.segs[exit_].a, v = out_pt;
+    else u = o.segs[first_seg].a, v = o.segs[first_seg].b;
+    const P start = int_left ? v : u;
+    size_t s0i = cyc.size();
+    for (size_t q = 0; q < cyc.size(); q++)
+      if (eq(cyc[q], start)) {
+        s0i = q;
+        break;
+      }
+    if (s0i == cyc.size()) return false;
+    std::vector<P> out;
+    out.reserve(cyc.size() + 1);
+    for (size_t q = 0; q < cyc.size(); q++) out.push_back(cyc[(s0i + q) % cyc.size()]);
+    out.push_back(out[0]);
+    if (is_ccw(out)) return false;  // (the graph would call it a hole)
+    pieces.clear();
+    pieces.push_back(Rings{std::move(out)});
+    return true;
+  }
 
   void build(const std::vector<std::vector<std::vector<P>>>& parts, const std::vector<uint8_t>& ring_ccw,
              const std::vector<std::vector<P>>& cell, std::vector<Rings>& pieces, bool* lower_dim,
@@ -486,7 +641,7 @@ struct Clipper {
       if (eq(a, b)) return;
       if (std::max(a.x, b.x) < cx0 || std::min(a.x, b.x) > cx1 || std::max(a.y, b.y) < cy0 || std::min(a.y, b.y) > cy1)
         return;
-      o.segs.push_back({a, b, 0, rid, (o.ring_hole[rid] == 0) == (bool)ring_ccw[rid]});
+      o.segs.push_back({a, b, 0, rid, (o.ring_hole[rid] == 0) == (bool)ring_ccw[rid], (int)k});
     };
     if (grid) {
       for (uint64_t c : grid->query(cx0, cy0, cx1, cy1)) add_seg((int)(c >> 32), (size_t)(c & 0xFFFFFFFFu));
@@ -497,17 +652,23 @@ struct Clipper {
     const size_t n_sub = o.segs.size();
     for (size_t ci = 0; ci < cell.size(); ci++)
       for (size_t k = 0; k + 1 < cell[ci].size(); k++)
-        if (!eq(cell[ci][k], cell[ci][k + 1])) o.segs.push_back({cell[ci][k], cell[ci][k + 1], 1, (int)ci, true});
+        if (!eq(cell[ci][k], cell[ci][k + 1])) o.segs.push_back({cell[ci][k], cell[ci][k + 1], 1, (int)ci, true, (int)k});
     // 2. noding: every subject segment against every cell segment (IntersectionAdder)
     o.seg_nodes.clear();
+    bool all_proper = true;
     for (size_t i = 0; i < n_sub; i++)
       for (size_t j = n_sub; j < o.segs.size(); j++) {
         const Hit h = line_intersect(o.segs[i].a, o.segs[i].b, o.segs[j].a, o.segs[j].b);
+        if (h.n && (h.n != 1 || !h.proper)) all_proper = false;
         for (int q = 0; q < h.n; q++) {
           o.seg_nodes.push_back({(int)i, h.pt[q]});
           o.seg_nodes.push_back({(int)j, h.pt[q]});
         }
       }
+    if (fast && all_proper && cell.size() == 1 && o.seg_nodes.size() == 4 && one_crossing_chain(parts, cell, pieces)) {
+      *lower_dim = false;
+      return;
+    }
     // 3. sub-edges between consecutive nodes along each segment (nodes by segment, then
     // in SegmentPointComparator order along it)
     std::sort(o.seg_nodes.begin(), o.seg_nodes.end(), [&](const std::pair<int, P>& u, const std::pair<int, P>& v) {
