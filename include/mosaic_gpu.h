@@ -491,6 +491,12 @@ int32_t mgpu_test_chip_contains_host(int32_t index_system, int64_t n_chips, cons
                                      const uint8_t* wkb, int64_t n, const int64_t* chip_row, const double* x,
                                      const double* y, int8_t* out_join_path, int8_t* out_point_locator);
 
+/* TEST ONLY -- while on, every border chip the overlay's one-crossing-chain shortcut cuts
+ * (jts_overlay.h Clipper::one_crossing_chain) is cut again by the general noded graph and
+ * the two compared; out2 = {cells so checked, cells that differed} since it was turned on
+ * (on = 1 resets the counts; on = 0 reads them and stops). */
+int32_t mgpu_test_overlay_verify(int32_t on, int64_t* out2);
+
 /* TEST ONLY -- the decimal parser of the WKT path (Double.parseDouble semantics) on one
  * string: characters consumed (0: not a number) and the value.  Host only. */
 int32_t mgpu_test_parse_number(const char* s, int32_t len, double* out);

@@ -43,6 +43,7 @@ EXPORTS = (
     "mgpu_ctx_set_option", "mgpu_ctx_get_option", "mgpu_build_opts_default", "mgpu_chips_host_blob_ex",
     "mgpu_test_h3_glibc_host", "mgpu_internal_geometry_to_cells", "mgpu_test_internal_centroid", "mgpu_test_join_counters",
     "mgpu_test_receive_blob", "mgpu_ring_join", "mgpu_ring_join_ex", "mgpu_ring_join_final",
+    "mgpu_test_overlay_verify",
 )
 MGPU_GEOM_WKB = 0
 MGPU_GEOM_WKT = 1
@@ -173,6 +174,7 @@ def lib():
         "mgpu_test_h3_elementary_host": (I32, [I32, P, P, I64, P]),
         "mgpu_test_h3_route_host": (I32, [P, P, I64, I32, P]),
         "mgpu_test_h3_boundary_host": (I32, [P, I64, P, P, P]),
+        "mgpu_test_overlay_verify": (I32, [ctypes.c_int32, P]),
         "mgpu_test_h3_cell_wkb_host": (I32, [I64, P, I64, P]),
         "mgpu_ctx_set_option": (I32, [P, ctypes.c_char_p, I64]),
         "mgpu_ctx_get_option": (I32, [P, ctypes.c_char_p, ctypes.POINTER(I64)]),

@@ -37,6 +37,7 @@
 // the pieces (disjoint pieces: no new node).
 #pragma once
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <vector>
@@ -434,6 +435,14 @@ struct SegGrid {
 // The result of one overlay: pieces (rings; ring 0 = shell, clockwise; holes ccw)
 using Rings = std::vector<std::vector<P>>;
 
+// test hook (mgpu_test_overlay_verify): when on, every cell the one-chain shortcut answers
+// is also run through the general graph and the two results compared
+struct OverlayVerify {
+  std::atomic<bool> on{false};
+  std::atomic<int64_t> shortcut{0}, differ{0};
+};
+inline OverlayVerify g_overlay_verify;
+
 // polygon (parts of closed rings) INTERSECTION cell (closed ccw rings), as OverlayNG
 // (header).  `whole_subject_rings[r]` must hold every subject ring (for point location);
 // ring_ccw[r] its orientation.  Returns the pieces; *lower_dim when the overlay also
@@ -667,6 +676,23 @@ struct Clipper {
       }
     if (fast && all_proper && cell.size() == 1 && o.seg_nodes.size() == 4 && one_crossing_chain(parts, cell, pieces)) {
       *lower_dim = false;
+      if (g_overlay_verify.on.load(std::memory_order_relaxed)) {
+        g_overlay_verify.shortcut++;
+        std::vector<Rings> gp;
+        bool gl = false;
+        fast = false;
+        build(parts, ring_ccw, cell, gp, &gl, grid);
+        fast = true;
+        bool same = !gl && gp.size() == pieces.size();
+        for (size_t a = 0; same && a < gp.size(); a++) {
+          same = gp[a].size() == pieces[a].size();
+          for (size_t r = 0; same && r < gp[a].size(); r++) {
+            same = gp[a][r].size() == pieces[a][r].size();
+            for (size_t q = 0; same && q < gp[a][r].size(); q++) same = eq(gp[a][r][q], pieces[a][r][q]);
+          }
+        }
+        if (!same) g_overlay_verify.differ++;
+      }
       return;
     }
     // 3. sub-edges between consecutive nodes along each segment (nodes by segment, then

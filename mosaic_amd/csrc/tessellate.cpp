@@ -1624,6 +1624,14 @@ int32_t mgpu_tess_destroy(mgpu_tess* t) {
   return MGPU_OK;
 }
 
+int32_t mgpu_test_overlay_verify(int32_t on, int64_t* out2) {
+  auto& v = mgpu::ovl::g_overlay_verify;
+  if (out2) out2[0] = v.shortcut.load(), out2[1] = v.differ.load();
+  if (on) v.shortcut = 0, v.differ = 0;
+  v.on = on != 0;
+  return MGPU_OK;
+}
+
 int32_t mgpu_test_h3_boundary_host(const int64_t* cells, int64_t n, double* out_lonlat, int32_t* out_nverts,
                                    double* out_center) {
   for (int64_t i = 0; i < n; i++) {

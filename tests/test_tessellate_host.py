@@ -777,3 +777,22 @@ def test_rows_in_cell_order_and_order_free_checksum(nyc_zones, nyc_chips_r9):
         h.update(np.int64(c.cell[i]).tobytes() + np.int32(pid[i]).tobytes() + np.uint8(c.is_core[i]).tobytes())
         h.update(c.wkb[c.wkb_offsets[i]:c.wkb_offsets[i + 1]].tobytes())
     assert (len(c), h.hexdigest()[:16]) == (11889, "9fe363c45cbaf510")
+
+
+@pytest.mark.parametrize("case", ["nyc_r9", "nyc_r10", "bng_r4"])
+def test_overlay_chain_shortcut_equals_general_graph(nyc_zones, case):
+    """The overlay's one-crossing-chain shortcut (jts_overlay.h Clipper::one_crossing_chain:
+    most border cells) writes the chip the general noded graph would: with the test hook on,
+    every cell it answers is cut again by the graph and compared vertex for vertex."""
+    import bench_workloads as W
+    L = _native.lib()
+    cnt = np.zeros(2, np.int64)
+    _native.check(L.mgpu_test_overlay_verify(1, cnt.ctypes.data))
+    try:
+        if case == "bng_r4":
+            M.tessellate(W.london_districts(), M.BNGIndexSystem(), 4)
+        else:
+            M.tessellate(nyc_zones, M.H3IndexSystem(), 9 if case == "nyc_r9" else 10)
+    finally:
+        _native.check(L.mgpu_test_overlay_verify(0, cnt.ctypes.data))
+    assert cnt[0] > 1000 and cnt[1] == 0, cnt
