@@ -300,8 +300,20 @@ struct LatLon {
   double lat, lon;  // radians
 };
 
-// h3ToGeoBoundary (radians, H3's vertex order, not closed)
-inline std::vector<LatLon> cell_boundary(uint64_t h) {
+// a substrate vertex's position: hex2d_to_geo of its hex2d point (a pure function of the
+// face, the normalized ijk and the resolution: callers may memoize it)
+struct VertexGeo {
+  LatLon operator()(const FaceIJK& f, int adj_res) const {
+    LatLon p;
+    hex2d_to_geo(ijk_to_hex2d(f.c), f.face, adj_res, true, &p.lat, &p.lon);
+    return p;
+  }
+};
+
+// h3ToGeoBoundary (radians, H3's vertex order, not closed); `vertex` computes the cell's
+// own substrate vertices (the distortion vertices on icosahedron edges are computed here)
+template <class Vertex = VertexGeo>
+inline std::vector<LatLon> cell_boundary(uint64_t h, const Vertex& vertex = Vertex()) {
   const int res = (int)((h >> 52) & 15);
   const FaceIJK center = h3_to_face_ijk(h);
   std::vector<LatLon> g;
@@ -334,11 +346,7 @@ inline std::vector<LatLon> cell_boundary(uint64_t h) {
         hex2d_to_geo(inter, tmp.face, adj_res, true, &p.lat, &p.lon);
         g.push_back(p);
       }
-      if (vert < 5) {
-        LatLon p;
-        hex2d_to_geo(ijk_to_hex2d(f.c), f.face, adj_res, true, &p.lat, &p.lon);
-        g.push_back(p);
-      }
+      if (vert < 5) g.push_back(vertex(f, adj_res));
       last = f;
     }
     return g;
@@ -364,11 +372,7 @@ inline std::vector<LatLon> cell_boundary(uint64_t h) {
         g.push_back(p);
       }
     }
-    if (vert < 6) {
-      LatLon p;
-      hex2d_to_geo(ijk_to_hex2d(f.c), f.face, adj_res, true, &p.lat, &p.lon);
-      g.push_back(p);
-    }
+    if (vert < 6) g.push_back(vertex(f, adj_res));
     last_face = f.face;
     last_ov = ov;
   }

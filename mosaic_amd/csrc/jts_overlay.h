@@ -321,6 +321,10 @@ struct SegGrid {
   std::vector<uint32_t> start;
   std::vector<uint64_t> items;  // ring << 32 | index
   mutable std::vector<uint64_t> out;
+  // the last query's box while `out` still holds its result (a cell's inside test and its
+  // overlay ask for the same box in a row)
+  mutable double qb[4] = {0, 0, 0, 0};
+  mutable bool q_valid = false;
 
   void build(const std::vector<std::vector<std::vector<P>>>& parts, double cell) {
     double minx = INFINITY, miny = INFINITY, maxx = -INFINITY, maxy = -INFINITY;
@@ -369,7 +373,9 @@ struct SegGrid {
   long row(double y) const { return std::min(std::max((long)std::floor((y - y0) * inv), 0L), ny - 1); }
   // the segments in buckets meeting [bx0, bx1] x [by0, by1], sorted, each once
   const std::vector<uint64_t>& query(double bx0, double by0, double bx1, double by1) const {
+    if (q_valid && qb[0] == bx0 && qb[1] == by0 && qb[2] == bx1 && qb[3] == by1) return out;
     out.clear();
+    q_valid = false;
     if (start.empty()) return out;
     for (long j = row(by0); j <= row(by1); j++)
       for (long i = col(bx0); i <= col(bx1); i++) {
@@ -378,6 +384,8 @@ struct SegGrid {
       }
     std::sort(out.begin(), out.end());
     out.erase(std::unique(out.begin(), out.end()), out.end());
+    qb[0] = bx0, qb[1] = by0, qb[2] = bx1, qb[3] = by1;
+    q_valid = true;
     return out;
   }
   // the segments a rightward ray from (px, py) can meet or (px, py) can lie on: a segment
@@ -385,6 +393,7 @@ struct SegGrid {
   // px's bucket (clamping keeps both monotone) -- sorted, each once
   const std::vector<uint64_t>& ray_right(double px, double py) const {
     out.clear();
+    q_valid = false;
     if (start.empty()) return out;
     const long j = row(py);
     for (long i = col(px); i < nx; i++) {

@@ -294,13 +294,51 @@ std::vector<Pt> pole_cap(const std::vector<Pt>& b, bool north) {
   return r;
 }
 
+// A thread's memo of substrate vertex positions (cell_boundary's VertexGeo: a pure function
+// of face, resolution and normalized ijk).  Neighbouring border cells share most of their
+// vertices; the table is emptied when half full.
+struct VertexCache {
+  struct E {
+    int32_t fr, i, j, k;
+    mgpu::h3b::LatLon v;
+  };
+  std::vector<E> t;
+  size_t n = 0;
+  VertexCache() : t((size_t)1 << 12, E{-1, 0, 0, 0, {}}) {}
+  mgpu::h3b::LatLon get(const mgpu::h3b::FaceIJK& f, int adj_res) {
+    const int32_t fr = f.face * 32 + adj_res;
+    uint64_t h = (uint64_t)(uint32_t)f.c.i * 0x9E3779B97F4A7C15ull ^ (uint64_t)(uint32_t)f.c.j * 0xC2B2AE3D27D4EB4Full ^
+                 (uint64_t)(uint32_t)f.c.k * 0x165667B19E3779F9ull ^ (uint64_t)(uint32_t)fr;
+    h ^= h >> 31;
+    const size_t mask = t.size() - 1;
+    for (size_t q = h & mask;; q = (q + 1) & mask) {
+      E& e = t[q];
+      if (e.fr == fr && e.i == f.c.i && e.j == f.c.j && e.k == f.c.k) return e.v;
+      if (e.fr >= 0) continue;
+      const mgpu::h3b::LatLon v = mgpu::h3b::VertexGeo()(f, adj_res);
+      if (2 * (n + 1) > t.size()) {
+        for (auto& x : t) x.fr = -1;
+        n = 0;
+        return v;
+      }
+      e = E{fr, f.c.i, f.c.j, f.c.k, v};
+      n++;
+      return v;
+    }
+  }
+};
+thread_local VertexCache t_vcache;
+struct CachedVertex {
+  mgpu::h3b::LatLon operator()(const mgpu::h3b::FaceIJK& f, int adj_res) const { return t_vcache.get(f, adj_res); }
+};
+
 // H3IndexSystem.indexToGeometry (H3IndexSystem.scala:103-121): h3ToGeoBoundary in
 // degrees, closed, ccw; the cell holding a pole as the cap between its boundary and
 // the pole (makePoleGeometry, :361-384); a cell across the antimeridian cut into its
 // western and eastern parts (makeSafeGeometry / crossesAntiMeridian, :386-410, :258-262)
 std::vector<std::vector<Pt>> h3_cell_rings(uint64_t id, int res) {
   std::vector<Pt> b;
-  for (auto& v : mgpu::h3b::cell_boundary(id))
+  for (auto& v : mgpu::h3b::cell_boundary(id, CachedVertex()))
     b.push_back({mgpu::h3b::to_degrees(v.lon), mgpu::h3b::to_degrees(v.lat)});
   const int pole = id == pole_cell(true, res) ? 1 : (id == pole_cell(false, res) ? -1 : 0);
   if (pole) return {pole_cap(b, pole > 0)};
