@@ -2107,6 +2107,13 @@ int32_t mgpu_points_to_cells_host(mgpu_ctx* ctx, int32_t is, int32_t res, const 
 
 #ifdef MGPU_BLOB_TIMING
 #define BLOB_T0() auto blob_t = std::chrono::steady_clock::now()
+#define SIDE_T0() auto side_t = std::chrono::steady_clock::now()
+#define SIDE_MARK(what)                                                                                   \
+  do {                                                                                                    \
+    const auto now = std::chrono::steady_clock::now();                                                    \
+    fprintf(stderr, "[blob]   side:%-8s %.3f s\n", what, std::chrono::duration<double>(now - side_t).count()); \
+    side_t = now;                                                                                         \
+  } while (0)
 #define BLOB_MARK(what)                                                                                   \
   do {                                                                                                    \
     const auto now = std::chrono::steady_clock::now();                                                    \
@@ -2118,6 +2125,12 @@ int32_t mgpu_points_to_cells_host(mgpu_ctx* ctx, int32_t is, int32_t res, const 
   do {            \
   } while (0)
 #define BLOB_MARK(what) \
+  do {                  \
+  } while (0)
+#define SIDE_T0() \
+  do {            \
+  } while (0)
+#define SIDE_MARK(what) \
   do {                  \
   } while (0)
 #endif
@@ -2442,11 +2455,15 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   uint32_t max_probe = 0;
   const HVec<uint8_t> cflags_pre = cflags;  // (build_strips adds kChipNoStrips to cflags meanwhile)
   auto cell_side = [&]() -> int32_t {
+  SIDE_T0();
   // H3: probe by lattice key when possible (chip_table.h)
   if (index_system == MGPU_H3 && build_lattice(distinct, keys, &lres, &face_mask, bbox)) {
     probe_mode = mgpu::kProbeLattice;
+    SIDE_MARK("lattice");
     mark_whole_cells(distinct, lres, bbox, cflags_pre, cpart, geo);
+    SIDE_MARK("whole");
     parallel_sort(keys, [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) { return a < b; });
+    SIDE_MARK("sort");
     // (per key in parallel: duplicate / collision, the entry's core mask; then in order)
     const int64_t nk = (int64_t)keys.size();
     std::vector<uint8_t> kdup(nk);
@@ -2471,6 +2488,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
       }
     });
     if (collide) return fail(MGPU_E_INTERNAL, "lattice key collision");
+    SIDE_MARK("keys");
     entries.reserve(nk);
     for (int64_t k = 0; k < nk; k++) {
       if (kdup[k]) continue;
@@ -2525,6 +2543,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
   }
   if (index_system == MGPU_BNG && build_bng_dense(distinct, &lres, &dense[0], &bng_edge, grid))
     probe_mode = mgpu::kProbeDense;
+  SIDE_MARK("dense");
   while (cap < 2 * entries.size()) cap <<= 1;
   slots.assign(cap, mgpu::HashSlot{0, 0, 0, 0});
   for (const auto& d : entries) {
@@ -2536,6 +2555,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     slots[h] = d;
     max_probe = std::max(max_probe, k);
   }
+  SIDE_MARK("hash");
 
     return MGPU_OK;
   };
@@ -2582,6 +2602,7 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
     }
     });
   }
+  BLOB_MARK("headers");
   if (side.joinable()) side.join();
   if (side_st != MGPU_OK) return fail(side_st, "%s", side_msg.c_str());
   BLOB_MARK("cells");
