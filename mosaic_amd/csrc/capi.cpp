@@ -2509,12 +2509,28 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
       *a = (int64_t)((key >> 28) & 0xFFFFFFFULL) - (1 << 27);
       *b = (int64_t)(key & 0xFFFFFFFULL) - (1 << 27);
     };
-    for (const auto& e : entries) {
-      int f;
-      int64_t a, b;
-      dec(e.cell, &f, &a, &b);
-      amin[f] = std::min(amin[f], a), amax[f] = std::max(amax[f], a);
-      bmin[f] = std::min(bmin[f], b), bmax[f] = std::max(bmax[f], b);
+    {
+      // (per-thread extents, then combined: the same minima and maxima)
+      const int64_t ne = (int64_t)entries.size();
+      const int T = mgpu::parallel_slots(ne, 1 << 16);
+      std::vector<std::array<int64_t, 80>> ext(T);
+      for (auto& x : ext)
+        for (int f = 0; f < 20; f++) x[f] = x[40 + f] = INT64_MAX, x[20 + f] = x[60 + f] = INT64_MIN;
+      mgpu::parallel_for(ne, 1 << 16, [&](int64_t kb, int64_t ke, int t) {
+        auto& x = ext[t];
+        for (int64_t k = kb; k < ke; k++) {
+          int f;
+          int64_t a, b;
+          dec(entries[k].cell, &f, &a, &b);
+          x[f] = std::min(x[f], a), x[20 + f] = std::max(x[20 + f], a);
+          x[40 + f] = std::min(x[40 + f], b), x[60 + f] = std::max(x[60 + f], b);
+        }
+      });
+      for (auto& x : ext)
+        for (int f = 0; f < 20; f++) {
+          amin[f] = std::min(amin[f], x[f]), amax[f] = std::max(amax[f], x[20 + f]);
+          bmin[f] = std::min(bmin[f], x[40 + f]), bmax[f] = std::max(bmax[f], x[60 + f]);
+        }
     }
     int64_t total = 0;
     for (int f = 0; f < 20; f++)
@@ -2530,14 +2546,21 @@ static int32_t build_blob(int32_t index_system, int64_t n_chips, const int64_t* 
         dense[f].base = base;
         base += dense[f].w * dense[f].h;
       }
-      grid.assign(base, 0);
-      for (const auto& e : entries) {
-        int f;
-        int64_t a, b;
-        dec(e.cell, &f, &a, &b);
-        grid[dense[f].base + (b - dense[f].b0) * dense[f].w + (a - dense[f].a0)] =
-            (uint64_t)e.first | ((uint64_t)e.count << 32) | ((uint64_t)e.core_mask << 48);
-      }
+      // (zeroed and filled on the host threads: each entry owns its grid position)
+      grid.resize(base);
+      mgpu::parallel_for((int64_t)base, 1 << 20, [&](int64_t kb, int64_t ke, int) {
+        std::fill(grid.begin() + kb, grid.begin() + ke, 0ull);
+      });
+      mgpu::parallel_for((int64_t)entries.size(), 1 << 16, [&](int64_t kb, int64_t ke, int) {
+        for (int64_t k = kb; k < ke; k++) {
+          const auto& e = entries[k];
+          int f;
+          int64_t a, b;
+          dec(e.cell, &f, &a, &b);
+          grid[dense[f].base + (b - dense[f].b0) * dense[f].w + (a - dense[f].a0)] =
+              (uint64_t)e.first | ((uint64_t)e.count << 32) | ((uint64_t)e.core_mask << 48);
+        }
+      });
       probe_mode = mgpu::kProbeDense;
     }
   }
