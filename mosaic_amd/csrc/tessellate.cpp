@@ -771,7 +771,7 @@ struct CoreRule {
     }
     return o;
   }
-  // a centre decided core by its exact distance (>= 1.05 r deep): a point of buffer(-r)
+  // a centre decided core by its exact distance (>= 1.02 r deep): a point of buffer(-r)
   bool have_deep = false;
   mgpu::jtsbuf::XY deep{};
   void ensure_carved() {
